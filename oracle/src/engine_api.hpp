@@ -1,0 +1,14 @@
+// ORACLE — test infrastructure only (see ovalue.hpp header).
+#pragma once
+#include <string>
+
+#include "ovalue.hpp"
+
+namespace orc {
+// validateResourceElement / validateMap entry for matcher fixtures (entry 1 / 2)
+bool ValidateElementEntry(int entry, const Value& resource, Value& pattern, std::string* path, std::string* msg);
+// engine.Validate of one policy on one resource, serialized as JSON
+std::string ValidateToJSON(const Value& policy, const Value& resource, const Value& ctx);
+double BatchValidate(const char* policies_json, const char* resources_json, const char* ctx_json, int nthreads,
+                     unsigned char* status_out, long long* n_rules_out, long long* n_res_out);
+}  // namespace orc

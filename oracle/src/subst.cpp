@@ -1,0 +1,329 @@
+// ORACLE — test infrastructure only (see ovalue.hpp header).
+// Restatement of the reference's pattern-relative `$(...)` reference resolution
+// and escape handling, which runs per (policy, resource) before matching:
+//   pkg/engine/variables/vars.go:20-28   RegexVariables / RegexReferences / escapes
+//   pkg/engine/variables/vars.go:253-309 substituteReferencesIfAny
+//   pkg/engine/variables/vars.go:450-554 resolveReference / formAbsolutePath /
+//                                        getValueFromReference / valFromReferenceToString
+//   pkg/engine/jsonutils/traverse.go:58-130 traversal (keys and leafs, path strings)
+// Map iteration order: canonical byte-lex by key.
+#include <algorithm>
+#include <vector>
+
+#include "matcher.hpp"
+
+namespace orc {
+
+namespace {
+
+// Extent of `.[^\ ]*\)` starting at position k (the '.' char). Returns end
+// (exclusive) of the greedy match or npos.
+size_t ref_tail(const std::string& s, size_t k) {
+  if (k >= s.size() || s[k] == '\n') return std::string::npos;
+  // '.' consumes one rune
+  size_t w = 1;
+  unsigned char c = (unsigned char)s[k];
+  if (c >= 0xF0) w = 4; else if (c >= 0xE0) w = 3; else if (c >= 0xC0) w = 2;
+  size_t st = k + w;
+  size_t runend = st;
+  while (runend < s.size() && s[runend] != ' ') runend++;
+  // last ')' in [st, runend)
+  for (size_t p = runend; p-- > st;) {
+    if (s[p] == ')') return p + 1;
+  }
+  return std::string::npos;
+}
+
+struct Match {
+  size_t b, e;
+};
+
+// RegexReferences = ^\$\(.[^\ ]*\)|[^\\]\$\(.[^\ ]*\)
+std::vector<Match> find_references(const std::string& s) {
+  std::vector<Match> out;
+  size_t i = 0;
+  while (i < s.size()) {
+    if (i == 0 && s.compare(0, 2, "$(") == 0) {
+      size_t e = ref_tail(s, 2);
+      if (e != std::string::npos) { out.push_back({0, e}); i = e; continue; }
+    }
+    if (s[i] != '\\' && i + 2 < s.size() + 0 && s.compare(i + 1, 2, "$(") == 0) {
+      // [^\\] consumes one rune at i
+      size_t e = ref_tail(s, i + 3);
+      if (e != std::string::npos) { out.push_back({i, e}); i = e; continue; }
+    }
+    i++;
+  }
+  return out;
+}
+
+// RegexEscpReferences = \\\$\(.[^\ ]*\)
+std::vector<std::string> find_escaped_references(const std::string& s) {
+  std::vector<std::string> out;
+  size_t i = 0;
+  while (i < s.size()) {
+    if (s[i] == '\\' && s.compare(i + 1, 2, "$(") == 0) {
+      size_t e = ref_tail(s, i + 3);
+      if (e != std::string::npos) { out.push_back(s.substr(i, e - i)); i = e; continue; }
+    }
+    i++;
+  }
+  return out;
+}
+
+// RegexEscpVariables = \\\{\{[^{}]*\}\}
+std::vector<std::string> find_escaped_vars(const std::string& s) {
+  std::vector<std::string> out;
+  size_t i = 0;
+  while (i < s.size()) {
+    if (s[i] == '\\' && s.compare(i + 1, 2, "{{") == 0) {
+      size_t k = i + 3;
+      while (k < s.size() && s[k] != '{' && s[k] != '}') k++;
+      if (s.compare(k, 2, "}}") == 0) { out.push_back(s.substr(i, k + 2 - i)); i = k + 2; continue; }
+    }
+    i++;
+  }
+  return out;
+}
+
+std::string replace_n(const std::string& s, const std::string& from, const std::string& to, int n) {
+  if (from.empty()) return s;
+  std::string out;
+  size_t i = 0;
+  int done = 0;
+  while (true) {
+    size_t j = (n < 0 || done < n) ? s.find(from, i) : std::string::npos;
+    if (j == std::string::npos) { out += s.substr(i); break; }
+    out += s.substr(i, j - i);
+    out += to;
+    i = j + from.size();
+    done++;
+  }
+  return out;
+}
+
+std::string trim_set(const std::string& s, const std::string& set) {
+  size_t b = 0, e = s.size();
+  while (b < e && set.find(s[b]) != std::string::npos) b++;
+  while (e > b && set.find(s[e - 1]) != std::string::npos) e--;
+  return s.substr(b, e - b);
+}
+
+std::string path_clean(const std::string& p) {
+  if (p.empty()) return ".";
+  bool rooted = p[0] == '/';
+  std::vector<std::string> parts;
+  size_t i = 0;
+  while (i <= p.size()) {
+    size_t j = p.find('/', i);
+    if (j == std::string::npos) j = p.size();
+    std::string c = p.substr(i, j - i);
+    if (c.empty() || c == ".") {
+    } else if (c == "..") {
+      if (!parts.empty() && parts.back() != "..") parts.pop_back();
+      else if (!rooted) parts.push_back("..");
+    } else {
+      parts.push_back(c);
+    }
+    i = j + 1;
+  }
+  std::string out = rooted ? "/" : "";
+  for (size_t k = 0; k < parts.size(); k++) {
+    if (k) out += "/";
+    out += parts[k];
+  }
+  return out.empty() ? "." : out;
+}
+
+// path.Join(a, b)
+std::string path_join2(const std::string& a, const std::string& b) {
+  if (a.empty() && b.empty()) return "";
+  if (a.empty()) return path_clean(b);
+  if (b.empty()) return path_clean(a);
+  return path_clean(a + "/" + b);
+}
+
+std::vector<const Value::Entry*> sorted_entries(const Value& m) {
+  std::vector<const Value::Entry*> es;
+  for (const auto& e : m.m) es.push_back(&e);
+  std::sort(es.begin(), es.end(), [](const Value::Entry* a, const Value::Entry* b) { return a->order < b->order; });
+  return es;
+}
+
+// getValueFromReference: last matching key/leaf in traversal order.
+void find_by_path(const Value& v, const std::string& path, const std::string& target, const Value** found,
+                  std::string* found_key, bool* found_is_key) {
+  switch (v.t) {
+    case T::Map:
+      for (const auto* e : sorted_entries(v)) {
+        if (RemoveAnchorsFromPath(path) == target) { *found = nullptr; *found_key = e->key; *found_is_key = true; }
+        find_by_path(*e->val, path + "/" + e->key, target, found, found_key, found_is_key);
+      }
+      break;
+    case T::Arr:
+      for (size_t k = 0; k < v.a.size(); k++) find_by_path(*v.a[k], path + "/" + std::to_string(k), target, found, found_key, found_is_key);
+      break;
+    default:
+      if (RemoveAnchorsFromPath(path) == target) { *found = &v; *found_is_key = false; }
+  }
+}
+
+struct Ctx {
+  const Value* doc;
+};
+
+// Returns 0 ok (value updated), else error message.
+bool subst_string(const Ctx& cx, std::string& value, const std::string& dpath, std::string* err) {
+  std::string orig = value;
+  for (const auto& m : find_references(orig)) {
+    std::string v = orig.substr(m.b, m.e - m.b);
+    bool initial = v.compare(0, 2, "$(") == 0;
+    std::string old = v;
+    if (!initial) v = v.substr(1);
+    // resolveReference
+    std::string p = trim_set(v, "$()");
+    std::string op = GetOperatorFromStringPattern(p);
+    p = p.substr(op.size());
+    if (p.empty()) {
+      *err = "failed to resolve " + v + " at path " + dpath + ": expected path, found empty reference";
+      return false;
+    }
+    std::string abs = (!p.empty() && p[0] == '/') ? p : path_join2(dpath, p);
+    const Value* found = nullptr;
+    std::string fkey;
+    bool is_key = false;
+    find_by_path(*cx.doc, "", abs, &found, &fkey, &is_key);
+    Value keyval;
+    if (is_key) { keyval = Value::mk_str(fkey); found = &keyval; }
+    std::string resolved;
+    bool resolved_is_string = false;
+    if (op.empty()) {
+      if (!found) {
+        *err = "failed to resolve " + v + " at path " + dpath + ": <nil>";
+        return false;
+      }
+      if (found->t == T::Str) { resolved = found->s; resolved_is_string = true; }
+      else if (found->t == T::Null) {
+        *err = "failed to resolve " + v + " at path " + dpath + ": <nil>";
+        return false;
+      }
+    } else {
+      std::string fv;
+      if (found && found->t == T::Str) fv = found->s;
+      else if (found && found->t == T::Int) fv = std::to_string(found->i);
+      else if (found && found->t == T::Float) fv = go_format_f6(found->f);
+      else {
+        *err = "failed to resolve " + v + " at path " + dpath + ": incorrect expression: operator " + op +
+               " does not match with value " + go_format_v(found);
+        return false;
+      }
+      resolved = op + fv;
+      resolved_is_string = true;
+    }
+    if (resolved_is_string) {
+      std::string repl = initial ? "" : old.substr(0, 1);
+      repl += resolved;
+      value = replace_n(value, old, repl, 1);
+      continue;
+    }
+    *err = "NotResolvedReferenceErr,reference " + v + " not resolved at path " + dpath;
+    return false;
+  }
+  for (const auto& e : find_escaped_references(value)) value = replace_n(value, e, e.substr(1), -1);
+  return true;
+}
+
+bool traverse(const Ctx& cx, Value& v, const std::string& path, std::string* err) {
+  if (v.t == T::Map) {
+    // keys first (per entry: key action, then value), canonical order
+    std::vector<std::string> keys;
+    for (const auto* e : sorted_entries(v)) keys.push_back(e->key);
+    for (const auto& k : keys) {
+      std::string nk = k;
+      if (!subst_string(cx, nk, path, err)) return false;
+      Value* child = v.get_mut(k);
+      if (!traverse(cx, *child, path + "/" + k, err)) return false;
+      if (nk != k) {
+        Value copy = *child;
+        std::string order;
+        for (auto& e : v.m)
+          if (e.key == k) order = e.order;
+        v.erase(k);
+        v.set(nk, copy, order);
+      }
+    }
+    return true;
+  }
+  if (v.t == T::Arr) {
+    for (size_t k = 0; k < v.a.size(); k++)
+      if (!traverse(cx, *v.a[k], path + "/" + std::to_string(k), err)) return false;
+    return true;
+  }
+  if (v.t == T::Str) return subst_string(cx, v.s, path, err);
+  return true;
+}
+
+void unescape_vars(Value& v) {
+  if (v.t == T::Map) {
+    std::vector<std::string> keys;
+    for (const auto& e : v.m) keys.push_back(e.key);
+    for (const auto& k : keys) {
+      std::string nk = k;
+      for (const auto& e : find_escaped_vars(k)) nk = replace_n(nk, e, e.substr(1), -1);
+      Value* child = v.get_mut(k);
+      unescape_vars(*child);
+      if (nk != k) {
+        Value copy = *child;
+        std::string order;
+        for (auto& e : v.m)
+          if (e.key == k) order = e.order;
+        v.erase(k);
+        v.set(nk, copy, order);
+      }
+    }
+  } else if (v.t == T::Arr) {
+    for (auto* x : v.a) unescape_vars(*x);
+  } else if (v.t == T::Str) {
+    for (const auto& e : find_escaped_vars(v.s)) v.s = replace_n(v.s, e, e.substr(1), -1);
+  }
+}
+
+}  // namespace
+
+bool HasVariable(const std::string& s) {
+  // RegexVariables = ^\{\{[^{}]*\}\}|[^\\]\{\{[^{}]*\}\}
+  for (size_t j = 0; j + 1 < s.size(); j++) {
+    if (s[j] == '{' && s[j + 1] == '{') {
+      if (j > 0 && s[j - 1] == '\\') continue;
+      size_t k = j + 2;
+      while (k < s.size() && s[k] != '{' && s[k] != '}') k++;
+      if (s.compare(k, 2, "}}") == 0) return true;
+    }
+  }
+  return false;
+}
+
+bool DocHasVariable(const Value& v) {
+  switch (v.t) {
+    case T::Str: return HasVariable(v.s);
+    case T::Map:
+      for (const auto& e : v.m)
+        if (HasVariable(e.key) || DocHasVariable(*e.val)) return true;
+      return false;
+    case T::Arr:
+      for (const auto* x : v.a)
+        if (DocHasVariable(*x)) return true;
+      return false;
+    default: return false;
+  }
+}
+
+bool SubstituteReferences(Value& document, std::string* err) {
+  Value original = document;  // references resolve against the unmodified document
+  Ctx cx{&original};
+  if (!traverse(cx, document, "", err)) return false;
+  unescape_vars(document);
+  return true;
+}
+
+}  // namespace orc
