@@ -1,0 +1,119 @@
+/*
+ * kvgpu.h — C ABI of the MI355X-native batch validate.pattern engine.
+ *
+ * Drop-in boundary for Kyverno's validate hot path (isabella232/kyverno v1.5.x):
+ *   engine.Validate(policyContext *PolicyContext) *response.EngineResponse
+ *       pkg/engine/validation.go:26
+ * called per (policy, resource) by
+ *   CLI apply        pkg/kyverno/common/common.go:541 (loop at pkg/kyverno/apply/apply_command.go:270-310)
+ *   background scan  pkg/policy/apply.go:72 (via pkg/policy/existing.go:55-58)
+ *   test runner      pkg/testrunner/scenario.go:169
+ * The batch form evaluates every (resource, rule) pair of a policy set at once.
+ * Plain C types only; all handles are opaque and library-owned until kv_free_*.
+ * Return value: 0 on success, negative KV_E_* on failure (with *err set when
+ * err != NULL; free with kv_free_error). Per-pair evaluation never fails: it
+ * yields status KV_STATUS_ERROR exactly like the reference.
+ */
+#ifndef KVGPU_H
+#define KVGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* response.RuleStatus (pkg/engine/response/status.go:14-28) + batch extras */
+enum {
+  KV_STATUS_PASS = 0,
+  KV_STATUS_FAIL = 1,
+  KV_STATUS_WARN = 2,
+  KV_STATUS_ERROR = 3,
+  KV_STATUS_SKIP = 4,
+  KV_STATUS_NOMATCH = 5, /* no RuleResponse: rule not matched / not a pattern rule (CLI counts skip) */
+  KV_STATUS_CPU = 6      /* route the pair to the reference CPU engine (processValidationRule) */
+};
+
+/* rule routes decided at compile time */
+enum { KV_ROUTE_GPU = 0, KV_ROUTE_CPU = 1, KV_ROUTE_NORESPONSE = 2, KV_ROUTE_CONSTANT = 3 };
+
+/* kv_validate modes (bit set) */
+enum { KV_MODE_STATUS = 1, KV_MODE_ERRORS = 2, KV_MODE_COUNTS = 4 };
+
+enum { KV_E_INVALID = -1, KV_E_PARSE = -2, KV_E_DEVICE = -3, KV_E_RANGE = -4, KV_E_NOMEM = -5 };
+
+typedef struct kv_policyset kv_policyset;
+typedef struct kv_batch kv_batch;
+typedef struct kv_result kv_result;
+typedef struct kv_error {
+  int code;
+  char* message;
+} kv_error;
+
+typedef struct kv_rule_info {
+  uint32_t policy;          /* index of the policy in the compiled list */
+  const char* policy_name;  /* metadata.name */
+  const char* name;         /* rule name */
+  uint32_t route;           /* KV_ROUTE_* */
+  const char* route_reason; /* why CPU / no-response ("" for GPU) */
+  const char* message;      /* validate.message */
+  uint32_t any_pattern;     /* 1 for anyPattern rules */
+  uint32_t const_status;    /* KV_ROUTE_CONSTANT */
+  const char* const_message;
+} kv_rule_info;
+
+/* Compile a JSON list of ClusterPolicy/Policy objects (already through
+ * policymutation autogen, as the reference CLI does before engine.Validate).
+ * Replaces the per-call interpretation in pkg/engine/validate, pkg/engine/anchor,
+ * pkg/engine/operator and the $() reference substitution of
+ * pkg/engine/variables/vars.go:253-309. */
+int kv_compile(const char* policies_json, size_t len, uint32_t flags, kv_policyset** out, kv_error** err);
+int kv_policyset_info(const kv_policyset* ps, uint32_t* n_policies, uint32_t* n_rules);
+int kv_rule_info_get(const kv_policyset* ps, uint32_t rule, kv_rule_info* out);
+
+/* Ingest resources (JSON array or NDJSON of unstructured objects; numbers typed
+ * like unstructured.UnmarshalJSON). ns_labels_json: {"<namespace>": {"k":"v"}}
+ * (PolicyContext.NamespaceLabels per namespace) or NULL. */
+int kv_ingest(const kv_policyset* ps, const char* resources_json, size_t len, const char* ns_labels_json,
+              kv_batch** out, kv_error** err);
+int kv_batch_info(const kv_batch* b, uint64_t* n_res, uint64_t* store_bytes);
+
+/* Evaluate every (resource, rule) pair on HIP device `device`.
+ * ctx_json: {"admission": {"roles":[], "clusterRoles":[], "groups":[], "username":""},
+ *            "excludeGroupRole": []}  (PolicyContext.AdmissionInfo / ExcludeGroupRole) or NULL. */
+int kv_validate(const kv_policyset* ps, const kv_batch* b, const char* ctx_json, int device, uint32_t mode,
+                kv_result** out, kv_error** err);
+
+/* status[rule * n_res + res] (rule-major) */
+int kv_result_status(const kv_result* r, const uint8_t** status, uint64_t* n_rules, uint64_t* n_res);
+/* counts[rule * 8 + status] */
+int kv_result_counts(const kv_result* r, const int64_t** counts);
+/* failing path of a FAIL pair, e.g. "/spec/containers/0/image/" (needs KV_MODE_ERRORS);
+ * returns the string length, or a negative code. */
+int kv_result_path(const kv_result* r, uint32_t rule, uint64_t res, char* buf, size_t cap);
+/* raw error record: kind (validate.go/anchor.go error form) and anchor-wrap flags */
+int kv_result_error(const kv_result* r, uint32_t rule, uint64_t res, uint32_t* kind, uint32_t* flags);
+double kv_result_kernel_ms(const kv_result* r);
+
+/* Benchmark entry: device-resident inputs, `iters` timed launches on one stream
+ * bracketed by HIP events. Returns mean kernel milliseconds per pass over all
+ * rules of the batch. */
+int kv_bench(const kv_policyset* ps, const kv_batch* b, const char* ctx_json, int device, uint32_t mode, int warmup,
+             int iters, double* ms_per_iter, kv_error** err);
+
+/* Synthetic resource generator for the benchmark configs:
+ * kind_mix 0 = Pods; 1 = Pods/Deployments/Services 60/25/15. Returns NDJSON
+ * (free with kv_free_buffer). */
+int kv_synth(uint64_t seed, uint64_t n, uint32_t kind_mix, char** json_out, size_t* len);
+
+void kv_free_policyset(kv_policyset* ps);
+void kv_free_batch(kv_batch* b);
+void kv_free_result(kv_result* r);
+void kv_free_error(kv_error* e);
+void kv_free_buffer(char* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KVGPU_H */

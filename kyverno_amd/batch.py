@@ -1,0 +1,190 @@
+"""Batch API over the C ABI: compile a policy set once, ingest resources once,
+evaluate every (resource, rule) pair on a MI355X.
+
+This is the batch form of ``engine.Validate`` (reference
+``pkg/engine/validation.go:26``): statuses use ``response.RuleStatus`` codes
+(``pkg/engine/response/status.go:14-28``) plus ``NOMATCH`` (no RuleResponse)
+and ``CPU`` (the pair needs the reference CPU engine: context, preconditions,
+deny, foreach or ``{{ }}`` variables).
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native
+from ._native import RuleInfo, check, lib, new_err
+
+PASS, FAIL, WARN, ERROR, SKIP, NOMATCH, CPU = range(7)
+STATUS_NAMES = ["pass", "fail", "warn", "error", "skip", "nomatch", "cpu"]
+
+MODE_STATUS, MODE_ERRORS, MODE_COUNTS = 1, 2, 4
+ROUTE_GPU, ROUTE_CPU, ROUTE_NORESPONSE, ROUTE_CONSTANT = range(4)
+
+
+def _dumps(x) -> bytes:
+    if isinstance(x, (bytes, bytearray)):
+        return bytes(x)
+    if isinstance(x, str):
+        return x.encode("utf-8")
+    return json.dumps(x, ensure_ascii=False, separators=(",", ":")).encode("utf-8")
+
+
+@dataclass
+class Rule:
+    index: int
+    policy: int
+    policy_name: str
+    name: str
+    route: int
+    route_reason: str
+    message: str
+    any_pattern: bool
+    const_status: int
+    const_message: str
+
+
+class PolicySet:
+    """Compiled policies (``kv_compile``). Input: list of policy dicts or JSON text."""
+
+    def __init__(self, policies):
+        L = lib()
+        data = _dumps(policies)
+        h = ctypes.c_void_p()
+        err = new_err()
+        check(L.kv_compile(data, len(data), 0, ctypes.byref(h), ctypes.byref(err)), err)
+        self._h = h
+        np_, nr = ctypes.c_uint32(), ctypes.c_uint32()
+        L.kv_policyset_info(h, ctypes.byref(np_), ctypes.byref(nr))
+        self.n_policies, self.n_rules = np_.value, nr.value
+        self.rules: list[Rule] = []
+        for i in range(self.n_rules):
+            ri = RuleInfo()
+            L.kv_rule_info_get(h, i, ctypes.byref(ri))
+            d = lambda b: (b or b"").decode("utf-8")  # noqa: E731
+            self.rules.append(Rule(i, ri.policy, d(ri.policy_name), d(ri.name), ri.route, d(ri.route_reason),
+                                   d(ri.message), bool(ri.any_pattern), ri.const_status, d(ri.const_message)))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().kv_free_policyset(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def policy_rules(self, policy: int) -> list[Rule]:
+        return [r for r in self.rules if r.policy == policy]
+
+
+class Batch:
+    """Ingested resources (``kv_ingest``): list of dicts, JSON array text or NDJSON."""
+
+    def __init__(self, policyset: PolicySet, resources, namespace_labels: dict | None = None):
+        L = lib()
+        if isinstance(resources, (list, tuple)):
+            data = b"\n".join(_dumps(r) for r in resources)
+        else:
+            data = _dumps(resources)
+        ns = _dumps(namespace_labels) if namespace_labels else None
+        h = ctypes.c_void_p()
+        err = new_err()
+        check(L.kv_ingest(policyset._h, data, len(data), ns, ctypes.byref(h), ctypes.byref(err)), err)
+        self._h = h
+        self.policyset = policyset
+        n, b = ctypes.c_uint64(), ctypes.c_uint64()
+        L.kv_batch_info(h, ctypes.byref(n), ctypes.byref(b))
+        self.n_res, self.store_bytes = n.value, b.value
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().kv_free_batch(h)
+            except Exception:
+                pass
+            self._h = None
+
+
+class Result:
+    def __init__(self, h, policyset: PolicySet, batch: Batch):
+        self._h = h
+        self.policyset = policyset
+        self.batch = batch
+        L = lib()
+        p = ctypes.c_void_p()
+        nr, nn = ctypes.c_uint64(), ctypes.c_uint64()
+        L.kv_result_status(h, ctypes.byref(p), ctypes.byref(nr), ctypes.byref(nn))
+        self.n_rules, self.n_res = nr.value, nn.value
+        if p.value:
+            buf = (ctypes.c_uint8 * (self.n_rules * self.n_res)).from_address(p.value)
+            self.status = np.frombuffer(buf, dtype=np.uint8).reshape(self.n_rules, self.n_res).copy()
+        else:
+            self.status = None
+        c = ctypes.c_void_p()
+        L.kv_result_counts(h, ctypes.byref(c))
+        cb = (ctypes.c_int64 * (self.n_rules * 8)).from_address(c.value) if self.n_rules else []
+        self.counts = np.frombuffer(cb, dtype=np.int64).reshape(self.n_rules, 8).copy() if self.n_rules else \
+            np.zeros((0, 8), np.int64)
+        self.kernel_ms = L.kv_result_kernel_ms(h)
+
+    def path(self, rule: int, res: int) -> str | None:
+        buf = ctypes.create_string_buffer(4096)
+        n = lib().kv_result_path(self._h, rule, res, buf, 4096)
+        if n < 0:
+            return None
+        return buf.value.decode("utf-8")
+
+    def error(self, rule: int, res: int):
+        k, f = ctypes.c_uint32(), ctypes.c_uint32()
+        if lib().kv_result_error(self._h, rule, res, ctypes.byref(k), ctypes.byref(f)) != 0:
+            return None
+        return k.value, f.value
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().kv_free_result(h)
+            except Exception:
+                pass
+            self._h = None
+
+
+def validate(policyset: PolicySet, batch: Batch, admission: dict | None = None,
+             exclude_group_role: list | None = None, device: int = 0,
+             mode: int = MODE_STATUS | MODE_ERRORS) -> Result:
+    ctx = {}
+    if admission:
+        ctx["admission"] = admission
+    if exclude_group_role:
+        ctx["excludeGroupRole"] = list(exclude_group_role)
+    h = ctypes.c_void_p()
+    err = new_err()
+    check(lib().kv_validate(policyset._h, batch._h, _dumps(ctx), device, mode, ctypes.byref(h), ctypes.byref(err)),
+          err)
+    return Result(h, policyset, batch)
+
+
+def bench(policyset: PolicySet, batch: Batch, device: int = 0, mode: int = MODE_COUNTS, warmup: int = 2,
+          iters: int = 10, ctx: dict | None = None) -> float:
+    ms = ctypes.c_double()
+    err = new_err()
+    check(lib().kv_bench(policyset._h, batch._h, _dumps(ctx or {}), device, mode, warmup, iters, ctypes.byref(ms),
+                         ctypes.byref(err)), err)
+    return ms.value
+
+
+def synth(seed: int, n: int, kind_mix: int = 0) -> bytes:
+    p = ctypes.c_void_p()
+    ln = ctypes.c_size_t()
+    rc = lib().kv_synth(seed, n, kind_mix, ctypes.byref(p), ctypes.byref(ln))
+    if rc != 0:
+        raise _native.KvError(rc, "kv_synth failed")
+    data = ctypes.string_at(p.value, ln.value)
+    lib().kv_free_buffer(p)
+    return data

@@ -1,0 +1,542 @@
+// C ABI (include/kvgpu.h) + device runtime: HBM residency of compiled policy
+// sets and ingested batches, launch-time folding of batch-constant user info,
+// result decoding (failing paths) on the host.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/kvgpu.h"
+#include "kvdev.h"
+#include "kvinternal.hpp"
+
+using namespace kv;
+using namespace kvh;
+
+namespace {
+
+struct HipError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define HIPCHK(x)                                                                              \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess) throw HipError(std::string(#x) + ": " + hipGetErrorString(e_));      \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  int dev = -1;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (p) {
+      int cur;
+      if (hipGetDevice(&cur) == hipSuccess) {
+        (void)hipSetDevice(dev);
+        (void)hipFree(p);
+        (void)hipSetDevice(cur);
+      }
+    }
+  }
+  template <class T>
+  void upload(const std::vector<T>& v, int device) {
+    upload_raw(v.data(), v.size() * sizeof(T), device);
+  }
+  void upload_raw(const void* src, size_t bytes, int device) {
+    dev = device;
+    n = bytes;
+    HIPCHK(hipMalloc(&p, std::max<size_t>(bytes, 16)));
+    if (bytes) HIPCHK(hipMemcpy(p, src, bytes, hipMemcpyHostToDevice));
+  }
+  void alloc(size_t bytes, int device) {
+    dev = device;
+    n = bytes;
+    HIPCHK(hipMalloc(&p, std::max<size_t>(bytes, 16)));
+  }
+};
+
+struct DevPolicySet {
+  DevBuf prog, preds, alts, conjs, atoms, rules, filters, kinds, strrefs, strpairs, sels, sellabels, selexprs, kgs, pstr;
+  DevPS view{};
+};
+
+struct DevBatchRes {
+  DevBuf nodes, vals, res, kvs, bstr, nsbits, koff, klen, kstr;
+  DevBatch view{};
+};
+
+}  // namespace
+
+struct kv_policyset {
+  PolicySet ps;
+  std::mutex mu;
+  std::map<int, std::unique_ptr<DevPolicySet>> dev;
+};
+
+struct kv_batch {
+  Batch b;
+  const kv_policyset* owner = nullptr;
+  std::mutex mu;
+  std::map<int, std::unique_ptr<DevBatchRes>> dev;
+};
+
+struct kv_result {
+  const kv_policyset* ps = nullptr;
+  const kv_batch* b = nullptr;
+  uint64_t n_rules = 0, n_res = 0;
+  std::vector<uint8_t> status;
+  std::vector<ErrRec> err;
+  std::vector<int64_t> counts;
+  double kernel_ms = 0;
+  uint32_t mode = 0;
+};
+
+namespace {
+
+int fail(kv_error** err, int code, const std::string& msg) {
+  if (err) {
+    *err = (kv_error*)malloc(sizeof(kv_error));
+    (*err)->code = code;
+    (*err)->message = strdup(msg.c_str());
+  }
+  return code;
+}
+
+DevPolicySet& dev_ps(kv_policyset* s, int device) {
+  std::lock_guard<std::mutex> g(s->mu);
+  auto it = s->dev.find(device);
+  if (it != s->dev.end()) return *it->second;
+  auto d = std::make_unique<DevPolicySet>();
+  const PolicySet& ps = s->ps;
+  d->prog.upload(ps.prog, device);
+  d->preds.upload(ps.preds, device);
+  d->alts.upload(ps.alts, device);
+  d->conjs.upload(ps.conjs, device);
+  d->atoms.upload(ps.atoms, device);
+  d->rules.upload(ps.rules, device);
+  d->filters.upload(ps.filters, device);
+  d->kinds.upload(ps.kinds, device);
+  d->strrefs.upload(ps.strrefs, device);
+  d->strpairs.upload(ps.strpairs, device);
+  d->sels.upload(ps.selectors, device);
+  d->sellabels.upload(ps.sellabels, device);
+  d->selexprs.upload(ps.selexprs, device);
+  d->kgs.upload(ps.kg_specs, device);
+  d->pstr.upload_raw(ps.strs.data(), ps.strs.size(), device);
+  DevPS& v = d->view;
+  v.prog = (const Inst*)d->prog.p;
+  v.preds = (const Pred*)d->preds.p;
+  v.alts = (const Alt*)d->alts.p;
+  v.conjs = (const Conj*)d->conjs.p;
+  v.atoms = (const Atom*)d->atoms.p;
+  v.rules = (const RuleRec*)d->rules.p;
+  v.filters = (const MFilter*)d->filters.p;
+  v.kinds = (const KindSpec*)d->kinds.p;
+  v.strrefs = (const StrRef*)d->strrefs.p;
+  v.strpairs = (const StrPair*)d->strpairs.p;
+  v.sels = (const Selector*)d->sels.p;
+  v.sellabels = (const SelLabel*)d->sellabels.p;
+  v.selexprs = (const SelExpr*)d->selexprs.p;
+  v.kg_specs = (const uint32_t*)d->kgs.p;
+  v.pstr = (const uint8_t*)d->pstr.p;
+  v.star_id = ps.lookup("*");
+  auto& ref = *d;
+  s->dev[device] = std::move(d);
+  return ref;
+}
+
+DevBatchRes& dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
+  std::lock_guard<std::mutex> g(bt->mu);
+  auto it = bt->dev.find(device);
+  if (it != bt->dev.end()) return *it->second;
+  auto d = std::make_unique<DevBatchRes>();
+  const Batch& b = bt->b;
+  d->nodes.upload(b.nodes, device);
+  d->vals.upload(b.vals, device);
+  d->res.upload(b.res, device);
+  d->kvs.upload(b.kvs, device);
+  d->bstr.upload_raw(b.strs.data(), b.strs.size(), device);
+  d->nsbits.upload(b.ns_bits, device);
+  // key string table: static dictionary then batch-dynamic keys
+  std::vector<uint32_t> off, len;
+  std::string ks;
+  for (auto& k : ps.keys) { off.push_back((uint32_t)ks.size()); len.push_back((uint32_t)k.size()); ks += k; }
+  for (auto& k : b.dyn_keys) { off.push_back((uint32_t)ks.size()); len.push_back((uint32_t)k.size()); ks += k; }
+  d->koff.upload(off, device);
+  d->klen.upload(len, device);
+  d->kstr.upload_raw(ks.data(), ks.size(), device);
+  DevBatch& v = d->view;
+  v.nodes = (const Node*)d->nodes.p;
+  v.vals = (const Val*)d->vals.p;
+  v.res = (const Res*)d->res.p;
+  v.kvs = (const KV*)d->kvs.p;
+  v.bstr = (const uint8_t*)d->bstr.p;
+  v.ns_bits = (const uint32_t*)d->nsbits.p;
+  v.key_off = (const uint32_t*)d->koff.p;
+  v.key_len = (const uint32_t*)d->klen.p;
+  v.kstr = (const uint8_t*)d->kstr.p;
+  v.ns_words = b.ns_words;
+  v.n_res = (uint32_t)b.res.size();
+  auto& ref = *d;
+  bt->dev[device] = std::move(d);
+  return ref;
+}
+
+struct AdmissionCtx {
+  std::vector<std::string> roles, clusterRoles, groups, dyn;
+  std::string username;
+  bool empty() const { return roles.empty() && clusterRoles.empty() && groups.empty() && username.empty(); }
+};
+
+AdmissionCtx parse_ctx(const char* ctx_json) {
+  AdmissionCtx c;
+  if (!ctx_json || !*ctx_json) return c;
+  JDoc d;
+  parse_json(ctx_json, strlen(ctx_json), NUM_FLOAT, &d);
+  auto list = [&](int64_t n, std::vector<std::string>* out) {
+    if (n < 0 || d.at((uint32_t)n).t != J_ARR) return;
+    const JNode& a = d.at((uint32_t)n);
+    for (uint32_t k = a.first; k < a.first + a.count; k++)
+      if (d.at(k).t == J_STR) out->push_back(std::string(d.sval(d.at(k))));
+  };
+  int64_t a = d.get(d.root, "admission");
+  if (a >= 0 && d.at((uint32_t)a).t == J_MAP) {
+    list(d.get((uint32_t)a, "roles"), &c.roles);
+    list(d.get((uint32_t)a, "clusterRoles"), &c.clusterRoles);
+    list(d.get((uint32_t)a, "groups"), &c.groups);
+    int64_t u = d.get((uint32_t)a, "username");
+    if (u >= 0 && d.at((uint32_t)u).t == J_STR) c.username = std::string(d.sval(d.at((uint32_t)u)));
+  }
+  list(d.get(d.root, "excludeGroupRole"), &c.dyn);
+  return c;
+}
+
+bool slice_contains(const std::vector<std::string>& s, const std::vector<std::string>& v) {
+  for (auto& x : v)
+    if (std::find(s.begin(), s.end(), x) != s.end()) return true;
+  return false;
+}
+
+// user-info part of doesResourceMatchConditionBlock (pkg/engine/utils.go:183-229):
+// true if it appends errors (every checked criterion failed)
+bool ui_fails(const UserInfoSpec& ui, const AdmissionCtx& ai) {
+  std::vector<std::string> keys = ai.groups;
+  keys.push_back(ai.username);
+  int checked = 0, uerr = 0;
+  if (!ui.roles.empty() && !slice_contains(keys, ai.dyn)) {
+    checked++;
+    if (!slice_contains(ui.roles, ai.roles)) uerr++;
+    else return false;
+  }
+  if (!ui.clusterRoles.empty() && !slice_contains(keys, ai.dyn)) {
+    checked++;
+    if (!slice_contains(ui.clusterRoles, ai.clusterRoles)) uerr++;
+    else return false;
+  }
+  if (!ui.subjects.empty()) {
+    checked++;
+    const std::string sa = "system:serviceaccount:";
+    std::vector<UserInfoSpec::Subj> subs = ui.subjects;
+    for (auto& e : ai.dyn) subs.push_back({"Group", e, ""});
+    bool m = false;
+    for (auto& s : subs) {
+      if (s.kind == "ServiceAccount") {
+        if (ai.username.size() <= sa.size()) continue;
+        if (ai.username.substr(sa.size()) == s.ns + ":" + s.name) { m = true; break; }
+      } else if (s.kind == "User" || s.kind == "Group") {
+        if (std::find(keys.begin(), keys.end(), s.name) != keys.end()) { m = true; break; }
+      }
+    }
+    if (!m) uerr++;
+    else return false;
+  }
+  return checked == uerr && uerr > 0;
+}
+
+std::vector<uint32_t> fold_filters(const PolicySet& ps, const AdmissionCtx& ai) {
+  std::vector<uint32_t> out(ps.filters.size());
+  size_t f = 0;
+  for (size_t r = 0; r < ps.rules.size(); r++) {
+    const RuleHost& rh = ps.rhost[r];
+    for (size_t k = 0; k < rh.filter_ui.size(); k++, f++) {
+      uint32_t fl = ps.filters[f].flags & ~(MF_EMPTY | MF_UI_FAIL);
+      bool rd_empty = ps.filters[f].flags & MF_EMPTY;
+      UserInfoSpec ui = rh.filter_ui[k];
+      if (rh.filter_is_match[k] && ai.empty()) ui = UserInfoSpec();
+      if (rd_empty && !ui.present) fl |= MF_EMPTY;
+      if (ui.present && ui_fails(ui, ai)) fl |= MF_UI_FAIL;
+      out[f] = fl;
+    }
+  }
+  return out;
+}
+
+std::string render_path(const PolicySet& ps, const Batch& b, const ErrRec& e) {
+  std::vector<std::string> segs;
+  uint32_t p = e.pnode;
+  while (p != 0xFFFFFFFFu && p < ps.pnodes.size()) {
+    const PNodeInfo& n = ps.pnodes[p];
+    switch (n.seg) {
+      case SEG_ROOT: break;
+      case SEG_KEY: segs.push_back(n.key); break;
+      case SEG_LOOP: segs.push_back(std::to_string(e.idx[n.level & 3])); break;
+      case SEG_CONST_INDEX: segs.push_back(std::to_string(n.level)); break;
+      case SEG_RESOLVED: {
+        if (e.keynode != ABSENT && e.keynode < b.nodes.size()) {
+          uint32_t k = b.nodes[e.keynode].key;
+          segs.push_back(k < ps.keys.size() ? ps.keys[k] : b.dyn_keys[k - ps.keys.size()]);
+        } else {
+          segs.push_back(n.key);
+        }
+        break;
+      }
+    }
+    p = n.parent;
+  }
+  std::string out = "/";
+  for (size_t i = segs.size(); i-- > 0;) out += segs[i] + "/";
+  return out;
+}
+
+void run(kv_policyset* ps, kv_batch* bt, const char* ctx_json, int device, uint32_t mode, kv_result* out, int warmup,
+         int iters, double* ms) {
+  HIPCHK(hipSetDevice(device));
+  DevPolicySet& dp = dev_ps(ps, device);
+  DevBatchRes& db = dev_batch(bt, ps->ps, device);
+  AdmissionCtx ai = parse_ctx(ctx_json);
+  std::vector<uint32_t> ff = fold_filters(ps->ps, ai);
+  DevBuf fflags;
+  fflags.upload(ff, device);
+  DevPS P = dp.view;
+  P.fflags = (const uint32_t*)fflags.p;
+  uint64_t nrules = ps->ps.rules.size(), nres = bt->b.res.size();
+  DevBuf st, er, cn;
+  DevOut O{};
+  O.full = 0;
+  if (mode & KV_MODE_STATUS) {
+    st.alloc(nrules * nres, device);
+    O.status = (uint8_t*)st.p;
+    O.full |= 1;
+  }
+  if (mode & KV_MODE_ERRORS) {
+    er.alloc(nrules * nres * sizeof(ErrRec), device);
+    O.err = (ErrRec*)er.p;
+    O.full |= 2 | 1;
+    if (!O.status) {
+      st.alloc(nrules * nres, device);
+      O.status = (uint8_t*)st.p;
+    }
+  }
+  cn.alloc(std::max<uint64_t>(nrules, 1) * KV_HIST * sizeof(unsigned long long), device);
+  O.counts = (unsigned long long*)cn.p;
+  hipStream_t stream;
+  HIPCHK(hipStreamCreate(&stream));
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  auto pass = [&]() {
+    HIPCHK(hipMemsetAsync(cn.p, 0, cn.n, stream));
+    HIPCHK(launch_validate(P, db.view, O, 0, (uint32_t)nrules, stream));
+  };
+  for (int i = 0; i < warmup; i++) pass();
+  HIPCHK(hipEventRecord(e0, stream));
+  for (int i = 0; i < std::max(iters, 1); i++) pass();
+  HIPCHK(hipEventRecord(e1, stream));
+  HIPCHK(hipEventSynchronize(e1));
+  float t = 0;
+  HIPCHK(hipEventElapsedTime(&t, e0, e1));
+  if (ms) *ms = t / std::max(iters, 1);
+  if (out) {
+    out->ps = ps;
+    out->b = bt;
+    out->n_rules = nrules;
+    out->n_res = nres;
+    out->mode = mode;
+    out->kernel_ms = t / std::max(iters, 1);
+    std::vector<unsigned long long> c(nrules * KV_HIST);
+    if (nrules) HIPCHK(hipMemcpy(c.data(), cn.p, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    out->counts.assign(c.begin(), c.end());
+    if (O.status) {
+      out->status.resize(nrules * nres);
+      if (!out->status.empty()) HIPCHK(hipMemcpy(out->status.data(), st.p, out->status.size(), hipMemcpyDeviceToHost));
+    }
+    if (O.err) {
+      out->err.resize(nrules * nres);
+      if (!out->err.empty()) HIPCHK(hipMemcpy(out->err.data(), er.p, out->err.size() * sizeof(ErrRec), hipMemcpyDeviceToHost));
+    }
+  }
+  HIPCHK(hipEventDestroy(e0));
+  HIPCHK(hipEventDestroy(e1));
+  HIPCHK(hipStreamDestroy(stream));
+}
+
+}  // namespace
+
+extern "C" {
+
+int kv_compile(const char* policies_json, size_t len, uint32_t flags, kv_policyset** out, kv_error** err) {
+  (void)flags;
+  if (!policies_json || !out) return fail(err, KV_E_INVALID, "null argument");
+  try {
+    auto* s = new kv_policyset();
+    try {
+      compile_policies(policies_json, len, &s->ps);
+    } catch (...) {
+      delete s;
+      throw;
+    }
+    *out = s;
+    return 0;
+  } catch (const std::exception& e) {
+    return fail(err, KV_E_PARSE, e.what());
+  }
+}
+
+int kv_policyset_info(const kv_policyset* ps, uint32_t* n_policies, uint32_t* n_rules) {
+  if (!ps) return KV_E_INVALID;
+  if (n_policies) *n_policies = (uint32_t)ps->ps.policy_names.size();
+  if (n_rules) *n_rules = (uint32_t)ps->ps.rules.size();
+  return 0;
+}
+
+int kv_rule_info_get(const kv_policyset* ps, uint32_t rule, kv_rule_info* out) {
+  if (!ps || !out) return KV_E_INVALID;
+  if (rule >= ps->ps.rules.size()) return KV_E_RANGE;
+  const RuleHost& rh = ps->ps.rhost[rule];
+  const RuleRec& rr = ps->ps.rules[rule];
+  out->policy = rh.policy;
+  out->policy_name = ps->ps.policy_names[rh.policy].c_str();
+  out->name = rh.name.c_str();
+  out->route = rr.route;
+  out->route_reason = rh.route_reason.c_str();
+  out->message = rh.message.c_str();
+  out->any_pattern = rh.anypattern ? 1 : 0;
+  out->const_status = rr.const_status;
+  out->const_message = rh.const_message.c_str();
+  return 0;
+}
+
+int kv_ingest(const kv_policyset* ps, const char* resources_json, size_t len, const char* ns_labels_json, kv_batch** out,
+              kv_error** err) {
+  if (!ps || !resources_json || !out) return fail(err, KV_E_INVALID, "null argument");
+  try {
+    auto* b = new kv_batch();
+    b->owner = ps;
+    try {
+      ingest_resources(ps->ps, resources_json, len, ns_labels_json, &b->b);
+    } catch (...) {
+      delete b;
+      throw;
+    }
+    *out = b;
+    return 0;
+  } catch (const std::exception& e) {
+    return fail(err, KV_E_PARSE, e.what());
+  }
+}
+
+int kv_batch_info(const kv_batch* b, uint64_t* n_res, uint64_t* store_bytes) {
+  if (!b) return KV_E_INVALID;
+  if (n_res) *n_res = b->b.res.size();
+  if (store_bytes) *store_bytes = b->b.bytes_referenced;
+  return 0;
+}
+
+int kv_validate(const kv_policyset* ps, const kv_batch* b, const char* ctx_json, int device, uint32_t mode,
+                kv_result** out, kv_error** err) {
+  if (!ps || !b || !out) return fail(err, KV_E_INVALID, "null argument");
+  if (b->owner != ps) return fail(err, KV_E_INVALID, "batch was ingested for a different policy set");
+  try {
+    auto* r = new kv_result();
+    try {
+      run(const_cast<kv_policyset*>(ps), const_cast<kv_batch*>(b), ctx_json, device, mode, r, 0, 1, nullptr);
+    } catch (...) {
+      delete r;
+      throw;
+    }
+    *out = r;
+    return 0;
+  } catch (const HipError& e) {
+    return fail(err, KV_E_DEVICE, e.what());
+  } catch (const std::exception& e) {
+    return fail(err, KV_E_PARSE, e.what());
+  }
+}
+
+int kv_bench(const kv_policyset* ps, const kv_batch* b, const char* ctx_json, int device, uint32_t mode, int warmup,
+             int iters, double* ms_per_iter, kv_error** err) {
+  if (!ps || !b || !ms_per_iter) return fail(err, KV_E_INVALID, "null argument");
+  try {
+    run(const_cast<kv_policyset*>(ps), const_cast<kv_batch*>(b), ctx_json, device, mode, nullptr, warmup, iters,
+        ms_per_iter);
+    return 0;
+  } catch (const HipError& e) {
+    return fail(err, KV_E_DEVICE, e.what());
+  } catch (const std::exception& e) {
+    return fail(err, KV_E_PARSE, e.what());
+  }
+}
+
+int kv_result_status(const kv_result* r, const uint8_t** status, uint64_t* n_rules, uint64_t* n_res) {
+  if (!r) return KV_E_INVALID;
+  if (status) *status = r->status.empty() ? nullptr : r->status.data();
+  if (n_rules) *n_rules = r->n_rules;
+  if (n_res) *n_res = r->n_res;
+  return 0;
+}
+
+int kv_result_counts(const kv_result* r, const int64_t** counts) {
+  if (!r || !counts) return KV_E_INVALID;
+  *counts = r->counts.data();
+  return 0;
+}
+
+int kv_result_path(const kv_result* r, uint32_t rule, uint64_t res, char* buf, size_t cap) {
+  if (!r || r->err.empty()) return KV_E_INVALID;
+  if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
+  size_t o = (size_t)rule * r->n_res + res;
+  if (r->status[o] != ST_FAIL) return KV_E_INVALID;
+  std::string p = render_path(r->ps->ps, r->b->b, r->err[o]);
+  if (buf && cap) {
+    size_t n = std::min(cap - 1, p.size());
+    memcpy(buf, p.data(), n);
+    buf[n] = 0;
+  }
+  return (int)p.size();
+}
+
+int kv_result_error(const kv_result* r, uint32_t rule, uint64_t res, uint32_t* kind, uint32_t* flags) {
+  if (!r || r->err.empty()) return KV_E_INVALID;
+  if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
+  const ErrRec& e = r->err[(size_t)rule * r->n_res + res];
+  if (kind) *kind = e.kind_flags & 0xFFFF;
+  if (flags) *flags = e.kind_flags >> 16;
+  return 0;
+}
+
+double kv_result_kernel_ms(const kv_result* r) { return r ? r->kernel_ms : -1.0; }
+
+void kv_free_policyset(kv_policyset* ps) { delete ps; }
+void kv_free_batch(kv_batch* b) { delete b; }
+void kv_free_result(kv_result* r) { delete r; }
+void kv_free_error(kv_error* e) {
+  if (e) {
+    free(e->message);
+    free(e);
+  }
+}
+void kv_free_buffer(char* p) { free(p); }
+
+}  // extern "C"

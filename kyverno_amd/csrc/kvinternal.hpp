@@ -1,0 +1,174 @@
+// Host-side internal structures of libkvgpu (compiled policy set, ingested batch).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "kv_layout.h"
+#include "kvjson.hpp"
+
+namespace kvh {
+
+// Mutable pattern tree (copy of an apiextensions.JSON value: numbers are float64)
+struct PV {
+  uint8_t t = J_NULL;
+  bool b = false;
+  double f = 0;
+  std::string s;
+  std::vector<std::string> mk;  // map keys
+  std::vector<std::string> mo;  // canonical order keys (== mk unless renamed)
+  std::vector<PV> mv;           // map values
+  std::vector<PV> a;            // array elements
+  int find(const std::string& k) const {
+    for (size_t i = 0; i < mk.size(); i++)
+      if (mk[i] == k) return (int)i;
+    return -1;
+  }
+};
+PV to_pv(const JDoc& d, uint32_t node);
+
+// Path template of a pattern node, for rendering failing paths on the host.
+enum SegKind : uint8_t { SEG_ROOT = 0, SEG_KEY = 1, SEG_LOOP = 2, SEG_CONST_INDEX = 3, SEG_RESOLVED = 4 };
+struct PNodeInfo {
+  uint32_t parent;   // 0xFFFFFFFF for root
+  uint8_t seg;       // SegKind
+  uint32_t level;    // SEG_LOOP: loop level; SEG_CONST_INDEX: index
+  std::string key;   // SEG_KEY text; SEG_RESOLVED: literal fallback (anchor-free pattern key)
+};
+
+// Projection trie over resource key paths referenced by any compiled pattern
+// or match block. Arrays are transparent: `elem` is the element trie.
+struct Trie {
+  struct N {
+    std::unordered_map<std::string, uint32_t> kids;
+    int32_t elem = -1;
+    bool keep_all = false;   // keep every child (labels/annotations with wildcard keys)
+    bool keep_subtree = false;
+  };
+  std::vector<N> nodes;
+  Trie() { nodes.emplace_back(); }
+  uint32_t child(uint32_t n, const std::string& k) {
+    auto it = nodes[n].kids.find(k);
+    if (it != nodes[n].kids.end()) return it->second;
+    uint32_t id = (uint32_t)nodes.size();
+    nodes.emplace_back();
+    nodes[n].kids[k] = id;
+    return id;
+  }
+  uint32_t elem(uint32_t n) {
+    if (nodes[n].elem >= 0) return (uint32_t)nodes[n].elem;
+    uint32_t id = (uint32_t)nodes.size();
+    nodes.emplace_back();
+    nodes[n].elem = (int32_t)id;
+    return id;
+  }
+};
+
+struct UserInfoSpec {
+  bool present = false;  // any of roles/clusterRoles/subjects non-nil
+  std::vector<std::string> roles, clusterRoles;
+  struct Subj { std::string kind, name, ns; };
+  std::vector<Subj> subjects;
+};
+
+struct SelectorHost {   // namespaceSelector, evaluated on the host per namespace (batch constant)
+  std::vector<std::pair<std::string, std::string>> matchLabels;
+  struct Expr { std::string key, op; std::vector<std::string> values; };
+  std::vector<Expr> exprs;
+};
+
+struct RuleHost {
+  uint32_t policy = 0;
+  std::string name;
+  std::string route_reason;  // "" for GPU
+  std::string message;
+  bool anypattern = false;
+  uint32_t root_pnode = 0;
+  std::vector<uint32_t> alt_roots;
+  std::vector<UserInfoSpec> filter_ui;  // per MFilter of this rule (match then exclude)
+  std::vector<bool> filter_is_match;
+  std::string const_message;            // route 3
+};
+
+struct PolicySet {
+  std::vector<std::string> policy_names;
+  std::vector<uint32_t> policy_rule_first, policy_rule_count;
+  // dictionary of keys (pattern keys, kinds, groups, versions)
+  std::vector<std::string> keys;
+  std::unordered_map<std::string, uint32_t> key_id;
+  uint32_t intern(const std::string& k) {
+    auto it = key_id.find(k);
+    if (it != key_id.end()) return it->second;
+    uint32_t id = (uint32_t)keys.size();
+    keys.push_back(k);
+    key_id.emplace(k, id);
+    return id;
+  }
+  uint32_t lookup(std::string_view k) const {
+    auto it = key_id.find(std::string(k));
+    return it == key_id.end() ? kv::KEY_NONE : it->second;
+  }
+  std::string strs;  // program string table
+  uint32_t add_str(const std::string& s) {
+    uint32_t off = (uint32_t)strs.size();
+    strs += s;
+    return off;
+  }
+  std::vector<kv::Inst> prog;
+  std::vector<kv::Pred> preds;
+  std::vector<kv::Alt> alts;
+  std::vector<kv::Conj> conjs;
+  std::vector<kv::Atom> atoms;
+  std::unordered_map<std::string, uint32_t> pred_cache;
+  std::vector<uint32_t> kg_specs;  // wildcard label-map sibling specs (OP_KEYGLOB)
+  std::vector<kv::RuleRec> rules;
+  std::vector<RuleHost> rhost;
+  std::vector<kv::MFilter> filters;
+  std::vector<kv::KindSpec> kinds;
+  std::vector<kv::StrRef> strrefs;
+  std::vector<kv::StrPair> strpairs;
+  std::vector<kv::Selector> selectors;
+  std::vector<kv::SelLabel> sellabels;
+  std::vector<kv::SelExpr> selexprs;
+  std::vector<SelectorHost> nsselectors;  // bit i of the namespace table
+  std::vector<PNodeInfo> pnodes;
+  Trie trie;
+  uint32_t max_depth = 0, max_loops = 0;
+  std::string flags_info;
+};
+
+// Compiles a JSON list of (already autogen-expanded) ClusterPolicy/Policy
+// objects. Throws std::runtime_error on malformed input.
+void compile_policies(const char* json, size_t len, PolicySet* ps);
+
+// Ingested batch (host mirror of the HBM store)
+struct Batch {
+  std::vector<kv::Node> nodes;
+  std::vector<kv::Val> vals;
+  std::vector<kv::Res> res;
+  std::vector<kv::KV> kvs;
+  std::string strs;                  // string heap
+  std::vector<std::string> dyn_keys; // key ids >= ps.keys.size()
+  std::vector<std::string> namespaces;
+  std::vector<std::vector<std::pair<std::string, std::string>>> ns_labels;
+  std::vector<uint32_t> ns_bits;     // [n_ns][ceil(n_nssel/32)]
+  uint32_t ns_words = 1;
+  uint64_t bytes_referenced = 0;     // algorithmic bytes of the projected store
+};
+
+void ingest_resources(const PolicySet& ps, const char* json, size_t len, const char* ns_labels_json, Batch* b);
+
+// Go-semantics helpers shared by compiler and ingest
+bool wildcard_match_host(std::string_view pattern, std::string_view name);
+bool valid_label_key(const std::string& k);
+bool valid_label_value(const std::string& v);
+std::string remove_anchor(const std::string& key, std::string* prefix);
+bool is_condition_anchor(const std::string& s);
+bool is_global_anchor(const std::string& s);
+bool is_negation_anchor(const std::string& s);
+bool is_equality_anchor(const std::string& s);
+bool is_existence_anchor(const std::string& s);
+int selector_eval_host(const SelectorHost& sel, std::vector<std::pair<std::string, std::string>> labels);
+
+}  // namespace kvh

@@ -1,0 +1,657 @@
+// HIP kernels of libkvgpu (gfx950 / CDNA4).
+//
+// kv_validate_kernel: one lane = one resource; every wave walks the rules of
+// the launch in order, so the rule's program, predicates and pattern strings
+// are wave-uniform (scalar loads), while resource nodes are per-lane gathers
+// from the projected HBM store. Per rule:
+//   1. match/exclude prefilter (MatchesResourceDescription, pkg/engine/utils.go:265-336)
+//   2. pattern VM: a uniform-pc SIMT interpreter over the structured program
+//      emitted by kvcompile.cpp (validate.go:29-194, anchor.go:21-277). Lanes
+//      that skip a subtree (absent anchored key) or raise an error park on a
+//      wake-up pc (the scope end / catch point) instead of branching, so the
+//      wave never diverges in program position; loops over resource arrays
+//      (containers[], volumes[] ...) run max(len) uniform iterations.
+//   3. MatchPattern epilogue (validate.go:29-50) -> status, error record.
+// Output: FULL mode = status[rule][res] (+ error records); COUNTS mode = per-rule
+// pass/fail/warn/error/skip/nomatch/cpu histogram (int64) accumulated in LDS and
+// flushed with one atomic per counter per workgroup.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kvdev.h"
+
+using namespace kv;
+
+#define KV_MAXD 16
+#define KV_MAXL 4
+#define KV_SENT 0xFFFFFFFFu
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ uint32_t rune_len(uint8_t c) {
+  return c < 0x80 ? 1u : c >= 0xF0 ? 4u : c >= 0xE0 ? 3u : c >= 0xC0 ? 2u : 1u;
+}
+
+// minio/pkg v1.1.3 wildcard.Match over valid UTF-8: '*' any run of runes,
+// '?' exactly one rune; star backtracking advances by whole runes.
+__device__ bool kv_glob(const uint8_t* p, uint32_t pl, const uint8_t* s, uint32_t sl) {
+  if (pl == 0) return sl == 0;
+  if (pl == 1 && p[0] == '*') return true;
+  uint32_t si = 0, pi = 0, star = KV_SENT, mark = 0;
+  while (si < sl) {
+    if (pi < pl) {
+      uint8_t pc = p[pi];
+      if (pc == '*') { star = pi++; mark = si; continue; }
+      if (pc == '?') { si += rune_len(s[si]); pi++; continue; }
+      uint32_t w = rune_len(pc);
+      bool eq = si + w <= sl && pi + w <= pl;
+      for (uint32_t k = 0; eq && k < w; k++) eq = p[pi + k] == s[si + k];
+      if (eq) { pi += w; si += w; continue; }
+    }
+    if (star != KV_SENT) {
+      pi = star + 1;
+      mark += rune_len(s[mark]);
+      si = mark;
+      continue;
+    }
+    return false;
+  }
+  while (pi < pl && p[pi] == '*') pi++;
+  return pi == pl && si == sl;
+}
+
+__device__ __forceinline__ bool bytes_eq(const uint8_t* a, uint32_t al, const uint8_t* b, uint32_t bl) {
+  if (al != bl) return false;
+  for (uint32_t k = 0; k < al; k++)
+    if (a[k] != b[k]) return false;
+  return true;
+}
+
+// magnitude/sign compare of canonical quantities: returns -1/0/1 (value vs pattern)
+__device__ __forceinline__ int q_cmp(uint32_t vf, int32_t ve, uint64_t vh, uint64_t vl, uint32_t pf, int32_t pe,
+                                     uint64_t ph, uint64_t pl) {
+  int sv = (vf & VF_Q_ZERO) ? 0 : ((vf & VF_Q_NEG) ? -1 : 1);
+  int sp = (pf & VF_Q_ZERO) ? 0 : ((pf & VF_Q_NEG) ? -1 : 1);
+  if (sv != sp) return sv < sp ? -1 : 1;
+  if (sv == 0) return 0;
+  int m;
+  if (ve != pe) m = ve < pe ? -1 : 1;
+  else if (vh != ph) m = vh < ph ? -1 : 1;
+  else if (vl != pl) m = vl < pl ? -1 : 1;
+  else m = 0;
+  return sv > 0 ? m : -m;
+}
+
+__device__ __forceinline__ bool cmp_ok(uint32_t op, int r) {
+  switch (op) {
+    case CO_EQ: return r == 0;
+    case CO_NE: return r != 0;
+    case CO_GT: return r == 1;
+    case CO_LT: return r == -1;
+    case CO_GE: return r >= 0;
+    default: return r <= 0;
+  }
+}
+
+// one atom of a string pattern against the value at `node` (ABSENT/NULL == Go nil)
+__device__ bool atom_eval(const DevPS& P, const DevBatch& B, uint32_t ai, uint32_t node) {
+  const Atom& A = P.atoms[ai];
+  uint32_t kind = uni(A.kind);
+  uint32_t type = node == ABSENT ? NT_NULL : B.nodes[node].type;
+  if (kind == AT_FALSE) return false;
+  if (type == NT_MAP || type == NT_ARR) return false;
+  if (kind == AT_GLOB_E) {
+    if (type == NT_NULL) return false;
+    const Val& v = B.vals[B.nodes[node].a];
+    bool r = kv_glob(P.pstr + A.s_off, A.s_len & 0x7FFFFFFFu, B.bstr + v.e_off, v.e_len);
+    return uni(A.op) == CO_NE ? !r : r;
+  }
+  if (type == NT_BOOL) return false;
+  if (kind == AT_GLOB_N) {
+    if (type == NT_NULL) {
+      const uint8_t zero = '0';
+      return kv_glob(P.pstr + A.s_off, A.s_len & 0x7FFFFFFFu, &zero, 1);
+    }
+    const Val& v = B.vals[B.nodes[node].a];
+    return kv_glob(P.pstr + A.s_off, A.s_len & 0x7FFFFFFFu, B.bstr + v.n_off, v.n_len);
+  }
+  // AT_QCMP
+  int r;
+  if (type == NT_NULL) {
+    r = q_cmp(VF_Q_ZERO, 0, 0, 0, A.q_flags, A.q_exp, A.q_hi, A.q_lo);
+  } else {
+    const Val& v = B.vals[B.nodes[node].a];
+    if (!(v.flags & VF_Q_VALID)) return false;
+    r = q_cmp(v.flags, v.q_exp, v.q_hi, v.q_lo, A.q_flags, A.q_exp, A.q_hi, A.q_lo);
+  }
+  return cmp_ok(uni(A.op), r);
+}
+
+// ValidateValueWithPattern(value, pattern) for a scalar-pattern leaf
+__device__ bool pred_eval(const DevPS& P, const DevBatch& B, uint32_t pi, uint32_t node) {
+  const Pred& pr = P.preds[pi];
+  uint32_t kind = uni(pr.kind);
+  uint32_t type = node == ABSENT ? NT_NULL : B.nodes[node].type;
+  switch (kind) {
+    case PK_BOOL: return type == NT_BOOL && B.nodes[node].b == uni(pr.flags);
+    case PK_FLOAT: {
+      if (type == NT_INT) return uni(pr.flags) && B.vals[B.nodes[node].a].i == pr.fi;
+      if (type == NT_FLOAT) return B.vals[B.nodes[node].a].f == pr.f;
+      if (type == NT_STR) {
+        const Val& v = B.vals[B.nodes[node].a];
+        return (v.flags & VF_PF_OK) && v.f == pr.f;
+      }
+      return false;
+    }
+    case PK_NIL:
+      if (type == NT_NULL) return true;
+      if (type == NT_MAP || type == NT_ARR) return false;
+      return (B.vals[B.nodes[node].a].flags & VF_NILLIKE) != 0;
+    case PK_MAPTYPE: return type == NT_MAP;
+    case PK_STRING: {
+      uint32_t af = uni(pr.first), an = uni(pr.count);
+      for (uint32_t a = af; a < af + an; a++) {
+        const Alt& al = P.alts[a];
+        uint32_t cf = uni(al.first), cn = uni(al.count);
+        bool all = true;
+        for (uint32_t c = cf; c < cf + cn && all; c++) {
+          const Conj& cj = P.conjs[c];
+          uint32_t ck = uni(cj.kind);
+          bool r = atom_eval(P, B, uni(cj.a0), node);
+          if (ck == CJ_INRANGE) r = r && atom_eval(P, B, uni(cj.a1), node);
+          else if (ck == CJ_NOTINRANGE) r = r || atom_eval(P, B, uni(cj.a1), node);
+          all = r;
+        }
+        if (all) return true;
+      }
+      return false;
+    }
+    default: return false;
+  }
+}
+
+__device__ __forceinline__ uint32_t lookup(const DevBatch& B, uint32_t m, uint32_t key) {
+  if (m == ABSENT) return ABSENT;
+  const Node n = B.nodes[m];
+  if (n.type != NT_MAP) return ABSENT;
+  for (uint32_t i = 0; i < n.b; i++)
+    if (B.nodes[n.a + i].key == key) return n.a + i;
+  return ABSENT;
+}
+
+// Resolved result key of sibling spec entry (OP_KEYGLOB): returns key id and node.
+__device__ __forceinline__ void kg_resolve(const DevPS& P, const DevBatch& B, uint32_t m, uint32_t w, uint32_t ref,
+                                           uint32_t* key, uint32_t* node) {
+  if (!w) {  // literal sibling: key id is the key
+    *key = ref;
+    *node = lookup(B, m, ref);
+    return;
+  }
+  const Atom& A = P.atoms[ref];
+  const Node mn = B.nodes[m];
+  for (uint32_t i = 0; i < mn.b; i++) {
+    uint32_t k = B.nodes[mn.a + i].key;
+    if (kv_glob(P.pstr + A.s_off, A.s_len & 0x7FFFFFFFu, B.kstr + B.key_off[k], B.key_len[k])) {
+      *key = k;
+      *node = mn.a + i;
+      return;
+    }
+  }
+  *key = KV_SENT;  // unresolved wildcard: unique literal result key
+  *node = ABSENT;
+}
+
+// ------------------------------------------------------------------ match/exclude
+__device__ bool selector_match(const DevPS& P, const DevBatch& B, const Res& R, uint32_t si) {
+  const Selector& S = P.sels[si];
+  uint32_t fl = uni(S.flags);
+  if (fl & SF_STATIC_INVALID) return false;
+  if (fl & SF_EVERYTHING) return true;
+  const KV* labels = B.kvs + R.labels_first;
+  uint32_t nl = R.labels_count;
+  uint32_t mf = uni(S.ml_first), mc = uni(S.ml_count);
+  // resolve every matchLabels entry: (key ptr/len, val ptr/len, valid)
+  for (uint32_t j = mf; j < mf + mc; j++) {
+    const SelLabel& L = P.sellabels[j];
+    const uint8_t *kp, *vp;
+    uint32_t kl, vl;
+    bool valid;
+    auto resolve = [&](const SelLabel& E, const uint8_t** ok, uint32_t* okl, const uint8_t** ov, uint32_t* ovl, bool* val) {
+      if (!(E.flags & SL_WILD)) {
+        *ok = P.pstr + E.k_off; *okl = E.k_len; *ov = P.pstr + E.v_off; *ovl = E.v_len;
+        *val = (E.flags & SL_VALID) != 0;
+        return;
+      }
+      for (uint32_t q = 0; q < nl; q++) {
+        const KV kv = labels[q];
+        const uint8_t* lk = B.bstr + kv.k_off;
+        const uint8_t* lv = B.bstr + kv.v_off;
+        uint32_t lkl = kv.k_len & KV_LEN_MASK, lvl = kv.v_len & KV_LEN_MASK;
+        if (kv_glob(P.pstr + E.k_off, E.k_len, lk, lkl) && kv_glob(P.pstr + E.v_off, E.v_len, lv, lvl)) {
+          *ok = lk; *okl = lkl; *ov = lv; *ovl = lvl;
+          *val = (kv.k_len & KV_VALID) && (kv.v_len & KV_VALID);
+          return;
+        }
+      }
+      *ok = P.pstr + E.rk_off; *okl = E.rk_len; *ov = P.pstr + E.rv_off; *ovl = E.rv_len;
+      *val = (E.flags & SL_VALID) != 0;
+    };
+    resolve(L, &kp, &kl, &vp, &vl, &valid);
+    // dropped if a later entry resolves to the same key (results[matchK] = matchV)
+    bool dropped = false;
+    for (uint32_t j2 = j + 1; j2 < mf + mc && !dropped; j2++) {
+      const uint8_t *k2, *v2;
+      uint32_t k2l, v2l;
+      bool val2;
+      resolve(P.sellabels[j2], &k2, &k2l, &v2, &v2l, &val2);
+      dropped = bytes_eq(kp, kl, k2, k2l);
+    }
+    if (dropped) continue;
+    if (!valid) return false;  // NewRequirement validation error
+    bool found = false;
+    for (uint32_t q = 0; q < nl && !found; q++) {
+      const KV kv = labels[q];
+      if (bytes_eq(B.bstr + kv.k_off, kv.k_len & KV_LEN_MASK, kp, kl))
+        found = bytes_eq(B.bstr + kv.v_off, kv.v_len & KV_LEN_MASK, vp, vl) ? true : (q = nl, false);
+    }
+    if (!found) return false;
+  }
+  uint32_t ef = uni(S.me_first), ec = uni(S.me_count);
+  for (uint32_t j = ef; j < ef + ec; j++) {
+    const SelExpr& E = P.selexprs[j];
+    bool has = false, in = false;
+    for (uint32_t q = 0; q < nl; q++) {
+      const KV kv = labels[q];
+      if (bytes_eq(B.bstr + kv.k_off, kv.k_len & KV_LEN_MASK, P.pstr + E.k_off, E.k_len)) {
+        has = true;
+        for (uint32_t v = E.v_first; v < E.v_first + E.v_count && !in; v++)
+          in = bytes_eq(B.bstr + kv.v_off, kv.v_len & KV_LEN_MASK, P.pstr + P.strrefs[v].off, P.strrefs[v].len);
+        break;
+      }
+    }
+    uint32_t op = uni(E.op);
+    if ((op == 0 && !in) || (op == 1 && in) || (op == 2 && !has) || (op == 3 && has)) return false;
+  }
+  return true;
+}
+
+// doesResourceMatchConditionBlock: number of failed criteria (0 == block matches)
+__device__ uint32_t block_errs(const DevPS& P, const DevBatch& B, const Res& R, uint32_t f) {
+  const MFilter& F = P.filters[f];
+  uint32_t fl = uni(P.fflags[f]);
+  uint32_t errs = 0;
+  if (fl & MF_KINDS) {
+    bool ok = false;
+    for (uint32_t k = uni(F.kinds_first); k < F.kinds_first + F.kinds_count && !ok; k++) {
+      const KindSpec ks = P.kinds[k];
+      switch (ks.form) {
+        case 3: ok = true; break;
+        case 0: ok = R.kind == ks.kind; break;
+        case 1: ok = R.kind == ks.kind && R.version == ks.version; break;
+        default: ok = R.group == ks.group && R.kind == ks.kind && (R.version == ks.version || R.version == P.star_id); break;
+      }
+    }
+    errs += ok ? 0 : 1;
+  }
+  if (fl & MF_NAME) errs += kv_glob(P.pstr + F.name_off, F.name_len, B.bstr + R.name_off, R.name_len) ? 0 : 1;
+  if (fl & MF_NAMES) {
+    bool any = false;
+    for (uint32_t k = F.names_first; k < F.names_first + F.names_count && !any; k++)
+      any = kv_glob(P.pstr + P.strrefs[k].off, P.strrefs[k].len, B.bstr + R.name_off, R.name_len);
+    errs += any ? 0 : 1;
+  }
+  if (fl & MF_NSS) {
+    bool any = false;
+    for (uint32_t k = F.nss_first; k < F.nss_first + F.nss_count && !any; k++)
+      any = kv_glob(P.pstr + P.strrefs[k].off, P.strrefs[k].len, B.bstr + R.ns_off, R.ns_len);
+    errs += any ? 0 : 1;
+  }
+  if (fl & MF_ANN) {
+    bool all = true;
+    for (uint32_t k = F.ann_first; k < F.ann_first + F.ann_count && all; k++) {
+      const StrPair sp = P.strpairs[k];
+      bool m = false;
+      for (uint32_t q = 0; q < R.annot_count && !m; q++) {
+        const KV kv = B.kvs[R.annot_first + q];
+        m = kv_glob(P.pstr + sp.k_off, sp.k_len, B.bstr + kv.k_off, kv.k_len & KV_LEN_MASK) &&
+            kv_glob(P.pstr + sp.v_off, sp.v_len, B.bstr + kv.v_off, kv.v_len & KV_LEN_MASK);
+      }
+      all = m;
+    }
+    errs += all ? 0 : 1;
+  }
+  if (fl & MF_SEL) errs += selector_match(P, B, R, F.sel) ? 0 : 1;
+  if ((fl & MF_NSSEL) && !(R.flags & (RF_KIND_NAMESPACE | RF_KIND_EMPTY))) {
+    uint32_t bit = F.nssel_bit;
+    errs += (B.ns_bits[R.ns_index * B.ns_words + bit / 32] >> (bit % 32)) & 1 ? 0 : 1;
+  }
+  if (fl & MF_UI_FAIL) errs += 1;
+  return errs;
+}
+
+__device__ bool rule_matches(const DevPS& P, const DevBatch& B, const Res& R, const RuleRec& rr) {
+  uint32_t mm = uni(rr.m_mode), mf = uni(rr.m_first), mc = uni(rr.m_count);
+  bool ok;
+  if (mm == 1) {
+    ok = false;
+    for (uint32_t f = mf; f < mf + mc && !ok; f++) ok = !(P.fflags[f] & MF_EMPTY) && block_errs(P, B, R, f) == 0;
+  } else if (mm == 2) {
+    ok = true;
+    for (uint32_t f = mf; f < mf + mc && ok; f++) ok = !(P.fflags[f] & MF_EMPTY) && block_errs(P, B, R, f) == 0;
+  } else {
+    ok = !(P.fflags[mf] & MF_EMPTY) && block_errs(P, B, R, mf) == 0;
+  }
+  if (!ok) return false;
+  uint32_t xm = uni(rr.x_mode), xf = uni(rr.x_first), xc = uni(rr.x_count);
+  if (xm == 1) {
+    for (uint32_t f = xf; f < xf + xc; f++)
+      if (!(P.fflags[f] & MF_EMPTY) && block_errs(P, B, R, f) == 0) return false;
+    return true;
+  }
+  if (xm == 2) {
+    for (uint32_t f = xf; f < xf + xc; f++)
+      if ((P.fflags[f] & MF_EMPTY) || block_errs(P, B, R, f) != 0) return true;
+    return false;
+  }
+  if (!(P.fflags[xf] & MF_EMPTY) && block_errs(P, B, R, xf) == 0) return false;
+  return true;
+}
+
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    uint32_t x = __shfl_xor(v, o, 64);
+    v = x < v ? x : v;
+  }
+  return v;
+}
+
+// ------------------------------------------------------------------ kernel
+extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(DevPS P, DevBatch B, DevOut O, uint32_t rule_begin,
+                                                                      uint32_t rule_end) {
+  __shared__ uint32_t s_cur[KV_MAXD][KV_WG];
+  __shared__ uint32_t s_lfirst[KV_MAXL][KV_WG];
+  __shared__ uint32_t s_llen[KV_MAXL][KV_WG];
+  __shared__ uint32_t s_li[KV_WG / 64][KV_MAXL];
+  __shared__ uint32_t s_hist[64][KV_HIST];
+
+  const uint32_t lane = threadIdx.x;
+  const uint32_t wv = lane >> 6;
+  const uint32_t r = blockIdx.x * KV_WG + lane;
+  const bool valid = r < B.n_res;
+  Res R;
+  if (valid) R = B.res[r];
+  else { R.root = ABSENT; R.flags = 0; R.labels_count = 0; R.annot_count = 0; R.kind = KEY_NONE; }
+
+  for (uint32_t rb = rule_begin; rb < rule_end; rb += 64) {
+    const uint32_t re = rb + 64 < rule_end ? rb + 64 : rule_end;
+    for (uint32_t q = lane; q < 64 * KV_HIST; q += KV_WG) (&s_hist[0][0])[q] = 0;
+    __syncthreads();
+    for (uint32_t ri = rb; ri < re; ri++) {
+      const RuleRec rr = P.rules[ri];
+      const uint32_t route = uni(rr.route);
+      uint32_t st = ST_NOMATCH;
+      bool run = false;
+      if (valid && rule_matches(P, B, R, rr)) {
+        if (route == 1) st = ST_CPU;
+        else if (route == 2) st = ST_NOMATCH;
+        else if (route == 3) st = (uint8_t)rr.const_status;
+        else if (R.flags & RF_MAGIC) st = ST_CPU;
+        else if ((uni(rr.flags) & RR_META_EXPAND) && (R.flags & RF_BAD_META)) st = ST_CPU;
+        else run = true;
+      }
+      uint32_t ekind = 0, eflags = 0, epn = 0, ekey = ABSENT, eres = ABSENT;
+      uint32_t eidx0 = 0, eidx1 = 0, eidx2 = 0, eidx3 = 0;
+      if (__ballot(run)) {
+        uint64_t areg = 0, apres = 0;
+        uint32_t keynode = ABSENT;
+        uint32_t wait = run ? 0u : KV_SENT;
+        uint32_t pc = uni(rr.prog);
+        s_cur[0][lane] = R.root;
+        auto raise = [&](uint32_t kind, uint32_t pn, uint32_t rn, uint32_t cpc) {
+          ekind = kind;
+          eflags = 0;
+          epn = pn;
+          eres = rn;
+          ekey = keynode;
+          eidx0 = s_li[wv][0];
+          eidx1 = s_li[wv][1];
+          eidx2 = s_li[wv][2];
+          eidx3 = s_li[wv][3];
+          wait = cpc;
+        };
+        while (true) {
+          if (wait == pc) wait = 0;
+          if (!__ballot(wait == 0)) {
+            uint32_t m = uni(wave_min(wait));
+            if (m == KV_SENT) break;
+            pc = m;
+            continue;
+          }
+          const Inst in = P.prog[pc];
+          const uint32_t op = uni(in.op) & 0xFF;
+          const uint32_t d = (uni(in.op) >> 8) & 0xFF;
+          const uint32_t aux = (uni(in.op) >> 16) & 0xFF;
+          const uint32_t ia = uni(in.a), ib = uni(in.b), ic = uni(in.c);
+          const bool A = wait == 0;
+          uint32_t next = pc + 1;
+          switch (op) {
+            case OP_MAPCHK:
+            case OP_ARRCHK:
+              if (A) {
+                uint32_t v = s_cur[d][lane];
+                uint32_t want = op == OP_MAPCHK ? NT_MAP : NT_ARR;
+                if (v == ABSENT || B.nodes[v].type != want) raise(op == OP_MAPCHK ? E_TYPE_MAP : E_TYPE_ARR, ia, v, ic);
+              }
+              break;
+            case OP_AREG:
+              if (A) {
+                areg |= 1ull << aux;
+                if (lookup(B, s_cur[d][lane], ia) != ABSENT) apres |= 1ull << aux;
+              }
+              break;
+            case OP_KEY:
+            case OP_KEYV:
+              if (A) {
+                uint32_t c = lookup(B, s_cur[d][lane], ia);
+                s_cur[d + 1][lane] = c;
+                if (op == OP_KEY && c == ABSENT) wait = ib;
+              }
+              break;
+            case OP_KEYGLOB:
+              if (A) {
+                const uint32_t j = uni(in.op) >> 24;
+                const Atom& at = P.atoms[ia];
+                const uint32_t spec = (uint32_t)at.q_hi;
+                const uint32_t mycls = (uint32_t)at.q_lo;
+                const uint32_t n = P.kg_specs[spec];
+                const uint32_t m = s_cur[d][lane];
+                uint32_t mykey, mynode;
+                const uint32_t myw = P.kg_specs[spec + 1 + 2 * j] & 1;
+                kg_resolve(P, B, m, myw, myw ? ia : ic, &mykey, &mynode);
+                bool dropped = false;
+                for (uint32_t j2 = j + 1; j2 < n && !dropped; j2++) {
+                  uint32_t cw = P.kg_specs[spec + 1 + 2 * j2];
+                  if ((cw >> 1) != mycls || mykey == KV_SENT) continue;
+                  uint32_t k2, n2;
+                  kg_resolve(P, B, m, cw & 1, P.kg_specs[spec + 2 + 2 * j2], &k2, &n2);
+                  dropped = k2 == mykey;
+                }
+                if (dropped) {
+                  wait = ib;
+                } else {
+                  uint32_t node = (myw && mykey != KV_SENT) ? mynode : lookup(B, m, ic);
+                  keynode = (myw && mykey != KV_SENT) ? mynode : ABSENT;
+                  s_cur[d + 1][lane] = node;
+                  if (node == ABSENT && (aux & 1)) wait = ib;
+                }
+              }
+              break;
+            case OP_SCOPE_END:
+            case OP_POS_END:
+              if (A && ekind) {
+                if (op == OP_POS_END) {
+                  if (eflags & EF_COND) ekind = 0;
+                  else wait = ic;
+                } else {
+                  eflags |= aux;
+                  wait = ic;
+                }
+              }
+              break;
+            case OP_NEG:
+              if (A && lookup(B, s_cur[d][lane], ia) != ABSENT) raise(E_NEG, ib, ABSENT, ic);
+              break;
+            case OP_STAR:
+              if (A) {
+                uint32_t v = s_cur[d + 1][lane];
+                if (v == ABSENT || B.nodes[v].type == NT_NULL) raise(E_STAR, ib, ABSENT, ic);
+              }
+              break;
+            case OP_LEAF:
+              if (A) {
+                uint32_t v = s_cur[d][lane];
+                bool ok;
+                if (v != ABSENT && B.nodes[v].type == NT_ARR) {
+                  const Node an = B.nodes[v];
+                  ok = true;
+                  for (uint32_t k = 0; k < an.b && ok; k++) ok = pred_eval(P, B, ia, an.a + k);
+                } else {
+                  ok = pred_eval(P, B, ia, v);
+                }
+                if (!ok) raise(E_VALUE, ib, v, ic);
+              }
+              break;
+            case OP_RAISE:
+              if (A) raise(ib, ia, s_cur[d][lane], ic);
+              break;
+            case OP_EXISTCHK:
+              if (A) {
+                uint32_t v = s_cur[d][lane];
+                if (v == ABSENT || B.nodes[v].type != NT_ARR) raise(E_EXIST_RESTYPE, ia, v, ic);
+              }
+              break;
+            case OP_LENCHK:
+              if (A && B.nodes[s_cur[d][lane]].b < ia) raise(E_LEN, ib, s_cur[d][lane], ic);
+              break;
+            case OP_INDEX:
+              if (A) s_cur[d + 1][lane] = B.nodes[s_cur[d][lane]].a + ia;
+              break;
+            case OP_LOOP_BEGIN:
+            case OP_EXIST_BEGIN: {
+              if (A) {
+                const Node an = B.nodes[s_cur[d][lane]];
+                s_lfirst[aux][lane] = an.a;
+                s_llen[aux][lane] = an.b;
+                if (an.b == 0) {
+                  if (op == OP_LOOP_BEGIN) wait = ia + 1;
+                  else raise(E_EXIST_FAIL, ib, s_cur[d][lane], ic);
+                } else {
+                  s_cur[d + 1][lane] = an.a;
+                }
+              }
+              if (lane % 64 == 0) s_li[wv][aux] = 0;
+              break;
+            }
+            case OP_LOOP_END:
+            case OP_EXIST_END: {
+              bool cont = false;
+              if (A) {
+                if (op == OP_LOOP_END) {
+                  if (ekind) {
+                    if (eflags & EF_COND) { ekind = 0; cont = true; }
+                    else wait = ic;
+                  } else {
+                    cont = true;
+                  }
+                } else {
+                  if (ekind) { ekind = 0; cont = true; }  // element failed: try the next one
+                  else wait = pc + 1;                       // found
+                }
+                if (cont) {
+                  uint32_t i = s_li[wv][aux] + 1;
+                  if (i < s_llen[aux][lane]) {
+                    s_cur[d + 1][lane] = s_lfirst[aux][lane] + i;
+                  } else {
+                    cont = false;
+                    if (op == OP_LOOP_END) wait = pc + 1;
+                    else raise(E_EXIST_FAIL, ib, s_cur[d][lane], ic);
+                  }
+                }
+              }
+              if (__ballot(cont)) {
+                if (lane % 64 == 0) s_li[wv][aux] += 1;
+                next = ia + 1;
+              }
+              break;
+            }
+            case OP_ALT_BEGIN:
+              if (A) { ekind = 0; eflags = 0; areg = 0; apres = 0; }
+              break;
+            case OP_ALT_END:
+              if (A) {
+                if (ekind == 0) { st = ST_PASS; wait = KV_SENT; }
+                else if (ekind == E_CPU) { st = ST_CPU; wait = KV_SENT; }
+                else if (ib) { st = ST_FAIL; wait = KV_SENT; }
+                else { ekind = 0; eflags = 0; areg = 0; apres = 0; }
+              }
+              break;
+            case OP_DONE:
+              if (A) {
+                if (ekind == 0) st = ST_PASS;
+                else if (ekind == E_CPU) st = ST_CPU;
+                else if (eflags & (EF_COND | EF_GLOBAL)) st = ST_SKIP;
+                else if (areg & ~apres) st = ST_ERROR;
+                else if (ekind == E_LEN) st = ST_ERROR;
+                else st = ST_FAIL;
+                wait = KV_SENT;
+              }
+              next = KV_SENT;
+              break;
+            default:
+              break;
+          }
+          if (next == KV_SENT) break;
+          pc = next;
+        }
+      }
+      if (valid) {
+        if (O.full) {
+          size_t o = (size_t)ri * B.n_res + r;
+          O.status[o] = (uint8_t)st;
+          if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP)) {
+            ErrRec e;
+            e.kind_flags = ekind | (eflags << 16);
+            e.pnode = epn;
+            e.keynode = ekey;
+            e.resnode = eres;
+            e.idx[0] = eidx0; e.idx[1] = eidx1; e.idx[2] = eidx2; e.idx[3] = eidx3;
+            O.err[o] = e;
+          }
+        }
+      }
+      // histogram: one LDS atomic per (wave, status) via ballot popcount
+      for (uint32_t s = 0; s < 7; s++) {
+        uint64_t bm = __ballot(valid && st == s);
+        if (bm && (lane % 64) == 0) atomicAdd(&s_hist[ri - rb][s], (uint32_t)__popcll(bm));
+      }
+    }
+    __syncthreads();
+    for (uint32_t q = lane; q < (re - rb) * KV_HIST; q += KV_WG) {
+      uint32_t v = (&s_hist[0][0])[q];
+      if (v) atomicAdd(&O.counts[(size_t)rb * KV_HIST + q], (unsigned long long)v);
+    }
+    __syncthreads();
+  }
+}
+
+namespace kv {
+hipError_t launch_validate(const DevPS& P, const DevBatch& B, const DevOut& O, uint32_t rule_begin, uint32_t rule_end,
+                           hipStream_t stream) {
+  if (B.n_res == 0 || rule_end <= rule_begin) return hipSuccess;
+  dim3 grid((B.n_res + KV_WG - 1) / KV_WG);
+  hipLaunchKernelGGL(kv_validate_kernel, grid, dim3(KV_WG), 0, stream, P, B, O, rule_begin, rule_end);
+  return hipGetLastError();
+}
+}  // namespace kv

@@ -1,0 +1,191 @@
+// Deterministic synthetic Kubernetes resources for the benchmark configs
+// (SURVEY.md §8d distributions). Output is NDJSON that goes through the normal
+// kv_ingest path, exactly like resources loaded from files.
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "../../include/kvgpu.h"
+
+namespace {
+
+struct Rng {
+  uint64_t s;
+  uint64_t next() {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  }
+  double u() { return (next() >> 11) * (1.0 / 9007199254740992.0); }
+  uint32_t n(uint32_t k) { return (uint32_t)(next() % k); }
+};
+
+const char* kRegistries[] = {"docker.io/", "gcr.io/", "quay.io/", "registry.local:5000/", ""};
+const char* kPull[] = {"Always", "IfNotPresent", "Never"};
+const char* kCpu[] = {"100m", "250m", "500m", "1", "2"};
+const char* kCpu2[] = {"200m", "500m", "1", "2", "4"};
+const char* kMem[] = {"64Mi", "128Mi", "256Mi", "512Mi", "1Gi", "2Gi"};
+const char* kMem2[] = {"128Mi", "256Mi", "512Mi", "1Gi", "2Gi", "4Gi"};
+const char* kApps[] = {"web", "api", "db", "cache", "worker", "frontend", "backend", "batch"};
+const char* kOwners[] = {"team-a", "team-b", "team-c", "platform"};
+const char* kTiers[] = {"frontend", "backend", "data"};
+const char* kSeccomp[] = {"RuntimeDefault", "Localhost", "Unconfined"};
+const char* kCaps[] = {"NET_ADMIN", "SYS_TIME", "CHOWN", "NET_BIND_SERVICE"};
+
+void repo_name(std::string& o, uint32_t k) {
+  static const char* a[] = {"nginx", "redis", "postgres", "busybox", "alpine", "envoy", "app", "svc",
+                            "mysql", "mongo", "kafka", "zookeeper", "etcd", "coredns", "proxy", "agent"};
+  o += a[k % 16];
+  o += "-";
+  o += std::to_string(k / 16);
+}
+
+void image(std::string& o, Rng& r) {
+  o += kRegistries[r.n(5)];
+  repo_name(o, r.n(256));
+  double t = r.u();
+  if (t < 0.15) {
+    o += ":latest";
+  } else if (t < 0.75) {
+    o += ":v" + std::to_string(r.n(4)) + "." + std::to_string(r.n(20)) + "." + std::to_string(r.n(10));
+  } else if (t < 0.85) {
+    o += "@sha256:";
+    static const char* hx = "0123456789abcdef";
+    for (int i = 0; i < 64; i++) o.push_back(hx[r.n(16)]);
+  }
+}
+
+void container(std::string& o, Rng& r, int idx, bool init) {
+  o += "{\"name\":\"";
+  o += init ? "init" : "c";
+  o += std::to_string(idx) + "\",\"image\":\"";
+  image(o, r);
+  o += "\"";
+  uint32_t pp = r.n(4);
+  if (pp < 3) { o += ",\"imagePullPolicy\":\""; o += kPull[pp]; o += "\""; }
+  if (r.u() < 0.7) {
+    uint32_t c = r.n(5), m = r.n(6);
+    double form = r.u();
+    std::string cpu = std::string("\"") + kCpu[c] + "\"";
+    if (form < 0.05) cpu = "1";
+    else if (form < 0.08) cpu = "0.5";
+    o += ",\"resources\":{\"requests\":{\"cpu\":" + cpu + ",\"memory\":\"" + kMem[m] + "\"},\"limits\":{\"cpu\":\"" +
+         kCpu2[c] + "\",\"memory\":\"" + kMem2[m] + "\"}}";
+  }
+  if (r.u() < 0.8) {
+    o += ",\"securityContext\":{";
+    bool first = true;
+    auto field = [&](const std::string& f) {
+      if (!first) o += ",";
+      first = false;
+      o += f;
+    };
+    if (r.u() < 0.6) field(std::string("\"privileged\":") + (r.u() < 0.1 ? "true" : "false"));
+    if (r.u() < 0.6) field(std::string("\"runAsNonRoot\":") + (r.u() < 0.8 ? "true" : "false"));
+    if (r.u() < 0.4) field("\"runAsGroup\":" + std::to_string(r.n(3) * 1000));
+    if (r.u() < 0.6) field(std::string("\"allowPrivilegeEscalation\":") + (r.u() < 0.2 ? "true" : "false"));
+    if (r.u() < 0.1) field(std::string("\"capabilities\":{\"add\":[\"") + kCaps[r.n(4)] + "\"]}");
+    if (r.u() < 0.5) field(std::string("\"seccompProfile\":{\"type\":\"") + kSeccomp[r.n(3)] + "\"}");
+    if (r.u() < 0.05) field(std::string("\"procMount\":\"") + (r.u() < 0.5 ? "Default" : "Unmasked") + "\"");
+    if (r.u() < 0.03) field("\"seLinuxOptions\":{\"type\":\"spc_t\"}");
+    o += "}";
+  }
+  if (r.u() < 0.6) {
+    o += ",\"ports\":[{\"containerPort\":" + std::to_string(8000 + r.n(100));
+    if (r.u() < 0.05) o += ",\"hostPort\":" + std::to_string(30000 + r.n(1000));
+    o += "}]";
+  }
+  o += "}";
+}
+
+void pod_spec(std::string& o, Rng& r) {
+  o += "{";
+  double ic = r.u();
+  if (ic >= 0.8) {
+    o += "\"initContainers\":[";
+    container(o, r, 0, true);
+    o += "],";
+  }
+  double cc = r.u();
+  int n = cc < 0.5 ? 1 : cc < 0.8 ? 2 : cc < 0.95 ? 3 : 4;
+  o += "\"containers\":[";
+  for (int i = 0; i < n; i++) {
+    if (i) o += ",";
+    container(o, r, i, false);
+  }
+  o += "]";
+  if (r.u() < 0.05) o += ",\"hostNetwork\":true";
+  if (r.u() < 0.05) o += ",\"hostPID\":true";
+  if (r.u() < 0.05) {
+    o += ",\"securityContext\":{\"sysctls\":[{\"name\":\"";
+    o += r.u() < 0.5 ? "kernel.shm_rmid_forced" : "net.core.somaxconn";
+    o += "\",\"value\":\"1\"}]}";
+  }
+  double v = r.u();
+  if (v < 0.05) o += ",\"volumes\":[{\"name\":\"host\",\"hostPath\":{\"path\":\"/var/run\"}}]";
+  else if (v < 0.4) o += ",\"volumes\":[{\"name\":\"data\",\"emptyDir\":{}}]";
+  o += "}";
+}
+
+void labels(std::string& o, Rng& r) {
+  o += "\"labels\":{";
+  bool first = true;
+  auto kv = [&](const char* k, const char* v) {
+    if (!first) o += ",";
+    first = false;
+    o += std::string("\"") + k + "\":\"" + v + "\"";
+  };
+  if (r.u() < 0.9) kv("app", kApps[r.n(8)]);
+  if (r.u() < 0.6) kv("owner", kOwners[r.n(4)]);
+  if (r.u() < 0.5) kv("tier", kTiers[r.n(3)]);
+  o += "}";
+}
+
+void metadata(std::string& o, Rng& r, const char* prefix, uint64_t i) {
+  o += "\"metadata\":{\"name\":\"";
+  o += prefix;
+  o += std::to_string(i) + "\",\"namespace\":\"ns-" + std::to_string(r.n(64)) + "\",";
+  labels(o, r);
+  if (r.u() < 0.05) o += ",\"annotations\":{\"container.apparmor.security.beta.kubernetes.io/c0\":\"runtime/default\"}";
+  o += "}";
+}
+
+}  // namespace
+
+extern "C" int kv_synth(uint64_t seed, uint64_t n, uint32_t kind_mix, char** json_out, size_t* len) {
+  if (!json_out || !len) return KV_E_INVALID;
+  std::string o;
+  o.reserve(n * 900);
+  Rng r{seed};
+  for (uint64_t i = 0; i < n; i++) {
+    double k = kind_mix == 1 ? r.u() : 0.0;
+    if (k < 0.60) {
+      o += "{\"apiVersion\":\"v1\",\"kind\":\"Pod\",";
+      metadata(o, r, "pod-", i);
+      o += ",\"spec\":";
+      pod_spec(o, r);
+      o += "}\n";
+    } else if (k < 0.85) {
+      o += "{\"apiVersion\":\"apps/v1\",\"kind\":\"Deployment\",";
+      metadata(o, r, "deploy-", i);
+      o += ",\"spec\":{\"replicas\":" + std::to_string(1 + r.n(5)) + ",\"template\":{\"metadata\":{";
+      labels(o, r);
+      o += "},\"spec\":";
+      pod_spec(o, r);
+      o += "}}}\n";
+    } else {
+      static const char* st[] = {"ClusterIP", "NodePort", "LoadBalancer"};
+      o += "{\"apiVersion\":\"v1\",\"kind\":\"Service\",";
+      metadata(o, r, "svc-", i);
+      o += std::string(",\"spec\":{\"type\":\"") + st[r.n(3)] + "\",\"ports\":[{\"port\":" + std::to_string(80 + r.n(1000)) + "}]}}\n";
+    }
+  }
+  *json_out = (char*)malloc(o.size() + 1);
+  if (!*json_out) return KV_E_NOMEM;
+  memcpy(*json_out, o.data(), o.size());
+  (*json_out)[o.size()] = 0;
+  *len = o.size();
+  return 0;
+}

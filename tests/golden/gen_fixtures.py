@@ -412,6 +412,33 @@ def gen_matcher():
     return cases
 
 
+def gen_corpus():
+    """Reference policy/resource YAML corpus (SURVEY.md Appendix B 'corpus'),
+    converted to JSON with the reference's YAML conventions (kyverno_amd.yamlio)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    from kyverno_amd import yamlio
+
+    pols, ress = [], []
+    for d in ("test/best_practices", "test/more", "test/policy/validate"):
+        for fn in sorted(os.listdir(os.path.join(REF, d))):
+            if not fn.endswith((".yaml", ".yml")):
+                continue
+            try:
+                for p in yamlio.load_policies_file(os.path.join(REF, d, fn)):
+                    pols.append({"src": f"{d}/{fn}", "policy": yamlio.to_go_json_obj(p)})
+            except Exception as e:  # malformed fixture files are skipped, as the CLI would reject them
+                print(f"skip {d}/{fn}: {e}", file=sys.stderr)
+    for fn in sorted(os.listdir(os.path.join(REF, "test/resources"))):
+        if not fn.endswith((".yaml", ".yml")):
+            continue
+        try:
+            for r in yamlio.load_resources_file(os.path.join(REF, "test/resources", fn)):
+                ress.append({"src": f"test/resources/{fn}", "resource": yamlio.to_go_json_obj(r)})
+        except Exception as e:
+            print(f"skip test/resources/{fn}: {e}", file=sys.stderr)
+    return [{"policies": pols, "resources": ress}]
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     outs = {
@@ -419,6 +446,7 @@ def main():
         "syntax.json": gen_syntax(),
         "expand.json": gen_expand(),
         "matcher.json": gen_matcher(),
+        "corpus.json": gen_corpus(),
     }
     for fn, cases in outs.items():
         with open(os.path.join(OUT, fn), "w") as f:

@@ -1,0 +1,104 @@
+"""CPU-only checks of the C ABI library: it loads, exports every symbol
+declared in include/kvgpu.h, and its host stages (compile, ingest, synth)
+behave. No kernel is launched here."""
+import ctypes
+import json
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    with open(os.path.join(ROOT, "include", "kvgpu.h")) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|double)\s+(kv_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_header_symbols():
+    from kyverno_amd import _native
+
+    L = _native.lib()
+    syms = _header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(L, s), s
+    assert sorted(_native.EXPORTED_SYMBOLS) == syms
+
+
+def test_compile_routes():
+    from kyverno_amd import batch
+
+    pol = {"metadata": {"name": "p"}, "spec": {"rules": [
+        {"name": "gpu", "match": {"resources": {"kinds": ["Pod"]}}, "validate": {"pattern": {"a": "b"}}},
+        {"name": "vars", "match": {"resources": {"kinds": ["Pod"]}},
+         "validate": {"pattern": {"a": "{{request.object.metadata.name}}"}}},
+        {"name": "deny", "match": {"resources": {"kinds": ["Pod"]}}, "validate": {"deny": {}}},
+        {"name": "ctx", "context": [{"name": "x"}], "match": {"resources": {"kinds": ["Pod"]}},
+         "validate": {"pattern": {"a": "b"}}},
+        {"name": "mutate", "match": {"resources": {"kinds": ["Pod"]}}, "mutate": {"overlay": {}}},
+        {"name": "badref", "match": {"resources": {"kinds": ["Pod"]}}, "validate": {"pattern": {"a": "$(./b)"}}},
+        {"name": "anyempty", "match": {"resources": {"kinds": ["Pod"]}}, "validate": {"anyPattern": []}},
+    ]}}
+    ps = batch.PolicySet([pol])
+    routes = {r.name: (r.route, r.route_reason) for r in ps.rules}
+    assert routes["gpu"][0] == batch.ROUTE_GPU
+    assert routes["vars"] == (batch.ROUTE_CPU, "variables")
+    assert routes["deny"] == (batch.ROUTE_CPU, "deny")
+    assert routes["ctx"] == (batch.ROUTE_CPU, "context")
+    assert routes["mutate"][0] == batch.ROUTE_NORESPONSE
+    assert routes["badref"][0] == batch.ROUTE_CONSTANT
+    badref = [r for r in ps.rules if r.name == "badref"][0]
+    assert badref.const_status == batch.ERROR and badref.const_message.startswith("variable substitution failed")
+    anyempty = [r for r in ps.rules if r.name == "anyempty"][0]
+    assert anyempty.const_status == batch.PASS
+
+
+def test_substitution_matches_oracle(orc):
+    """$() references are resolved once at compile time; the oracle resolves per
+    pair. Compare the error text of unresolvable references."""
+    from kyverno_amd import batch
+
+    pat = {"spec": {"containers": [{"resources": {"requests": {"memory": "$(<=./../../lim(its/mem)ory)"},
+                                                  "lim(its": {"mem)ory": "2048Mi"}}}]}}
+    pol = {"metadata": {"name": "p"}, "spec": {"rules": [{"name": "r", "match": {"resources": {"kinds": ["Pod"]}},
+                                                          "validate": {"pattern": pat}}]}}
+    ps = batch.PolicySet([pol])
+    assert ps.rules[0].route == batch.ROUTE_GPU
+    bad = {"spec": {"a": "$(./missing)"}}
+    pol2 = {"metadata": {"name": "p"}, "spec": {"rules": [{"name": "r", "match": {"resources": {"kinds": ["Pod"]}},
+                                                           "validate": {"pattern": bad}}]}}
+    ps2 = batch.PolicySet([pol2])
+    o = orc.validate(pol2, {"kind": "Pod", "metadata": {"name": "x"}})
+    assert o["rules"][0]["status"] == "error"
+    assert o["rules"][0]["message"] == ps2.rules[0].const_message
+
+
+def test_ingest_and_synth():
+    from kyverno_amd import batch, workloads
+
+    ps = batch.PolicySet(workloads.c2_policies())
+    assert ps.n_rules == 100 and all(r.route == batch.ROUTE_GPU for r in ps.rules)
+    data = batch.synth(workloads.SEED, 500)
+    assert data.count(b"\n") == 500
+    b = batch.Batch(ps, data)
+    assert b.n_res == 500 and b.store_bytes > 0
+    # same seed -> same bytes
+    assert batch.synth(workloads.SEED, 500) == data
+    # JSON array input is accepted as well as NDJSON
+    arr = "[" + ",".join(data.decode().strip().split("\n")) + "]"
+    b2 = batch.Batch(ps, arr)
+    assert b2.n_res == 500
+
+
+def test_ingest_rejects_malformed():
+    from kyverno_amd import batch
+    from kyverno_amd._native import KvError
+
+    ps = batch.PolicySet([{"metadata": {"name": "p"}, "spec": {"rules": []}}])
+    with pytest.raises(KvError):
+        batch.Batch(ps, b'{"kind": "Pod", ')
+    with pytest.raises(KvError):
+        batch.PolicySet(b"[{]")
