@@ -421,7 +421,14 @@ extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(DevPS P, 
           eidx3 = s_li[wv][3];
           wait = cpc;
         };
+        uint32_t guard = 0;
         while (true) {
+          // every program terminates (forward pcs, loops bounded by array lengths);
+          // the guard only turns an interpreter bug into a CPU-routed verdict instead of a hung wave
+          if (++guard > (1u << 24)) {
+            if (wait != KV_SENT) st = ST_CPU;
+            break;
+          }
           if (wait == pc) wait = 0;
           if (!__ballot(wait == 0)) {
             uint32_t m = uni(wave_min(wait));

@@ -60,10 +60,9 @@ def compare(orc, policies, resources, ctx=None, check_paths=True, max_path_check
             sel = np.random.default_rng(0).choice(len(fails), max_path_checks, replace=False)
             fails = fails[sel]
         for rule, res in fails:
-            pi, _ = ridx[rule]
+            pi, ri = ridx[rule]
             ov = orc.validate(policies[pi], resources[res], ctx)
-            orule = [x for x in ov["rules"] if x["name"] == ps.rules[rule].name]
-            opath = orule[0]["path"] if orule else None
+            opath = ov["rules"][ri]["path"]  # by position: rule names may repeat within a policy
             gpath = r.path(int(rule), int(res))
             if not ps.rules[rule].any_pattern and gpath != opath:
                 mism.append(f"path rule {rule} ({ps.rules[rule].name}) res {res}: gpu {gpath!r} oracle {opath!r}")
