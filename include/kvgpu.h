@@ -102,6 +102,17 @@ double kv_result_kernel_ms(const kv_result* r);
 int kv_bench(const kv_policyset* ps, const kv_batch* b, const char* ctx_json, int device, uint32_t mode, int warmup,
              int iters, double* ms_per_iter, kv_error** err);
 
+/* Session: device-resident inputs and output buffers allocated once
+ * (kv_session_create, untimed); kv_session_run enqueues `iters` passes on the
+ * session's stream and waits for them, returning the HIP-event time of the
+ * passes (ms, total). For benchmarks and repeated background scans. */
+typedef struct kv_session kv_session;
+int kv_session_create(const kv_policyset* ps, const kv_batch* b, const char* ctx_json, int device, uint32_t mode,
+                      kv_session** out, kv_error** err);
+int kv_session_run(kv_session* s, int iters, double* event_ms, kv_error** err);
+int kv_session_counts(kv_session* s, int64_t* counts /* [n_rules][8], last pass */);
+void kv_free_session(kv_session* s);
+
 /* Synthetic resource generator for the benchmark configs:
  * kind_mix 0 = Pods; 1 = Pods/Deployments/Services 60/25/15. Returns NDJSON
  * (free with kv_free_buffer). */

@@ -179,6 +179,42 @@ def bench(policyset: PolicySet, batch: Batch, device: int = 0, mode: int = MODE_
     return ms.value
 
 
+class Session:
+    """Device-resident launch configuration: inputs and output buffers allocated once."""
+
+    def __init__(self, policyset: PolicySet, batch: Batch, device: int = 0, mode: int = MODE_COUNTS,
+                 ctx: dict | None = None):
+        h = ctypes.c_void_p()
+        err = new_err()
+        check(lib().kv_session_create(policyset._h, batch._h, _dumps(ctx or {}), device, mode, ctypes.byref(h),
+                                      ctypes.byref(err)), err)
+        self._h = h
+        self.n_rules = policyset.n_rules
+
+    def run(self, iters: int) -> float:
+        """Enqueue `iters` passes and wait; returns total HIP-event milliseconds."""
+        ms = ctypes.c_double()
+        err = new_err()
+        check(lib().kv_session_run(self._h, iters, ctypes.byref(ms), ctypes.byref(err)), err)
+        return ms.value
+
+    def counts(self) -> np.ndarray:
+        out = np.zeros((self.n_rules, 8), dtype=np.int64)
+        rc = lib().kv_session_counts(self._h, out.ctypes.data)
+        if rc != 0:
+            raise _native.KvError(rc, "kv_session_counts failed")
+        return out
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().kv_free_session(h)
+            except Exception:
+                pass
+            self._h = None
+
+
 def synth(seed: int, n: int, kind_mix: int = 0) -> bytes:
     p = ctypes.c_void_p()
     ln = ctypes.c_size_t()

@@ -163,7 +163,23 @@ struct Atom {
   int32_t q_exp;
   uint32_t q_flags;       // VF_Q_NEG | VF_Q_ZERO
   uint64_t q_hi, q_lo;
+  // compiled glob (segments between '*'): see GlobFlags
+  uint32_t gflags, gfirst, gcount, gmin;
 };
+
+// Glob patterns are compiled into '*'-separated segments matched on 4-byte
+// words of 4-byte aligned value strings: anchored prefix, anchored suffix,
+// then middle segments leftmost-first. Exact for ASCII values, and for any
+// UTF-8 value when the pattern has no '?' (a '?' consumes one rune).
+enum GlobFlags : uint32_t {
+  G_ALL = 1,    // pattern "*" (or only stars): matches everything
+  G_LEAD = 2,   // pattern starts with '*'
+  G_TRAIL = 4,  // pattern ends with '*'
+  G_HASQ = 8,   // some segment contains '?'
+  G_EMPTY = 16, // empty pattern: matches only ""
+};
+struct GSeg { uint32_t wfirst, len; };   // words [wfirst, wfirst + (len+3)/4) in gwords[]
+struct GWord { uint32_t w, mask; };      // little-endian bytes, mask 0 on '?' and past the end
 
 // ---------------------------------------------------------------- match/exclude
 struct MFilter {          // one ResourceFilter / condition block

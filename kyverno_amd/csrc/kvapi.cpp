@@ -68,12 +68,13 @@ struct DevBuf {
 };
 
 struct DevPolicySet {
-  DevBuf prog, preds, alts, conjs, atoms, rules, filters, kinds, strrefs, strpairs, sels, sellabels, selexprs, kgs, pstr;
+  DevBuf prog, preds, alts, conjs, atoms, rules, filters, kinds, strrefs, strpairs, sels, sellabels, selexprs, kgs,
+      gsegs, gwords, pstr;
   DevPS view{};
 };
 
 struct DevBatchRes {
-  DevBuf nodes, vals, res, kvs, bstr, nsbits, koff, klen, kstr;
+  DevBuf nodes, vals, res, kvs, bstr, nsbits, koff, klen, kstr, view_dev;
   DevBatch view{};
 };
 
@@ -134,6 +135,8 @@ DevPolicySet& dev_ps(kv_policyset* s, int device) {
   d->sellabels.upload(ps.sellabels, device);
   d->selexprs.upload(ps.selexprs, device);
   d->kgs.upload(ps.kg_specs, device);
+  d->gsegs.upload(ps.gsegs, device);
+  d->gwords.upload(ps.gwords, device);
   d->pstr.upload_raw(ps.strs.data(), ps.strs.size(), device);
   DevPS& v = d->view;
   v.prog = (const Inst*)d->prog.p;
@@ -150,6 +153,9 @@ DevPolicySet& dev_ps(kv_policyset* s, int device) {
   v.sellabels = (const SelLabel*)d->sellabels.p;
   v.selexprs = (const SelExpr*)d->selexprs.p;
   v.kg_specs = (const uint32_t*)d->kgs.p;
+  v.gsegs = (const GSeg*)d->gsegs.p;
+  v.gwords = (const GWord*)d->gwords.p;
+  v.n_rules = (uint32_t)ps.rules.size();
   v.pstr = (const uint8_t*)d->pstr.p;
   v.star_id = ps.lookup("*");
   auto& ref = *d;
@@ -172,8 +178,15 @@ DevBatchRes& dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
   // key string table: static dictionary then batch-dynamic keys
   std::vector<uint32_t> off, len;
   std::string ks;
-  for (auto& k : ps.keys) { off.push_back((uint32_t)ks.size()); len.push_back((uint32_t)k.size()); ks += k; }
-  for (auto& k : b.dyn_keys) { off.push_back((uint32_t)ks.size()); len.push_back((uint32_t)k.size()); ks += k; }
+  auto addk = [&](const std::string& k) {  // 4-byte aligned (word-granular glob)
+    while (ks.size() & 3) ks.push_back('\0');
+    off.push_back((uint32_t)ks.size());
+    len.push_back((uint32_t)k.size());
+    ks += k;
+  };
+  for (auto& k : ps.keys) addk(k);
+  for (auto& k : b.dyn_keys) addk(k);
+  ks.append(16, '\0');
   d->koff.upload(off, device);
   d->klen.upload(len, device);
   d->kstr.upload_raw(ks.data(), ks.size(), device);
@@ -189,6 +202,7 @@ DevBatchRes& dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
   v.kstr = (const uint8_t*)d->kstr.p;
   v.ns_words = b.ns_words;
   v.n_res = (uint32_t)b.res.size();
+  d->view_dev.upload_raw(&d->view, sizeof(DevBatch), device);
   auto& ref = *d;
   bt->dev[device] = std::move(d);
   return ref;
@@ -310,61 +324,78 @@ std::string render_path(const PolicySet& ps, const Batch& b, const ErrRec& e) {
   return out;
 }
 
-void run(kv_policyset* ps, kv_batch* bt, const char* ctx_json, int device, uint32_t mode, kv_result* out, int warmup,
-         int iters, double* ms) {
-  HIPCHK(hipSetDevice(device));
-  DevPolicySet& dp = dev_ps(ps, device);
-  DevBatchRes& db = dev_batch(bt, ps->ps, device);
-  AdmissionCtx ai = parse_ctx(ctx_json);
-  std::vector<uint32_t> ff = fold_filters(ps->ps, ai);
-  DevBuf fflags;
-  fflags.upload(ff, device);
-  DevPS P = dp.view;
-  P.fflags = (const uint32_t*)fflags.p;
-  uint64_t nrules = ps->ps.rules.size(), nres = bt->b.res.size();
-  DevBuf st, er, cn;
+}  // namespace
+
+// A launch configuration with device-resident inputs and outputs.
+struct kv_session {
+  kv_policyset* ps = nullptr;
+  kv_batch* bt = nullptr;
+  int device = 0;
+  uint32_t mode = 0;
+  uint64_t nrules = 0, nres = 0;
+  DevBuf fflags, pview, st, er, cn;
   DevOut O{};
-  O.full = 0;
-  if (mode & KV_MODE_STATUS) {
-    st.alloc(nrules * nres, device);
-    O.status = (uint8_t*)st.p;
-    O.full |= 1;
-  }
-  if (mode & KV_MODE_ERRORS) {
-    er.alloc(nrules * nres * sizeof(ErrRec), device);
-    O.err = (ErrRec*)er.p;
-    O.full |= 2 | 1;
-    if (!O.status) {
+  const DevBatch* bview = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+
+  kv_session(kv_policyset* p, kv_batch* b, const char* ctx_json, int dev, uint32_t m)
+      : ps(p), bt(b), device(dev), mode(m) {
+    HIPCHK(hipSetDevice(device));
+    DevPolicySet& dp = dev_ps(ps, device);
+    DevBatchRes& db = dev_batch(bt, ps->ps, device);
+    bview = (const DevBatch*)db.view_dev.p;
+    AdmissionCtx ai = parse_ctx(ctx_json);
+    fflags.upload(fold_filters(ps->ps, ai), device);
+    DevPS P = dp.view;
+    P.fflags = (const uint32_t*)fflags.p;
+    pview.upload_raw(&P, sizeof(DevPS), device);  // read through a uniform pointer (scalar loads)
+    nrules = ps->ps.rules.size();
+    nres = bt->b.res.size();
+    O.full = 0;
+    if (mode & (KV_MODE_STATUS | KV_MODE_ERRORS)) {
       st.alloc(nrules * nres, device);
       O.status = (uint8_t*)st.p;
+      O.full |= 1;
     }
+    if (mode & KV_MODE_ERRORS) {
+      er.alloc(nrules * nres * sizeof(ErrRec), device);
+      O.err = (ErrRec*)er.p;
+      O.full |= 2;
+    }
+    cn.alloc(std::max<uint64_t>(nrules, 1) * KV_HIST * sizeof(unsigned long long), device);
+    O.counts = (unsigned long long*)cn.p;
+    HIPCHK(hipStreamCreate(&stream));
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
   }
-  cn.alloc(std::max<uint64_t>(nrules, 1) * KV_HIST * sizeof(unsigned long long), device);
-  O.counts = (unsigned long long*)cn.p;
-  hipStream_t stream;
-  HIPCHK(hipStreamCreate(&stream));
-  hipEvent_t e0, e1;
-  HIPCHK(hipEventCreate(&e0));
-  HIPCHK(hipEventCreate(&e1));
-  auto pass = [&]() {
-    HIPCHK(hipMemsetAsync(cn.p, 0, cn.n, stream));
-    HIPCHK(launch_validate(P, db.view, O, 0, (uint32_t)nrules, stream));
-  };
-  for (int i = 0; i < warmup; i++) pass();
-  HIPCHK(hipEventRecord(e0, stream));
-  for (int i = 0; i < std::max(iters, 1); i++) pass();
-  HIPCHK(hipEventRecord(e1, stream));
-  HIPCHK(hipEventSynchronize(e1));
-  float t = 0;
-  HIPCHK(hipEventElapsedTime(&t, e0, e1));
-  if (ms) *ms = t / std::max(iters, 1);
-  if (out) {
+  ~kv_session() {
+    (void)hipSetDevice(device);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+  // enqueue `iters` passes, wait, return HIP-event milliseconds of all passes
+  double run(int iters) {
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipEventRecord(e0, stream));
+    for (int i = 0; i < iters; i++) {
+      HIPCHK(hipMemsetAsync(cn.p, 0, cn.n, stream));
+      HIPCHK(launch_validate((const DevPS*)pview.p, bview, (uint32_t)nres, O, 0, (uint32_t)nrules, stream));
+    }
+    HIPCHK(hipEventRecord(e1, stream));
+    HIPCHK(hipEventSynchronize(e1));
+    float t = 0;
+    HIPCHK(hipEventElapsedTime(&t, e0, e1));
+    return t;
+  }
+  void fetch(kv_result* out, double ms) {
     out->ps = ps;
     out->b = bt;
     out->n_rules = nrules;
     out->n_res = nres;
     out->mode = mode;
-    out->kernel_ms = t / std::max(iters, 1);
+    out->kernel_ms = ms;
     std::vector<unsigned long long> c(nrules * KV_HIST);
     if (nrules) HIPCHK(hipMemcpy(c.data(), cn.p, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     out->counts.assign(c.begin(), c.end());
@@ -374,12 +405,22 @@ void run(kv_policyset* ps, kv_batch* bt, const char* ctx_json, int device, uint3
     }
     if (O.err) {
       out->err.resize(nrules * nres);
-      if (!out->err.empty()) HIPCHK(hipMemcpy(out->err.data(), er.p, out->err.size() * sizeof(ErrRec), hipMemcpyDeviceToHost));
+      if (!out->err.empty())
+        HIPCHK(hipMemcpy(out->err.data(), er.p, out->err.size() * sizeof(ErrRec), hipMemcpyDeviceToHost));
     }
   }
-  HIPCHK(hipEventDestroy(e0));
-  HIPCHK(hipEventDestroy(e1));
-  HIPCHK(hipStreamDestroy(stream));
+};
+
+namespace {
+
+void run(kv_policyset* ps, kv_batch* bt, const char* ctx_json, int device, uint32_t mode, kv_result* out, int warmup,
+         int iters, double* ms) {
+  kv_session s(ps, bt, ctx_json, device, mode);
+  if (warmup > 0) s.run(warmup);
+  int n = std::max(iters, 1);
+  double t = s.run(n) / n;
+  if (ms) *ms = t;
+  if (out) s.fetch(out, t);
 }
 
 }  // namespace
@@ -527,6 +568,45 @@ int kv_result_error(const kv_result* r, uint32_t rule, uint64_t res, uint32_t* k
 }
 
 double kv_result_kernel_ms(const kv_result* r) { return r ? r->kernel_ms : -1.0; }
+
+int kv_session_create(const kv_policyset* ps, const kv_batch* b, const char* ctx_json, int device, uint32_t mode,
+                      kv_session** out, kv_error** err) {
+  if (!ps || !b || !out) return fail(err, KV_E_INVALID, "null argument");
+  if (b->owner != ps) return fail(err, KV_E_INVALID, "batch was ingested for a different policy set");
+  try {
+    *out = new kv_session(const_cast<kv_policyset*>(ps), const_cast<kv_batch*>(b), ctx_json, device, mode);
+    return 0;
+  } catch (const HipError& e) {
+    return fail(err, KV_E_DEVICE, e.what());
+  } catch (const std::exception& e) {
+    return fail(err, KV_E_PARSE, e.what());
+  }
+}
+
+int kv_session_run(kv_session* s, int iters, double* event_ms, kv_error** err) {
+  if (!s || iters < 0) return fail(err, KV_E_INVALID, "bad argument");
+  try {
+    double t = s->run(iters);
+    if (event_ms) *event_ms = t;
+    return 0;
+  } catch (const HipError& e) {
+    return fail(err, KV_E_DEVICE, e.what());
+  }
+}
+
+int kv_session_counts(kv_session* s, int64_t* counts) {
+  if (!s || !counts) return KV_E_INVALID;
+  try {
+    std::vector<unsigned long long> c(s->nrules * KV_HIST);
+    if (s->nrules) HIPCHK(hipMemcpy(c.data(), s->cn.p, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < c.size(); i++) counts[i] = (int64_t)c[i];
+    return 0;
+  } catch (const HipError&) {
+    return KV_E_DEVICE;
+  }
+}
+
+void kv_free_session(kv_session* s) { delete s; }
 
 void kv_free_policyset(kv_policyset* ps) { delete ps; }
 void kv_free_batch(kv_batch* b) { delete b; }

@@ -51,6 +51,41 @@ std::string remove_anchor(const std::string& key, std::string* prefix) {
 
 static bool has_wild(const std::string& s) { return s.find_first_of("*?") != std::string::npos; }
 
+// ---------------------------------------------------------------- glob compilation
+void PolicySet::compile_glob(Atom& a, const std::string& p) {
+  a.gflags = 0;
+  a.gfirst = (uint32_t)gsegs.size();
+  a.gcount = 0;
+  a.gmin = 0;
+  if (p.empty()) { a.gflags = G_EMPTY; return; }
+  if (p.find_first_not_of('*') == std::string::npos) { a.gflags = G_ALL; return; }
+  if (p[0] == '*') a.gflags |= G_LEAD;
+  if (p.back() == '*') a.gflags |= G_TRAIL;
+  size_t i = 0;
+  while (i < p.size()) {
+    size_t j = p.find('*', i);
+    if (j == std::string::npos) j = p.size();
+    if (j > i) {
+      std::string seg = p.substr(i, j - i);
+      GSeg g{(uint32_t)gwords.size(), (uint32_t)seg.size()};
+      for (size_t w = 0; w < seg.size(); w += 4) {
+        GWord gw{0, 0};
+        for (size_t b = 0; b < 4 && w + b < seg.size(); b++) {
+          unsigned char c = (unsigned char)seg[w + b];
+          if (c == '?') { a.gflags |= G_HASQ; continue; }
+          gw.w |= (uint32_t)c << (8 * b);
+          gw.mask |= 0xFFu << (8 * b);
+        }
+        gwords.push_back(gw);
+      }
+      gsegs.push_back(g);
+      a.gcount++;
+      a.gmin += (uint32_t)seg.size();
+    }
+    i = j + 1;
+  }
+}
+
 // ---------------------------------------------------------------- glob (host)
 bool wildcard_match_host(std::string_view p, std::string_view s) {
   if (p.empty()) return s.empty();
@@ -520,6 +555,7 @@ struct Compiler {
         a.kind = AT_GLOB_E;
         a.s_off = ps.add_str(str);
         a.s_len = (uint32_t)str.size() | (utf8_ascii(str) ? 0x80000000u : 0);
+        ps.compile_glob(a, str);
       } else {
         a.kind = AT_FALSE;
       }
@@ -535,6 +571,7 @@ struct Compiler {
         a.kind = AT_GLOB_N;
         a.s_off = ps.add_str(pattern);
         a.s_len = (uint32_t)pattern.size() | (utf8_ascii(pattern) ? 0x80000000u : 0);
+        ps.compile_glob(a, pattern);
       }
     }
     ps.atoms.push_back(a);
@@ -931,6 +968,7 @@ struct Compiler {
     a.op = CO_EQ;
     a.s_off = ps.add_str(g);
     a.s_len = (uint32_t)g.size() | (utf8_ascii(g) ? 0x80000000u : 0);
+    ps.compile_glob(a, g);
     ps.atoms.push_back(a);
     return (uint32_t)ps.atoms.size() - 1;
   }

@@ -32,8 +32,11 @@ struct DevPS {
   const SelLabel* sellabels;
   const SelExpr* selexprs;
   const uint32_t* kg_specs;
+  const GSeg* gsegs;
+  const GWord* gwords;
   const uint8_t* pstr;
   uint32_t star_id;
+  uint32_t n_rules;
 };
 
 struct DevBatch {
@@ -61,7 +64,8 @@ constexpr int KV_WG = 256;
 constexpr int KV_HIST = 8;
 
 // Launch one pass over rules [rule_begin, rule_end) for every resource.
-hipError_t launch_validate(const DevPS& P, const DevBatch& B, const DevOut& O, uint32_t rule_begin, uint32_t rule_end,
-                           hipStream_t stream);
+// P and B point to device-resident copies of the views (uniform scalar loads).
+hipError_t launch_validate(const DevPS* P, const DevBatch* B, uint32_t n_res, const DevOut& O, uint32_t rule_begin,
+                           uint32_t rule_end, hipStream_t stream);
 
 }  // namespace kv

@@ -31,12 +31,17 @@ struct Ingest {
   std::unordered_map<std::string, uint32_t> ns_index;
   uint32_t nstatic;
 
-  Ingest(const PolicySet& p, Batch& bb) : ps(p), b(bb), nstatic((uint32_t)p.keys.size()) {}
+  Ingest(const PolicySet& p, Batch& bb) : ps(p), b(bb), nstatic((uint32_t)p.keys.size()) {
+    // offset 0 holds "0": convertNumberToString(nil) for the device glob (kvkernel.hip atom_eval)
+    str("0");
+  }
 
   uint32_t str(std::string_view s) {
     std::string k(s);
     auto it = str_off.find(k);
     if (it != str_off.end()) return it->second;
+    // 4-byte aligned: the device glob compares whole words (kvkernel.hip seg_at)
+    while (b.strs.size() & 3) b.strs.push_back('\0');
     uint32_t off = (uint32_t)b.strs.size();
     b.strs.append(s.data(), s.size());
     str_off.emplace(std::move(k), off);
@@ -310,6 +315,8 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
   for (size_t n = 0; n < b->namespaces.size(); n++)
     for (uint32_t s = 0; s < nsel; s++)
       if (selector_eval_host(ps.nsselectors[s], b->ns_labels[n]) == 1) b->ns_bits[n * b->ns_words + s / 32] |= 1u << (s % 32);
+  // word-granular readers may touch up to 8 bytes past the last string
+  b->strs.append(16, '\0');
   b->bytes_referenced = b->nodes.size() * sizeof(Node) + b->vals.size() * sizeof(Val) + b->res.size() * sizeof(Res) +
                         b->kvs.size() * sizeof(KV) + b->strs.size();
 }

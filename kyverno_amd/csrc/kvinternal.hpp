@@ -122,6 +122,9 @@ struct PolicySet {
   std::vector<kv::Atom> atoms;
   std::unordered_map<std::string, uint32_t> pred_cache;
   std::vector<uint32_t> kg_specs;  // wildcard label-map sibling specs (OP_KEYGLOB)
+  std::vector<kv::GSeg> gsegs;     // compiled glob segments
+  std::vector<kv::GWord> gwords;
+  void compile_glob(kv::Atom& a, const std::string& pattern);
   std::vector<kv::RuleRec> rules;
   std::vector<RuleHost> rhost;
   std::vector<kv::MFilter> filters;

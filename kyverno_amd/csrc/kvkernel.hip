@@ -1,9 +1,10 @@
 // HIP kernels of libkvgpu (gfx950 / CDNA4).
 //
-// kv_validate_kernel: one lane = one resource; every wave walks the rules of
-// the launch in order, so the rule's program, predicates and pattern strings
-// are wave-uniform (scalar loads), while resource nodes are per-lane gathers
-// from the projected HBM store. Per rule:
+// kv_validate_kernel: one lane = one resource; a workgroup owns 256 resources
+// and a chunk of rules, and every wave walks its rules in order, so the rule's
+// program, predicates and compiled glob segments are wave-uniform (scalar
+// loads), while resource nodes are per-lane gathers from the projected HBM
+// store. Per rule:
 //   1. match/exclude prefilter (MatchesResourceDescription, pkg/engine/utils.go:265-336)
 //   2. pattern VM: a uniform-pc SIMT interpreter over the structured program
 //      emitted by kvcompile.cpp (validate.go:29-194, anchor.go:21-277). Lanes
@@ -12,9 +13,10 @@
 //      wave never diverges in program position; loops over resource arrays
 //      (containers[], volumes[] ...) run max(len) uniform iterations.
 //   3. MatchPattern epilogue (validate.go:29-50) -> status, error record.
-// Output: FULL mode = status[rule][res] (+ error records); COUNTS mode = per-rule
-// pass/fail/warn/error/skip/nomatch/cpu histogram (int64) accumulated in LDS and
-// flushed with one atomic per counter per workgroup.
+// Workgroup -> (resource block, rule chunk) mapping is XCD-aware: all rule
+// chunks of one resource block land on the same XCD (same L2) back to back.
+// Output: status[rule][res] (+ error records) and a per-rule histogram
+// accumulated in LDS and flushed with one atomic per counter per workgroup.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -25,6 +27,7 @@ using namespace kv;
 #define KV_MAXD 16
 #define KV_MAXL 4
 #define KV_SENT 0xFFFFFFFFu
+#define KV_RCHUNK 64
 
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -35,7 +38,8 @@ __device__ __forceinline__ uint32_t rune_len(uint8_t c) {
 
 // minio/pkg v1.1.3 wildcard.Match over valid UTF-8: '*' any run of runes,
 // '?' exactly one rune; star backtracking advances by whole runes.
-__device__ bool kv_glob(const uint8_t* p, uint32_t pl, const uint8_t* s, uint32_t sl) {
+// General path (non-ASCII value with '?' in the pattern, selector/label globs).
+__device__ __noinline__ bool kv_glob(const uint8_t* p, uint32_t pl, const uint8_t* s, uint32_t sl) {
   if (pl == 0) return sl == 0;
   if (pl == 1 && p[0] == '*') return true;
   uint32_t si = 0, pi = 0, star = KV_SENT, mark = 0;
@@ -59,6 +63,62 @@ __device__ bool kv_glob(const uint8_t* p, uint32_t pl, const uint8_t* s, uint32_
   }
   while (pi < pl && p[pi] == '*') pi++;
   return pi == pl && si == sl;
+}
+
+// segment (uniform words) == value bytes [k, k+len) ; value base 4-byte aligned
+__device__ __forceinline__ bool seg_at(const GWord* __restrict__ wd, uint32_t len, const uint32_t* __restrict__ base,
+                                       uint32_t k) {
+  const uint32_t nw = (len + 3) >> 2;
+  const uint32_t a = k >> 2, sh = k & 3;
+  uint32_t lo = base[a];
+  for (uint32_t i = 0; i < nw; i++) {
+    uint32_t hi = base[a + i + 1];
+    uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, sh);
+    const GWord g = wd[i];
+    if ((v ^ g.w) & g.mask) return false;
+    lo = hi;
+  }
+  return true;
+}
+
+// compiled glob over a 4-byte aligned value string (see kv_layout.h GlobFlags)
+__device__ bool glob_fast(const DevPS& P, const Atom& A, const uint8_t* s, uint32_t sl) {
+  const uint32_t fl = uni(A.gflags);
+  if (fl & G_ALL) return true;
+  if (fl & G_EMPTY) return sl == 0;
+  if (sl < uni(A.gmin)) return false;
+  const uint32_t* base = (const uint32_t*)s;
+  const GSeg* segs = P.gsegs + uni(A.gfirst);
+  const uint32_t n = uni(A.gcount);
+  uint32_t pos = 0, end = sl, i0 = 0, i1 = n;
+  if (!(fl & G_LEAD)) {
+    const GSeg s0 = segs[0];
+    if (n == 1 && !(fl & G_TRAIL)) return sl == s0.len && seg_at(P.gwords + s0.wfirst, s0.len, base, 0);
+    if (!seg_at(P.gwords + s0.wfirst, s0.len, base, 0)) return false;
+    pos = s0.len;
+    i0 = 1;
+  }
+  if (!(fl & G_TRAIL)) {
+    const GSeg st = segs[n - 1];
+    if (end < pos + st.len) return false;
+    if (!seg_at(P.gwords + st.wfirst, st.len, base, end - st.len)) return false;
+    end -= st.len;
+    i1 = n - 1;
+  }
+  for (uint32_t i = i0; i < i1; i++) {
+    const GSeg sg = segs[i];
+    bool found = false;
+    for (uint32_t k = pos; k + sg.len <= end; k++) {
+      if (seg_at(P.gwords + sg.wfirst, sg.len, base, k)) { pos = k + sg.len; found = true; break; }
+    }
+    if (!found) return false;
+  }
+  return true;
+}
+
+__device__ __forceinline__ bool glob_atom(const DevPS& P, const Atom& A, const uint8_t* s, uint32_t sl, bool ascii) {
+  if (ascii || !(uni(A.gflags) & G_HASQ)) return glob_fast(P, A, s, sl);
+  return kv_glob(P.pstr + A.s_off, A.s_len & 0x7FFFFFFFu, s, sl);
 }
 
 __device__ __forceinline__ bool bytes_eq(const uint8_t* a, uint32_t al, const uint8_t* b, uint32_t bl) {
@@ -95,33 +155,29 @@ __device__ __forceinline__ bool cmp_ok(uint32_t op, int r) {
 }
 
 // one atom of a string pattern against the value at `node` (ABSENT/NULL == Go nil)
-__device__ bool atom_eval(const DevPS& P, const DevBatch& B, uint32_t ai, uint32_t node) {
+__device__ bool atom_eval(const DevPS& P, const DevBatch& B, uint32_t ai, uint32_t type, uint32_t vid) {
   const Atom& A = P.atoms[ai];
-  uint32_t kind = uni(A.kind);
-  uint32_t type = node == ABSENT ? NT_NULL : B.nodes[node].type;
+  const uint32_t kind = uni(A.kind);
   if (kind == AT_FALSE) return false;
   if (type == NT_MAP || type == NT_ARR) return false;
   if (kind == AT_GLOB_E) {
     if (type == NT_NULL) return false;
-    const Val& v = B.vals[B.nodes[node].a];
-    bool r = kv_glob(P.pstr + A.s_off, A.s_len & 0x7FFFFFFFu, B.bstr + v.e_off, v.e_len);
+    const Val& v = B.vals[vid];
+    bool r = glob_atom(P, A, B.bstr + v.e_off, v.e_len, v.flags & VF_ASCII_E);
     return uni(A.op) == CO_NE ? !r : r;
   }
   if (type == NT_BOOL) return false;
   if (kind == AT_GLOB_N) {
-    if (type == NT_NULL) {
-      const uint8_t zero = '0';
-      return kv_glob(P.pstr + A.s_off, A.s_len & 0x7FFFFFFFu, &zero, 1);
-    }
-    const Val& v = B.vals[B.nodes[node].a];
-    return kv_glob(P.pstr + A.s_off, A.s_len & 0x7FFFFFFFu, B.bstr + v.n_off, v.n_len);
+    if (type == NT_NULL) return glob_atom(P, A, B.bstr, 1, true);  // convertNumberToString(nil) == "0" (bstr[0..1))
+    const Val& v = B.vals[vid];
+    return glob_atom(P, A, B.bstr + v.n_off, v.n_len, v.flags & VF_ASCII_N);
   }
   // AT_QCMP
   int r;
   if (type == NT_NULL) {
     r = q_cmp(VF_Q_ZERO, 0, 0, 0, A.q_flags, A.q_exp, A.q_hi, A.q_lo);
   } else {
-    const Val& v = B.vals[B.nodes[node].a];
+    const Val& v = B.vals[vid];
     if (!(v.flags & VF_Q_VALID)) return false;
     r = q_cmp(v.flags, v.q_exp, v.q_hi, v.q_lo, A.q_flags, A.q_exp, A.q_hi, A.q_lo);
   }
@@ -131,15 +187,21 @@ __device__ bool atom_eval(const DevPS& P, const DevBatch& B, uint32_t ai, uint32
 // ValidateValueWithPattern(value, pattern) for a scalar-pattern leaf
 __device__ bool pred_eval(const DevPS& P, const DevBatch& B, uint32_t pi, uint32_t node) {
   const Pred& pr = P.preds[pi];
-  uint32_t kind = uni(pr.kind);
-  uint32_t type = node == ABSENT ? NT_NULL : B.nodes[node].type;
+  const uint32_t kind = uni(pr.kind);
+  uint32_t type = NT_NULL, va = 0, vb = 0;
+  if (node != ABSENT) {
+    const Node n = B.nodes[node];
+    type = n.type;
+    va = n.a;
+    vb = n.b;
+  }
   switch (kind) {
-    case PK_BOOL: return type == NT_BOOL && B.nodes[node].b == uni(pr.flags);
+    case PK_BOOL: return type == NT_BOOL && vb == uni(pr.flags);
     case PK_FLOAT: {
-      if (type == NT_INT) return uni(pr.flags) && B.vals[B.nodes[node].a].i == pr.fi;
-      if (type == NT_FLOAT) return B.vals[B.nodes[node].a].f == pr.f;
+      if (type == NT_INT) return uni(pr.flags) && B.vals[va].i == pr.fi;
+      if (type == NT_FLOAT) return B.vals[va].f == pr.f;
       if (type == NT_STR) {
-        const Val& v = B.vals[B.nodes[node].a];
+        const Val& v = B.vals[va];
         return (v.flags & VF_PF_OK) && v.f == pr.f;
       }
       return false;
@@ -147,20 +209,20 @@ __device__ bool pred_eval(const DevPS& P, const DevBatch& B, uint32_t pi, uint32
     case PK_NIL:
       if (type == NT_NULL) return true;
       if (type == NT_MAP || type == NT_ARR) return false;
-      return (B.vals[B.nodes[node].a].flags & VF_NILLIKE) != 0;
+      return (B.vals[va].flags & VF_NILLIKE) != 0;
     case PK_MAPTYPE: return type == NT_MAP;
     case PK_STRING: {
-      uint32_t af = uni(pr.first), an = uni(pr.count);
+      const uint32_t af = uni(pr.first), an = uni(pr.count);
       for (uint32_t a = af; a < af + an; a++) {
         const Alt& al = P.alts[a];
-        uint32_t cf = uni(al.first), cn = uni(al.count);
+        const uint32_t cf = uni(al.first), cn = uni(al.count);
         bool all = true;
         for (uint32_t c = cf; c < cf + cn && all; c++) {
           const Conj& cj = P.conjs[c];
-          uint32_t ck = uni(cj.kind);
-          bool r = atom_eval(P, B, uni(cj.a0), node);
-          if (ck == CJ_INRANGE) r = r && atom_eval(P, B, uni(cj.a1), node);
-          else if (ck == CJ_NOTINRANGE) r = r || atom_eval(P, B, uni(cj.a1), node);
+          const uint32_t ck = uni(cj.kind);
+          bool r = atom_eval(P, B, uni(cj.a0), type, va);
+          if (ck == CJ_INRANGE) r = r && atom_eval(P, B, uni(cj.a1), type, va);
+          else if (ck == CJ_NOTINRANGE) r = r || atom_eval(P, B, uni(cj.a1), type, va);
           all = r;
         }
         if (all) return true;
@@ -181,8 +243,8 @@ __device__ __forceinline__ uint32_t lookup(const DevBatch& B, uint32_t m, uint32
 }
 
 // Resolved result key of sibling spec entry (OP_KEYGLOB): returns key id and node.
-__device__ __forceinline__ void kg_resolve(const DevPS& P, const DevBatch& B, uint32_t m, uint32_t w, uint32_t ref,
-                                           uint32_t* key, uint32_t* node) {
+__device__ void kg_resolve(const DevPS& P, const DevBatch& B, uint32_t m, uint32_t w, uint32_t ref, uint32_t* key,
+                           uint32_t* node) {
   if (!w) {  // literal sibling: key id is the key
     *key = ref;
     *node = lookup(B, m, ref);
@@ -191,8 +253,8 @@ __device__ __forceinline__ void kg_resolve(const DevPS& P, const DevBatch& B, ui
   const Atom& A = P.atoms[ref];
   const Node mn = B.nodes[m];
   for (uint32_t i = 0; i < mn.b; i++) {
-    uint32_t k = B.nodes[mn.a + i].key;
-    if (kv_glob(P.pstr + A.s_off, A.s_len & 0x7FFFFFFFu, B.kstr + B.key_off[k], B.key_len[k])) {
+    const uint32_t k = B.nodes[mn.a + i].key;
+    if (glob_atom(P, A, B.kstr + B.key_off[k], B.key_len[k], false)) {
       *key = k;
       *node = mn.a + i;
       return;
@@ -203,41 +265,40 @@ __device__ __forceinline__ void kg_resolve(const DevPS& P, const DevBatch& B, ui
 }
 
 // ------------------------------------------------------------------ match/exclude
-__device__ bool selector_match(const DevPS& P, const DevBatch& B, const Res& R, uint32_t si) {
+__device__ bool selector_match(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t si) {
   const Selector& S = P.sels[si];
-  uint32_t fl = uni(S.flags);
+  const uint32_t fl = uni(S.flags);
   if (fl & SF_STATIC_INVALID) return false;
   if (fl & SF_EVERYTHING) return true;
-  const KV* labels = B.kvs + R.labels_first;
-  uint32_t nl = R.labels_count;
-  uint32_t mf = uni(S.ml_first), mc = uni(S.ml_count);
-  // resolve every matchLabels entry: (key ptr/len, val ptr/len, valid)
+  const KV* labels = B.kvs + R->labels_first;
+  const uint32_t nl = R->labels_count;
+  const uint32_t mf = uni(S.ml_first), mc = uni(S.ml_count);
+  auto resolve = [&](const SelLabel& E, const uint8_t** ok, uint32_t* okl, const uint8_t** ov, uint32_t* ovl,
+                     bool* val) {
+    if (!(E.flags & SL_WILD)) {
+      *ok = P.pstr + E.k_off; *okl = E.k_len; *ov = P.pstr + E.v_off; *ovl = E.v_len;
+      *val = (E.flags & SL_VALID) != 0;
+      return;
+    }
+    for (uint32_t q = 0; q < nl; q++) {
+      const KV kv = labels[q];
+      const uint8_t* lk = B.bstr + kv.k_off;
+      const uint8_t* lv = B.bstr + kv.v_off;
+      const uint32_t lkl = kv.k_len & KV_LEN_MASK, lvl = kv.v_len & KV_LEN_MASK;
+      if (kv_glob(P.pstr + E.k_off, E.k_len, lk, lkl) && kv_glob(P.pstr + E.v_off, E.v_len, lv, lvl)) {
+        *ok = lk; *okl = lkl; *ov = lv; *ovl = lvl;
+        *val = (kv.k_len & KV_VALID) && (kv.v_len & KV_VALID);
+        return;
+      }
+    }
+    *ok = P.pstr + E.rk_off; *okl = E.rk_len; *ov = P.pstr + E.rv_off; *ovl = E.rv_len;
+    *val = (E.flags & SL_VALID) != 0;
+  };
   for (uint32_t j = mf; j < mf + mc; j++) {
-    const SelLabel& L = P.sellabels[j];
     const uint8_t *kp, *vp;
     uint32_t kl, vl;
     bool valid;
-    auto resolve = [&](const SelLabel& E, const uint8_t** ok, uint32_t* okl, const uint8_t** ov, uint32_t* ovl, bool* val) {
-      if (!(E.flags & SL_WILD)) {
-        *ok = P.pstr + E.k_off; *okl = E.k_len; *ov = P.pstr + E.v_off; *ovl = E.v_len;
-        *val = (E.flags & SL_VALID) != 0;
-        return;
-      }
-      for (uint32_t q = 0; q < nl; q++) {
-        const KV kv = labels[q];
-        const uint8_t* lk = B.bstr + kv.k_off;
-        const uint8_t* lv = B.bstr + kv.v_off;
-        uint32_t lkl = kv.k_len & KV_LEN_MASK, lvl = kv.v_len & KV_LEN_MASK;
-        if (kv_glob(P.pstr + E.k_off, E.k_len, lk, lkl) && kv_glob(P.pstr + E.v_off, E.v_len, lv, lvl)) {
-          *ok = lk; *okl = lkl; *ov = lv; *ovl = lvl;
-          *val = (kv.k_len & KV_VALID) && (kv.v_len & KV_VALID);
-          return;
-        }
-      }
-      *ok = P.pstr + E.rk_off; *okl = E.rk_len; *ov = P.pstr + E.rv_off; *ovl = E.rv_len;
-      *val = (E.flags & SL_VALID) != 0;
-    };
-    resolve(L, &kp, &kl, &vp, &vl, &valid);
+    resolve(P.sellabels[j], &kp, &kl, &vp, &vl, &valid);
     // dropped if a later entry resolves to the same key (results[matchK] = matchV)
     bool dropped = false;
     for (uint32_t j2 = j + 1; j2 < mf + mc && !dropped; j2++) {
@@ -250,14 +311,16 @@ __device__ bool selector_match(const DevPS& P, const DevBatch& B, const Res& R, 
     if (dropped) continue;
     if (!valid) return false;  // NewRequirement validation error
     bool found = false;
-    for (uint32_t q = 0; q < nl && !found; q++) {
+    for (uint32_t q = 0; q < nl; q++) {
       const KV kv = labels[q];
-      if (bytes_eq(B.bstr + kv.k_off, kv.k_len & KV_LEN_MASK, kp, kl))
-        found = bytes_eq(B.bstr + kv.v_off, kv.v_len & KV_LEN_MASK, vp, vl) ? true : (q = nl, false);
+      if (bytes_eq(B.bstr + kv.k_off, kv.k_len & KV_LEN_MASK, kp, kl)) {
+        found = bytes_eq(B.bstr + kv.v_off, kv.v_len & KV_LEN_MASK, vp, vl);
+        break;
+      }
     }
     if (!found) return false;
   }
-  uint32_t ef = uni(S.me_first), ec = uni(S.me_count);
+  const uint32_t ef = uni(S.me_first), ec = uni(S.me_count);
   for (uint32_t j = ef; j < ef + ec; j++) {
     const SelExpr& E = P.selexprs[j];
     bool has = false, in = false;
@@ -270,41 +333,44 @@ __device__ bool selector_match(const DevPS& P, const DevBatch& B, const Res& R, 
         break;
       }
     }
-    uint32_t op = uni(E.op);
+    const uint32_t op = uni(E.op);
     if ((op == 0 && !in) || (op == 1 && in) || (op == 2 && !has) || (op == 3 && has)) return false;
   }
   return true;
 }
 
 // doesResourceMatchConditionBlock: number of failed criteria (0 == block matches)
-__device__ uint32_t block_errs(const DevPS& P, const DevBatch& B, const Res& R, uint32_t f) {
+__device__ uint32_t block_errs(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t rkind,
+                               uint32_t rflags, uint32_t f) {
   const MFilter& F = P.filters[f];
-  uint32_t fl = uni(P.fflags[f]);
+  const uint32_t fl = uni(P.fflags[f]);
   uint32_t errs = 0;
   if (fl & MF_KINDS) {
     bool ok = false;
-    for (uint32_t k = uni(F.kinds_first); k < F.kinds_first + F.kinds_count && !ok; k++) {
+    const uint32_t kf = uni(F.kinds_first), kc = uni(F.kinds_count);
+    for (uint32_t k = kf; k < kf + kc && !ok; k++) {
       const KindSpec ks = P.kinds[k];
       switch (ks.form) {
         case 3: ok = true; break;
-        case 0: ok = R.kind == ks.kind; break;
-        case 1: ok = R.kind == ks.kind && R.version == ks.version; break;
-        default: ok = R.group == ks.group && R.kind == ks.kind && (R.version == ks.version || R.version == P.star_id); break;
+        case 0: ok = rkind == ks.kind; break;
+        case 1: ok = rkind == ks.kind && R->version == ks.version; break;
+        default: ok = R->group == ks.group && rkind == ks.kind && (R->version == ks.version || R->version == P.star_id); break;
       }
     }
     errs += ok ? 0 : 1;
+    if (errs) return errs;  // later criteria cannot turn an error count back to zero
   }
-  if (fl & MF_NAME) errs += kv_glob(P.pstr + F.name_off, F.name_len, B.bstr + R.name_off, R.name_len) ? 0 : 1;
+  if (fl & MF_NAME) errs += kv_glob(P.pstr + F.name_off, F.name_len, B.bstr + R->name_off, R->name_len) ? 0 : 1;
   if (fl & MF_NAMES) {
     bool any = false;
     for (uint32_t k = F.names_first; k < F.names_first + F.names_count && !any; k++)
-      any = kv_glob(P.pstr + P.strrefs[k].off, P.strrefs[k].len, B.bstr + R.name_off, R.name_len);
+      any = kv_glob(P.pstr + P.strrefs[k].off, P.strrefs[k].len, B.bstr + R->name_off, R->name_len);
     errs += any ? 0 : 1;
   }
   if (fl & MF_NSS) {
     bool any = false;
     for (uint32_t k = F.nss_first; k < F.nss_first + F.nss_count && !any; k++)
-      any = kv_glob(P.pstr + P.strrefs[k].off, P.strrefs[k].len, B.bstr + R.ns_off, R.ns_len);
+      any = kv_glob(P.pstr + P.strrefs[k].off, P.strrefs[k].len, B.bstr + R->ns_off, R->ns_len);
     errs += any ? 0 : 1;
   }
   if (fl & MF_ANN) {
@@ -312,8 +378,8 @@ __device__ uint32_t block_errs(const DevPS& P, const DevBatch& B, const Res& R, 
     for (uint32_t k = F.ann_first; k < F.ann_first + F.ann_count && all; k++) {
       const StrPair sp = P.strpairs[k];
       bool m = false;
-      for (uint32_t q = 0; q < R.annot_count && !m; q++) {
-        const KV kv = B.kvs[R.annot_first + q];
+      for (uint32_t q = 0; q < R->annot_count && !m; q++) {
+        const KV kv = B.kvs[R->annot_first + q];
         m = kv_glob(P.pstr + sp.k_off, sp.k_len, B.bstr + kv.k_off, kv.k_len & KV_LEN_MASK) &&
             kv_glob(P.pstr + sp.v_off, sp.v_len, B.bstr + kv.v_off, kv.v_len & KV_LEN_MASK);
       }
@@ -322,39 +388,40 @@ __device__ uint32_t block_errs(const DevPS& P, const DevBatch& B, const Res& R, 
     errs += all ? 0 : 1;
   }
   if (fl & MF_SEL) errs += selector_match(P, B, R, F.sel) ? 0 : 1;
-  if ((fl & MF_NSSEL) && !(R.flags & (RF_KIND_NAMESPACE | RF_KIND_EMPTY))) {
-    uint32_t bit = F.nssel_bit;
-    errs += (B.ns_bits[R.ns_index * B.ns_words + bit / 32] >> (bit % 32)) & 1 ? 0 : 1;
+  if ((fl & MF_NSSEL) && !(rflags & (RF_KIND_NAMESPACE | RF_KIND_EMPTY))) {
+    const uint32_t bit = F.nssel_bit;
+    errs += (B.ns_bits[R->ns_index * B.ns_words + bit / 32] >> (bit % 32)) & 1 ? 0 : 1;
   }
   if (fl & MF_UI_FAIL) errs += 1;
   return errs;
 }
 
-__device__ bool rule_matches(const DevPS& P, const DevBatch& B, const Res& R, const RuleRec& rr) {
-  uint32_t mm = uni(rr.m_mode), mf = uni(rr.m_first), mc = uni(rr.m_count);
+__device__ bool rule_matches(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t rkind,
+                             uint32_t rflags, const RuleRec& rr) {
+  const uint32_t mm = uni(rr.m_mode), mf = uni(rr.m_first), mc = uni(rr.m_count);
   bool ok;
   if (mm == 1) {
     ok = false;
-    for (uint32_t f = mf; f < mf + mc && !ok; f++) ok = !(P.fflags[f] & MF_EMPTY) && block_errs(P, B, R, f) == 0;
+    for (uint32_t f = mf; f < mf + mc && !ok; f++) ok = !(P.fflags[f] & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, f) == 0;
   } else if (mm == 2) {
     ok = true;
-    for (uint32_t f = mf; f < mf + mc && ok; f++) ok = !(P.fflags[f] & MF_EMPTY) && block_errs(P, B, R, f) == 0;
+    for (uint32_t f = mf; f < mf + mc && ok; f++) ok = !(P.fflags[f] & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, f) == 0;
   } else {
-    ok = !(P.fflags[mf] & MF_EMPTY) && block_errs(P, B, R, mf) == 0;
+    ok = !(P.fflags[mf] & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, mf) == 0;
   }
   if (!ok) return false;
-  uint32_t xm = uni(rr.x_mode), xf = uni(rr.x_first), xc = uni(rr.x_count);
+  const uint32_t xm = uni(rr.x_mode), xf = uni(rr.x_first), xc = uni(rr.x_count);
   if (xm == 1) {
     for (uint32_t f = xf; f < xf + xc; f++)
-      if (!(P.fflags[f] & MF_EMPTY) && block_errs(P, B, R, f) == 0) return false;
+      if (!(P.fflags[f] & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, f) == 0) return false;
     return true;
   }
   if (xm == 2) {
     for (uint32_t f = xf; f < xf + xc; f++)
-      if ((P.fflags[f] & MF_EMPTY) || block_errs(P, B, R, f) != 0) return true;
+      if ((P.fflags[f] & MF_EMPTY) || block_errs(P, B, R, rkind, rflags, f) != 0) return true;
     return false;
   }
-  if (!(P.fflags[xf] & MF_EMPTY) && block_errs(P, B, R, xf) == 0) return false;
+  if (!(P.fflags[xf] & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, xf) == 0) return false;
   return true;
 }
 
@@ -368,37 +435,57 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 }
 
 // ------------------------------------------------------------------ kernel
-extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(DevPS P, DevBatch B, DevOut O, uint32_t rule_begin,
-                                                                      uint32_t rule_end) {
+extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(const DevPS* __restrict__ Pp,
+                                                                      const DevBatch* __restrict__ Bp, DevOut O,
+                                                                      uint32_t rule_begin, uint32_t rule_end,
+                                                                      uint32_t n_chunks, uint32_t rblocks) {
   __shared__ uint32_t s_cur[KV_MAXD][KV_WG];
   __shared__ uint32_t s_lfirst[KV_MAXL][KV_WG];
   __shared__ uint32_t s_llen[KV_MAXL][KV_WG];
   __shared__ uint32_t s_li[KV_WG / 64][KV_MAXL];
-  __shared__ uint32_t s_hist[64][KV_HIST];
+  __shared__ uint32_t s_hist[KV_RCHUNK][KV_HIST];
+
+  const DevPS& P = *Pp;
+  const DevBatch& B = *Bp;
+  // XCD-aware work mapping: block ids b and b+8 share an XCD (and its L2), so
+  // every rule chunk of one resource block is placed on the same XCD.
+  const uint32_t xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const uint32_t rblock = (slot / n_chunks) * 8 + xcd;
+  const uint32_t chunk = slot % n_chunks;
+  if (rblock >= rblocks) return;
+  const uint32_t per = (rule_end - rule_begin + n_chunks - 1) / n_chunks;
+  const uint32_t cb = rule_begin + chunk * per;
+  const uint32_t ce = cb + per < rule_end ? cb + per : rule_end;
+  if (cb >= ce) return;
 
   const uint32_t lane = threadIdx.x;
   const uint32_t wv = lane >> 6;
-  const uint32_t r = blockIdx.x * KV_WG + lane;
-  const bool valid = r < B.n_res;
-  Res R;
-  if (valid) R = B.res[r];
-  else { R.root = ABSENT; R.flags = 0; R.labels_count = 0; R.annot_count = 0; R.kind = KEY_NONE; }
+  const uint32_t r = rblock * KV_WG + lane;
+  const uint32_t n_res = B.n_res;
+  const bool valid = r < n_res;
+  const Res* R = B.res + (valid ? r : 0);
+  uint32_t rroot = ABSENT, rkind = KEY_NONE, rflags = 0;
+  if (valid) {
+    rroot = R->root;
+    rkind = R->kind;
+    rflags = R->flags;
+  }
 
-  for (uint32_t rb = rule_begin; rb < rule_end; rb += 64) {
-    const uint32_t re = rb + 64 < rule_end ? rb + 64 : rule_end;
-    for (uint32_t q = lane; q < 64 * KV_HIST; q += KV_WG) (&s_hist[0][0])[q] = 0;
+  for (uint32_t rb = cb; rb < ce; rb += KV_RCHUNK) {
+    const uint32_t re = rb + KV_RCHUNK < ce ? rb + KV_RCHUNK : ce;
+    for (uint32_t q = lane; q < KV_RCHUNK * KV_HIST; q += KV_WG) (&s_hist[0][0])[q] = 0;
     __syncthreads();
     for (uint32_t ri = rb; ri < re; ri++) {
-      const RuleRec rr = P.rules[ri];
+      const RuleRec& rr = P.rules[ri];
       const uint32_t route = uni(rr.route);
       uint32_t st = ST_NOMATCH;
       bool run = false;
-      if (valid && rule_matches(P, B, R, rr)) {
+      if (valid && rule_matches(P, B, R, rkind, rflags, rr)) {
         if (route == 1) st = ST_CPU;
         else if (route == 2) st = ST_NOMATCH;
-        else if (route == 3) st = (uint8_t)rr.const_status;
-        else if (R.flags & RF_MAGIC) st = ST_CPU;
-        else if ((uni(rr.flags) & RR_META_EXPAND) && (R.flags & RF_BAD_META)) st = ST_CPU;
+        else if (route == 3) st = (uint8_t)uni(rr.const_status);
+        else if (rflags & RF_MAGIC) st = ST_CPU;
+        else if ((uni(rr.flags) & RR_META_EXPAND) && (rflags & RF_BAD_META)) st = ST_CPU;
         else run = true;
       }
       uint32_t ekind = 0, eflags = 0, epn = 0, ekey = ABSENT, eres = ABSENT;
@@ -408,7 +495,7 @@ extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(DevPS P, 
         uint32_t keynode = ABSENT;
         uint32_t wait = run ? 0u : KV_SENT;
         uint32_t pc = uni(rr.prog);
-        s_cur[0][lane] = R.root;
+        s_cur[0][lane] = rroot;
         auto raise = [&](uint32_t kind, uint32_t pn, uint32_t rn, uint32_t cpc) {
           ekind = kind;
           eflags = 0;
@@ -431,15 +518,16 @@ extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(DevPS P, 
           }
           if (wait == pc) wait = 0;
           if (!__ballot(wait == 0)) {
-            uint32_t m = uni(wave_min(wait));
+            const uint32_t m = uni(wave_min(wait));
             if (m == KV_SENT) break;
             pc = m;
             continue;
           }
-          const Inst in = P.prog[pc];
-          const uint32_t op = uni(in.op) & 0xFF;
-          const uint32_t d = (uni(in.op) >> 8) & 0xFF;
-          const uint32_t aux = (uni(in.op) >> 16) & 0xFF;
+          const Inst& in = P.prog[pc];
+          const uint32_t opw = uni(in.op);
+          const uint32_t op = opw & 0xFF;
+          const uint32_t d = (opw >> 8) & 0xFF;
+          const uint32_t aux = (opw >> 16) & 0xFF;
           const uint32_t ia = uni(in.a), ib = uni(in.b), ic = uni(in.c);
           const bool A = wait == 0;
           uint32_t next = pc + 1;
@@ -447,8 +535,8 @@ extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(DevPS P, 
             case OP_MAPCHK:
             case OP_ARRCHK:
               if (A) {
-                uint32_t v = s_cur[d][lane];
-                uint32_t want = op == OP_MAPCHK ? NT_MAP : NT_ARR;
+                const uint32_t v = s_cur[d][lane];
+                const uint32_t want = op == OP_MAPCHK ? NT_MAP : NT_ARR;
                 if (v == ABSENT || B.nodes[v].type != want) raise(op == OP_MAPCHK ? E_TYPE_MAP : E_TYPE_ARR, ia, v, ic);
               }
               break;
@@ -461,17 +549,17 @@ extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(DevPS P, 
             case OP_KEY:
             case OP_KEYV:
               if (A) {
-                uint32_t c = lookup(B, s_cur[d][lane], ia);
+                const uint32_t c = lookup(B, s_cur[d][lane], ia);
                 s_cur[d + 1][lane] = c;
                 if (op == OP_KEY && c == ABSENT) wait = ib;
               }
               break;
             case OP_KEYGLOB:
               if (A) {
-                const uint32_t j = uni(in.op) >> 24;
+                const uint32_t j = opw >> 24;
                 const Atom& at = P.atoms[ia];
-                const uint32_t spec = (uint32_t)at.q_hi;
-                const uint32_t mycls = (uint32_t)at.q_lo;
+                const uint32_t spec = uni((uint32_t)at.q_hi);
+                const uint32_t mycls = uni((uint32_t)at.q_lo);
                 const uint32_t n = P.kg_specs[spec];
                 const uint32_t m = s_cur[d][lane];
                 uint32_t mykey, mynode;
@@ -479,7 +567,7 @@ extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(DevPS P, 
                 kg_resolve(P, B, m, myw, myw ? ia : ic, &mykey, &mynode);
                 bool dropped = false;
                 for (uint32_t j2 = j + 1; j2 < n && !dropped; j2++) {
-                  uint32_t cw = P.kg_specs[spec + 1 + 2 * j2];
+                  const uint32_t cw = P.kg_specs[spec + 1 + 2 * j2];
                   if ((cw >> 1) != mycls || mykey == KV_SENT) continue;
                   uint32_t k2, n2;
                   kg_resolve(P, B, m, cw & 1, P.kg_specs[spec + 2 + 2 * j2], &k2, &n2);
@@ -488,7 +576,7 @@ extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(DevPS P, 
                 if (dropped) {
                   wait = ib;
                 } else {
-                  uint32_t node = (myw && mykey != KV_SENT) ? mynode : lookup(B, m, ic);
+                  const uint32_t node = (myw && mykey != KV_SENT) ? mynode : lookup(B, m, ic);
                   keynode = (myw && mykey != KV_SENT) ? mynode : ABSENT;
                   s_cur[d + 1][lane] = node;
                   if (node == ABSENT && (aux & 1)) wait = ib;
@@ -512,13 +600,13 @@ extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(DevPS P, 
               break;
             case OP_STAR:
               if (A) {
-                uint32_t v = s_cur[d + 1][lane];
+                const uint32_t v = s_cur[d + 1][lane];
                 if (v == ABSENT || B.nodes[v].type == NT_NULL) raise(E_STAR, ib, ABSENT, ic);
               }
               break;
             case OP_LEAF:
               if (A) {
-                uint32_t v = s_cur[d][lane];
+                const uint32_t v = s_cur[d][lane];
                 bool ok;
                 if (v != ABSENT && B.nodes[v].type == NT_ARR) {
                   const Node an = B.nodes[v];
@@ -535,7 +623,7 @@ extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(DevPS P, 
               break;
             case OP_EXISTCHK:
               if (A) {
-                uint32_t v = s_cur[d][lane];
+                const uint32_t v = s_cur[d][lane];
                 if (v == ABSENT || B.nodes[v].type != NT_ARR) raise(E_EXIST_RESTYPE, ia, v, ic);
               }
               break;
@@ -577,7 +665,7 @@ extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(DevPS P, 
                   else wait = pc + 1;                       // found
                 }
                 if (cont) {
-                  uint32_t i = s_li[wv][aux] + 1;
+                  const uint32_t i = s_li[wv][aux] + 1;
                   if (i < s_llen[aux][lane]) {
                     s_cur[d + 1][lane] = s_lfirst[aux][lane] + i;
                   } else {
@@ -623,30 +711,28 @@ extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(DevPS P, 
           pc = next;
         }
       }
-      if (valid) {
-        if (O.full) {
-          size_t o = (size_t)ri * B.n_res + r;
-          O.status[o] = (uint8_t)st;
-          if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP)) {
-            ErrRec e;
-            e.kind_flags = ekind | (eflags << 16);
-            e.pnode = epn;
-            e.keynode = ekey;
-            e.resnode = eres;
-            e.idx[0] = eidx0; e.idx[1] = eidx1; e.idx[2] = eidx2; e.idx[3] = eidx3;
-            O.err[o] = e;
-          }
+      if (valid && (O.full & 1)) {
+        const size_t o = (size_t)ri * n_res + r;
+        O.status[o] = (uint8_t)st;
+        if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP)) {
+          ErrRec e;
+          e.kind_flags = ekind | (eflags << 16);
+          e.pnode = epn;
+          e.keynode = ekey;
+          e.resnode = eres;
+          e.idx[0] = eidx0; e.idx[1] = eidx1; e.idx[2] = eidx2; e.idx[3] = eidx3;
+          O.err[o] = e;
         }
       }
       // histogram: one LDS atomic per (wave, status) via ballot popcount
       for (uint32_t s = 0; s < 7; s++) {
-        uint64_t bm = __ballot(valid && st == s);
+        const uint64_t bm = __ballot(valid && st == s);
         if (bm && (lane % 64) == 0) atomicAdd(&s_hist[ri - rb][s], (uint32_t)__popcll(bm));
       }
     }
     __syncthreads();
     for (uint32_t q = lane; q < (re - rb) * KV_HIST; q += KV_WG) {
-      uint32_t v = (&s_hist[0][0])[q];
+      const uint32_t v = (&s_hist[0][0])[q];
       if (v) atomicAdd(&O.counts[(size_t)rb * KV_HIST + q], (unsigned long long)v);
     }
     __syncthreads();
@@ -654,11 +740,21 @@ extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(DevPS P, 
 }
 
 namespace kv {
-hipError_t launch_validate(const DevPS& P, const DevBatch& B, const DevOut& O, uint32_t rule_begin, uint32_t rule_end,
-                           hipStream_t stream) {
-  if (B.n_res == 0 || rule_end <= rule_begin) return hipSuccess;
-  dim3 grid((B.n_res + KV_WG - 1) / KV_WG);
-  hipLaunchKernelGGL(kv_validate_kernel, grid, dim3(KV_WG), 0, stream, P, B, O, rule_begin, rule_end);
+hipError_t launch_validate(const DevPS* P, const DevBatch* B, uint32_t n_res, const DevOut& O, uint32_t rule_begin,
+                           uint32_t rule_end, hipStream_t stream) {
+  if (n_res == 0 || rule_end <= rule_begin) return hipSuccess;
+  const uint32_t rblocks = (n_res + KV_WG - 1) / KV_WG;
+  const uint32_t nrules = rule_end - rule_begin;
+  // enough workgroups to fill 256 CUs several times over; each chunk re-reads
+  // its resources from L2, so chunks stay >= 8 rules
+  uint32_t n_chunks = (16384 + rblocks - 1) / rblocks;
+  uint32_t max_chunks = (nrules + 7) / 8;
+  if (n_chunks > max_chunks) n_chunks = max_chunks;
+  if (n_chunks < 1) n_chunks = 1;
+  const uint32_t rb8 = (rblocks + 7) / 8 * 8;
+  dim3 grid(rb8 * n_chunks);
+  hipLaunchKernelGGL(kv_validate_kernel, grid, dim3(KV_WG), 0, stream, P, B, O, rule_begin, rule_end, n_chunks,
+                     rblocks);
   return hipGetLastError();
 }
 }  // namespace kv
