@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--config", choices=["c2", "c3"], default="c2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=40_000)
+    ap.add_argument("--rule-filter", default="", help="diagnostics: regex over C2 rule names")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -74,6 +75,12 @@ def main():
 
     if args.config == "c2":
         pols = workloads.c2_policies()
+        if args.rule_filter:  # diagnostics only: evaluate a subset of the C2 rules
+            import re
+
+            rx = re.compile(args.rule_filter)
+            for p in pols:
+                p["spec"]["rules"] = [r for r in p["spec"]["rules"] if rx.search(r["name"])]
         kind_mix = 0
         workload = "C2: synthetic Pods x 100 validate.pattern rules (image globs, ?*, quantities, |-lists)"
     else:
