@@ -1,0 +1,30 @@
+#!/bin/bash
+# PMC counter passes (one rocprofv3 --pmc run per counter group), kernel-trace/stats only.
+set -o pipefail
+R="${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p "$R/gpurun_out/pmc"
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+cd /tmp
+ARGS="--no-cpu-baseline --steps 2 --warmup 0 --n-res ${NRES:-1000000} ${EXTRA}"
+i=0
+for grp in "FETCH_SIZE" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" \
+           "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
+           "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace --stats -d "$R/gpurun_out/pmc" -o pass$i --output-format csv -- \
+      python -u "$R/bench.py" $ARGS > "$R/gpurun_out/pmc/pass$i.json" 2> "$R/gpurun_out/pmc/pass$i.err" || { echo "pass $i failed"; exit 1; }
+done
+cd "$R"
+for f in $(find gpurun_out/pmc -name "*counter_collection.csv"); do echo "== $f"; python - "$f" <<'PY'
+import csv, sys, collections
+rows = list(csv.DictReader(open(sys.argv[1])))
+agg = collections.defaultdict(list)
+for r in rows:
+    if "kv_validate" in r.get("Kernel_Name", ""):
+        agg[(r["Dispatch_Id"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+per = collections.defaultdict(list)
+for (d, c), v in agg.items():
+    per[c].append(sum(v))
+for c, v in sorted(per.items()):
+    print(f"{c}: dispatches={len(v)} mean={sum(v)/len(v):.6g}")
+PY
+done
