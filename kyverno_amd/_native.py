@@ -11,7 +11,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkvgpu.so")
+# KVGPU_LIB: alternative in-tree build of the same library (A/B kernel experiments)
+LIB_PATH = os.environ.get("KVGPU_LIB") or os.path.join(_HERE, "libkvgpu.so")
 
 
 class NativeUnavailable(RuntimeError):

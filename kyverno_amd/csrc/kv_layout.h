@@ -4,22 +4,48 @@
 #pragma once
 #include <stdint.h>
 
+#if defined(__HIP__)
+#define KV_HD __host__ __device__
+#else
+#define KV_HD
+#endif
+
 namespace kv {
 
 // ---------------------------------------------------------------- resources
-// Node types (Go dynamic types of unstructured values)
-enum NodeType : uint32_t { NT_NULL = 0, NT_BOOL = 1, NT_INT = 2, NT_FLOAT = 3, NT_STR = 4, NT_MAP = 5, NT_ARR = 6 };
+// Node types (Go dynamic types of unstructured values). NT_ABSENT marks an
+// empty slot of a slot-addressed map (the resource lacks that pattern key).
+enum NodeType : uint32_t {
+  NT_NULL = 0, NT_BOOL = 1, NT_INT = 2, NT_FLOAT = 3, NT_STR = 4, NT_MAP = 5, NT_ARR = 6, NT_ABSENT = 7
+};
 
 constexpr uint32_t ABSENT = 0xFFFFFFFFu;  // "key not present" (Go: nil interface, ok=false)
 
-// One JSON value of a projected resource tree. Map children are contiguous
-// and sorted byte-lexicographically by key; array children contiguous in index order.
+// One JSON value of a projected resource tree (16 B).
+//   kt = key id << 4 | type (key id: this node's key in its parent map, KEY_NONE28 for array elements/roots)
+// Nodes live in rows of KV_LANES cells (wave-group layout): node index =
+// row * KV_LANES + lane, where lane = resource index % KV_LANES.
+//   MAP/ARR: a = ROW of the first child (the child block is shared by the group), b = child count
+//   scalars: a = Val id, b = e_off, c = e_len | NC_ASCII_E | NC_BOOLV | NC_NILLIKE (validateString form inline,
+//            so string globs need no Val load)
+// Map children are either slot-addressed (the map's projection-trie node has a
+// fixed, byte-sorted key list: child i is slot i, NT_ABSENT when missing) or,
+// for keep-all maps (metadata labels/annotations), every key sorted by bytes.
+// Array children are contiguous in index order.
 struct Node {
-  uint32_t key;   // key id of this node inside its parent map (kv::KEY_NONE for array elements / roots)
-  uint32_t type;  // NodeType
-  uint32_t a;     // MAP/ARR: first child index; scalar: value id; BOOL: 0/1
-  uint32_t b;     // MAP/ARR: child count
+  uint32_t kt;
+  uint32_t a;
+  uint32_t b;
+  uint32_t c;
 };
+constexpr uint32_t KEY_NONE28 = 0x0FFFFFFFu;
+constexpr uint32_t KV_LANES = 64;  // resources per node-row group (one wavefront)
+constexpr uint32_t NC_ASCII_E = 1u << 31;
+constexpr uint32_t NC_BOOLV = 1u << 30;
+constexpr uint32_t NC_NILLIKE = 1u << 29;  // validateValueWithNilPattern true (0, 0.0, "", false)
+constexpr uint32_t NC_LEN_MASK = 0x1FFFFFFFu;
+KV_HD inline uint32_t node_type(uint32_t kt) { return kt & 15u; }
+KV_HD inline uint32_t node_key(uint32_t kt) { return kt >> 4; }
 
 constexpr uint32_t KEY_NONE = 0xFFFFFFFFu;
 
@@ -53,7 +79,7 @@ enum ValFlags : uint32_t {
 
 // Per-resource header used by the match/exclude prefilter and as the tree root.
 struct Res {
-  uint32_t root;          // root node (a map for any real resource)
+  uint32_t root;          // ROW of the root node (node index root * KV_LANES + r % KV_LANES)
   uint32_t kind;          // key-dictionary id of .kind (KEY_NONE if not in dictionary)
   uint32_t group, version;// dictionary ids of the apiVersion group / version
   uint32_t name_off, name_len;
@@ -128,6 +154,10 @@ enum Op : uint32_t {
   OP_ALT_END,     // anyPattern alternative end: PASS lanes finish
   OP_DONE,        // program end
 };
+
+// Key-lookup ops (KEY, KEYV, AREG, NEG): `a` is the slot index of the key in
+// the parent map's slot list, or (aux & AUX_SCAN) the key id for a keep-all map.
+constexpr uint32_t AUX_SCAN = 0x80;
 
 struct Inst {
   uint32_t op;     // Op | (depth << 8) | (aux << 16)

@@ -309,7 +309,7 @@ std::string render_path(const PolicySet& ps, const Batch& b, const ErrRec& e) {
       case SEG_CONST_INDEX: segs.push_back(std::to_string(n.level)); break;
       case SEG_RESOLVED: {
         if (e.keynode != ABSENT && e.keynode < b.nodes.size()) {
-          uint32_t k = b.nodes[e.keynode].key;
+          uint32_t k = node_key(b.nodes[e.keynode].kt);
           segs.push_back(k < ps.keys.size() ? ps.keys[k] : b.dyn_keys[k - ps.keys.size()]);
         } else {
           segs.push_back(n.key);

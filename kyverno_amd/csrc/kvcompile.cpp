@@ -741,7 +741,12 @@ struct Compiler {
   }
 
   // validateResourceElement(cur[d], P) ; errors -> catch scope
-  void elem(const PV& P, uint32_t d, uint32_t pn, uint32_t cs, int expand_tag = 0) {
+  // slot fixups of this rule's key-lookup ops: (pc, trie node of the map, key)
+  std::vector<std::tuple<uint32_t, uint32_t, std::string>> slot_fix;
+  void lookup_fix(uint32_t pc, uint32_t t, const std::string& k) { slot_fix.emplace_back(pc, t, k); }
+
+  // validateResourceElement(cur[d], P); t = projection-trie node of cur[d]
+  void elem(const PV& P, uint32_t d, uint32_t pn, uint32_t cs, uint32_t t, int expand_tag = 0) {
     if (d >= 30) { cpu_reason = "pattern too deep"; return; }
     if (P.t == J_MAP) {
       emit(OP_MAPCHK, d, 0, pn, 0, cs);
@@ -759,7 +764,8 @@ struct Compiler {
           } else {
             bit = it->second;
           }
-          emit(OP_AREG, d, bit, key(remove_anchor(k, nullptr)), 0, 0xFFFFFFFFu);
+          uint32_t apc = emit(OP_AREG, d, bit, key(remove_anchor(k, nullptr)), 0, 0xFFFFFFFFu);
+          lookup_fix(apc, t, remove_anchor(k, nullptr));
         }
       }
       // ExpandInMetadata site: this map has a key whose anchor-free form is "metadata"
@@ -786,7 +792,7 @@ struct Compiler {
         }
         if (rule_flags & RR_META_EXPAND) emit(OP_METACHK, d, 0, 0, 0, cs);
       }
-      children(P, d, pn, cs, meta, expand_tag);
+      children(P, d, pn, cs, meta, expand_tag, t);
       return;
     }
     if (P.t == J_ARR) {
@@ -803,7 +809,7 @@ struct Compiler {
         uint32_t epn = pnode(pn, SEG_LOOP, L, "");
         uint32_t b = emit(OP_LOOP_BEGIN, d, L, 0, 0, 0xFFFFFFFFu);
         array_ctx++;
-        elem(p0, d + 1, epn, s);
+        elem(p0, d + 1, epn, s, ps.trie.elem(t));
         array_ctx--;
         uint32_t e = emit(OP_LOOP_END, d, L, b, 0, cs);
         ps.prog[b].a = e;
@@ -822,7 +828,7 @@ struct Compiler {
         emit(OP_INDEX, d, 0, (uint32_t)i, 0, 0xFFFFFFFFu);
         uint32_t ipn = pnode(pn, SEG_CONST_INDEX, (uint32_t)i, "");
         array_ctx++;
-        elem(P.a[i], d + 1, ipn, s);
+        elem(P.a[i], d + 1, ipn, s, ps.trie.elem(t));
         array_ctx--;
         uint32_t e = emit(OP_POS_END, d, 0, 0, 0, cs);
         end_scope(s, e);
@@ -832,7 +838,7 @@ struct Compiler {
     emit(OP_LEAF, d, 0, pred(P), pn, cs);
   }
 
-  void children(const PV& P, uint32_t d, uint32_t pn, uint32_t cs, int meta_idx, int expand_tag) {
+  void children(const PV& P, uint32_t d, uint32_t pn, uint32_t cs, int meta_idx, int expand_tag, uint32_t t) {
     std::vector<size_t> order = canonical_children(P);
     // Label/annotation map below an ExpandInMetadata site: wildcard keys are
     // resolved per resource (OP_KEYGLOB) and a later canonical sibling that
@@ -861,9 +867,9 @@ struct Compiler {
         std::string ak = remove_anchor(k, nullptr);
         uint32_t cpn = pnode(pn, wildkey ? SEG_RESOLVED : SEG_KEY, 0, ak);
         uint32_t s = new_scope();
-        uint32_t kpc = key_op(d, ak, wildkey, true);
+        uint32_t kpc = key_op(d, ak, wildkey, true, t);
         skip_fix.push_back({kpc, s});
-        elem(Pk, d + 1, cpn, s, child_tag);
+        elem(Pk, d + 1, cpn, s, ps.trie.child(t, ak), child_tag);
         uint32_t e = emit(OP_SCOPE_END, d, global ? EF_GLOBAL : EF_COND, 0, 0, cs);
         end_scope(s, e);
       } else if (is_existence_anchor(k)) {
@@ -871,9 +877,10 @@ struct Compiler {
         if (wildkey) { cpu_reason = "anchored wildcard metadata key"; break; }
         uint32_t cpn = pnode(pn, SEG_KEY, 0, ak);
         uint32_t s = new_scope();
-        uint32_t kpc = key_op(d, ak, false, true);
+        uint32_t kpc = key_op(d, ak, false, true, t);
         skip_fix.push_back({kpc, s});
         emit(OP_EXISTCHK, d + 1, 0, cpn, 0, cs);
+        const uint32_t et = ps.trie.elem(ps.trie.child(t, ak));
         if (Pk.t != J_ARR) {
           emit(OP_RAISE, d + 1, 0, cpn, E_EXIST_PATLIST, cs);
         } else {
@@ -888,7 +895,7 @@ struct Compiler {
             uint32_t epn = pnode(cpn, SEG_LOOP, L, "");
             uint32_t b = emit(OP_EXIST_BEGIN, d + 1, L, 0, cpn, cs);
             array_ctx++;
-            elem(pm, d + 2, epn, es);
+            elem(pm, d + 2, epn, es, et);
             array_ctx--;
             uint32_t e = emit(OP_EXIST_END, d + 1, L, b, cpn, cs);
             ps.prog[b].a = e;
@@ -902,31 +909,31 @@ struct Compiler {
         std::string ak = remove_anchor(k, nullptr);
         uint32_t cpn = pnode(pn, wildkey ? SEG_RESOLVED : SEG_KEY, 0, ak);
         uint32_t s = new_scope();
-        uint32_t kpc = key_op(d, ak, wildkey, true);
+        uint32_t kpc = key_op(d, ak, wildkey, true, t);
         skip_fix.push_back({kpc, s});
-        elem(Pk, d + 1, cpn, cs, child_tag);
+        elem(Pk, d + 1, cpn, cs, ps.trie.child(t, ak), child_tag);
         uint32_t e = emit(OP_SCOPE_END, d, 0, 0, 0, 0xFFFFFFFFu);
         end_scope(s, e);
       } else if (is_negation_anchor(k)) {
         std::string ak = remove_anchor(k, nullptr);
         if (wildkey) { cpu_reason = "anchored wildcard metadata key"; break; }
         uint32_t cpn = pnode(pn, SEG_KEY, 0, ak);
-        emit(OP_NEG, d, 0, key(ak), cpn, cs);
+        lookup_fix(emit(OP_NEG, d, 0, key(ak), cpn, cs), t, ak);
         if (kg) pending_keyglob.push_back(0xFFFFFFFFu);  // keeps sibling numbering aligned
       } else {
         uint32_t cpn = pnode(pn, wildkey ? SEG_RESOLVED : SEG_KEY, 0, k);
         if (kg) {
           uint32_t s = new_scope();
-          uint32_t kpc = key_op(d, k, wildkey, false);
+          uint32_t kpc = key_op(d, k, wildkey, false, t);
           skip_fix.push_back({kpc, s});
           if (Pk.t == J_STR && Pk.s == "*") emit(OP_STAR, d, 0, 0, pn, cs);
-          else elem(Pk, d + 1, cpn, cs, child_tag);
+          else elem(Pk, d + 1, cpn, cs, ps.trie.child(t, k), child_tag);
           uint32_t e = emit(OP_SCOPE_END, d, 0, 0, 0, 0xFFFFFFFFu);
           end_scope(s, e);
         } else {
-          emit(OP_KEYV, d, 0, key(k), 0, 0xFFFFFFFFu);
+          lookup_fix(emit(OP_KEYV, d, 0, key(k), 0, 0xFFFFFFFFu), t, k);
           if (Pk.t == J_STR && Pk.s == "*") emit(OP_STAR, d, 0, 0, pn, cs);
-          else elem(Pk, d + 1, cpn, cs, child_tag);
+          else elem(Pk, d + 1, cpn, cs, ps.trie.child(t, k), child_tag);
         }
       }
       if (!cpu_reason.empty()) break;
@@ -974,8 +981,12 @@ struct Compiler {
   }
 
   // Key lookup op (absent -> skip target when skip_absent; patched by caller).
-  uint32_t key_op(uint32_t d, const std::string& ak, bool wild, bool skip_absent) {
-    if (!in_label_map_with_wild) return emit(skip_absent ? OP_KEY : OP_KEYV, d, 0, key(ak), 0, 0xFFFFFFFFu);
+  uint32_t key_op(uint32_t d, const std::string& ak, bool wild, bool skip_absent, uint32_t t) {
+    if (!in_label_map_with_wild) {
+      uint32_t pc = emit(skip_absent ? OP_KEY : OP_KEYV, d, 0, key(ak), 0, 0xFFFFFFFFu);
+      lookup_fix(pc, t, ak);
+      return pc;
+    }
     // OP_KEYGLOB: a = atom (glob, AT_FALSE for a literal sibling), b = skip target, c = literal key id
     uint32_t at = glob_atom(wild ? ak : std::string());
     if (!wild) ps.atoms[at].kind = AT_FALSE;
@@ -1231,6 +1242,7 @@ static bool compile_pattern_program(Compiler& C, const std::vector<PV>& patterns
   C.skip_fix.clear();
   C.cpu_reason.clear();
   C.rule_flags = 0;
+  C.slot_fix.clear();
   uint32_t root_scope = C.new_scope();
   for (size_t ai = 0; ai < patterns.size(); ai++) {
     C.anchor_bits = 0;
@@ -1242,7 +1254,8 @@ static bool compile_pattern_program(Compiler& C, const std::vector<PV>& patterns
     uint32_t root = C.pnode(0xFFFFFFFFu, SEG_ROOT, 0, "");
     if (any) rh.alt_roots.push_back(root);
     else rh.root_pnode = root;
-    C.elem(patterns[ai], 0, root, alt_scope);
+    C.trie_of(patterns[ai], 0);  // before emission: key ops resolve their trie slots
+    C.elem(patterns[ai], 0, root, alt_scope, 0);
     if (!C.cpu_reason.empty()) {
       ps.prog.resize(rr.prog);
       rh.route_reason = C.cpu_reason;
@@ -1252,13 +1265,13 @@ static bool compile_pattern_program(Compiler& C, const std::vector<PV>& patterns
       uint32_t e = C.emit(OP_ALT_END, 0, 0, (uint32_t)ai, ai + 1 == patterns.size() ? 1u : 0u, 0xFFFFFFFFu);
       C.end_scope(alt_scope, e);
     }
-    C.trie_of(patterns[ai], 0);
   }
   uint32_t done = C.emit(OP_DONE, 0, 0, 0, 0, 0xFFFFFFFFu);
   C.end_scope(root_scope, done);
   for (auto& f : C.catch_fix) ps.prog[f.first].c = C.scopes[f.second].end_pc;
   for (auto& f : C.skip_fix) ps.prog[f.first].b = C.scopes[f.second].end_pc;
   rr.flags |= C.rule_flags;
+  for (auto& f : C.slot_fix) ps.slot_fix.push_back(f);
   return true;
 }
 
@@ -1374,6 +1387,24 @@ void compile_policies(const char* json, size_t len, PolicySet* ps) {
       }
     }
     ps->policy_rule_count.push_back(nrules);
+  }
+  // Slot-addressed map layout: every non-keep-all trie node gets a byte-sorted
+  // key list; key-lookup ops get the slot index (keep-all maps: key id + AUX_SCAN).
+  for (auto& tn : ps->trie.nodes) {
+    for (auto& kv : tn.kids) tn.slot_keys.push_back(kv.first);
+    std::sort(tn.slot_keys.begin(), tn.slot_keys.end());
+    for (uint32_t i = 0; i < tn.slot_keys.size(); i++) tn.slot.emplace(tn.slot_keys[i], i);
+  }
+  for (auto& f : ps->slot_fix) {
+    Inst& in = ps->prog[std::get<0>(f)];
+    const Trie::N& tn = ps->trie.nodes[std::get<1>(f)];
+    if (tn.keep_all) {
+      in.op |= AUX_SCAN << 16;
+      continue;
+    }
+    auto it = tn.slot.find(std::get<2>(f));
+    if (it == tn.slot.end()) throw std::runtime_error("compiler: key missing from projection trie: " + std::get<2>(f));
+    in.a = it->second;
   }
 }
 

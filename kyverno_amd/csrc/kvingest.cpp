@@ -30,8 +30,9 @@ struct Ingest {
   std::unordered_map<std::string, uint32_t> dyn_key;   // batch-local key ids
   std::unordered_map<std::string, uint32_t> ns_index;
   uint32_t nstatic;
+  std::vector<std::vector<uint32_t>> slot_ids;  // per trie node: key ids of its slots
 
-  Ingest(const PolicySet& p, Batch& bb) : ps(p), b(bb), nstatic((uint32_t)p.keys.size()) {
+  Ingest(const PolicySet& p, Batch& bb) : ps(p), b(bb), nstatic((uint32_t)p.keys.size()), slot_ids(p.trie.nodes.size()) {
     // offset 0 holds "0": convertNumberToString(nil) for the device glob (kvkernel.hip atom_eval)
     str("0");
   }
@@ -55,6 +56,7 @@ struct Ingest {
     auto it = dyn_key.find(ks);
     if (it != dyn_key.end()) return it->second;
     uint32_t nid = nstatic + (uint32_t)b.dyn_keys.size();
+    if (nid >= KEY_NONE28) throw std::runtime_error("ingest: too many distinct keys in one batch");
     b.dyn_keys.push_back(ks);
     dyn_key.emplace(ks, nid);
     return nid;
@@ -129,54 +131,160 @@ struct Ingest {
     return id;
   }
 
-  // Fill node `slot` from JSON node jn projected through trie node t (-1: leaf only)
-  void fill(const JDoc& d, uint32_t jn, int32_t t, uint32_t slot, uint32_t key) {
+  // ---------------------------------------------------------------- wave-group layout
+  // Resources are laid out in groups of KV_LANES (one wavefront): the group's
+  // nodes form rows of KV_LANES cells, cell (row, lane) = node of resource
+  // 64*g + lane. Rows follow the union shape of the group's projected trees
+  // (slot-addressed maps share a fixed slot block; arrays get max-length element
+  // blocks; keep-all maps max-count blocks), so one logical position has the
+  // same row in every lane and the device's uniform-pc walk reads whole rows
+  // (coalesced) instead of 64 scattered nodes. Node index = row * 64 + lane.
+  struct Shape {
+    int32_t t = -1;            // projection-trie node (-1: leaf-only)
+    uint32_t row = 0;          // row within the group
+    bool has_map = false, has_arr = false, keep_all = false;
+    uint32_t map_row = 0, arr_row = 0;
+    std::vector<Shape> kids;   // map block (slot-addressed: one per slot key; keep-all: max count)
+    std::vector<Shape> elems;  // array block (max length)
+  };
+
+  void sorted_children(const JDoc& d, const JNode& n, std::vector<uint32_t>* out) {
+    out->clear();
+    for (uint32_t c = n.first; c < n.first + n.count; c++) out->push_back(c);
+    std::sort(out->begin(), out->end(), [&](uint32_t x, uint32_t y) { return d.key(d.at(x)) < d.key(d.at(y)); });
+  }
+
+  void unite(Shape& s, const JDoc& d, uint32_t jn) {
     const JNode& n = d.at(jn);
-    Node out{key, NT_NULL, 0, 0};
+    if (n.t == J_MAP) {
+      if (s.t < 0) return;
+      const Trie::N& tn = ps.trie.nodes[s.t];
+      if (!s.has_map) {
+        s.has_map = true;
+        s.keep_all = tn.keep_all;
+        if (!tn.keep_all) {
+          s.kids.resize(tn.slot_keys.size());
+          for (size_t i = 0; i < tn.slot_keys.size(); i++) s.kids[i].t = (int32_t)tn.kids.at(tn.slot_keys[i]);
+        }
+      }
+      if (tn.keep_all) {
+        if (s.kids.size() < n.count) s.kids.resize(n.count);  // children leaf-only (t = -1)
+        std::vector<uint32_t> ch;
+        sorted_children(d, n, &ch);
+        for (size_t i = 0; i < ch.size(); i++) unite(s.kids[i], d, ch[i]);
+      } else {
+        for (uint32_t c = n.first; c < n.first + n.count; c++) {
+          auto it = tn.slot.find(std::string(d.key(d.at(c))));
+          if (it != tn.slot.end()) unite(s.kids[it->second], d, c);
+        }
+      }
+    } else if (n.t == J_ARR) {
+      s.has_arr = true;
+      const int32_t et = s.t >= 0 ? ps.trie.nodes[s.t].elem : -1;
+      if (s.elems.size() < n.count) {
+        size_t old = s.elems.size();
+        s.elems.resize(n.count);
+        for (size_t j = old; j < n.count; j++) s.elems[j].t = et;
+      }
+      for (uint32_t j = 0; j < n.count; j++) unite(s.elems[j], d, n.first + j);
+    }
+  }
+
+  void assign(Shape& s, uint32_t* next) {
+    if (s.has_map) {
+      s.map_row = *next;
+      *next += (uint32_t)s.kids.size();
+      for (size_t i = 0; i < s.kids.size(); i++) s.kids[i].row = s.map_row + (uint32_t)i;
+    }
+    if (s.has_arr) {
+      s.arr_row = *next;
+      *next += (uint32_t)s.elems.size();
+      for (size_t j = 0; j < s.elems.size(); j++) s.elems[j].row = s.arr_row + (uint32_t)j;
+    }
+    for (auto& k : s.kids) assign(k, next);
+    for (auto& e : s.elems) assign(e, next);
+  }
+
+  Node scalar(const JDoc& d, const JNode& n, uint32_t type, uint32_t key) {
+    const uint32_t vid = val(d, n);
+    const Val& v = b.vals[vid];
+    Node out{(key & KEY_NONE28) << 4 | type, vid, v.e_off, v.e_len};
+    if (v.e_len > NC_LEN_MASK) throw std::runtime_error("ingest: string value too long");
+    if (v.flags & VF_ASCII_E) out.c |= NC_ASCII_E;
+    if (v.flags & VF_BOOLV) out.c |= NC_BOOLV;
+    if (v.flags & VF_NILLIKE) out.c |= NC_NILLIKE;
+    return out;
+  }
+
+  uint64_t base_row = 0;  // first row of the current group
+  Node& cell(uint32_t row, uint32_t lane) { return b.nodes[(size_t)(base_row + row) * KV_LANES + lane]; }
+
+  // Write lane's value at shape position s (key = key id in the parent map)
+  void put(const Shape& s, const JDoc& d, uint32_t jn, uint32_t lane, uint32_t key) {
+    const JNode& n = d.at(jn);
+    Node out{(key & KEY_NONE28) << 4 | NT_NULL, 0, 0, 0};
     switch (n.t) {
-      case J_NULL: out.type = NT_NULL; break;
-      case J_BOOL: out.type = NT_BOOL; out.a = val(d, n); out.b = n.b ? 1 : 0; break;
-      case J_INT: out.type = NT_INT; out.a = val(d, n); break;
-      case J_FLOAT: out.type = NT_FLOAT; out.a = val(d, n); break;
-      case J_STR: out.type = NT_STR; out.a = val(d, n); break;
+      case J_NULL: break;
+      case J_BOOL: out = scalar(d, n, NT_BOOL, key); break;
+      case J_INT: out = scalar(d, n, NT_INT, key); break;
+      case J_FLOAT: out = scalar(d, n, NT_FLOAT, key); break;
+      case J_STR: out = scalar(d, n, NT_STR, key); break;
       case J_MAP: {
-        out.type = NT_MAP;
-        if (t >= 0) {
-          const Trie::N& tn = ps.trie.nodes[t];
-          std::vector<std::pair<std::string_view, uint32_t>> kept;  // key, json child
-          std::vector<int32_t> ktrie;
+        out.kt = (key & KEY_NONE28) << 4 | NT_MAP;
+        if (s.t < 0) break;
+        const Trie::N& tn = ps.trie.nodes[s.t];
+        out.a = (uint32_t)(base_row + s.map_row);
+        if (tn.keep_all) {
+          out.b = n.count;
+          std::vector<uint32_t> ch;
+          sorted_children(d, n, &ch);
+          for (size_t i = 0; i < ch.size(); i++) put(s.kids[i], d, ch[i], lane, key_of(d.key(d.at(ch[i]))));
+        } else {
+          const uint32_t K = (uint32_t)tn.slot_keys.size();
+          out.b = K;
+          auto& ids = slot_ids[s.t];
+          for (uint32_t i = (uint32_t)ids.size(); i < K; i++) ids.push_back(key_of(tn.slot_keys[i]));
+          for (uint32_t i = 0; i < K; i++) cell(s.map_row + i, lane) = Node{(ids[i] & KEY_NONE28) << 4 | NT_ABSENT, 0, 0, 0};
           for (uint32_t c = n.first; c < n.first + n.count; c++) {
-            std::string_view k = d.key(d.at(c));
-            auto it = tn.kids.find(std::string(k));
-            if (it != tn.kids.end()) { kept.push_back({k, c}); ktrie.push_back((int32_t)it->second); }
-            else if (tn.keep_all) { kept.push_back({k, c}); ktrie.push_back(-1); }
-          }
-          std::vector<size_t> ord(kept.size());
-          for (size_t i = 0; i < ord.size(); i++) ord[i] = i;
-          std::sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return kept[x].first < kept[y].first; });
-          uint32_t first = (uint32_t)b.nodes.size();
-          b.nodes.resize(b.nodes.size() + kept.size());
-          out.a = first;
-          out.b = (uint32_t)kept.size();
-          for (size_t i = 0; i < ord.size(); i++) {
-            size_t x = ord[i];
-            fill(d, kept[x].second, ktrie[x], first + (uint32_t)i, key_of(kept[x].first));
+            auto it = tn.slot.find(std::string(d.key(d.at(c))));
+            if (it != tn.slot.end()) put(s.kids[it->second], d, c, lane, ids[it->second]);
           }
         }
         break;
       }
       case J_ARR: {
-        out.type = NT_ARR;
-        int32_t et = t >= 0 ? ps.trie.nodes[t].elem : -1;
-        uint32_t first = (uint32_t)b.nodes.size();
-        b.nodes.resize(b.nodes.size() + n.count);
-        out.a = first;
+        out.kt = (key & KEY_NONE28) << 4 | NT_ARR;
+        out.a = (uint32_t)(base_row + s.arr_row);
         out.b = n.count;
-        for (uint32_t i = 0; i < n.count; i++) fill(d, n.first + i, et, first + i, KEY_NONE);
+        for (uint32_t j = 0; j < n.count; j++) put(s.elems[j], d, n.first + j, lane, KEY_NONE);
         break;
       }
     }
-    b.nodes[slot] = out;
+    cell(s.row, lane) = out;
+  }
+
+  std::vector<JDoc> group;
+  uint32_t group_n = 0;
+
+  void flush_group() {
+    if (group_n == 0) return;
+    Shape root;
+    root.t = 0;
+    for (uint32_t l = 0; l < group_n; l++) unite(root, group[l], group[l].root);
+    uint32_t rows = 1;
+    root.row = 0;
+    assign(root, &rows);
+    base_row = b.n_rows;
+    b.n_rows += rows;
+    if (b.n_rows * KV_LANES >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: batch too large for 32-bit node indices");
+    b.nodes.resize((size_t)b.n_rows * KV_LANES, Node{NT_NULL, 0, 0, 0});
+    for (uint32_t l = 0; l < group_n; l++) {
+      put(root, group[l], group[l].root, l, KEY_NONE);
+      b.res[b.res.size() - group_n + l].root = (uint32_t)base_row;
+    }
+    for (size_t c = (size_t)base_row * KV_LANES; c < b.nodes.size(); c++)
+      if (b.nodes[c].kt | b.nodes[c].a | b.nodes[c].b | b.nodes[c].c) b.cells_used++;
+    group_n = 0;
   }
 
   static bool is_str_map(const JDoc& d, const JNode& m) {
@@ -228,7 +336,7 @@ struct Ingest {
     *count = (uint32_t)pairs.size();
   }
 
-  void add(const JDoc& d) {
+  void add(const JDoc& d) {  // per-resource header (match/exclude inputs)
     const JNode& root = d.at(d.root);
     Res r{};
     if (root.t != J_MAP) throw std::runtime_error("ingest: resource is not a JSON object");
@@ -277,11 +385,14 @@ struct Ingest {
     if (d.strs.find("conditional anchor mismatch") != std::string::npos ||
         d.strs.find("global anchor mismatch") != std::string::npos)
       r.flags |= RF_MAGIC;
-    uint32_t slot = (uint32_t)b.nodes.size();
-    b.nodes.emplace_back();
-    r.root = slot;
-    fill(d, d.root, 0, slot, KEY_NONE);
-    b.res.push_back(r);
+    b.res.push_back(r);  // root row assigned by flush_group
+  }
+
+  void take(JDoc& d) {
+    if (group.size() < KV_LANES) group.resize(KV_LANES);
+    add(d);
+    std::swap(group[group_n++], d);
+    if (group_n == KV_LANES) flush_group();
   }
 };
 
@@ -289,7 +400,8 @@ struct Ingest {
 
 void ingest_resources(const PolicySet& ps, const char* json, size_t len, const char* ns_labels_json, Batch* b) {
   Ingest in(ps, *b);
-  parse_json_stream(json, len, NUM_UNSTRUCTURED, [&](const JDoc& d) { in.add(d); });
+  parse_json_stream(json, len, NUM_UNSTRUCTURED, [&](JDoc& d) { in.take(d); });
+  in.flush_group();
   // namespace labels (CLI --values-file namespaceSelector map / cluster namespaces)
   b->ns_labels.assign(b->namespaces.size(), {});
   if (ns_labels_json && *ns_labels_json) {
@@ -317,7 +429,8 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
       if (selector_eval_host(ps.nsselectors[s], b->ns_labels[n]) == 1) b->ns_bits[n * b->ns_words + s / 32] |= 1u << (s % 32);
   // word-granular readers may touch up to 8 bytes past the last string
   b->strs.append(16, '\0');
-  b->bytes_referenced = b->nodes.size() * sizeof(Node) + b->vals.size() * sizeof(Val) + b->res.size() * sizeof(Res) +
+  // algorithmic bytes: populated cells only (row padding of the wave-group layout excluded)
+  b->bytes_referenced = b->cells_used * sizeof(Node) + b->vals.size() * sizeof(Val) + b->res.size() * sizeof(Res) +
                         b->kvs.size() * sizeof(KV) + b->strs.size();
 }
 

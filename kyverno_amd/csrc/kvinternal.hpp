@@ -2,6 +2,7 @@
 #pragma once
 #include <cstdint>
 #include <string>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
@@ -45,6 +46,10 @@ struct Trie {
     int32_t elem = -1;
     bool keep_all = false;   // keep every child (labels/annotations with wildcard keys)
     bool keep_subtree = false;
+    // slot-addressed layout (finalize_slots): kid keys sorted by bytes; a
+    // resource map at this trie node stores child i in slot i (NT_ABSENT if missing)
+    std::vector<std::string> slot_keys;
+    std::unordered_map<std::string, uint32_t> slot;
   };
   std::vector<N> nodes;
   Trie() { nodes.emplace_back(); }
@@ -137,6 +142,7 @@ struct PolicySet {
   std::vector<SelectorHost> nsselectors;  // bit i of the namespace table
   std::vector<PNodeInfo> pnodes;
   Trie trie;
+  std::vector<std::tuple<uint32_t, uint32_t, std::string>> slot_fix;  // (pc, trie node, key)
   uint32_t max_depth = 0, max_loops = 0;
   std::string flags_info;
 };
@@ -147,7 +153,9 @@ void compile_policies(const char* json, size_t len, PolicySet* ps);
 
 // Ingested batch (host mirror of the HBM store)
 struct Batch {
-  std::vector<kv::Node> nodes;
+  std::vector<kv::Node> nodes;       // [n_rows][KV_LANES] (wave-group layout, kvingest.cpp)
+  uint64_t n_rows = 0;
+  uint64_t cells_used = 0;           // populated cells (incl. absent-slot markers)
   std::vector<kv::Val> vals;
   std::vector<kv::Res> res;
   std::vector<kv::KV> kvs;

@@ -32,6 +32,9 @@ using namespace kv;
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// node index of this lane's cell in a row (wave-group layout, kv_layout.h)
+__device__ __forceinline__ uint32_t ni(uint32_t row) { return row * KV_LANES + (threadIdx.x & (KV_LANES - 1)); }
+
 __device__ __forceinline__ uint32_t rune_len(uint8_t c) {
   return c < 0x80 ? 1u : c >= 0xF0 ? 4u : c >= 0xE0 ? 3u : c >= 0xC0 ? 2u : 1u;
 }
@@ -154,22 +157,22 @@ __device__ __forceinline__ bool cmp_ok(uint32_t op, int r) {
   }
 }
 
-// one atom of a string pattern against the value at `node` (ABSENT/NULL == Go nil)
-__device__ bool atom_eval(const DevPS& P, const DevBatch& B, uint32_t ai, uint32_t type, uint32_t vid) {
+// one atom of a string pattern against a scalar/absent node (type NT_NULL == Go nil)
+__device__ bool atom_eval(const DevPS& P, const DevBatch& B, uint32_t ai, uint32_t type, const Node& n) {
   const Atom& A = P.atoms[ai];
   const uint32_t kind = uni(A.kind);
   if (kind == AT_FALSE) return false;
   if (type == NT_MAP || type == NT_ARR) return false;
   if (kind == AT_GLOB_E) {
     if (type == NT_NULL) return false;
-    const Val& v = B.vals[vid];
-    bool r = glob_atom(P, A, B.bstr + v.e_off, v.e_len, v.flags & VF_ASCII_E);
+    bool r = glob_atom(P, A, B.bstr + n.b, n.c & NC_LEN_MASK, n.c & NC_ASCII_E);
     return uni(A.op) == CO_NE ? !r : r;
   }
   if (type == NT_BOOL) return false;
   if (kind == AT_GLOB_N) {
     if (type == NT_NULL) return glob_atom(P, A, B.bstr, 1, true);  // convertNumberToString(nil) == "0" (bstr[0..1))
-    const Val& v = B.vals[vid];
+    if (type != NT_FLOAT) return glob_atom(P, A, B.bstr + n.b, n.c & NC_LEN_MASK, n.c & NC_ASCII_E);  // == e-form
+    const Val& v = B.vals[n.a];
     return glob_atom(P, A, B.bstr + v.n_off, v.n_len, v.flags & VF_ASCII_N);
   }
   // AT_QCMP
@@ -177,31 +180,25 @@ __device__ bool atom_eval(const DevPS& P, const DevBatch& B, uint32_t ai, uint32
   if (type == NT_NULL) {
     r = q_cmp(VF_Q_ZERO, 0, 0, 0, A.q_flags, A.q_exp, A.q_hi, A.q_lo);
   } else {
-    const Val& v = B.vals[vid];
+    const Val& v = B.vals[n.a];
     if (!(v.flags & VF_Q_VALID)) return false;
     r = q_cmp(v.flags, v.q_exp, v.q_hi, v.q_lo, A.q_flags, A.q_exp, A.q_hi, A.q_lo);
   }
   return cmp_ok(uni(A.op), r);
 }
 
-// ValidateValueWithPattern(value, pattern) for a scalar-pattern leaf
-__device__ bool pred_eval(const DevPS& P, const DevBatch& B, uint32_t pi, uint32_t node) {
+// ValidateValueWithPattern(value, pattern) for a scalar-pattern leaf; n = the
+// value node (ignored when type == NT_NULL, which also stands for absent)
+__device__ bool pred_eval(const DevPS& P, const DevBatch& B, uint32_t pi, uint32_t type, const Node& n) {
   const Pred& pr = P.preds[pi];
   const uint32_t kind = uni(pr.kind);
-  uint32_t type = NT_NULL, va = 0, vb = 0;
-  if (node != ABSENT) {
-    const Node n = B.nodes[node];
-    type = n.type;
-    va = n.a;
-    vb = n.b;
-  }
   switch (kind) {
-    case PK_BOOL: return type == NT_BOOL && vb == uni(pr.flags);
+    case PK_BOOL: return type == NT_BOOL && ((n.c & NC_BOOLV) ? 1u : 0u) == uni(pr.flags);
     case PK_FLOAT: {
-      if (type == NT_INT) return uni(pr.flags) && B.vals[va].i == pr.fi;
-      if (type == NT_FLOAT) return B.vals[va].f == pr.f;
+      if (type == NT_INT) return uni(pr.flags) && B.vals[n.a].i == pr.fi;
+      if (type == NT_FLOAT) return B.vals[n.a].f == pr.f;
       if (type == NT_STR) {
-        const Val& v = B.vals[va];
+        const Val& v = B.vals[n.a];
         return (v.flags & VF_PF_OK) && v.f == pr.f;
       }
       return false;
@@ -209,7 +206,7 @@ __device__ bool pred_eval(const DevPS& P, const DevBatch& B, uint32_t pi, uint32
     case PK_NIL:
       if (type == NT_NULL) return true;
       if (type == NT_MAP || type == NT_ARR) return false;
-      return (B.vals[va].flags & VF_NILLIKE) != 0;
+      return (n.c & NC_NILLIKE) != 0;
     case PK_MAPTYPE: return type == NT_MAP;
     case PK_STRING: {
       const uint32_t af = uni(pr.first), an = uni(pr.count);
@@ -220,9 +217,9 @@ __device__ bool pred_eval(const DevPS& P, const DevBatch& B, uint32_t pi, uint32
         for (uint32_t c = cf; c < cf + cn && all; c++) {
           const Conj& cj = P.conjs[c];
           const uint32_t ck = uni(cj.kind);
-          bool r = atom_eval(P, B, uni(cj.a0), type, va);
-          if (ck == CJ_INRANGE) r = r && atom_eval(P, B, uni(cj.a1), type, va);
-          else if (ck == CJ_NOTINRANGE) r = r || atom_eval(P, B, uni(cj.a1), type, va);
+          bool r = atom_eval(P, B, uni(cj.a0), type, n);
+          if (ck == CJ_INRANGE) r = r && atom_eval(P, B, uni(cj.a1), type, n);
+          else if (ck == CJ_NOTINRANGE) r = r || atom_eval(P, B, uni(cj.a1), type, n);
           all = r;
         }
         if (all) return true;
@@ -233,13 +230,30 @@ __device__ bool pred_eval(const DevPS& P, const DevBatch& B, uint32_t pi, uint32
   }
 }
 
+__device__ __forceinline__ bool pred_node(const DevPS& P, const DevBatch& B, uint32_t pi, uint32_t node) {
+  Node n{NT_NULL, 0, 0, 0};
+  if (node != ABSENT) n = B.nodes[node];
+  return pred_eval(P, B, pi, node_type(n.kt), n);
+}
+
+// keep-all map (labels/annotations): scan for key id
 __device__ __forceinline__ uint32_t lookup(const DevBatch& B, uint32_t m, uint32_t key) {
   if (m == ABSENT) return ABSENT;
   const Node n = B.nodes[m];
-  if (n.type != NT_MAP) return ABSENT;
+  if (node_type(n.kt) != NT_MAP) return ABSENT;
   for (uint32_t i = 0; i < n.b; i++)
-    if (B.nodes[n.a + i].key == key) return n.a + i;
+    if (node_key(B.nodes[ni(n.a + i)].kt) == key) return ni(n.a + i);
   return ABSENT;
+}
+
+// key-lookup op operand: slot of a slot-addressed map, or key id (AUX_SCAN)
+__device__ __forceinline__ uint32_t lookup_op(const DevBatch& B, uint32_t m, uint32_t a, uint32_t aux) {
+  if (aux & AUX_SCAN) return lookup(B, m, a);
+  if (m == ABSENT) return ABSENT;
+  const Node n = B.nodes[m];
+  if (node_type(n.kt) != NT_MAP || a >= n.b) return ABSENT;
+  const uint32_t c = ni(n.a + a);
+  return node_type(B.nodes[c].kt) == NT_ABSENT ? ABSENT : c;
 }
 
 // Resolved result key of sibling spec entry (OP_KEYGLOB): returns key id and node.
@@ -253,10 +267,10 @@ __device__ void kg_resolve(const DevPS& P, const DevBatch& B, uint32_t m, uint32
   const Atom& A = P.atoms[ref];
   const Node mn = B.nodes[m];
   for (uint32_t i = 0; i < mn.b; i++) {
-    const uint32_t k = B.nodes[mn.a + i].key;
+    const uint32_t k = node_key(B.nodes[ni(mn.a + i)].kt);
     if (glob_atom(P, A, B.kstr + B.key_off[k], B.key_len[k], false)) {
       *key = k;
-      *node = mn.a + i;
+      *node = ni(mn.a + i);
       return;
     }
   }
@@ -435,7 +449,7 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 }
 
 // ------------------------------------------------------------------ kernel
-extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(const DevPS* __restrict__ Pp,
+extern "C" __global__ __launch_bounds__(KV_WG) __attribute__((amdgpu_waves_per_eu(4))) void kv_validate_kernel(const DevPS* __restrict__ Pp,
                                                                       const DevBatch* __restrict__ Bp, DevOut O,
                                                                       uint32_t rule_begin, uint32_t rule_end,
                                                                       uint32_t n_chunks, uint32_t rblocks) {
@@ -466,7 +480,7 @@ extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(const Dev
   const Res* R = B.res + (valid ? r : 0);
   uint32_t rroot = ABSENT, rkind = KEY_NONE, rflags = 0;
   if (valid) {
-    rroot = R->root;
+    rroot = ni(R->root);
     rkind = R->kind;
     rflags = R->flags;
   }
@@ -537,19 +551,19 @@ extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(const Dev
               if (A) {
                 const uint32_t v = s_cur[d][lane];
                 const uint32_t want = op == OP_MAPCHK ? NT_MAP : NT_ARR;
-                if (v == ABSENT || B.nodes[v].type != want) raise(op == OP_MAPCHK ? E_TYPE_MAP : E_TYPE_ARR, ia, v, ic);
+                if (v == ABSENT || node_type(B.nodes[v].kt) != want) raise(op == OP_MAPCHK ? E_TYPE_MAP : E_TYPE_ARR, ia, v, ic);
               }
               break;
             case OP_AREG:
               if (A) {
-                areg |= 1ull << aux;
-                if (lookup(B, s_cur[d][lane], ia) != ABSENT) apres |= 1ull << aux;
+                areg |= 1ull << (aux & 63);
+                if (lookup_op(B, s_cur[d][lane], ia, aux) != ABSENT) apres |= 1ull << (aux & 63);
               }
               break;
             case OP_KEY:
             case OP_KEYV:
               if (A) {
-                const uint32_t c = lookup(B, s_cur[d][lane], ia);
+                const uint32_t c = lookup_op(B, s_cur[d][lane], ia, aux);
                 s_cur[d + 1][lane] = c;
                 if (op == OP_KEY && c == ABSENT) wait = ib;
               }
@@ -596,24 +610,26 @@ extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(const Dev
               }
               break;
             case OP_NEG:
-              if (A && lookup(B, s_cur[d][lane], ia) != ABSENT) raise(E_NEG, ib, ABSENT, ic);
+              if (A && lookup_op(B, s_cur[d][lane], ia, aux) != ABSENT) raise(E_NEG, ib, ABSENT, ic);
               break;
             case OP_STAR:
               if (A) {
                 const uint32_t v = s_cur[d + 1][lane];
-                if (v == ABSENT || B.nodes[v].type == NT_NULL) raise(E_STAR, ib, ABSENT, ic);
+                if (v == ABSENT || node_type(B.nodes[v].kt) == NT_NULL) raise(E_STAR, ib, ABSENT, ic);
               }
               break;
             case OP_LEAF:
               if (A) {
                 const uint32_t v = s_cur[d][lane];
+                Node vn{NT_NULL, 0, 0, 0};
+                if (v != ABSENT) vn = B.nodes[v];
+                const uint32_t vt = node_type(vn.kt);
                 bool ok;
-                if (v != ABSENT && B.nodes[v].type == NT_ARR) {
-                  const Node an = B.nodes[v];
+                if (vt == NT_ARR) {
                   ok = true;
-                  for (uint32_t k = 0; k < an.b && ok; k++) ok = pred_eval(P, B, ia, an.a + k);
+                  for (uint32_t k = 0; k < vn.b && ok; k++) ok = pred_node(P, B, ia, ni(vn.a + k));
                 } else {
-                  ok = pred_eval(P, B, ia, v);
+                  ok = pred_eval(P, B, ia, vt, vn);
                 }
                 if (!ok) raise(E_VALUE, ib, v, ic);
               }
@@ -624,14 +640,14 @@ extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(const Dev
             case OP_EXISTCHK:
               if (A) {
                 const uint32_t v = s_cur[d][lane];
-                if (v == ABSENT || B.nodes[v].type != NT_ARR) raise(E_EXIST_RESTYPE, ia, v, ic);
+                if (v == ABSENT || node_type(B.nodes[v].kt) != NT_ARR) raise(E_EXIST_RESTYPE, ia, v, ic);
               }
               break;
             case OP_LENCHK:
               if (A && B.nodes[s_cur[d][lane]].b < ia) raise(E_LEN, ib, s_cur[d][lane], ic);
               break;
             case OP_INDEX:
-              if (A) s_cur[d + 1][lane] = B.nodes[s_cur[d][lane]].a + ia;
+              if (A) s_cur[d + 1][lane] = ni(B.nodes[s_cur[d][lane]].a + ia);
               break;
             case OP_LOOP_BEGIN:
             case OP_EXIST_BEGIN: {
@@ -643,7 +659,7 @@ extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(const Dev
                   if (op == OP_LOOP_BEGIN) wait = ia + 1;
                   else raise(E_EXIST_FAIL, ib, s_cur[d][lane], ic);
                 } else {
-                  s_cur[d + 1][lane] = an.a;
+                  s_cur[d + 1][lane] = ni(an.a);
                 }
               }
               if (lane % 64 == 0) s_li[wv][aux] = 0;
@@ -667,7 +683,7 @@ extern "C" __global__ __launch_bounds__(KV_WG) void kv_validate_kernel(const Dev
                 if (cont) {
                   const uint32_t i = s_li[wv][aux] + 1;
                   if (i < s_llen[aux][lane]) {
-                    s_cur[d + 1][lane] = s_lfirst[aux][lane] + i;
+                    s_cur[d + 1][lane] = ni(s_lfirst[aux][lane] + i);
                   } else {
                     cont = false;
                     if (op == OP_LOOP_END) wait = pc + 1;
