@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=40_000)
     ap.add_argument("--rule-filter", default="", help="diagnostics: regex over C2 rule names")
+    ap.add_argument("--engine", choices=["vm", "specialized"], default="specialized",
+                    help="bytecode interpreter kernel, or per-policy-set specialized kernels (hiprtc)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -88,7 +90,11 @@ def main():
         kind_mix = 1
         workload = "C3: Pods/Deployments/Services 60/25/15 x 1000 policies with match/exclude"
     t0 = time.time()
-    ps = batch.PolicySet(pols)
+    ps = batch.PolicySet(pols, specialize=args.engine == "specialized")
+    jit = ps.jit_info
+    if jit["kernels"]:
+        log(f"[rank {rank}] specialized kernels: {jit['kernels']} ({jit['code_bytes'] / 1e3:.0f} KB code), "
+            f"hiprtc {jit['compile_ms'] / 1e3:.1f}s")
     data = batch.synth(workloads.SEED + rank, args.n_res, kind_mix)
     t1 = time.time()
     b = batch.Batch(ps, data)
@@ -151,7 +157,8 @@ def main():
         "dtype": "u8",
         "data": "synthetic (kv_synth, seed 0x6B79766E + rank)",
         "config": {"workload": workload, "resources_per_gpu": b.n_res, "rules": ps.n_rules,
-                   "pairs_per_gpu": n_pairs_rank, "output": args.mode, "parallelism": f"resource-shard x{world}"},
+                   "pairs_per_gpu": n_pairs_rank, "output": args.mode, "parallelism": f"resource-shard x{world}",
+                   "engine": args.engine},
         "kernel_ms_per_step": kernel_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,

@@ -38,6 +38,13 @@ enum {
 /* rule routes decided at compile time */
 enum { KV_ROUTE_GPU = 0, KV_ROUTE_CPU = 1, KV_ROUTE_NORESPONSE = 2, KV_ROUTE_CONSTANT = 3 };
 
+/* kv_compile flags */
+enum {
+  /* also lower every rule to a specialized gfx950 kernel (hiprtc, at compile
+   * time); kv_validate/kv_session then run those instead of the bytecode VM */
+  KV_COMPILE_SPECIALIZE = 1
+};
+
 /* kv_validate modes (bit set) */
 enum { KV_MODE_STATUS = 1, KV_MODE_ERRORS = 2, KV_MODE_COUNTS = 4 };
 
@@ -70,6 +77,9 @@ typedef struct kv_rule_info {
  * pkg/engine/variables/vars.go:253-309. */
 int kv_compile(const char* policies_json, size_t len, uint32_t flags, kv_policyset** out, kv_error** err);
 int kv_policyset_info(const kv_policyset* ps, uint32_t* n_policies, uint32_t* n_rules);
+/* specialized kernels of a KV_COMPILE_SPECIALIZE policy set (zeros otherwise) */
+int kv_policyset_jit_info(const kv_policyset* ps, uint32_t* n_kernels, double* gen_ms, double* compile_ms,
+                          uint64_t* code_bytes);
 int kv_rule_info_get(const kv_policyset* ps, uint32_t rule, kv_rule_info* out);
 
 /* Ingest resources (JSON array or NDJSON of unstructured objects; numbers typed

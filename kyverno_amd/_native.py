@@ -64,6 +64,8 @@ def lib():
         errpp = ctypes.POINTER(ctypes.POINTER(_KvErrorStruct))
         L.kv_compile.argtypes = [ctypes.c_char_p, sz, u32, ctypes.POINTER(vp), errpp]
         L.kv_policyset_info.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32)]
+        L.kv_policyset_jit_info.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_double),
+                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64)]
         L.kv_rule_info_get.argtypes = [vp, u32, ctypes.POINTER(RuleInfo)]
         L.kv_ingest.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_char_p, ctypes.POINTER(vp), errpp]
         L.kv_batch_info.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]
@@ -89,7 +91,7 @@ def lib():
 
 
 EXPORTED_SYMBOLS = [
-    "kv_compile", "kv_policyset_info", "kv_rule_info_get", "kv_ingest", "kv_batch_info", "kv_validate",
+    "kv_compile", "kv_policyset_info", "kv_policyset_jit_info", "kv_rule_info_get", "kv_ingest", "kv_batch_info", "kv_validate",
     "kv_result_status", "kv_result_counts", "kv_result_path", "kv_result_error", "kv_result_kernel_ms",
     "kv_bench", "kv_synth", "kv_free_policyset", "kv_free_batch", "kv_free_result", "kv_free_error",
     "kv_free_buffer", "kv_session_create", "kv_session_run", "kv_session_counts", "kv_free_session",

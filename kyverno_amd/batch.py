@@ -22,6 +22,7 @@ PASS, FAIL, WARN, ERROR, SKIP, NOMATCH, CPU = range(7)
 STATUS_NAMES = ["pass", "fail", "warn", "error", "skip", "nomatch", "cpu"]
 
 MODE_STATUS, MODE_ERRORS, MODE_COUNTS = 1, 2, 4
+COMPILE_SPECIALIZE = 1
 ROUTE_GPU, ROUTE_CPU, ROUTE_NORESPONSE, ROUTE_CONSTANT = range(4)
 
 
@@ -48,15 +49,22 @@ class Rule:
 
 
 class PolicySet:
-    """Compiled policies (``kv_compile``). Input: list of policy dicts or JSON text."""
+    """Compiled policies (``kv_compile``). Input: list of policy dicts or JSON text.
 
-    def __init__(self, policies):
+    ``specialize=True`` also lowers every rule to specialized gfx950 kernels
+    (hiprtc, at construction); evaluation then runs those instead of the
+    bytecode interpreter. ``jit_info`` reports their build cost.
+    """
+
+    def __init__(self, policies, specialize: bool = False):
         L = lib()
         data = _dumps(policies)
         h = ctypes.c_void_p()
         err = new_err()
-        check(L.kv_compile(data, len(data), 0, ctypes.byref(h), ctypes.byref(err)), err)
+        flags = COMPILE_SPECIALIZE if specialize else 0
+        check(L.kv_compile(data, len(data), flags, ctypes.byref(h), ctypes.byref(err)), err)
         self._h = h
+        self.specialize = specialize
         np_, nr = ctypes.c_uint32(), ctypes.c_uint32()
         L.kv_policyset_info(h, ctypes.byref(np_), ctypes.byref(nr))
         self.n_policies, self.n_rules = np_.value, nr.value
@@ -76,6 +84,13 @@ class PolicySet:
             except Exception:
                 pass
             self._h = None
+
+    @property
+    def jit_info(self) -> dict:
+        nk, cb = ctypes.c_uint32(), ctypes.c_uint64()
+        g, c = ctypes.c_double(), ctypes.c_double()
+        lib().kv_policyset_jit_info(self._h, ctypes.byref(nk), ctypes.byref(g), ctypes.byref(c), ctypes.byref(cb))
+        return {"kernels": nk.value, "gen_ms": g.value, "compile_ms": c.value, "code_bytes": cb.value}
 
     def policy_rules(self, policy: int) -> list[Rule]:
         return [r for r in self.rules if r.policy == policy]

@@ -17,6 +17,7 @@
 #include "../../include/kvgpu.h"
 #include "kvdev.h"
 #include "kvinternal.hpp"
+#include "kvjit.hpp"
 
 using namespace kv;
 using namespace kvh;
@@ -71,6 +72,20 @@ struct DevPolicySet {
   DevBuf prog, preds, alts, conjs, atoms, rules, filters, kinds, strrefs, strpairs, sels, sellabels, selexprs, kgs,
       gsegs, gwords, pstr;
   DevPS view{};
+  // specialized kernels (KV_COMPILE_SPECIALIZE): one function per rule chunk
+  hipModule_t mod = nullptr;
+  std::vector<hipFunction_t> fns;
+  int dev = -1;
+  ~DevPolicySet() {
+    if (mod) {
+      int cur;
+      if (hipGetDevice(&cur) == hipSuccess) {
+        (void)hipSetDevice(dev);
+        (void)hipModuleUnload(mod);
+        (void)hipSetDevice(cur);
+      }
+    }
+  }
 };
 
 struct DevBatchRes {
@@ -82,6 +97,7 @@ struct DevBatchRes {
 
 struct kv_policyset {
   PolicySet ps;
+  std::unique_ptr<JitImage> jit;  // KV_COMPILE_SPECIALIZE
   std::mutex mu;
   std::map<int, std::unique_ptr<DevPolicySet>> dev;
 };
@@ -158,6 +174,15 @@ DevPolicySet& dev_ps(kv_policyset* s, int device) {
   v.n_rules = (uint32_t)ps.rules.size();
   v.pstr = (const uint8_t*)d->pstr.p;
   v.star_id = ps.lookup("*");
+  d->dev = device;
+  if (s->jit) {
+    HIPCHK(hipModuleLoadData(&d->mod, s->jit->code.data()));
+    for (auto& ch : s->jit->chunks) {
+      hipFunction_t f;
+      HIPCHK(hipModuleGetFunction(&f, d->mod, ch.name.c_str()));
+      d->fns.push_back(f);
+    }
+  }
   auto& ref = *d;
   s->dev[device] = std::move(d);
   return ref;
@@ -336,6 +361,8 @@ struct kv_session {
   DevBuf fflags, pview, st, er, cn;
   DevOut O{};
   const DevBatch* bview = nullptr;
+  const DevBatch* bhost = nullptr;  // host copy of the batch view (device pointers)
+  DevPolicySet* dps = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
 
@@ -345,6 +372,8 @@ struct kv_session {
     DevPolicySet& dp = dev_ps(ps, device);
     DevBatchRes& db = dev_batch(bt, ps->ps, device);
     bview = (const DevBatch*)db.view_dev.p;
+    bhost = &db.view;
+    dps = &dp;
     AdmissionCtx ai = parse_ctx(ctx_json);
     fflags.upload(fold_filters(ps->ps, ai), device);
     DevPS P = dp.view;
@@ -381,13 +410,27 @@ struct kv_session {
     HIPCHK(hipEventRecord(e0, stream));
     for (int i = 0; i < iters; i++) {
       HIPCHK(hipMemsetAsync(cn.p, 0, cn.n, stream));
-      HIPCHK(launch_validate((const DevPS*)pview.p, bview, (uint32_t)nres, O, 0, (uint32_t)nrules, stream));
+      if (dps->mod) launch_specialized();
+      else HIPCHK(launch_validate((const DevPS*)pview.p, bview, (uint32_t)nres, O, 0, (uint32_t)nrules, stream));
     }
     HIPCHK(hipEventRecord(e1, stream));
     HIPCHK(hipEventSynchronize(e1));
     float t = 0;
     HIPCHK(hipEventElapsedTime(&t, e0, e1));
     return t;
+  }
+  // one launch per rule chunk of the specialized kernels, 256 resources per workgroup
+  void launch_specialized() {
+    if (nres == 0) return;
+    const uint32_t blocks = (uint32_t)((nres + KV_WG - 1) / KV_WG);
+    const DevPS* P = (const DevPS*)pview.p;
+    const Node* N = bhost->nodes;
+    const Val* V = bhost->vals;
+    const uint8_t* S = bhost->bstr;
+    DevOut Ov = O;
+    void* args[] = {(void*)&P, (void*)&bview, (void*)&N, (void*)&V, (void*)&S, (void*)&Ov};
+    for (hipFunction_t f : dps->fns)
+      HIPCHK(hipModuleLaunchKernel(f, blocks, 1, 1, KV_WG, 1, 1, 0, stream, args, nullptr));
   }
   void fetch(kv_result* out, double ms) {
     out->ps = ps;
@@ -428,12 +471,23 @@ void run(kv_policyset* ps, kv_batch* bt, const char* ctx_json, int device, uint3
 extern "C" {
 
 int kv_compile(const char* policies_json, size_t len, uint32_t flags, kv_policyset** out, kv_error** err) {
-  (void)flags;
   if (!policies_json || !out) return fail(err, KV_E_INVALID, "null argument");
   try {
     auto* s = new kv_policyset();
     try {
       compile_policies(policies_json, len, &s->ps);
+      if (flags & KV_COMPILE_SPECIALIZE) {
+        s->jit = std::make_unique<JitImage>();
+        const char* ch = getenv("KVGPU_JIT_CHUNK");  // rules per specialized kernel (experiments)
+        jit_generate(s->ps, ch ? (uint32_t)atoi(ch) : 32u, s->jit.get());
+        if (const char* dump = getenv("KVGPU_JIT_DUMP")) {
+          if (FILE* f = fopen(dump, "w")) {
+            fwrite(s->jit->source.data(), 1, s->jit->source.size(), f);
+            fclose(f);
+          }
+        }
+        jit_compile(s->jit.get());
+      }
     } catch (...) {
       delete s;
       throw;
@@ -449,6 +503,17 @@ int kv_policyset_info(const kv_policyset* ps, uint32_t* n_policies, uint32_t* n_
   if (!ps) return KV_E_INVALID;
   if (n_policies) *n_policies = (uint32_t)ps->ps.policy_names.size();
   if (n_rules) *n_rules = (uint32_t)ps->ps.rules.size();
+  return 0;
+}
+
+int kv_policyset_jit_info(const kv_policyset* ps, uint32_t* n_kernels, double* gen_ms, double* compile_ms,
+                          uint64_t* code_bytes) {
+  if (!ps) return KV_E_INVALID;
+  const JitImage* j = ps->jit.get();
+  if (n_kernels) *n_kernels = j ? (uint32_t)j->chunks.size() : 0;
+  if (gen_ms) *gen_ms = j ? j->gen_ms : 0;
+  if (compile_ms) *compile_ms = j ? j->compile_ms : 0;
+  if (code_bytes) *code_bytes = j ? j->code.size() : 0;
   return 0;
 }
 

@@ -5,63 +5,9 @@
 #include <stdint.h>
 
 #include "kv_layout.h"
+#include "kvdevtypes.h"
 
 namespace kv {
-
-struct ErrRec {
-  uint32_t kind_flags;  // kind | flags << 16
-  uint32_t pnode;
-  uint32_t keynode;
-  uint32_t resnode;
-  uint32_t idx[4];
-};
-
-struct DevPS {
-  const Inst* prog;
-  const Pred* preds;
-  const Alt* alts;
-  const Conj* conjs;
-  const Atom* atoms;
-  const RuleRec* rules;
-  const MFilter* filters;
-  const uint32_t* fflags;  // per-filter flags folded with the launch's admission info
-  const KindSpec* kinds;
-  const StrRef* strrefs;
-  const StrPair* strpairs;
-  const Selector* sels;
-  const SelLabel* sellabels;
-  const SelExpr* selexprs;
-  const uint32_t* kg_specs;
-  const GSeg* gsegs;
-  const GWord* gwords;
-  const uint8_t* pstr;
-  uint32_t star_id;
-  uint32_t n_rules;
-};
-
-struct DevBatch {
-  const Node* nodes;
-  const Val* vals;
-  const Res* res;
-  const KV* kvs;
-  const uint8_t* bstr;
-  const uint32_t* ns_bits;
-  const uint32_t* key_off;
-  const uint32_t* key_len;
-  const uint8_t* kstr;
-  uint32_t ns_words;
-  uint32_t n_res;
-};
-
-struct DevOut {
-  uint8_t* status;             // [rule][res]
-  ErrRec* err;                 // [rule][res] (written for fail/error/skip)
-  unsigned long long* counts;  // [rule][8]
-  uint32_t full;               // bit0 status, bit1 error records
-};
-
-constexpr int KV_WG = 256;
-constexpr int KV_HIST = 8;
 
 // Launch one pass over rules [rule_begin, rule_end) for every resource.
 // P and B point to device-resident copies of the views (uniform scalar loads).

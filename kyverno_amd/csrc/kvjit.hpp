@@ -1,0 +1,33 @@
+// Specialized kernels: the compiled policy set (bytecode, predicates, globs) is
+// lowered once more, to HIP C++ with every rule as straight-line device code
+// (constants as immediates, cursors in registers, per-lane control flow done by
+// the hardware exec mask instead of the interpreter's uniform-pc emulation),
+// and compiled for gfx950 with hiprtc when the policy set is compiled.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "kvinternal.hpp"
+
+namespace kvh {
+
+struct JitChunk {
+  uint32_t rule_begin = 0, rule_end = 0;  // rules [begin, end) evaluated by kernel `name`
+  std::string name;
+};
+
+struct JitImage {
+  std::string source;       // generated HIP source (kept for diagnostics)
+  std::vector<JitChunk> chunks;
+  std::vector<char> code;   // gfx950 code object
+  double gen_ms = 0, compile_ms = 0;
+};
+
+// Generate the specialized source for every rule of `ps` (chunks of at most
+// `chunk_rules` rules per kernel).
+void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out);
+// Compile out->source with hiprtc for gfx950; throws std::runtime_error with the log on failure.
+void jit_compile(JitImage* img);
+
+}  // namespace kvh

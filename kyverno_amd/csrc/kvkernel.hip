@@ -26,427 +26,9 @@ using namespace kv;
 
 #define KV_MAXD 16
 #define KV_MAXL 4
-#define KV_SENT 0xFFFFFFFFu
 #define KV_RCHUNK 64
 
-// ------------------------------------------------------------------ helpers
-__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-
-// node index of this lane's cell in a row (wave-group layout, kv_layout.h)
-__device__ __forceinline__ uint32_t ni(uint32_t row) { return row * KV_LANES + (threadIdx.x & (KV_LANES - 1)); }
-
-__device__ __forceinline__ uint32_t rune_len(uint8_t c) {
-  return c < 0x80 ? 1u : c >= 0xF0 ? 4u : c >= 0xE0 ? 3u : c >= 0xC0 ? 2u : 1u;
-}
-
-// minio/pkg v1.1.3 wildcard.Match over valid UTF-8: '*' any run of runes,
-// '?' exactly one rune; star backtracking advances by whole runes.
-// General path (non-ASCII value with '?' in the pattern, selector/label globs).
-__device__ __noinline__ bool kv_glob(const uint8_t* p, uint32_t pl, const uint8_t* s, uint32_t sl) {
-  if (pl == 0) return sl == 0;
-  if (pl == 1 && p[0] == '*') return true;
-  uint32_t si = 0, pi = 0, star = KV_SENT, mark = 0;
-  while (si < sl) {
-    if (pi < pl) {
-      uint8_t pc = p[pi];
-      if (pc == '*') { star = pi++; mark = si; continue; }
-      if (pc == '?') { si += rune_len(s[si]); pi++; continue; }
-      uint32_t w = rune_len(pc);
-      bool eq = si + w <= sl && pi + w <= pl;
-      for (uint32_t k = 0; eq && k < w; k++) eq = p[pi + k] == s[si + k];
-      if (eq) { pi += w; si += w; continue; }
-    }
-    if (star != KV_SENT) {
-      pi = star + 1;
-      mark += rune_len(s[mark]);
-      si = mark;
-      continue;
-    }
-    return false;
-  }
-  while (pi < pl && p[pi] == '*') pi++;
-  return pi == pl && si == sl;
-}
-
-// segment (uniform words) == value bytes [k, k+len) ; value base 4-byte aligned
-__device__ __forceinline__ bool seg_at(const GWord* __restrict__ wd, uint32_t len, const uint32_t* __restrict__ base,
-                                       uint32_t k) {
-  const uint32_t nw = (len + 3) >> 2;
-  const uint32_t a = k >> 2, sh = k & 3;
-  uint32_t lo = base[a];
-  for (uint32_t i = 0; i < nw; i++) {
-    uint32_t hi = base[a + i + 1];
-    uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, sh);
-    const GWord g = wd[i];
-    if ((v ^ g.w) & g.mask) return false;
-    lo = hi;
-  }
-  return true;
-}
-
-// compiled glob over a 4-byte aligned value string (see kv_layout.h GlobFlags)
-__device__ bool glob_fast(const DevPS& P, const Atom& A, const uint8_t* s, uint32_t sl) {
-  const uint32_t fl = uni(A.gflags);
-  if (fl & G_ALL) return true;
-  if (fl & G_EMPTY) return sl == 0;
-  if (sl < uni(A.gmin)) return false;
-  const uint32_t* base = (const uint32_t*)s;
-  const GSeg* segs = P.gsegs + uni(A.gfirst);
-  const uint32_t n = uni(A.gcount);
-  uint32_t pos = 0, end = sl, i0 = 0, i1 = n;
-  if (!(fl & G_LEAD)) {
-    const GSeg s0 = segs[0];
-    if (n == 1 && !(fl & G_TRAIL)) return sl == s0.len && seg_at(P.gwords + s0.wfirst, s0.len, base, 0);
-    if (!seg_at(P.gwords + s0.wfirst, s0.len, base, 0)) return false;
-    pos = s0.len;
-    i0 = 1;
-  }
-  if (!(fl & G_TRAIL)) {
-    const GSeg st = segs[n - 1];
-    if (end < pos + st.len) return false;
-    if (!seg_at(P.gwords + st.wfirst, st.len, base, end - st.len)) return false;
-    end -= st.len;
-    i1 = n - 1;
-  }
-  for (uint32_t i = i0; i < i1; i++) {
-    const GSeg sg = segs[i];
-    bool found = false;
-    for (uint32_t k = pos; k + sg.len <= end; k++) {
-      if (seg_at(P.gwords + sg.wfirst, sg.len, base, k)) { pos = k + sg.len; found = true; break; }
-    }
-    if (!found) return false;
-  }
-  return true;
-}
-
-__device__ __forceinline__ bool glob_atom(const DevPS& P, const Atom& A, const uint8_t* s, uint32_t sl, bool ascii) {
-  if (ascii || !(uni(A.gflags) & G_HASQ)) return glob_fast(P, A, s, sl);
-  return kv_glob(P.pstr + A.s_off, A.s_len & 0x7FFFFFFFu, s, sl);
-}
-
-__device__ __forceinline__ bool bytes_eq(const uint8_t* a, uint32_t al, const uint8_t* b, uint32_t bl) {
-  if (al != bl) return false;
-  for (uint32_t k = 0; k < al; k++)
-    if (a[k] != b[k]) return false;
-  return true;
-}
-
-// magnitude/sign compare of canonical quantities: returns -1/0/1 (value vs pattern)
-__device__ __forceinline__ int q_cmp(uint32_t vf, int32_t ve, uint64_t vh, uint64_t vl, uint32_t pf, int32_t pe,
-                                     uint64_t ph, uint64_t pl) {
-  int sv = (vf & VF_Q_ZERO) ? 0 : ((vf & VF_Q_NEG) ? -1 : 1);
-  int sp = (pf & VF_Q_ZERO) ? 0 : ((pf & VF_Q_NEG) ? -1 : 1);
-  if (sv != sp) return sv < sp ? -1 : 1;
-  if (sv == 0) return 0;
-  int m;
-  if (ve != pe) m = ve < pe ? -1 : 1;
-  else if (vh != ph) m = vh < ph ? -1 : 1;
-  else if (vl != pl) m = vl < pl ? -1 : 1;
-  else m = 0;
-  return sv > 0 ? m : -m;
-}
-
-__device__ __forceinline__ bool cmp_ok(uint32_t op, int r) {
-  switch (op) {
-    case CO_EQ: return r == 0;
-    case CO_NE: return r != 0;
-    case CO_GT: return r == 1;
-    case CO_LT: return r == -1;
-    case CO_GE: return r >= 0;
-    default: return r <= 0;
-  }
-}
-
-// one atom of a string pattern against a scalar/absent node (type NT_NULL == Go nil)
-__device__ bool atom_eval(const DevPS& P, const DevBatch& B, uint32_t ai, uint32_t type, const Node& n) {
-  const Atom& A = P.atoms[ai];
-  const uint32_t kind = uni(A.kind);
-  if (kind == AT_FALSE) return false;
-  if (type == NT_MAP || type == NT_ARR) return false;
-  if (kind == AT_GLOB_E) {
-    if (type == NT_NULL) return false;
-    bool r = glob_atom(P, A, B.bstr + n.b, n.c & NC_LEN_MASK, n.c & NC_ASCII_E);
-    return uni(A.op) == CO_NE ? !r : r;
-  }
-  if (type == NT_BOOL) return false;
-  if (kind == AT_GLOB_N) {
-    if (type == NT_NULL) return glob_atom(P, A, B.bstr, 1, true);  // convertNumberToString(nil) == "0" (bstr[0..1))
-    if (type != NT_FLOAT) return glob_atom(P, A, B.bstr + n.b, n.c & NC_LEN_MASK, n.c & NC_ASCII_E);  // == e-form
-    const Val& v = B.vals[n.a];
-    return glob_atom(P, A, B.bstr + v.n_off, v.n_len, v.flags & VF_ASCII_N);
-  }
-  // AT_QCMP
-  int r;
-  if (type == NT_NULL) {
-    r = q_cmp(VF_Q_ZERO, 0, 0, 0, A.q_flags, A.q_exp, A.q_hi, A.q_lo);
-  } else {
-    const Val& v = B.vals[n.a];
-    if (!(v.flags & VF_Q_VALID)) return false;
-    r = q_cmp(v.flags, v.q_exp, v.q_hi, v.q_lo, A.q_flags, A.q_exp, A.q_hi, A.q_lo);
-  }
-  return cmp_ok(uni(A.op), r);
-}
-
-// ValidateValueWithPattern(value, pattern) for a scalar-pattern leaf; n = the
-// value node (ignored when type == NT_NULL, which also stands for absent)
-__device__ bool pred_eval(const DevPS& P, const DevBatch& B, uint32_t pi, uint32_t type, const Node& n) {
-  const Pred& pr = P.preds[pi];
-  const uint32_t kind = uni(pr.kind);
-  switch (kind) {
-    case PK_BOOL: return type == NT_BOOL && ((n.c & NC_BOOLV) ? 1u : 0u) == uni(pr.flags);
-    case PK_FLOAT: {
-      if (type == NT_INT) return uni(pr.flags) && B.vals[n.a].i == pr.fi;
-      if (type == NT_FLOAT) return B.vals[n.a].f == pr.f;
-      if (type == NT_STR) {
-        const Val& v = B.vals[n.a];
-        return (v.flags & VF_PF_OK) && v.f == pr.f;
-      }
-      return false;
-    }
-    case PK_NIL:
-      if (type == NT_NULL) return true;
-      if (type == NT_MAP || type == NT_ARR) return false;
-      return (n.c & NC_NILLIKE) != 0;
-    case PK_MAPTYPE: return type == NT_MAP;
-    case PK_STRING: {
-      const uint32_t af = uni(pr.first), an = uni(pr.count);
-      for (uint32_t a = af; a < af + an; a++) {
-        const Alt& al = P.alts[a];
-        const uint32_t cf = uni(al.first), cn = uni(al.count);
-        bool all = true;
-        for (uint32_t c = cf; c < cf + cn && all; c++) {
-          const Conj& cj = P.conjs[c];
-          const uint32_t ck = uni(cj.kind);
-          bool r = atom_eval(P, B, uni(cj.a0), type, n);
-          if (ck == CJ_INRANGE) r = r && atom_eval(P, B, uni(cj.a1), type, n);
-          else if (ck == CJ_NOTINRANGE) r = r || atom_eval(P, B, uni(cj.a1), type, n);
-          all = r;
-        }
-        if (all) return true;
-      }
-      return false;
-    }
-    default: return false;
-  }
-}
-
-__device__ __forceinline__ bool pred_node(const DevPS& P, const DevBatch& B, uint32_t pi, uint32_t node) {
-  Node n{NT_NULL, 0, 0, 0};
-  if (node != ABSENT) n = B.nodes[node];
-  return pred_eval(P, B, pi, node_type(n.kt), n);
-}
-
-// keep-all map (labels/annotations): scan for key id
-__device__ __forceinline__ uint32_t lookup(const DevBatch& B, uint32_t m, uint32_t key) {
-  if (m == ABSENT) return ABSENT;
-  const Node n = B.nodes[m];
-  if (node_type(n.kt) != NT_MAP) return ABSENT;
-  for (uint32_t i = 0; i < n.b; i++)
-    if (node_key(B.nodes[ni(n.a + i)].kt) == key) return ni(n.a + i);
-  return ABSENT;
-}
-
-// key-lookup op operand: slot of a slot-addressed map, or key id (AUX_SCAN)
-__device__ __forceinline__ uint32_t lookup_op(const DevBatch& B, uint32_t m, uint32_t a, uint32_t aux) {
-  if (aux & AUX_SCAN) return lookup(B, m, a);
-  if (m == ABSENT) return ABSENT;
-  const Node n = B.nodes[m];
-  if (node_type(n.kt) != NT_MAP || a >= n.b) return ABSENT;
-  const uint32_t c = ni(n.a + a);
-  return node_type(B.nodes[c].kt) == NT_ABSENT ? ABSENT : c;
-}
-
-// Resolved result key of sibling spec entry (OP_KEYGLOB): returns key id and node.
-__device__ void kg_resolve(const DevPS& P, const DevBatch& B, uint32_t m, uint32_t w, uint32_t ref, uint32_t* key,
-                           uint32_t* node) {
-  if (!w) {  // literal sibling: key id is the key
-    *key = ref;
-    *node = lookup(B, m, ref);
-    return;
-  }
-  const Atom& A = P.atoms[ref];
-  const Node mn = B.nodes[m];
-  for (uint32_t i = 0; i < mn.b; i++) {
-    const uint32_t k = node_key(B.nodes[ni(mn.a + i)].kt);
-    if (glob_atom(P, A, B.kstr + B.key_off[k], B.key_len[k], false)) {
-      *key = k;
-      *node = ni(mn.a + i);
-      return;
-    }
-  }
-  *key = KV_SENT;  // unresolved wildcard: unique literal result key
-  *node = ABSENT;
-}
-
-// ------------------------------------------------------------------ match/exclude
-__device__ bool selector_match(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t si) {
-  const Selector& S = P.sels[si];
-  const uint32_t fl = uni(S.flags);
-  if (fl & SF_STATIC_INVALID) return false;
-  if (fl & SF_EVERYTHING) return true;
-  const KV* labels = B.kvs + R->labels_first;
-  const uint32_t nl = R->labels_count;
-  const uint32_t mf = uni(S.ml_first), mc = uni(S.ml_count);
-  auto resolve = [&](const SelLabel& E, const uint8_t** ok, uint32_t* okl, const uint8_t** ov, uint32_t* ovl,
-                     bool* val) {
-    if (!(E.flags & SL_WILD)) {
-      *ok = P.pstr + E.k_off; *okl = E.k_len; *ov = P.pstr + E.v_off; *ovl = E.v_len;
-      *val = (E.flags & SL_VALID) != 0;
-      return;
-    }
-    for (uint32_t q = 0; q < nl; q++) {
-      const KV kv = labels[q];
-      const uint8_t* lk = B.bstr + kv.k_off;
-      const uint8_t* lv = B.bstr + kv.v_off;
-      const uint32_t lkl = kv.k_len & KV_LEN_MASK, lvl = kv.v_len & KV_LEN_MASK;
-      if (kv_glob(P.pstr + E.k_off, E.k_len, lk, lkl) && kv_glob(P.pstr + E.v_off, E.v_len, lv, lvl)) {
-        *ok = lk; *okl = lkl; *ov = lv; *ovl = lvl;
-        *val = (kv.k_len & KV_VALID) && (kv.v_len & KV_VALID);
-        return;
-      }
-    }
-    *ok = P.pstr + E.rk_off; *okl = E.rk_len; *ov = P.pstr + E.rv_off; *ovl = E.rv_len;
-    *val = (E.flags & SL_VALID) != 0;
-  };
-  for (uint32_t j = mf; j < mf + mc; j++) {
-    const uint8_t *kp, *vp;
-    uint32_t kl, vl;
-    bool valid;
-    resolve(P.sellabels[j], &kp, &kl, &vp, &vl, &valid);
-    // dropped if a later entry resolves to the same key (results[matchK] = matchV)
-    bool dropped = false;
-    for (uint32_t j2 = j + 1; j2 < mf + mc && !dropped; j2++) {
-      const uint8_t *k2, *v2;
-      uint32_t k2l, v2l;
-      bool val2;
-      resolve(P.sellabels[j2], &k2, &k2l, &v2, &v2l, &val2);
-      dropped = bytes_eq(kp, kl, k2, k2l);
-    }
-    if (dropped) continue;
-    if (!valid) return false;  // NewRequirement validation error
-    bool found = false;
-    for (uint32_t q = 0; q < nl; q++) {
-      const KV kv = labels[q];
-      if (bytes_eq(B.bstr + kv.k_off, kv.k_len & KV_LEN_MASK, kp, kl)) {
-        found = bytes_eq(B.bstr + kv.v_off, kv.v_len & KV_LEN_MASK, vp, vl);
-        break;
-      }
-    }
-    if (!found) return false;
-  }
-  const uint32_t ef = uni(S.me_first), ec = uni(S.me_count);
-  for (uint32_t j = ef; j < ef + ec; j++) {
-    const SelExpr& E = P.selexprs[j];
-    bool has = false, in = false;
-    for (uint32_t q = 0; q < nl; q++) {
-      const KV kv = labels[q];
-      if (bytes_eq(B.bstr + kv.k_off, kv.k_len & KV_LEN_MASK, P.pstr + E.k_off, E.k_len)) {
-        has = true;
-        for (uint32_t v = E.v_first; v < E.v_first + E.v_count && !in; v++)
-          in = bytes_eq(B.bstr + kv.v_off, kv.v_len & KV_LEN_MASK, P.pstr + P.strrefs[v].off, P.strrefs[v].len);
-        break;
-      }
-    }
-    const uint32_t op = uni(E.op);
-    if ((op == 0 && !in) || (op == 1 && in) || (op == 2 && !has) || (op == 3 && has)) return false;
-  }
-  return true;
-}
-
-// doesResourceMatchConditionBlock: number of failed criteria (0 == block matches)
-__device__ uint32_t block_errs(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t rkind,
-                               uint32_t rflags, uint32_t f) {
-  const MFilter& F = P.filters[f];
-  const uint32_t fl = uni(P.fflags[f]);
-  uint32_t errs = 0;
-  if (fl & MF_KINDS) {
-    bool ok = false;
-    const uint32_t kf = uni(F.kinds_first), kc = uni(F.kinds_count);
-    for (uint32_t k = kf; k < kf + kc && !ok; k++) {
-      const KindSpec ks = P.kinds[k];
-      switch (ks.form) {
-        case 3: ok = true; break;
-        case 0: ok = rkind == ks.kind; break;
-        case 1: ok = rkind == ks.kind && R->version == ks.version; break;
-        default: ok = R->group == ks.group && rkind == ks.kind && (R->version == ks.version || R->version == P.star_id); break;
-      }
-    }
-    errs += ok ? 0 : 1;
-    if (errs) return errs;  // later criteria cannot turn an error count back to zero
-  }
-  if (fl & MF_NAME) errs += kv_glob(P.pstr + F.name_off, F.name_len, B.bstr + R->name_off, R->name_len) ? 0 : 1;
-  if (fl & MF_NAMES) {
-    bool any = false;
-    for (uint32_t k = F.names_first; k < F.names_first + F.names_count && !any; k++)
-      any = kv_glob(P.pstr + P.strrefs[k].off, P.strrefs[k].len, B.bstr + R->name_off, R->name_len);
-    errs += any ? 0 : 1;
-  }
-  if (fl & MF_NSS) {
-    bool any = false;
-    for (uint32_t k = F.nss_first; k < F.nss_first + F.nss_count && !any; k++)
-      any = kv_glob(P.pstr + P.strrefs[k].off, P.strrefs[k].len, B.bstr + R->ns_off, R->ns_len);
-    errs += any ? 0 : 1;
-  }
-  if (fl & MF_ANN) {
-    bool all = true;
-    for (uint32_t k = F.ann_first; k < F.ann_first + F.ann_count && all; k++) {
-      const StrPair sp = P.strpairs[k];
-      bool m = false;
-      for (uint32_t q = 0; q < R->annot_count && !m; q++) {
-        const KV kv = B.kvs[R->annot_first + q];
-        m = kv_glob(P.pstr + sp.k_off, sp.k_len, B.bstr + kv.k_off, kv.k_len & KV_LEN_MASK) &&
-            kv_glob(P.pstr + sp.v_off, sp.v_len, B.bstr + kv.v_off, kv.v_len & KV_LEN_MASK);
-      }
-      all = m;
-    }
-    errs += all ? 0 : 1;
-  }
-  if (fl & MF_SEL) errs += selector_match(P, B, R, F.sel) ? 0 : 1;
-  if ((fl & MF_NSSEL) && !(rflags & (RF_KIND_NAMESPACE | RF_KIND_EMPTY))) {
-    const uint32_t bit = F.nssel_bit;
-    errs += (B.ns_bits[R->ns_index * B.ns_words + bit / 32] >> (bit % 32)) & 1 ? 0 : 1;
-  }
-  if (fl & MF_UI_FAIL) errs += 1;
-  return errs;
-}
-
-__device__ bool rule_matches(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t rkind,
-                             uint32_t rflags, const RuleRec& rr) {
-  const uint32_t mm = uni(rr.m_mode), mf = uni(rr.m_first), mc = uni(rr.m_count);
-  bool ok;
-  if (mm == 1) {
-    ok = false;
-    for (uint32_t f = mf; f < mf + mc && !ok; f++) ok = !(P.fflags[f] & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, f) == 0;
-  } else if (mm == 2) {
-    ok = true;
-    for (uint32_t f = mf; f < mf + mc && ok; f++) ok = !(P.fflags[f] & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, f) == 0;
-  } else {
-    ok = !(P.fflags[mf] & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, mf) == 0;
-  }
-  if (!ok) return false;
-  const uint32_t xm = uni(rr.x_mode), xf = uni(rr.x_first), xc = uni(rr.x_count);
-  if (xm == 1) {
-    for (uint32_t f = xf; f < xf + xc; f++)
-      if (!(P.fflags[f] & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, f) == 0) return false;
-    return true;
-  }
-  if (xm == 2) {
-    for (uint32_t f = xf; f < xf + xc; f++)
-      if ((P.fflags[f] & MF_EMPTY) || block_errs(P, B, R, rkind, rflags, f) != 0) return true;
-    return false;
-  }
-  if (!(P.fflags[xf] & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, xf) == 0) return false;
-  return true;
-}
-
-__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    uint32_t x = __shfl_xor(v, o, 64);
-    v = x < v ? x : v;
-  }
-  return v;
-}
+#include "kvdevfn.h"
 
 // ------------------------------------------------------------------ kernel
 extern "C" __global__ __launch_bounds__(KV_WG) __attribute__((amdgpu_waves_per_eu(4))) void kv_validate_kernel(const DevPS* __restrict__ Pp,
@@ -461,6 +43,7 @@ extern "C" __global__ __launch_bounds__(KV_WG) __attribute__((amdgpu_waves_per_e
 
   const DevPS& P = *Pp;
   const DevBatch& B = *Bp;
+  const Node* __restrict__ N = B.nodes;
   // XCD-aware work mapping: block ids b and b+8 share an XCD (and its L2), so
   // every rule chunk of one resource block is placed on the same XCD.
   const uint32_t xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
@@ -551,50 +134,28 @@ extern "C" __global__ __launch_bounds__(KV_WG) __attribute__((amdgpu_waves_per_e
               if (A) {
                 const uint32_t v = s_cur[d][lane];
                 const uint32_t want = op == OP_MAPCHK ? NT_MAP : NT_ARR;
-                if (v == ABSENT || node_type(B.nodes[v].kt) != want) raise(op == OP_MAPCHK ? E_TYPE_MAP : E_TYPE_ARR, ia, v, ic);
+                if (v == ABSENT || node_type(N[v].kt) != want) raise(op == OP_MAPCHK ? E_TYPE_MAP : E_TYPE_ARR, ia, v, ic);
               }
               break;
             case OP_AREG:
               if (A) {
                 areg |= 1ull << (aux & 63);
-                if (lookup_op(B, s_cur[d][lane], ia, aux) != ABSENT) apres |= 1ull << (aux & 63);
+                if (lookup_op(N, s_cur[d][lane], ia, aux) != ABSENT) apres |= 1ull << (aux & 63);
               }
               break;
             case OP_KEY:
             case OP_KEYV:
               if (A) {
-                const uint32_t c = lookup_op(B, s_cur[d][lane], ia, aux);
+                const uint32_t c = lookup_op(N, s_cur[d][lane], ia, aux);
                 s_cur[d + 1][lane] = c;
                 if (op == OP_KEY && c == ABSENT) wait = ib;
               }
               break;
             case OP_KEYGLOB:
               if (A) {
-                const uint32_t j = opw >> 24;
-                const Atom& at = P.atoms[ia];
-                const uint32_t spec = uni((uint32_t)at.q_hi);
-                const uint32_t mycls = uni((uint32_t)at.q_lo);
-                const uint32_t n = P.kg_specs[spec];
-                const uint32_t m = s_cur[d][lane];
-                uint32_t mykey, mynode;
-                const uint32_t myw = P.kg_specs[spec + 1 + 2 * j] & 1;
-                kg_resolve(P, B, m, myw, myw ? ia : ic, &mykey, &mynode);
-                bool dropped = false;
-                for (uint32_t j2 = j + 1; j2 < n && !dropped; j2++) {
-                  const uint32_t cw = P.kg_specs[spec + 1 + 2 * j2];
-                  if ((cw >> 1) != mycls || mykey == KV_SENT) continue;
-                  uint32_t k2, n2;
-                  kg_resolve(P, B, m, cw & 1, P.kg_specs[spec + 2 + 2 * j2], &k2, &n2);
-                  dropped = k2 == mykey;
-                }
-                if (dropped) {
-                  wait = ib;
-                } else {
-                  const uint32_t node = (myw && mykey != KV_SENT) ? mynode : lookup(B, m, ic);
-                  keynode = (myw && mykey != KV_SENT) ? mynode : ABSENT;
-                  s_cur[d + 1][lane] = node;
-                  if (node == ABSENT && (aux & 1)) wait = ib;
-                }
+                uint32_t node;
+                if (keyglob_op(P, B, N, s_cur[d][lane], opw, ia, ic, &node, &keynode)) s_cur[d + 1][lane] = node;
+                else wait = ib;
               }
               break;
             case OP_SCOPE_END:
@@ -610,24 +171,24 @@ extern "C" __global__ __launch_bounds__(KV_WG) __attribute__((amdgpu_waves_per_e
               }
               break;
             case OP_NEG:
-              if (A && lookup_op(B, s_cur[d][lane], ia, aux) != ABSENT) raise(E_NEG, ib, ABSENT, ic);
+              if (A && lookup_op(N, s_cur[d][lane], ia, aux) != ABSENT) raise(E_NEG, ib, ABSENT, ic);
               break;
             case OP_STAR:
               if (A) {
                 const uint32_t v = s_cur[d + 1][lane];
-                if (v == ABSENT || node_type(B.nodes[v].kt) == NT_NULL) raise(E_STAR, ib, ABSENT, ic);
+                if (v == ABSENT || node_type(N[v].kt) == NT_NULL) raise(E_STAR, ib, ABSENT, ic);
               }
               break;
             case OP_LEAF:
               if (A) {
                 const uint32_t v = s_cur[d][lane];
                 Node vn{NT_NULL, 0, 0, 0};
-                if (v != ABSENT) vn = B.nodes[v];
+                if (v != ABSENT) vn = N[v];
                 const uint32_t vt = node_type(vn.kt);
                 bool ok;
                 if (vt == NT_ARR) {
                   ok = true;
-                  for (uint32_t k = 0; k < vn.b && ok; k++) ok = pred_node(P, B, ia, ni(vn.a + k));
+                  for (uint32_t k = 0; k < vn.b && ok; k++) ok = pred_node(P, B, N, ia, ni(vn.a + k));
                 } else {
                   ok = pred_eval(P, B, ia, vt, vn);
                 }
@@ -640,19 +201,19 @@ extern "C" __global__ __launch_bounds__(KV_WG) __attribute__((amdgpu_waves_per_e
             case OP_EXISTCHK:
               if (A) {
                 const uint32_t v = s_cur[d][lane];
-                if (v == ABSENT || node_type(B.nodes[v].kt) != NT_ARR) raise(E_EXIST_RESTYPE, ia, v, ic);
+                if (v == ABSENT || node_type(N[v].kt) != NT_ARR) raise(E_EXIST_RESTYPE, ia, v, ic);
               }
               break;
             case OP_LENCHK:
-              if (A && B.nodes[s_cur[d][lane]].b < ia) raise(E_LEN, ib, s_cur[d][lane], ic);
+              if (A && N[s_cur[d][lane]].b < ia) raise(E_LEN, ib, s_cur[d][lane], ic);
               break;
             case OP_INDEX:
-              if (A) s_cur[d + 1][lane] = ni(B.nodes[s_cur[d][lane]].a + ia);
+              if (A) s_cur[d + 1][lane] = ni(N[s_cur[d][lane]].a + ia);
               break;
             case OP_LOOP_BEGIN:
             case OP_EXIST_BEGIN: {
               if (A) {
-                const Node an = B.nodes[s_cur[d][lane]];
+                const Node an = N[s_cur[d][lane]];
                 s_lfirst[aux][lane] = an.a;
                 s_llen[aux][lane] = an.b;
                 if (an.b == 0) {

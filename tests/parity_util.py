@@ -24,10 +24,10 @@ def oracle_status(orc, policies, resources, ctx=None, nthreads=8):
     return st
 
 
-def gpu_run(policies, resources, ns_labels=None, admission=None, exclude_group_role=None):
+def gpu_run(policies, resources, ns_labels=None, admission=None, exclude_group_role=None, specialize=False):
     from kyverno_amd import batch
 
-    ps = batch.PolicySet(policies)
+    ps = batch.PolicySet(policies, specialize=specialize)
     b = batch.Batch(ps, resources, namespace_labels=ns_labels)
     r = batch.validate(ps, b, admission=admission, exclude_group_role=exclude_group_role)
     return ps, b, r
@@ -42,10 +42,11 @@ def rule_index(policies):
     return out
 
 
-def compare(orc, policies, resources, ctx=None, check_paths=True, max_path_checks=400):
-    """Returns list of mismatch descriptions (empty == parity)."""
+def compare(orc, policies, resources, ctx=None, check_paths=True, max_path_checks=400, specialize=False):
+    """Returns list of mismatch descriptions (empty == parity). specialize: run the
+    hiprtc-specialized kernels instead of the bytecode interpreter."""
     ps, b, r = gpu_run(policies, resources, admission=(ctx or {}).get("admission"),
-                       exclude_group_role=(ctx or {}).get("excludeGroupRole"))
+                       exclude_group_role=(ctx or {}).get("excludeGroupRole"), specialize=specialize)
     ost = oracle_status(orc, policies, resources, ctx=ctx)
     gst = r.status
     mism = []

@@ -14,6 +14,10 @@ from parity_util import compare, load_gold
 
 pytestmark = pytest.mark.gpu
 
+# every parity case runs on both device engines: the bytecode interpreter
+# (kvkernel.hip) and the per-policy-set specialized kernels (kvjit.cpp)
+engines = pytest.mark.parametrize("spec", [False, True], ids=["vm", "specialized"])
+
 
 def _policy(pattern, name="fixture", any_pattern=False):
     v = {"anyPattern": pattern} if any_pattern else {"pattern": pattern}
@@ -21,62 +25,68 @@ def _policy(pattern, name="fixture", any_pattern=False):
             "spec": {"rules": [{"name": "r", "match": {"resources": {"kinds": ["*"]}}, "validate": v}]}}
 
 
-def test_matcher_fixtures(orc):
+@engines
+def test_matcher_fixtures(orc, spec):
     """validate_test.go cases (map resources) wrapped as single-rule policies."""
     cases = [c for c in load_gold("matcher.json") if json.loads(c["resource"]).__class__ is dict]
     pols = [_policy(json.loads(c["pattern"]), name=f"m{i}") for i, c in enumerate(cases)]
     ress = [json.loads(c["resource"]) for c in cases]
-    mism, r, ost = compare(orc, pols, ress)
+    mism, r, ost = compare(orc, pols, ress, specialize=spec)
     # only the diagonal (policy i x resource i) is the fixture; the cross product is extra coverage
     assert not mism, "\n".join(mism)
 
 
-def test_comparator_fixtures(orc):
+@engines
+def test_comparator_fixtures(orc, spec):
     """pattern_test.go ValidateValueWithPattern cases as {key: pattern} vs {key: value}."""
     cases = [c for c in load_gold("comparator.json") if c.get("kind") == 0]
     pols = [_policy({"key": json.loads(c["pattern"]["json"])}, name=f"c{i}") for i, c in enumerate(cases)]
     ress = [{"key": json.loads(c["value"]["json"])} for c in cases]
-    mism, r, ost = compare(orc, pols, ress)
+    mism, r, ost = compare(orc, pols, ress, specialize=spec)
     assert not mism, "\n".join(mism)
 
 
-def test_reference_corpus(orc):
+@engines
+def test_reference_corpus(orc, spec):
     c = load_gold("corpus.json")[0]
     pols = [p["policy"] for p in c["policies"]]
     ress = [r["resource"] for r in c["resources"]]
-    mism, r, ost = compare(orc, pols, ress)
+    mism, r, ost = compare(orc, pols, ress, specialize=spec)
     assert not mism, "\n".join(mism)
     # the corpus must exercise the GPU path, not only CPU routes
     assert (r.status <= 4).sum() > 50
 
 
-def test_c2_synthetic(orc):
+@engines
+def test_c2_synthetic(orc, spec):
     from kyverno_amd import batch, workloads
 
     pols = workloads.c2_policies()
     data = batch.synth(workloads.SEED, 3000).decode()
     ress = [json.loads(l) for l in data.strip().split("\n")]
-    mism, r, ost = compare(orc, pols, ress)
+    mism, r, ost = compare(orc, pols, ress, specialize=spec)
     assert not mism, "\n".join(mism)
     assert (r.status == 1).sum() > 1000 and (r.status == 0).sum() > 1000
 
 
-def test_c3_synthetic_match_exclude(orc):
+@engines
+def test_c3_synthetic_match_exclude(orc, spec):
     from kyverno_amd import batch, workloads
 
     pols = workloads.c3_policies(60)
     data = batch.synth(workloads.SEED + 1, 1500, kind_mix=1).decode()
     ress = [json.loads(l) for l in data.strip().split("\n")]
-    mism, r, ost = compare(orc, pols, ress, check_paths=True, max_path_checks=200)
+    mism, r, ost = compare(orc, pols, ress, check_paths=True, max_path_checks=200, specialize=spec)
     assert not mism, "\n".join(mism)
     assert (r.status == 5).sum() > 0 and (r.status <= 1).sum() > 0
 
 
-def test_counts_mode_matches_status(orc):
+@engines
+def test_counts_mode_matches_status(orc, spec):
     from kyverno_amd import batch, workloads
 
     pols = workloads.c2_policies()
-    ps = batch.PolicySet(pols)
+    ps = batch.PolicySet(pols, specialize=spec)
     b = batch.Batch(ps, batch.synth(workloads.SEED, 5000))
     full = batch.validate(ps, b)
     counts = batch.validate(ps, b, mode=batch.MODE_COUNTS)
