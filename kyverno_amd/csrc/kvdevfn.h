@@ -362,10 +362,11 @@ __device__ bool selector_match(const DevPS& P, const DevBatch& B, const Res* __r
 }
 
 // doesResourceMatchConditionBlock: number of failed criteria (0 == block matches)
-__device__ uint32_t block_errs(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t rkind,
-                               uint32_t rflags, uint32_t f) {
+// (criteria restricted to the flag bits in `mask`)
+__device__ uint32_t block_errs_masked(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t rkind,
+                                      uint32_t rflags, uint32_t f, uint32_t mask) {
   const MFilter& F = P.filters[f];
-  const uint32_t fl = uni(P.fflags[f]);
+  const uint32_t fl = uni(P.fflags[f]) & mask;
   uint32_t errs = 0;
   if (fl & MF_KINDS) {
     bool ok = false;
@@ -416,6 +417,11 @@ __device__ uint32_t block_errs(const DevPS& P, const DevBatch& B, const Res* __r
   }
   if (fl & MF_UI_FAIL) errs += 1;
   return errs;
+}
+
+__device__ __forceinline__ uint32_t block_errs(const DevPS& P, const DevBatch& B, const Res* __restrict__ R,
+                                               uint32_t rkind, uint32_t rflags, uint32_t f) {
+  return block_errs_masked(P, B, R, rkind, rflags, f, 0xFFFFFFFFu);
 }
 
 __device__ bool rule_matches(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t rkind,

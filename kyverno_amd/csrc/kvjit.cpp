@@ -214,6 +214,78 @@ struct Gen {
     o << "}\n";
   }
 
+  // ---------------------------------------------------------------- match / exclude
+  // blk_ok(f) == !(MF_EMPTY) && doesResourceMatchConditionBlock(f) has no errors
+  // (pkg/engine/utils.go:265-336); MF_EMPTY / MF_UI_FAIL are folded per launch
+  // (user info), so they are read from P.fflags; every other criterion is static.
+  std::set<uint32_t> blks_done;
+  void blk_fn(uint32_t f) {
+    if (!blks_done.insert(f).second) return;
+    const MFilter& F = ps.filters[f];
+    o << "__device__ __forceinline__ bool g_blk_" << f
+      << "(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t rkind, uint32_t rflags) {\n"
+      << "  if (uni(P.fflags[" << f << "]) & (MF_EMPTY | MF_UI_FAIL)) return false;\n";
+    if (F.flags & MF_KINDS) {
+      bool any_star = false;
+      std::ostringstream k;
+      k << "false";
+      for (uint32_t i = F.kinds_first; i < F.kinds_first + F.kinds_count; i++) {
+        const KindSpec& ks = ps.kinds[i];
+        switch (ks.form) {
+          case 3: any_star = true; break;
+          case 0: k << " || rkind == " << u32(ks.kind); break;
+          case 1: k << " || (rkind == " << u32(ks.kind) << " && R->version == " << u32(ks.version) << ")"; break;
+          default:
+            k << " || (R->group == " << u32(ks.group) << " && rkind == " << u32(ks.kind) << " && (R->version == "
+              << u32(ks.version) << " || R->version == P.star_id))";
+            break;
+        }
+      }
+      if (!any_star) o << "  if (!(" << k.str() << ")) return false;\n";
+    }
+    auto glob_any = [&](uint32_t first, uint32_t count, const char* off, const char* len) {
+      o << "  if (!(false";
+      for (uint32_t i = first; i < first + count; i++)
+        o << " || kv_glob(P.pstr + " << u32(ps.strrefs[i].off) << ", " << u32(ps.strrefs[i].len) << ", B.bstr + R->" << off
+          << ", R->" << len << ")";
+      o << ")) return false;\n";
+    };
+    if (F.flags & MF_NAME)
+      o << "  if (!kv_glob(P.pstr + " << u32(F.name_off) << ", " << u32(F.name_len)
+        << ", B.bstr + R->name_off, R->name_len)) return false;\n";
+    if (F.flags & MF_NAMES) glob_any(F.names_first, F.names_count, "name_off", "name_len");
+    if (F.flags & MF_NSS) glob_any(F.nss_first, F.nss_count, "ns_off", "ns_len");
+    if (F.flags & (MF_ANN | MF_SEL))  // rarer criteria: the generic evaluator, restricted to them
+      o << "  if (block_errs_masked(P, B, R, rkind, rflags, " << f << "u, MF_ANN | MF_SEL) != 0u) return false;\n";
+    if (F.flags & MF_NSSEL)
+      o << "  if (!(rflags & (RF_KIND_NAMESPACE | RF_KIND_EMPTY)) && !((B.ns_bits[R->ns_index * B.ns_words + "
+        << (F.nssel_bit / 32) << "u] >> " << (F.nssel_bit % 32) << "u) & 1u)) return false;\n";
+    o << "  return true;\n}\n";
+  }
+
+  // rule_matches (kvdevfn.h) for one rule, with its filter list unrolled
+  void match_fn(uint32_t ri) {
+    const RuleRec& rr = ps.rules[ri];
+    for (uint32_t f = rr.m_first; f < rr.m_first + rr.m_count; f++) blk_fn(f);
+    for (uint32_t f = rr.x_first; f < rr.x_first + rr.x_count; f++) blk_fn(f);
+    auto call = [&](uint32_t f) { return "g_blk_" + std::to_string(f) + "(P, B, R, rkind, rflags)"; };
+    auto combine = [&](uint32_t mode, uint32_t first, uint32_t count) {
+      std::ostringstream e;
+      if (mode == 0 || count == 0) {
+        e << call(first);
+      } else {
+        e << "(";
+        for (uint32_t f = first; f < first + count; f++) e << (f > first ? (mode == 1 ? " || " : " && ") : "") << call(f);
+        e << ")";
+      }
+      return e.str();
+    };
+    o << "__device__ __forceinline__ bool g_match_" << ri
+      << "(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t rkind, uint32_t rflags) {\n"
+      << "  if (!" << combine(rr.m_mode, rr.m_first, rr.m_count) << ") return false;\n"
+      << "  return !" << combine(rr.x_mode, rr.x_first, rr.x_count) << ";\n}\n";
+  }
+
   // ---------------------------------------------------------------- rule programs
   static uint32_t prog_end(const PolicySet& ps, uint32_t pc) {
     while ((ps.prog[pc].op & 0xFF) != OP_DONE) pc++;
@@ -378,7 +450,7 @@ struct Gen {
       o << "  { // rule " << ri << "\n"
         << "    uint32_t st = ST_NOMATCH;\n"
         << "    EState e{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u};\n"
-        << "    if (valid && rule_matches(P, B, R, rkind, rflags, P.rules[" << ri << "])) {\n";
+        << "    if (valid && g_match_" << ri << "(P, B, R, rkind, rflags)) {\n";
       switch (rr.route) {
         case 1: o << "      st = ST_CPU;\n"; break;
         case 2: o << "      st = ST_NOMATCH;\n"; break;
@@ -407,8 +479,10 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   auto t0 = std::chrono::steady_clock::now();
   Gen g(ps);
   g.o << kPrelude << "\nusing namespace kv;\n\n";
-  for (uint32_t ri = 0; ri < ps.rules.size(); ri++)
+  for (uint32_t ri = 0; ri < ps.rules.size(); ri++) {
+    g.match_fn(ri);
     if (ps.rules[ri].route == 0) g.rule_fn(ri);
+  }
   out->chunks.clear();
   const uint32_t n = (uint32_t)ps.rules.size();
   if (chunk_rules == 0) chunk_rules = 32;
