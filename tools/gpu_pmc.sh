@@ -17,14 +17,20 @@ cd "$R"
 for f in $(find gpurun_out/pmc -name "*counter_collection.csv"); do echo "== $f"; python - "$f" <<'PY'
 import csv, sys, collections
 rows = list(csv.DictReader(open(sys.argv[1])))
-agg = collections.defaultdict(list)
+agg = collections.defaultdict(float)  # (kernel, dispatch, counter) -> value summed over dimensions
 for r in rows:
-    if "kv_validate" in r.get("Kernel_Name", ""):
-        agg[(r["Dispatch_Id"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+    k = r.get("Kernel_Name", "")
+    if "kv_validate" in k or "kvj_chunk" in k:
+        agg[(k, r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
 per = collections.defaultdict(list)
-for (d, c), v in agg.items():
-    per[c].append(sum(v))
-for c, v in sorted(per.items()):
-    print(f"{c}: dispatches={len(v)} mean={sum(v)/len(v):.6g}")
+for (k, d, c), v in agg.items():
+    per[(k, c)].append(v)
+tot = collections.defaultdict(float)
+for (k, c), v in sorted(per.items()):
+    m = sum(v) / len(v)
+    tot[c] += m
+    print(f"{k} {c}: dispatches={len(v)} mean={m:.6g}")
+for c, v in sorted(tot.items()):
+    print(f"PER-STEP (sum of kernel means) {c}: {v:.6g}")
 PY
 done
