@@ -479,14 +479,14 @@ int kv_compile(const char* policies_json, size_t len, uint32_t flags, kv_policys
       if (flags & KV_COMPILE_SPECIALIZE) {
         s->jit = std::make_unique<JitImage>();
         const char* ch = getenv("KVGPU_JIT_CHUNK");  // rules per specialized kernel (experiments)
-        jit_generate(s->ps, ch ? (uint32_t)atoi(ch) : 32u, s->jit.get());
+        jit_generate(s->ps, ch ? (uint32_t)atoi(ch) : 16u, s->jit.get());
         if (const char* dump = getenv("KVGPU_JIT_DUMP")) {
           if (FILE* f = fopen(dump, "w")) {
             fwrite(s->jit->source.data(), 1, s->jit->source.size(), f);
             fclose(f);
           }
         }
-        jit_compile(s->jit.get());
+        if (!getenv("KVGPU_JIT_SKIP_COMPILE")) jit_compile(s->jit.get());  // dump-only analysis runs
       }
     } catch (...) {
       delete s;

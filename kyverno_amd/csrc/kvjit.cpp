@@ -14,7 +14,9 @@
 
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <map>
 #include <set>
 #include <sstream>
 #include <stdexcept>
@@ -471,7 +473,553 @@ struct Gen {
       << "    if (v) atomicAdd(&O.counts[(size_t)" << ch.rule_begin << "u * KV_HIST + q], (unsigned long long)v);\n"
       << "  }\n}\n\n";
   }
+
+  // ================================================================ fused chunk kernels
+  // All rules of a chunk run in one kernel body as interleaved sequential
+  // programs. Rules never interact, so any interleaving that keeps each rule's
+  // own op order is exact; the interleaving is chosen to share memory traffic:
+  //  * cursor lookups whose path from the resource root (or from the element
+  //    of a shared array loop) is known statically are hoisted: computed once
+  //    (per kernel, or per loop iteration), just before the first rule that
+  //    walks them, together with the 16-B node they land on;
+  //  * every rule program is split at its top-level array loops into stages;
+  //    at stage k the k-th loops of all rules iterating the same array
+  //    (e.g. spec.containers) become ONE loop whose body runs each active
+  //    rule's loop body for that element.
+  // Per-rule registers: rs (resume pc between stages | ACTIVE bit, or FIN |
+  // status once the rule's DONE ran), ek (error kind | flags << 4 | pattern
+  // node << 8), loop indices of the raise (ei0..), anchor bitsets when used.
+  static constexpr uint32_t FIN = 0x7F000000u, ACT = 0x80000000u;
+
+  struct HVar { std::string idx, node; };  // hoisted cursor: node index var + Node var
+  struct HoistTable {
+    std::string prefix;
+    std::map<std::string, HVar> vars;
+    std::vector<std::string> code;  // one statement group per entry, dependency order
+    size_t flushed = 0;
+    uint32_t n = 0;
+    std::string flush() {
+      std::string s;
+      for (; flushed < code.size(); flushed++) s += code[flushed];
+      return s;
+    }
+  };
+
+  struct RGen {  // per-rule generation state
+    uint32_t ri = 0, b = 0, e = 0, maxd = 1;
+    std::vector<std::pair<uint32_t, uint32_t>> loops;  // stage loops (LOOP_BEGIN pc, LOOP_END pc)
+    std::vector<std::string> expr;                      // symbolic cursor per depth ("" = unknown)
+    std::vector<HVar> hv;                               // hoisted vars per depth (when expr known)
+    std::set<uint32_t> resume;                          // resume targets of later segments
+    bool uses_anchor = false, uses_keyglob = false;
+    uint32_t max_level = 0;
+    std::string s;                                      // "_<ri>"
+  };
+
+  HVar hoist(HoistTable& T, const std::string& pexpr, const HVar& p, uint32_t a, uint32_t aux) {
+    const bool scan = (aux & AUX_SCAN) != 0;
+    const std::string ex = pexpr + (scan ? "/k" : "/s") + std::to_string(a);
+    auto it = T.vars.find(ex);
+    if (it != T.vars.end()) return it->second;
+    HVar h{T.prefix + "h" + std::to_string(T.n), T.prefix + "hn" + std::to_string(T.n)};
+    T.n++;
+    std::ostringstream c;
+    c << "  uint32_t " << h.idx << " = ABSENT; Node " << h.node << "{0u, 0u, 0u, 0u};\n";
+    if (scan) {
+      c << "  if (node_type(" << p.node << ".kt) == NT_MAP) for (uint32_t q_ = 0u; q_ < " << p.node << ".b; q_++) { "
+        << "const uint32_t c_ = ni(" << p.node << ".a + q_); const Node t_ = N[c_]; if (node_key(t_.kt) == " << u32(a)
+        << ") { " << h.idx << " = c_; " << h.node << " = t_; break; } }\n";
+    } else {
+      c << "  if (node_type(" << p.node << ".kt) == NT_MAP && " << u32(a) << " < " << p.node << ".b) { "
+        << "const uint32_t c_ = ni(" << p.node << ".a + " << u32(a) << "); const Node t_ = N[c_]; "
+        << "if (node_type(t_.kt) != NT_ABSENT) { " << h.idx << " = c_; " << h.node << " = t_; } }\n";
+    }
+    T.code.push_back(c.str());
+    T.vars.emplace(ex, h);
+    return h;
+  }
+
+  // a region of one rule's program: a segment between stage loops (kind 0) or
+  // the body of a fused loop (kind 1)
+  struct Region {
+    int kind = 0;
+    uint32_t rb = 0, re = 0;  // ops emitted: [rb, re)
+    uint32_t jre = 0;         // local jump targets: [rb, jre)
+    std::string se;           // segment end label
+    std::string li0;          // level-0 loop index expression
+    HoistTable* T = nullptr;  // hoist table for exprs rooted at this region's loop element
+    std::string troot;        // expr root of T
+  };
+
+  HoistTable* gT = nullptr;  // global (root-derived) hoist table of the current chunk
+
+  void emit_region(RGen& g, const Region& R, std::ostringstream& w) {
+    const std::string& s = g.s;
+    auto C = [&](uint32_t d) { return "c" + std::to_string(d) + s; };
+    auto L = [&](uint32_t pc) { return "R" + std::to_string(g.ri) + "_L" + std::to_string(pc); };
+    auto jump = [&](uint32_t t) -> std::string {
+      if (t >= R.rb && t < R.jre) return "goto " + L(t) + ";";
+      if (R.kind == 0 && t >= R.jre) {
+        g.resume.insert(t);
+        return "{ rs" + s + " = " + u32(t) + "; goto " + R.se + "; }";
+      }
+      throw std::runtime_error("kvjit: jump out of a fused region (rule " + std::to_string(g.ri) + ")");
+    };
+    auto finish = [&](const std::string& st) {
+      if (R.kind != 0) throw std::runtime_error("kvjit: rule end inside a fused loop");
+      return "{ rs" + s + " = FIN_ | " + st + "; goto " + R.se + "; }";
+    };
+    auto li = [&](uint32_t lv) { return lv == 0 && R.kind == 1 ? R.li0 : "li" + std::to_string(lv) + s; };
+    auto raise = [&](const std::string& kind, uint32_t pn, uint32_t catch_pc) {
+      if (pn >= (1u << 24)) throw std::runtime_error("kvjit: pattern node id exceeds 24 bits");
+      std::ostringstream r;
+      r << "{ ek" << s << " = " << kind << " | " << u32(pn << 8) << ";";
+      for (uint32_t lv = 0; lv <= g.max_level && lv < 4; lv++) r << " ei" << lv << s << " = " << li(lv) << ";";
+      if (g.uses_keyglob) r << " ekn" << s << " = kn" << s << ";";
+      r << " " << jump(catch_pc) << " }";
+      return r.str();
+    };
+    auto known = [&](uint32_t d) {
+      if (d >= g.expr.size() || g.expr[d].empty()) return false;
+      const std::string& ex = g.expr[d];
+      return ex[0] == 'R' || (R.T && ex.compare(0, R.troot.size(), R.troot) == 0);
+    };
+    auto NODE = [&](uint32_t d) -> std::string {
+      if (known(d)) return g.hv[d].node;
+      return "N[" + C(d) + "]";
+    };
+    auto table_for = [&](uint32_t d) -> HoistTable* {
+      const std::string& ex = g.expr[d];
+      if (ex[0] == 'R') return gT;
+      if (R.T && ex.compare(0, R.troot.size(), R.troot) == 0) return R.T;
+      return nullptr;
+    };
+    auto set_unknown = [&](uint32_t from) {
+      for (uint32_t x = from; x < g.expr.size(); x++) g.expr[x].clear();
+    };
+    // key lookup: returns the index expression; records the child cursor expr at d+1 when assign
+    auto lookup = [&](uint32_t d, uint32_t a, uint32_t aux, bool assign) -> std::string {
+      const uint32_t laux = aux & AUX_SCAN;
+      HoistTable* T = known(d) ? table_for(d) : nullptr;
+      if (T) {
+        HVar h = hoist(*T, g.expr[d], g.hv[d], a, laux);
+        if (assign) {
+          set_unknown(d + 1);
+          g.expr[d + 1] = g.expr[d] + (laux ? "/k" : "/s") + std::to_string(a);
+          g.hv[d + 1] = h;
+        }
+        return h.idx;
+      }
+      if (assign) set_unknown(d + 1);
+      return "lookup_op(N, " + C(d) + ", " + u32(a) + ", " + u32(laux) + ")";
+    };
+    const std::string ek = "ek" + s;
+    const std::string kindof = "(" + ek + " & 15u)";
+
+    for (uint32_t pc = R.rb; pc < R.re; pc++) {
+      const Inst& in = ps.prog[pc];
+      const uint32_t op = in.op & 0xFF, d = (in.op >> 8) & 0xFF, aux = (in.op >> 16) & 0xFF;
+      const std::string cd = C(d), cn = C(d + 1);
+      const uint32_t lv = aux & 3;
+      const std::string L_lv = std::to_string(lv);
+      w << L(pc) << ":;\n";
+      switch (op) {
+        case OP_MAPCHK:
+        case OP_ARRCHK: {
+          const char* t = op == OP_MAPCHK ? "NT_MAP" : "NT_ARR";
+          if (known(d)) w << "  if (node_type(" << NODE(d) << ".kt) != " << t << ") ";
+          else w << "  if (" << cd << " == ABSENT || node_type(N[" << cd << "].kt) != " << t << ") ";
+          w << raise(op == OP_MAPCHK ? "E_TYPE_MAP" : "E_TYPE_ARR", in.a, in.c) << "\n";
+          break;
+        }
+        case OP_AREG: {
+          const std::string bit = "(1ull << " + std::to_string(aux & 63) + ")";
+          w << "  areg" << s << " |= " << bit << "; if (" << lookup(d, in.a, aux, false) << " != ABSENT) apres" << s
+            << " |= " << bit << ";\n";
+          break;
+        }
+        case OP_KEY: {
+          std::string x = lookup(d, in.a, aux, true);
+          w << "  " << cn << " = " << x << "; if (" << cn << " == ABSENT) " << jump(in.b) << "\n";
+          break;
+        }
+        case OP_KEYV: {
+          std::string x = lookup(d, in.a, aux, true);
+          w << "  " << cn << " = " << x << ";\n";
+          break;
+        }
+        case OP_KEYGLOB:
+          set_unknown(d + 1);
+          w << "  { uint32_t nd_; if (!keyglob_op(P, B, N, " << cd << ", " << u32(in.op) << ", " << u32(in.a) << ", "
+            << u32(in.c) << ", &nd_, &kn" << s << ")) " << jump(in.b) << " " << cn << " = nd_; }\n";
+          break;
+        case OP_SCOPE_END:
+          if (in.c == 0) w << "  if (" << kindof << ") " << ek << " |= " << u32(aux << 4) << ";\n";
+          else w << "  if (" << kindof << ") { " << ek << " |= " << u32(aux << 4) << "; " << jump(in.c) << " }\n";
+          break;
+        case OP_POS_END:
+          w << "  if (" << kindof << ") { if (" << ek << " & " << u32(EF_COND << 4) << ") " << ek << " = 0u; else "
+            << jump(in.c) << " }\n";
+          break;
+        case OP_NEG:
+          w << "  if (" << lookup(d, in.a, aux, false) << " != ABSENT) " << raise("E_NEG", in.b, in.c) << "\n";
+          break;
+        case OP_STAR:
+          if (known(d + 1)) w << "  if (node_type(" << NODE(d + 1) << ".kt) == NT_NULL) ";
+          else w << "  if (" << cn << " == ABSENT || node_type(N[" << cn << "].kt) == NT_NULL) ";
+          w << raise("E_STAR", in.b, in.c) << "\n";
+          break;
+        case OP_LEAF:
+          if (known(d)) w << "  { const Node vn_ = " << NODE(d) << ";\n";
+          else w << "  { Node vn_{0u, 0u, 0u, 0u}; if (" << cd << " != ABSENT) vn_ = N[" << cd << "];\n";
+          w << "    const uint32_t vt_ = node_type(vn_.kt); bool ok_;\n"
+            << "    if (vt_ == NT_ARR) { ok_ = true; for (uint32_t k_ = 0; k_ < vn_.b && ok_; k_++) { const Node en_ = "
+               "N[ni(vn_.a + k_)]; ok_ = g_pred_"
+            << in.a << "(V, S, pstr, node_type(en_.kt), en_); } }\n"
+            << "    else ok_ = g_pred_" << in.a << "(V, S, pstr, vt_, vn_);\n"
+            << "    if (!ok_) " << raise("E_VALUE", in.b, in.c) << " }\n";
+          break;
+        case OP_RAISE:
+          w << "  " << raise(u32(in.b), in.a, in.c) << "\n";
+          break;
+        case OP_EXISTCHK:
+          if (known(d)) w << "  if (node_type(" << NODE(d) << ".kt) != NT_ARR) ";
+          else w << "  if (" << cd << " == ABSENT || node_type(N[" << cd << "].kt) != NT_ARR) ";
+          w << raise("E_EXIST_RESTYPE", in.a, in.c) << "\n";
+          break;
+        case OP_LENCHK:
+          w << "  if (" << NODE(d) << ".b < " << u32(in.a) << ") " << raise("E_LEN", in.b, in.c) << "\n";
+          break;
+        case OP_INDEX:
+          w << "  " << cn << " = ni(" << NODE(d) << ".a + " << u32(in.a) << ");\n";
+          set_unknown(d + 1);
+          break;
+        case OP_LOOP_BEGIN:
+          if (R.kind == 0 && lv == 0) {  // stage loop: hand over to the fused loop
+            set_unknown(d + 1);
+            w << "  { rs" << s << " = " << u32(in.a + 1) << " | ACT_; goto " << R.se << "; }\n";
+            break;
+          }
+          [[fallthrough]];  // nested loop, per rule
+        case OP_EXIST_BEGIN:
+          set_unknown(d + 1);
+          w << "  { const Node an_ = " << NODE(d) << "; lf" << L_lv << s << " = an_.a; ll" << L_lv << s << " = an_.b; li"
+            << L_lv << s << " = 0u;\n    if (an_.b == 0u) ";
+          if (op == OP_LOOP_BEGIN) w << jump(in.a + 1);
+          else w << raise("E_EXIST_FAIL", in.b, in.c);
+          w << "\n    " << cn << " = ni(an_.a); }\n";
+          break;
+        case OP_LOOP_END:
+          w << "  if (" << kindof << ") { if (" << ek << " & " << u32(EF_COND << 4) << ") " << ek << " = 0u; else "
+            << jump(in.c) << " }\n"
+            << "  if (li" << L_lv << s << " + 1u < ll" << L_lv << s << ") { li" << L_lv << s << "++; " << cn << " = ni(lf"
+            << L_lv << s << " + li" << L_lv << s << "); " << jump(in.a + 1) << " }\n";
+          set_unknown(d + 1);
+          break;
+        case OP_EXIST_END:
+          w << "  if (!" << kindof << ") " << jump(pc + 1) << "\n  " << ek << " = 0u;\n"
+            << "  if (li" << L_lv << s << " + 1u < ll" << L_lv << s << ") { li" << L_lv << s << "++; " << cn << " = ni(lf"
+            << L_lv << s << " + li" << L_lv << s << "); " << jump(in.a + 1) << " }\n"
+            << "  " << raise("E_EXIST_FAIL", in.b, in.c) << "\n";
+          set_unknown(d + 1);
+          break;
+        case OP_ALT_BEGIN:
+          w << "  " << ek << " = 0u;";
+          if (g.uses_anchor) w << " areg" << s << " = 0ull; apres" << s << " = 0ull;";
+          w << "\n";
+          break;
+        case OP_ALT_END:
+          w << "  if (" << kindof << " == 0u) " << finish("ST_PASS") << "\n  if (" << kindof << " == E_CPU) "
+            << finish("ST_CPU") << "\n";
+          if (in.b) w << "  " << finish("ST_FAIL") << "\n";
+          else {
+            w << "  " << ek << " = 0u;";
+            if (g.uses_anchor) w << " areg" << s << " = 0ull; apres" << s << " = 0ull;";
+            w << "\n";
+          }
+          break;
+        case OP_DONE:
+          w << "  if (" << kindof << " == 0u) " << finish("ST_PASS") << "\n"
+            << "  if (" << kindof << " == E_CPU) " << finish("ST_CPU") << "\n"
+            << "  if (" << ek << " & " << u32((EF_COND | EF_GLOBAL) << 4) << ") " << finish("ST_SKIP") << "\n";
+          if (g.uses_anchor) w << "  if (areg" << s << " & ~apres" << s << ") " << finish("ST_ERROR") << "\n";
+          w << "  if (" << kindof << " == E_LEN) " << finish("ST_ERROR") << "\n"
+            << "  " << finish("ST_FAIL") << "\n";
+          break;
+        default:  // OP_NOP, OP_METACHK (handled per resource by RF_BAD_META)
+          break;
+      }
+    }
+  }
+
+  RGen analyze(uint32_t ri) {
+    RGen g;
+    g.ri = ri;
+    g.s = "_" + std::to_string(ri);
+    g.b = ps.rules[ri].prog;
+    g.e = prog_end(ps, g.b);
+    int nest = 0;
+    for (uint32_t pc = g.b; pc <= g.e; pc++) {
+      const Inst& in = ps.prog[pc];
+      const uint32_t op = in.op & 0xFF, d = (in.op >> 8) & 0xFF, aux = (in.op >> 16) & 0xFF;
+      g.maxd = std::max(g.maxd, d + 2);
+      if (op == OP_AREG) g.uses_anchor = true;
+      if (op == OP_KEYGLOB) g.uses_keyglob = true;
+      if (op == OP_LOOP_BEGIN || op == OP_EXIST_BEGIN) {
+        if (op == OP_LOOP_BEGIN && nest == 0 && (aux & 3) == 0) g.loops.push_back({pc, in.a});
+        g.max_level = std::max(g.max_level, aux & 3);
+        nest++;
+      } else if (op == OP_LOOP_END || op == OP_EXIST_END) {
+        nest--;
+      }
+    }
+    g.expr.assign(g.maxd + 1, "");
+    g.hv.assign(g.maxd + 1, HVar{});
+    g.expr[0] = "R";
+    g.hv[0] = HVar{"root", "rootn"};
+    return g;
+  }
+
+  void chunk_kernel_fused(const JitChunk& ch) {
+    const uint32_t nr = (uint32_t)ch.rules.size();
+    std::vector<RGen> gs;
+    HoistTable global;
+    global.prefix = "g";
+    gT = &global;
+    size_t K = 0;
+    for (uint32_t ri : ch.rules) {
+      if (ps.rules[ri].route != 0) continue;
+      RGen g = analyze(ri);
+      for (uint32_t pc = g.b; pc <= g.e; pc++)
+        if ((ps.prog[pc].op & 0xFF) == OP_LEAF) pred_fn(ps.prog[pc].a);
+      K = std::max(K, g.loops.size());
+      gs.push_back(std::move(g));
+    }
+    std::ostringstream body;  // everything after the per-rule declarations
+    for (size_t k = 0; k <= K; k++) {
+      for (RGen& g : gs) {
+        if (k > g.loops.size()) continue;
+        const uint32_t sb = k == 0 ? g.b : g.loops[k - 1].second + 1;
+        const uint32_t se = k < g.loops.size() ? g.loops[k].first + 1 : g.e + 1;  // include the LOOP_BEGIN
+        Region R;
+        R.kind = 0;
+        R.rb = sb;
+        R.re = se;
+        R.jre = se;
+        R.se = "R" + std::to_string(g.ri) + "_S" + std::to_string(k);
+        std::ostringstream w;
+        emit_region(g, R, w);
+        // hoisted lookups first used by this segment, then the resume dispatch
+        body << global.flush() << "  // rule " << g.ri << " stage " << k << "\n  switch (rs" << g.s << ") {\n";
+        if (k == 0) body << "    case " << u32(g.b) << ": goto R" << g.ri << "_L" << g.b << ";\n";
+        for (uint32_t t : g.resume)
+          if (t >= sb && t < se) body << "    case " << u32(t) << ": goto R" << g.ri << "_L" << t << ";\n";
+        body << "    default: goto " << R.se << ";\n  }\n" << w.str() << R.se << ":;\n";
+      }
+      if (k == K) break;
+      // fused loops of stage k: group rules by the symbolic array cursor
+      std::map<std::string, std::vector<RGen*>> groups;
+      std::vector<std::string> order;
+      for (RGen& g : gs) {
+        if (k >= g.loops.size()) continue;
+        const uint32_t lb = g.loops[k].first;
+        const uint32_t d = (ps.prog[lb].op >> 8) & 0xFF;
+        std::string key = g.expr[d].empty() ? "U" + std::to_string(g.ri) : g.expr[d];
+        if (!groups.count(key)) order.push_back(key);
+        groups[key].push_back(&g);
+      }
+      uint32_t li = 0;
+      for (const std::string& key : order) {
+        std::vector<RGen*>& grp = groups[key];
+        const std::string tag = std::to_string(k) + "_" + std::to_string(li++);
+        const RGen& g0 = *grp[0];
+        const uint32_t d0 = (ps.prog[g0.loops[k].first].op >> 8) & 0xFF;
+        const std::string arr_node = key[0] == 'U' ? "N[c" + std::to_string(d0) + g0.s + "]" : g0.hv[d0].node;
+        HoistTable T;
+        T.prefix = "l" + tag + "_";
+        const std::string troot = "E" + tag;
+        std::ostringstream bodies;
+        for (RGen* gp : grp) {
+          RGen& g = *gp;
+          const uint32_t lb = g.loops[k].first, le = g.loops[k].second;
+          const uint32_t d = (ps.prog[lb].op >> 8) & 0xFF;
+          g.expr[d + 1] = troot;
+          g.hv[d + 1] = HVar{"el" + tag, "eln" + tag};
+          Region R;
+          R.kind = 1;
+          R.rb = lb + 1;
+          R.re = le;  // LOOP_END emitted below
+          R.jre = le + 1;
+          R.li0 = "fli" + tag;
+          R.T = &T;
+          R.troot = troot;
+          std::ostringstream w;
+          emit_region(g, R, w);
+          const Inst& end = ps.prog[le];
+          bodies << T.flush() << "    if (rs" << g.s << " & ACT_) {\n      c" << (d + 1) << g.s << " = el" << tag << ";\n"
+                 << w.str() << "R" << g.ri << "_L" << le << ":;\n"
+                 << "      if (ek" << g.s << " & 15u) { if (ek" << g.s << " & " << u32(EF_COND << 4) << ") ek" << g.s
+                 << " = 0u; else rs" << g.s << " = " << u32(end.c) << "; }\n    }\n";
+          if (end.c <= le) throw std::runtime_error("kvjit: loop exit target inside the loop");
+          g.resume.insert(end.c);
+          g.resume.insert(le + 1);
+          for (uint32_t x = d + 1; x < g.expr.size(); x++) g.expr[x].clear();  // loop-local exprs end here
+        }
+        body << "  { // fused loop " << tag << " over " << key << " (" << grp.size() << " rules)\n"
+             << "    uint32_t fn" << tag << " = 0u, ff" << tag << " = 0u;\n    if ((0u";
+        for (RGen* gp : grp) body << " | rs" << gp->s;
+        body << ") & ACT_) { const Node an_ = " << arr_node << "; ff" << tag << " = an_.a; fn" << tag << " = an_.b; }\n"
+             << "    for (uint32_t fli" << tag << " = 0u; fli" << tag << " < fn" << tag << "; fli" << tag << "++) {\n"
+             << "      const uint32_t el" << tag << " = ni(ff" << tag << " + fli" << tag << ");\n"
+             << "      const Node eln" << tag << " = N[el" << tag << "];\n"
+             << bodies.str() << "    }\n";
+        for (RGen* gp : grp) body << "    rs" << gp->s << " &= ~ACT_;\n";
+        body << "  }\n";
+      }
+    }
+    // every resume pc must lie in a segment (else the rule would never finish)
+    for (const RGen& g : gs)
+      for (uint32_t t : g.resume) {
+        bool ok = false;
+        for (size_t k = 0; k <= g.loops.size() && !ok; k++) {
+          const uint32_t sb = k == 0 ? g.b : g.loops[k - 1].second + 1;
+          const uint32_t se = k < g.loops.size() ? g.loops[k].first + 1 : g.e + 1;
+          ok = t >= sb && t < se;
+        }
+        if (!ok) throw std::runtime_error("kvjit: resume target " + std::to_string(t) + " of rule " +
+                                         std::to_string(g.ri) + " is not in a segment");
+      }
+
+    // kernel (rule ids of the chunk's histogram rows in a device table)
+    o << "__device__ const uint32_t " << ch.name << "_rules[" << nr << "] = {";
+    for (uint32_t q = 0; q < nr; q++) o << (q ? ", " : "") << u32(ch.rules[q]);
+    o << "};\n";
+    o << "extern \"C\" __global__ __launch_bounds__(KV_WG) void " << ch.name
+      << "(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp, const Node* __restrict__ N, "
+         "const Val* __restrict__ V, const uint8_t* __restrict__ S, DevOut O) {\n"
+      << "  constexpr uint32_t FIN_ = " << u32(FIN) << ", ACT_ = " << u32(ACT) << ";\n"
+      << "  __shared__ uint32_t s_hist[" << nr << "][KV_HIST];\n"
+      << "  const DevPS& P = *Pp;\n  const DevBatch& B = *Bp;\n  const uint8_t* __restrict__ pstr = P.pstr;\n"
+      << "  for (uint32_t q = threadIdx.x; q < " << nr << "u * KV_HIST; q += KV_WG) (&s_hist[0][0])[q] = 0u;\n"
+      << "  __syncthreads();\n"
+      << "  const uint32_t r = blockIdx.x * KV_WG + threadIdx.x;\n"
+      << "  const uint32_t n_res = B.n_res;\n"
+      << "  const bool valid = r < n_res;\n"
+      << "  const Res* __restrict__ R = B.res + (valid ? r : 0u);\n"
+      << "  uint32_t root = ABSENT, rkind = KEY_NONE, rflags = 0u;\n"
+      << "  if (valid) { root = ni(R->root); rkind = R->kind; rflags = R->flags; }\n"
+      << "  Node rootn{0u, 0u, 0u, 0u};\n  if (valid) rootn = N[root];\n";
+    // per-rule state (rules of other routes only carry rs = FIN | status)
+    for (uint32_t ri : ch.rules) o << "  uint32_t rs_" << ri << " = FIN_ | ST_NOMATCH;\n";
+    for (const RGen& g : gs) {
+      const std::string& s = g.s;
+      o << "  uint32_t ek" << s << " = 0u";
+      for (uint32_t lv = 0; lv <= g.max_level && lv < 4; lv++) o << ", ei" << lv << s << " = 0u";
+      if (g.uses_keyglob) o << ", kn" << s << " = ABSENT, ekn" << s << " = ABSENT";
+      o << ";\n";
+      if (g.uses_anchor) o << "  uint64_t areg" << s << " = 0ull, apres" << s << " = 0ull;\n";
+      o << "  uint32_t c0" << s << " = root";
+      for (uint32_t d = 1; d < g.maxd; d++) o << ", c" << d << s << " = ABSENT";
+      o << ";\n";
+      if (g.max_level > 0 || !g.loops.empty() || true) {
+        o << "  uint32_t";
+        for (uint32_t l = 0; l <= g.max_level && l < 4; l++)
+          o << (l ? "," : "") << " li" << l << s << " = 0u, lf" << l << s << " = 0u, ll" << l << s << " = 0u";
+        o << ";\n";
+      }
+    }
+    // match / route
+    for (uint32_t ri : ch.rules) {
+      const RuleRec& rr = ps.rules[ri];
+      const std::string s = "_" + std::to_string(ri);
+      o << "  if (valid && g_match_" << ri << "(P, B, R, rkind, rflags)) {\n";
+      switch (rr.route) {
+        case 1: o << "    rs" << s << " = FIN_ | ST_CPU;\n"; break;
+        case 2: o << "    rs" << s << " = FIN_ | ST_NOMATCH;\n"; break;
+        case 3: o << "    rs" << s << " = FIN_ | " << u32(rr.const_status) << ";\n"; break;
+        default:
+          o << "    if (rflags & RF_MAGIC) rs" << s << " = FIN_ | ST_CPU;\n";
+          if (rr.flags & RR_META_EXPAND) o << "    else if (rflags & RF_BAD_META) rs" << s << " = FIN_ | ST_CPU;\n";
+          o << "    else rs" << s << " = " << u32(rr.prog) << ";\n";
+          break;
+      }
+      o << "  }\n";
+    }
+    o << body.str();
+    std::set<uint32_t> gpu;
+    for (const RGen& g : gs) gpu.insert(g.ri);
+    for (uint32_t q = 0; q < nr; q++) {
+      const uint32_t ri = ch.rules[q];
+      const std::string s = "_" + std::to_string(ri);
+      if (gpu.count(ri)) {
+        const RGen* g = nullptr;
+        for (const RGen& x : gs)
+          if (x.ri == ri) g = &x;
+        o << "  { EState e_{ek" << s << " & 15u, (ek" << s << " >> 4) & 15u, ek" << s << " >> 8, "
+          << (g->uses_keyglob ? "ekn" + s : std::string("ABSENT")) << ", ABSENT";
+        for (uint32_t lv = 0; lv < 4; lv++) o << ", " << (lv <= g->max_level ? "ei" + std::to_string(lv) + s : "0u");
+        o << "};\n";
+      } else {
+        o << "  { EState e_{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u};\n";
+      }
+      o << "    store_result(O, " << ri << "u, n_res, r, valid, rs" << s << " & 0xFFu, e_, &s_hist[" << q << "][0]); }\n";
+    }
+    o << "  __syncthreads();\n"
+      << "  for (uint32_t q = threadIdx.x; q < " << nr << "u * KV_HIST; q += KV_WG) {\n"
+      << "    const uint32_t v = (&s_hist[0][0])[q];\n"
+      << "    if (v) atomicAdd(&O.counts[(size_t)" << ch.name << "_rules[q / KV_HIST] * KV_HIST + q % KV_HIST], "
+         "(unsigned long long)v);\n"
+      << "  }\n}\n\n";
+  }
 };
+
+// Sort key grouping rules with the same walk: the symbolic path of the first
+// top-level array loop, then the sorted paths of the leaves it tests.
+std::string rule_signature(const PolicySet& ps, uint32_t ri) {
+  std::vector<std::string> expr(64);
+  expr[0] = "R";
+  std::string arr;
+  std::vector<std::string> leaves;
+  int nest = 0;
+  for (uint32_t pc = ps.rules[ri].prog;; pc++) {
+    const Inst& in = ps.prog[pc];
+    const uint32_t op = in.op & 0xFF, d = (in.op >> 8) & 0xFF, aux = (in.op >> 16) & 0xFF;
+    if (op == OP_DONE || d + 1 >= expr.size()) break;
+    switch (op) {
+      case OP_KEY:
+      case OP_KEYV:
+        expr[d + 1] = expr[d].empty() ? "" : expr[d] + ((aux & AUX_SCAN) ? "/k" : "/s") + std::to_string(in.a);
+        break;
+      case OP_LEAF:
+        leaves.push_back(expr[d]);
+        break;
+      case OP_LOOP_BEGIN:
+      case OP_EXIST_BEGIN:
+        if (op == OP_LOOP_BEGIN && nest == 0 && arr.empty()) {
+          arr = expr[d].empty() ? "?" : expr[d];
+          expr[d + 1] = "E";
+        } else {
+          expr[d + 1].clear();
+        }
+        nest++;
+        break;
+      case OP_LOOP_END:
+      case OP_EXIST_END:
+        nest--;
+        break;
+      case OP_KEYGLOB:
+      case OP_INDEX:
+        expr[d + 1].clear();
+        break;
+      default:
+        break;
+    }
+  }
+  std::sort(leaves.begin(), leaves.end());
+  std::string sig = (arr.empty() ? "~" : arr) + "|";
+  for (auto& l : leaves) sig += l + ",";
+  return sig;
+}
 
 }  // namespace
 
@@ -479,20 +1027,38 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   auto t0 = std::chrono::steady_clock::now();
   Gen g(ps);
   g.o << kPrelude << "\nusing namespace kv;\n\n";
+  // KVGPU_JIT_FUSE=0: one device function per rule (no cross-rule sharing), for A/B runs
+  const char* fz = getenv("KVGPU_JIT_FUSE");
+  const bool fused = !(fz && fz[0] == '0');
   for (uint32_t ri = 0; ri < ps.rules.size(); ri++) {
     g.match_fn(ri);
-    if (ps.rules[ri].route == 0) g.rule_fn(ri);
+    if (!fused && ps.rules[ri].route == 0) g.rule_fn(ri);
   }
   out->chunks.clear();
   const uint32_t n = (uint32_t)ps.rules.size();
   if (chunk_rules == 0) chunk_rules = 32;
-  for (uint32_t b = 0; b < n; b += chunk_rules) {
-    JitChunk ch;
-    ch.rule_begin = b;
-    ch.rule_end = std::min(n, b + chunk_rules);
-    ch.name = "kvj_chunk_" + std::to_string(out->chunks.size());
-    g.chunk_kernel(ch);
-    out->chunks.push_back(ch);
+  if (!fused) {
+    for (uint32_t b = 0; b < n; b += chunk_rules) {
+      JitChunk ch;
+      ch.rule_begin = b;
+      ch.rule_end = std::min(n, b + chunk_rules);
+      ch.name = "kvj_chunk_" + std::to_string(out->chunks.size());
+      g.chunk_kernel(ch);
+      out->chunks.push_back(ch);
+    }
+  } else {
+    // rules that walk the same arrays and leaves share a kernel (and its hoisted lookups)
+    std::vector<std::pair<std::string, uint32_t>> order;
+    for (uint32_t ri = 0; ri < n; ri++)
+      order.push_back({ps.rules[ri].route == 0 ? "0" + rule_signature(ps, ri) : "1", ri});
+    std::stable_sort(order.begin(), order.end());
+    for (uint32_t b = 0; b < n; b += chunk_rules) {
+      JitChunk ch;
+      for (uint32_t q = b; q < std::min(n, b + chunk_rules); q++) ch.rules.push_back(order[q].second);
+      ch.name = "kvj_chunk_" + std::to_string(out->chunks.size());
+      g.chunk_kernel_fused(ch);
+      out->chunks.push_back(ch);
+    }
   }
   out->source = g.o.str();
   out->gen_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -13,7 +13,8 @@
 namespace kvh {
 
 struct JitChunk {
-  uint32_t rule_begin = 0, rule_end = 0;  // rules [begin, end) evaluated by kernel `name`
+  uint32_t rule_begin = 0, rule_end = 0;  // unfused kernels: rules [begin, end) evaluated by kernel `name`
+  std::vector<uint32_t> rules;            // fused kernels: the rules evaluated by kernel `name`
   std::string name;
 };
 
