@@ -181,6 +181,13 @@ DevPolicySet& dev_ps(kv_policyset* s, int device) {
       hipFunction_t f;
       HIPCHK(hipModuleGetFunction(&f, d->mod, ch.name.c_str()));
       d->fns.push_back(f);
+      if (getenv("KVGPU_VERBOSE")) {  // register / scratch use of each specialized kernel
+        int regs = 0, local = 0;
+        (void)hipFuncGetAttribute(&regs, HIP_FUNC_ATTRIBUTE_NUM_REGS, f);
+        (void)hipFuncGetAttribute(&local, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, f);
+        fprintf(stderr, "[kvgpu] %s: %zu rules, %d VGPRs, %d B scratch/lane\n", ch.name.c_str(),
+                ch.rules.empty() ? (size_t)(ch.rule_end - ch.rule_begin) : ch.rules.size(), regs, local);
+      }
     }
   }
   auto& ref = *d;
@@ -479,7 +486,7 @@ int kv_compile(const char* policies_json, size_t len, uint32_t flags, kv_policys
       if (flags & KV_COMPILE_SPECIALIZE) {
         s->jit = std::make_unique<JitImage>();
         const char* ch = getenv("KVGPU_JIT_CHUNK");  // rules per specialized kernel (experiments)
-        jit_generate(s->ps, ch ? (uint32_t)atoi(ch) : 16u, s->jit.get());
+        jit_generate(s->ps, ch ? (uint32_t)atoi(ch) : 8u, s->jit.get());
         if (const char* dump = getenv("KVGPU_JIT_DUMP")) {
           if (FILE* f = fopen(dump, "w")) {
             fwrite(s->jit->source.data(), 1, s->jit->source.size(), f);

@@ -469,6 +469,36 @@ struct EState {
   uint32_t kind, flags, pn, key, res, i0, i1, i2, i3;
 };
 
+// status + error record (FAIL/ERROR/SKIP) + per-rule histogram with the
+// common statuses counted by one ballot each (fused specialized kernels)
+__device__ __forceinline__ void store_result2(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, bool valid,
+                                              uint32_t st, const EState& e, uint32_t* hist) {
+  if (valid && (O.full & 1)) {
+    const size_t o = (size_t)ri * n_res + r;
+    O.status[o] = (uint8_t)st;
+    if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP)) {
+      uint4* x = (uint4*)(O.err + o);
+      x[0] = make_uint4(e.kind | (e.flags << 16), e.pn, e.key, e.res);
+      x[1] = make_uint4(e.i0, e.i1, e.i2, e.i3);
+    }
+  }
+  const uint64_t m_pass = __ballot(valid && st == ST_PASS), m_fail = __ballot(valid && st == ST_FAIL);
+  const uint64_t m_nm = __ballot(valid && st == ST_NOMATCH);
+  const uint64_t m_rest = __ballot(valid && st != ST_PASS && st != ST_FAIL && st != ST_NOMATCH);
+  if ((threadIdx.x & 63) == 0) {
+    if (m_pass) atomicAdd(&hist[ST_PASS], (uint32_t)__popcll(m_pass));
+    if (m_fail) atomicAdd(&hist[ST_FAIL], (uint32_t)__popcll(m_fail));
+    if (m_nm) atomicAdd(&hist[ST_NOMATCH], (uint32_t)__popcll(m_nm));
+  }
+  if (m_rest) {
+    for (uint32_t s = ST_WARN; s <= ST_CPU; s++) {
+      if (s == ST_NOMATCH) continue;
+      const uint64_t bm = __ballot(valid && st == s);
+      if (bm && (threadIdx.x & 63) == 0) atomicAdd(&hist[s], (uint32_t)__popcll(bm));
+    }
+  }
+}
+
 // status[rule][res] (+ error record for FAIL/ERROR/SKIP) and the per-rule
 // status histogram (one LDS atomic per wave and status)
 __device__ __forceinline__ void store_result(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, bool valid,

@@ -117,9 +117,39 @@ struct Gen {
     }
     for (uint32_t i = i0; i < i1; i++) {
       const GSeg& sg = segs[i];
-      o << "  { bool found = false;\n"
-        << "    for (uint32_t k = pos; k + " << u32(sg.len) << " <= end; k++)\n"
-        << "      if (" << seg_expr(sg, "k", false) << ") { pos = k + " << u32(sg.len) << "; found = true; break; }\n"
+      // leftmost occurrence of the segment in [pos, end): candidates are the
+      // positions of its first literal byte, found 4 bytes at a time (SWAR
+      // zero-byte test, exact: it never misses a match, false candidates are
+      // rejected by the full word compare)
+      int32_t j = -1;
+      uint32_t cbyte = 0;
+      for (uint32_t q = 0; q < sg.len && j < 0; q++) {
+        const GWord& gw = ps.gwords[sg.wfirst + q / 4];
+        if ((gw.mask >> (8 * (q % 4))) & 0xFFu) {
+          j = (int32_t)q;
+          cbyte = (gw.w >> (8 * (q % 4))) & 0xFFu;
+        }
+      }
+      if (j < 0) {  // all-'?' segment: plain scan
+        o << "  { bool found = false;\n"
+          << "    for (uint32_t k = pos; k + " << u32(sg.len) << " <= end; k++)\n"
+          << "      if (" << seg_expr(sg, "k", false) << ") { pos = k + " << u32(sg.len) << "; found = true; break; }\n"
+          << "    if (!found) return false; }\n";
+        continue;
+      }
+      o << "  { if (end < pos + " << u32(sg.len) << ") return false;\n"
+        << "    const uint32_t plo = pos + " << u32(j) << ", phi = end - " << u32(sg.len) << " + " << u32(j) << ";\n"
+        << "    bool found = false;\n"
+        << "    for (uint32_t wa = plo >> 2; wa <= (phi >> 2) && !found; wa++) {\n"
+        << "      const uint32_t w = base[wa] ^ " << hex32(cbyte * 0x01010101u) << ";\n"
+        << "      uint32_t m = (w - 0x01010101u) & ~w & 0x80808080u;\n"
+        << "      while (m) {\n"
+        << "        const uint32_t p = wa * 4u + ((uint32_t)__builtin_ctz(m) >> 3); m &= m - 1u;\n"
+        << "        if (p < plo || p > phi) continue;\n"
+        << "        const uint32_t k = p - " << u32(j) << ";\n"
+        << "        if (" << seg_expr(sg, "k", false) << ") { pos = k + " << u32(sg.len) << "; found = true; break; }\n"
+        << "      }\n"
+        << "    }\n"
         << "    if (!found) return false; }\n";
     }
     o << "  (void)pos; (void)end;\n  return true;\n}\n";
@@ -962,7 +992,7 @@ struct Gen {
       } else {
         o << "  { EState e_{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u};\n";
       }
-      o << "    store_result(O, " << ri << "u, n_res, r, valid, rs" << s << " & 0xFFu, e_, &s_hist[" << q << "][0]); }\n";
+      o << "    store_result2(O, " << ri << "u, n_res, r, valid, rs" << s << " & 0xFFu, e_, &s_hist[" << q << "][0]); }\n";
     }
     o << "  __syncthreads();\n"
       << "  for (uint32_t q = threadIdx.x; q < " << nr << "u * KV_HIST; q += KV_WG) {\n"

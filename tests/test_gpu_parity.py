@@ -92,3 +92,35 @@ def test_counts_mode_matches_status(orc, spec):
     counts = batch.validate(ps, b, mode=batch.MODE_COUNTS)
     for s in range(7):
         assert np.array_equal((full.status == s).sum(axis=1), counts.counts[:, s])
+
+
+@engines
+def test_glob_stress(orc, spec):
+    """Random globs (`*`, `?`, literal runs, `|`, `!`) x random ASCII values: exercises
+    the compiled prefix/suffix/middle-segment search of the device glob."""
+    import random
+
+    rnd = random.Random(7)
+    alpha = "ab:/.-"
+
+    def word(n):
+        return "".join(rnd.choice(alpha) for _ in range(n))
+
+    pats = set()
+    while len(pats) < 120:
+        parts = []
+        for _ in range(rnd.randrange(1, 5)):
+            r = rnd.random()
+            parts.append("*" if r < 0.35 else "?" if r < 0.45 else word(rnd.randrange(1, 4)))
+        p = "".join(parts)
+        if rnd.random() < 0.15:
+            p = "!" + p
+        if rnd.random() < 0.1:
+            p = p + " | " + word(2) + "*"
+        pats.add(p)
+    vals = [word(rnd.randrange(0, 40)) for _ in range(400)]
+    pols = [_policy({"key": p}, name=f"g{i}") for i, p in enumerate(sorted(pats))]
+    ress = [{"key": v} for v in vals]
+    mism, r, ost = compare(orc, pols, ress, specialize=spec)
+    assert not mism, "\n".join(mism)
+    assert (r.status == 0).sum() > 1000 and (r.status == 1).sum() > 1000
