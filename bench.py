@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=40_000)
     ap.add_argument("--rule-filter", default="", help="diagnostics: regex over C2 rule names")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_v4", "traffic.json"),
+                    help="PMC-derived HBM bytes per pass of this same command (tools/collect_profile.py)")
     ap.add_argument("--engine", choices=["vm", "specialized"], default="specialized",
                     help="bytecode interpreter kernel, or per-policy-set specialized kernels (hiprtc)")
     args = ap.parse_args()
@@ -143,6 +145,14 @@ def main():
     out_bytes = n_pairs_rank * (1 if args.mode == "full" else 0) + (32 * n_fail if args.mode == "full" else 0)
     b_alg = b.store_bytes + prog_bytes + out_bytes
     achieved = b_alg / (kernel_ms / 1e3) / 1e9
+    traffic, traffic_src = None, None
+    try:  # HBM bytes from the PMC passes of the same workload (rocprofv3 cannot run inside this process)
+        tj = json.load(open(args.traffic_json))
+        if (tj["workload"], tj["resources_per_gpu"], tj["rules"], tj["output"], tj["engine"]) == \
+                (workload, b.n_res, ps.n_rules, args.mode, args.engine):
+            traffic, traffic_src = tj["bytes_per_pass"], tj["source"]
+    except (OSError, ValueError, KeyError):
+        pass
     out = {
         "metric": "resource×rule validate evals/sec (node)",
         "value": value,
@@ -161,7 +171,7 @@ def main():
                    "engine": args.engine},
         "kernel_ms_per_step": kernel_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "bytes_per_launch": b_alg, "bytes_per_eval": b_alg / n_pairs_rank},
         "status_counts": {n: int(counts[:, i].sum()) for i, n in enumerate(batch.STATUS_NAMES)},
     }
