@@ -29,19 +29,19 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(policies, n_sample: int, threads: int) -> dict:
+def cpu_baseline(policies, n_sample: int, threads: int, kind_mix: int = 0, label: str = "C2") -> dict:
     """Oracle (CPU restatement of the reference engine) on a bounded sample."""
     import oracle
     from kyverno_amd import batch, workloads
 
     orc = oracle.get()
-    data = batch.synth(workloads.SEED + 999, n_sample).decode()
+    data = batch.synth(workloads.SEED + 999, n_sample, kind_mix).decode()
     ress = "[" + ",".join(data.strip().split("\n")) + "]"
     st, secs = orc.validate_batch(json.dumps(policies), ress, nthreads=threads)
     n_rules = st.shape[0]
     return {"value": n_sample * n_rules / secs, "unit": "resource×rule evals/s", "cores": threads,
             "kind": "port",
-            "sample": f"{n_sample} synthetic Pods x {n_rules} rules (C2 rule set), evaluation only "
+            "sample": f"{n_sample} synthetic resources x {n_rules} rules ({label} rule set), evaluation only "
                       f"(inputs pre-parsed), oracle/ C++ restatement on {threads} host threads, {secs:.2f} s"}
 
 
@@ -52,7 +52,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n-res", type=int, default=1_000_000, help="resources per GPU")
     ap.add_argument("--mode", choices=["full", "counts"], default="full")
-    ap.add_argument("--config", choices=["c2", "c3"], default="c2")
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
+                    help="c2: Pods x 100 pattern rules; c3: mixed kinds x 1000 policies with match/exclude; "
+                         "c4: anchor-heavy chart + test/policy/validate (138 rules) x Pods; "
+                         "c5: background scan, chart after autogen (105 rules) x mixed kinds, counts")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=40_000)
     ap.add_argument("--rule-filter", default="", help="diagnostics: regex over C2 rule names")
@@ -87,10 +90,20 @@ def main():
                 p["spec"]["rules"] = [r for r in p["spec"]["rules"] if rx.search(r["name"])]
         kind_mix = 0
         workload = "C2: synthetic Pods x 100 validate.pattern rules (image globs, ?*, quantities, |-lists)"
-    else:
+    elif args.config == "c3":
         pols = workloads.c3_policies(1000)
         kind_mix = 1
         workload = "C3: Pods/Deployments/Services 60/25/15 x 1000 policies with match/exclude"
+    elif args.config == "c4":
+        pols = workloads.c4_policies()
+        kind_mix = 0
+        workload = "C4: anchor-heavy kyverno-policies chart (restricted) + test/policy/validate, autogen, x Pods"
+    else:
+        pols = workloads.c5_policies()
+        kind_mix = 1
+        workload = "C5: background scan, kyverno-policies chart (restricted) after autogen x Pods/Deployments/Services"
+        if args.mode == "full" and "--mode" not in " ".join(sys.argv):
+            args.mode = "counts"
     t0 = time.time()
     ps = batch.PolicySet(pols, specialize=args.engine == "specialized")
     jit = ps.jit_info
@@ -175,9 +188,9 @@ def main():
                      "bytes_per_launch": b_alg, "bytes_per_eval": b_alg / n_pairs_rank},
         "status_counts": {n: int(counts[:, i].sum()) for i, n in enumerate(batch.STATUS_NAMES)},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(pols, args.cpu_sample, threads)
+        out["cpu_baseline"] = cpu_baseline(pols, args.cpu_sample, threads, kind_mix, args.config.upper())
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

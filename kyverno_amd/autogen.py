@@ -375,24 +375,35 @@ def mutate_policy(policy: dict) -> dict:
             else:
                 rules.append(gen)
     # checkForGVKFormatPatch (policymutation.go:93-148): replace by the changed kinds only
-    orules = ospec.get("rules") or []
+    for path, value in gvk_format_patches(orig):
+        node = p
+        for k in path[:-1]:
+            node = node[k]
+        node[path[-1]] = value
+    return p
+
+
+def gvk_format_patches(policy: dict) -> list[tuple[list, list]]:
+    """checkForGVKFormatPatch / convertGVKForKinds (policymutation.go:93-148, :150-171): for every
+    kinds list with at least one kind whose formatted form differs, a replace patch whose value is
+    only the changed kinds (the reference's own quirk). Returns [(path as key list, value)]."""
+    out = []
 
     def fmt(kinds):
-        changed = [get_formated_kind(k) for k in kinds or [] if get_formated_kind(k) != k]
-        return changed or None
+        return [get_formated_kind(k) for k in kinds or [] if get_formated_kind(k) != k]
 
-    for i, r in enumerate(orules):
+    for i, r in enumerate((policy.get("spec") or {}).get("rules") or []):
         for blk_key in ("match", "exclude"):
             blk = r.get(blk_key) or {}
             new = fmt(_rd(blk).get("kinds"))
             if new:
-                rules[i][blk_key]["resources"]["kinds"] = new
+                out.append((["spec", "rules", i, blk_key, "resources", "kinds"], new))
             for key in ("all", "any"):
                 for j, f in enumerate(_filters(blk, key)):
                     new = fmt(_rd(f).get("kinds"))
                     if new:
-                        rules[i][blk_key][key][j]["resources"]["kinds"] = new
-    return p
+                        out.append((["spec", "rules", i, blk_key, key, j, "resources", "kinds"], new))
+    return out
 
 
 def mutate_policies(policies: list[dict]) -> list[dict]:

@@ -118,14 +118,33 @@ void pod_spec(std::string& o, Rng& r) {
   o += "]";
   if (r.u() < 0.05) o += ",\"hostNetwork\":true";
   if (r.u() < 0.05) o += ",\"hostPID\":true";
+  // pod-level fields for the anchor-heavy chart rules (configs C4/C5) come from a side stream
+  // so the main stream (and every earlier workload) is unchanged
+  Rng q{r.s ^ 0xC4C5A11CE5ull};
+  std::string sc;
+  auto scf = [&](const std::string& f) { sc += sc.empty() ? "" : ","; sc += f; };
   if (r.u() < 0.05) {
-    o += ",\"securityContext\":{\"sysctls\":[{\"name\":\"";
-    o += r.u() < 0.5 ? "kernel.shm_rmid_forced" : "net.core.somaxconn";
-    o += "\",\"value\":\"1\"}]}";
+    std::string sy = "\"sysctls\":[{\"name\":\"";
+    sy += r.u() < 0.5 ? "kernel.shm_rmid_forced" : "net.core.somaxconn";
+    sy += "\",\"value\":\"1\"}]";
+    scf(sy);
   }
+  if (q.u() < 0.25) scf(std::string("\"runAsNonRoot\":") + (q.u() < 0.85 ? "true" : "false"));
+  if (q.u() < 0.20) scf("\"runAsGroup\":" + std::to_string(q.u() < 0.1 ? 0 : 1000 + q.n(3) * 1000));
+  if (q.u() < 0.20) scf("\"fsGroup\":" + std::to_string(q.u() < 0.1 ? 0 : 2000));
+  if (q.u() < 0.10) scf(std::string("\"supplementalGroups\":[") + (q.u() < 0.2 ? "0" : "3000") + ",4000]");
+  if (q.u() < 0.20) scf(std::string("\"seccompProfile\":{\"type\":\"") + kSeccomp[q.n(3)] + "\"}");
+  if (!sc.empty()) o += ",\"securityContext\":{" + sc + "}";
+  if (q.u() < 0.03) o += ",\"hostIPC\":true";
   double v = r.u();
   if (v < 0.05) o += ",\"volumes\":[{\"name\":\"host\",\"hostPath\":{\"path\":\"/var/run\"}}]";
-  else if (v < 0.4) o += ",\"volumes\":[{\"name\":\"data\",\"emptyDir\":{}}]";
+  else if (v < 0.4) {
+    // restricted volume types (restrict-volume-types) on a small share
+    double t = q.u();
+    if (t < 0.04) o += ",\"volumes\":[{\"name\":\"data\",\"nfs\":{\"server\":\"nfs\",\"path\":\"/x\"}}]";
+    else if (t < 0.06) o += ",\"volumes\":[{\"name\":\"data\",\"csi\":{\"driver\":\"d\"}}]";
+    else o += ",\"volumes\":[{\"name\":\"data\",\"emptyDir\":{}}]";
+  }
   o += "}";
 }
 

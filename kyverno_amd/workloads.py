@@ -9,6 +9,9 @@ Synthetic resources come from the library's deterministic generator
 """
 from __future__ import annotations
 
+import json
+import os
+
 SEED = 0x6B79766E
 
 
@@ -148,3 +151,37 @@ def c3_policies(n_policies: int = 1000, seed: int = SEED) -> list[dict]:
             rules.append(_rule(f"p{p}-r{r}", pat, match=match, exclude=exclude))
         pols.append(_policy(f"c3-policy-{p:04d}", rules))
     return pols
+
+
+_GOLDEN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
+
+
+def chart_policies() -> list[dict]:
+    """The kyverno-policies chart (charts/kyverno-policies/templates/**) rendered with
+    podSecurityStandard=restricted: 14 policies / 35 rules, anchor-heavy (conditional, equality,
+    existence, negation anchors over containers[] arrays). Rendered by
+    tests/golden/gen_cli_fixtures.py into tests/golden/chart.json."""
+    with open(os.path.join(_GOLDEN, "chart.json")) as f:
+        return [c["policy"] for c in json.load(f)["cases"]]
+
+
+def validate_corpus_policies() -> list[dict]:
+    """test/policy/validate/*.yaml policies of the reference (tests/golden/corpus.json)."""
+    with open(os.path.join(_GOLDEN, "corpus.json")) as f:
+        pols = json.load(f)["cases"][0]["policies"]
+    return [p["policy"] for p in pols if p["src"].startswith("test/policy/validate/")]
+
+
+def c4_policies() -> list[dict]:
+    """C4: anchor-heavy set = chart + test/policy/validate, after the CLI's defaults + autogen
+    (pkg/kyverno/common/common.go:177-216): 138 rules, every one device-routed."""
+    from . import autogen
+
+    return autogen.mutate_policies(chart_policies() + validate_corpus_policies())
+
+
+def c5_policies() -> list[dict]:
+    """C5 background scan: the full chart after autogen (35 + 70 = 105 rules)."""
+    from . import autogen
+
+    return autogen.mutate_policies(chart_policies())

@@ -1,0 +1,132 @@
+"""`kyverno apply` / `kyverno test` front end (kyverno_amd.cli) against the reference's CLI known
+answers: policy-report summaries of pkg/kyverno/apply/apply_command_test.go:18-47 and the expected
+results of test/cli/test/{simple,autogen}/test.yaml (fixtures: tests/golden/cli.json).
+
+CPU tests drive the host logic (loading, autogen, counting, report building, test-result lookup)
+with statuses from the oracle; `gpu` tests run the same fixtures end to end on the device and
+compare the printed failure messages with the oracle's RuleResponse messages."""
+import io
+import json
+import os
+
+import numpy as np
+import pytest
+
+from kyverno_amd import autogen, batch, cli
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+CASES = json.load(open(os.path.join(GOLDEN, "cli.json")))["cases"]
+APPLY = [c for c in CASES if c["kind"] == "apply_summary"]
+TESTS = [c for c in CASES if c["kind"] == "kyverno_test"]
+
+
+def oracle_evaluation(policies, resources):
+    """Evaluation whose statuses come from the oracle (host-logic tests; no device)."""
+    import oracle
+
+    ps = batch.PolicySet(policies)  # host-side compile only: rule table / routes
+    st, _ = oracle.get().validate_batch(json.dumps(policies), json.dumps(resources))
+    st[st == 7] = cli.CPU
+    st[[r.index for r in ps.rules if r.route == batch.ROUTE_CPU]] = np.where(
+        st[[r.index for r in ps.rules if r.route == batch.ROUTE_CPU]] == cli.NOMATCH, cli.NOMATCH, cli.CPU)
+    ev = cli.Evaluation(policies, resources, ps.rules, st)
+    return ev
+
+
+def _summary(reports):
+    tot = {k: 0 for k in ("pass", "fail", "warn", "error", "skip")}
+    for r in reports:
+        for k in tot:
+            tot[k] += r["summary"][k]
+    return tot
+
+
+@pytest.mark.parametrize("case", APPLY, ids=lambda c: os.path.basename(c["resource_src"]))
+def test_apply_policy_report_summary_oracle(case):
+    out = io.StringIO()
+    rc, infos = cli.apply_docs(case["policies"], case["resources"], policy_report=True, out=out,
+                               evaluation_fn=oracle_evaluation)
+    assert _summary(cli.build_policy_reports(infos)) == case["expected"], case["src"]
+    assert (rc.pass_, rc.fail, rc.warn, rc.error, rc.skip) == tuple(
+        case["expected"][k] for k in ("pass", "fail", "warn", "error", "skip"))
+
+
+@pytest.mark.parametrize("case", TESTS, ids=lambda c: c["src"])
+def test_kyverno_test_results_oracle(case):
+    rows = cli.run_test(case, case["policies"], case["resources"], evaluation_fn=oracle_evaluation)
+    bad = [r for r in rows if r["ok"] is False]
+    assert not bad, bad
+    routed = [r for r in rows if r["ok"] is None]
+    # only the deny-condition rules of test/cli/test/simple (duration-test) go to the reference engine
+    assert all(r["policy"] == "duration-test" for r in routed)
+    assert len(rows) - len(routed) == {"test/cli/test/simple/test.yaml": 5,
+                                       "test/cli/test/autogen/test.yaml": 8}[case["src"]]
+
+
+def test_autogen_rule_counts_c1():
+    """C1 (BASELINE.json configs[0]): disallow_latest_tag (autogen none) + require_pod_requests_limits
+    (autogen on) = 2 + 3 validate rules."""
+    pols = json.load(open(os.path.join(GOLDEN, "corpus.json")))["cases"][0]["policies"]
+    sel = [p["policy"] for p in pols if p["src"].endswith(("disallow_latest_tag.yaml",
+                                                           "require_pod_requests_limits.yaml"))]
+    mutated = autogen.mutate_policies(sel)
+    assert [len(p["spec"]["rules"]) for p in mutated] == [2, 3]
+
+
+def test_unset_variables_skip():
+    p = {"metadata": {"name": "x"}, "spec": {"rules": [{"name": "r", "validate": {"message": "{{ foo.bar }}"}}]}}
+    assert cli.has_unset_variables(p)
+    p["spec"]["rules"][0]["validate"]["message"] = "{{ request.object.metadata.name }}"
+    assert not cli.has_unset_variables(p)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", APPLY, ids=lambda c: os.path.basename(c["resource_src"]))
+def test_apply_summary_gpu(case):
+    import oracle
+
+    out = io.StringIO()
+    rc, infos = cli.apply_docs(case["policies"], case["resources"], policy_report=False, out=out)
+    assert {"pass": rc.pass_, "fail": rc.fail, "warn": rc.warn, "error": rc.error, "skip": rc.skip} == \
+        case["expected"], case["src"]
+    # printed violations carry the reference's RuleResponse message
+    orc = oracle.get()
+    text = out.getvalue()
+    for pol in autogen.mutate_policies(case["policies"]):
+        for res in case["resources"]:
+            for rr in orc.validate(pol, res)["rules"]:
+                if rr["status"] == "fail":
+                    assert f"{rr['name']}: {rr['message']} \n" in text
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", TESTS, ids=lambda c: c["src"])
+def test_kyverno_test_results_gpu(case):
+    rows = cli.run_test(case, case["policies"], case["resources"])
+    assert not [r for r in rows if r["ok"] is False]
+    assert sum(r["ok"] is True for r in rows) == {"test/cli/test/simple/test.yaml": 5,
+                                                  "test/cli/test/autogen/test.yaml": 8}[case["src"]]
+
+
+@pytest.mark.gpu
+def test_messages_match_oracle_on_corpus():
+    """Messages of every pass/fail RuleResponse over the reference corpus (after autogen), device vs
+    oracle. anyPattern messages come from the per-pattern device evaluation."""
+    import oracle
+
+    corpus = json.load(open(os.path.join(GOLDEN, "corpus.json")))["cases"][0]
+    pols = autogen.mutate_policies([p["policy"] for p in corpus["policies"]])
+    ress = [r["resource"] for r in corpus["resources"]]
+    ev = cli.evaluate(pols, ress)
+    orc = oracle.get()
+    checked = 0
+    for pi, pol in enumerate(pols):
+        rules = {r.name: r for r in ev.policy_rules(pi)}
+        for j, res in enumerate(ress):
+            for rr in orc.validate(pol, res)["rules"]:
+                r = rules[rr["name"]]
+                st = int(ev.status[r.index, j])
+                if st in (cli.PASS, cli.FAIL) and not rr.get("message_needs_vars"):
+                    assert cli.rule_message(ev, r, j) == rr["message"], (pol["metadata"]["name"], rr["name"], j)
+                    checked += 1
+    assert checked > 100

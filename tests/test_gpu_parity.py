@@ -124,3 +124,37 @@ def test_glob_stress(orc, spec):
     mism, r, ost = compare(orc, pols, ress, specialize=spec)
     assert not mism, "\n".join(mism)
     assert (r.status == 0).sum() > 1000 and (r.status == 1).sum() > 1000
+
+
+@engines
+def test_c4_anchor_heavy_chart(orc, spec):
+    """C4: chart (restricted) + test/policy/validate after autogen x synthetic Pods with pod- and
+    container-level securityContext, host namespaces/ports/paths, sysctls, volumes, apparmor."""
+    from kyverno_amd import batch, workloads
+
+    pols = workloads.c4_policies()
+    data = batch.synth(workloads.SEED + 4, 3000).decode()
+    ress = [json.loads(l) for l in data.strip().split("\n")]
+    mism, r, ost = compare(orc, pols, ress, check_paths=True, max_path_checks=600, specialize=spec)
+    assert not mism, "\n".join(mism)
+    for s in (0, 1, 4, 5):  # pass, fail, skip (conditional anchors), not matched (autogen rules)
+        assert (r.status == s).sum() > 100, s
+
+
+@engines
+def test_c5_background_scan_counts(orc, spec):
+    """C5: full chart after autogen x Pods/Deployments/Services, COUNTS mode (PolicyReport
+    summaries) against the oracle's per-pair statuses."""
+    from kyverno_amd import batch, workloads
+
+    pols = workloads.c5_policies()
+    data = batch.synth(workloads.SEED + 5, 4000, kind_mix=1)
+    ps = batch.PolicySet(pols, specialize=spec)
+    b = batch.Batch(ps, data)
+    counts = batch.validate(ps, b, mode=batch.MODE_COUNTS)
+    ress = "[" + ",".join(data.decode().strip().split("\n")) + "]"
+    ost, _ = orc.validate_batch(json.dumps(pols), ress, nthreads=8)
+    ost[ost == 7] = 6
+    for s in range(7):
+        assert np.array_equal((ost == s).sum(axis=1), counts.counts[:, s]), s
+    assert counts.counts[:, 0].sum() > 1000 and counts.counts[:, 1].sum() > 100
