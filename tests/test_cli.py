@@ -121,10 +121,13 @@ def test_messages_match_oracle_on_corpus():
     orc = oracle.get()
     checked = 0
     for pi, pol in enumerate(pols):
-        rules = {r.name: r for r in ev.policy_rules(pi)}
         for j, res in enumerate(ress):
-            for rr in orc.validate(pol, res)["rules"]:
-                r = rules[rr["name"]]
+            # rule names may repeat inside a policy: pair the responses in policy order
+            resp = [r for r in ev.policy_rules(pi)
+                    if ev.status[r.index, j] != cli.NOMATCH and r.route != cli.ROUTE_NORESPONSE]
+            orules = [rr for rr in orc.validate(pol, res)["rules"] if rr["status"] != "nomatch"]
+            assert [r.name for r in resp] == [rr["name"] for rr in orules]
+            for r, rr in zip(resp, orules):
                 st = int(ev.status[r.index, j])
                 if st in (cli.PASS, cli.FAIL) and not rr.get("message_needs_vars"):
                     assert cli.rule_message(ev, r, j) == rr["message"], (pol["metadata"]["name"], rr["name"], j)
