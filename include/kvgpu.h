@@ -45,8 +45,11 @@ enum {
   KV_COMPILE_SPECIALIZE = 1
 };
 
-/* kv_validate modes (bit set) */
-enum { KV_MODE_STATUS = 1, KV_MODE_ERRORS = 2, KV_MODE_COUNTS = 4 };
+/* kv_validate modes (bit set). KV_MODE_SCOPES adds per-scope counts
+ * (scope = namespace; "" = cluster scope), the PolicyReport / ClusterPolicyReport
+ * summaries of pkg/kyverno/apply/report.go:76-179 and the background controller's
+ * pkg/policyreport/builder.go:245-308; it keeps the status matrix on the device. */
+enum { KV_MODE_STATUS = 1, KV_MODE_ERRORS = 2, KV_MODE_COUNTS = 4, KV_MODE_SCOPES = 8 };
 
 enum { KV_E_INVALID = -1, KV_E_PARSE = -2, KV_E_DEVICE = -3, KV_E_RANGE = -4, KV_E_NOMEM = -5 };
 
@@ -88,6 +91,11 @@ int kv_rule_info_get(const kv_policyset* ps, uint32_t rule, kv_rule_info* out);
 int kv_ingest(const kv_policyset* ps, const char* resources_json, size_t len, const char* ns_labels_json,
               kv_batch** out, kv_error** err);
 int kv_batch_info(const kv_batch* b, uint64_t* n_res, uint64_t* store_bytes);
+/* namespace table of a batch (first-seen order; index = scope of kv_result_scope_counts);
+ * the name lives as long as the batch. Reference: resource.GetNamespace() keys the report
+ * scope in buildPolicyResults (pkg/kyverno/apply/report.go:80-87). */
+int kv_batch_namespaces(const kv_batch* b, uint32_t* n);
+const char* kv_batch_namespace(const kv_batch* b, uint32_t i);
 
 /* Evaluate every (resource, rule) pair on HIP device `device`.
  * ctx_json: {"admission": {"roles":[], "clusterRoles":[], "groups":[], "username":""},
@@ -99,6 +107,8 @@ int kv_validate(const kv_policyset* ps, const kv_batch* b, const char* ctx_json,
 int kv_result_status(const kv_result* r, const uint8_t** status, uint64_t* n_rules, uint64_t* n_res);
 /* counts[rule * 8 + status] */
 int kv_result_counts(const kv_result* r, const int64_t** counts);
+/* counts[(scope * n_rules + rule) * 8 + status] (KV_MODE_SCOPES) */
+int kv_result_scope_counts(const kv_result* r, const int64_t** counts, uint32_t* n_scopes);
 /* failing path of a FAIL pair, e.g. "/spec/containers/0/image/" (needs KV_MODE_ERRORS);
  * returns the string length, or a negative code. */
 int kv_result_path(const kv_result* r, uint32_t rule, uint64_t res, char* buf, size_t cap);
@@ -121,6 +131,7 @@ int kv_session_create(const kv_policyset* ps, const kv_batch* b, const char* ctx
                       kv_session** out, kv_error** err);
 int kv_session_run(kv_session* s, int iters, double* event_ms, kv_error** err);
 int kv_session_counts(kv_session* s, int64_t* counts /* [n_rules][8], last pass */);
+int kv_session_scope_counts(kv_session* s, int64_t* counts /* [n_scopes][n_rules][8], last pass */);
 void kv_free_session(kv_session* s);
 
 /* Synthetic resource generator for the benchmark configs:

@@ -81,6 +81,11 @@ def lib():
         L.kv_session_create.argtypes = [vp, vp, ctypes.c_char_p, i32, u32, ctypes.POINTER(vp), errpp]
         L.kv_session_run.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_double), errpp]
         L.kv_session_counts.argtypes = [vp, vp]
+        L.kv_session_scope_counts.argtypes = [vp, vp]
+        L.kv_result_scope_counts.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(u32)]
+        L.kv_batch_namespaces.argtypes = [vp, ctypes.POINTER(u32)]
+        L.kv_batch_namespace.argtypes = [vp, u32]
+        L.kv_batch_namespace.restype = ctypes.c_char_p
         for fn in ("kv_free_policyset", "kv_free_batch", "kv_free_result", "kv_free_buffer", "kv_free_session"):
             getattr(L, fn).argtypes = [vp]
             getattr(L, fn).restype = None
@@ -95,6 +100,7 @@ EXPORTED_SYMBOLS = [
     "kv_result_status", "kv_result_counts", "kv_result_path", "kv_result_error", "kv_result_kernel_ms",
     "kv_bench", "kv_synth", "kv_free_policyset", "kv_free_batch", "kv_free_result", "kv_free_error",
     "kv_free_buffer", "kv_session_create", "kv_session_run", "kv_session_counts", "kv_free_session",
+    "kv_session_scope_counts", "kv_result_scope_counts", "kv_batch_namespaces", "kv_batch_namespace",
 ]
 
 

@@ -21,7 +21,7 @@ from ._native import RuleInfo, check, lib, new_err
 PASS, FAIL, WARN, ERROR, SKIP, NOMATCH, CPU = range(7)
 STATUS_NAMES = ["pass", "fail", "warn", "error", "skip", "nomatch", "cpu"]
 
-MODE_STATUS, MODE_ERRORS, MODE_COUNTS = 1, 2, 4
+MODE_STATUS, MODE_ERRORS, MODE_COUNTS, MODE_SCOPES = 1, 2, 4, 8
 COMPILE_SPECIALIZE = 1
 ROUTE_GPU, ROUTE_CPU, ROUTE_NORESPONSE, ROUTE_CONSTANT = range(4)
 
@@ -115,6 +115,13 @@ class Batch:
         L.kv_batch_info(h, ctypes.byref(n), ctypes.byref(b))
         self.n_res, self.store_bytes = n.value, b.value
 
+    @property
+    def namespaces(self) -> list[str]:
+        """Batch namespace table: index = scope of per-scope counts ("" = cluster scope)."""
+        n = ctypes.c_uint32()
+        lib().kv_batch_namespaces(self._h, ctypes.byref(n))
+        return [lib().kv_batch_namespace(self._h, i).decode("utf-8") for i in range(n.value)]
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:
@@ -146,6 +153,11 @@ class Result:
         self.counts = np.frombuffer(cb, dtype=np.int64).reshape(self.n_rules, 8).copy() if self.n_rules else \
             np.zeros((0, 8), np.int64)
         self.kernel_ms = L.kv_result_kernel_ms(h)
+        sc, ns = ctypes.c_void_p(), ctypes.c_uint32()
+        self.scope_counts = None  # [scope][rule][8] with MODE_SCOPES
+        if L.kv_result_scope_counts(h, ctypes.byref(sc), ctypes.byref(ns)) == 0 and self.n_rules and ns.value:
+            buf = (ctypes.c_int64 * (ns.value * self.n_rules * 8)).from_address(sc.value)
+            self.scope_counts = np.frombuffer(buf, dtype=np.int64).reshape(ns.value, self.n_rules, 8).copy()
 
     def path(self, rule: int, res: int) -> str | None:
         buf = ctypes.create_string_buffer(4096)
@@ -218,6 +230,14 @@ class Session:
         rc = lib().kv_session_counts(self._h, out.ctypes.data)
         if rc != 0:
             raise _native.KvError(rc, "kv_session_counts failed")
+        return out
+
+    def scope_counts(self, n_scopes: int) -> np.ndarray:
+        """[scope][rule][8] of the last pass (MODE_SCOPES)."""
+        out = np.zeros((n_scopes, self.n_rules, 8), dtype=np.int64)
+        rc = lib().kv_session_scope_counts(self._h, out.ctypes.data)
+        if rc != 0:
+            raise _native.KvError(rc, "kv_session_scope_counts failed")
         return out
 
     def __del__(self):

@@ -116,6 +116,7 @@ struct kv_result {
   std::vector<uint8_t> status;
   std::vector<ErrRec> err;
   std::vector<int64_t> counts;
+  std::vector<int64_t> scope_counts;  // [scope][rule][KV_HIST] (KV_MODE_SCOPES)
   double kernel_ms = 0;
   uint32_t mode = 0;
 };
@@ -365,7 +366,8 @@ struct kv_session {
   int device = 0;
   uint32_t mode = 0;
   uint64_t nrules = 0, nres = 0;
-  DevBuf fflags, pview, st, er, cn;
+  DevBuf fflags, pview, st, er, cn, scope, scn;
+  uint32_t nscopes = 0;
   DevOut O{};
   const DevBatch* bview = nullptr;
   const DevBatch* bhost = nullptr;  // host copy of the batch view (device pointers)
@@ -389,7 +391,7 @@ struct kv_session {
     nrules = ps->ps.rules.size();
     nres = bt->b.res.size();
     O.full = 0;
-    if (mode & (KV_MODE_STATUS | KV_MODE_ERRORS)) {
+    if (mode & (KV_MODE_STATUS | KV_MODE_ERRORS | KV_MODE_SCOPES)) {
       st.alloc(nrules * nres, device);
       O.status = (uint8_t*)st.p;
       O.full |= 1;
@@ -401,6 +403,14 @@ struct kv_session {
     }
     cn.alloc(std::max<uint64_t>(nrules, 1) * KV_HIST * sizeof(unsigned long long), device);
     O.counts = (unsigned long long*)cn.p;
+    if (mode & KV_MODE_SCOPES) {
+      // scope of every resource = its namespace index in the batch namespace table
+      std::vector<uint32_t> sc(nres);
+      for (uint64_t i = 0; i < nres; i++) sc[i] = bt->b.res[i].ns_index;
+      nscopes = (uint32_t)bt->b.namespaces.size();
+      scope.upload(sc, device);
+      scn.alloc(std::max<uint64_t>((uint64_t)nscopes * nrules, 1) * KV_HIST * sizeof(unsigned long long), device);
+    }
     HIPCHK(hipStreamCreate(&stream));
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
@@ -419,6 +429,11 @@ struct kv_session {
       HIPCHK(hipMemsetAsync(cn.p, 0, cn.n, stream));
       if (dps->mod) launch_specialized();
       else HIPCHK(launch_validate((const DevPS*)pview.p, bview, (uint32_t)nres, O, 0, (uint32_t)nrules, stream));
+      if (mode & KV_MODE_SCOPES) {
+        HIPCHK(hipMemsetAsync(scn.p, 0, scn.n, stream));
+        HIPCHK(launch_scope_counts(O.status, (const uint32_t*)scope.p, (uint32_t)nres, (uint32_t)nrules, nscopes,
+                                   (unsigned long long*)scn.p, stream));
+      }
     }
     HIPCHK(hipEventRecord(e1, stream));
     HIPCHK(hipEventSynchronize(e1));
@@ -439,6 +454,11 @@ struct kv_session {
     for (hipFunction_t f : dps->fns)
       HIPCHK(hipModuleLaunchKernel(f, blocks, 1, 1, KV_WG, 1, 1, 0, stream, args, nullptr));
   }
+  std::vector<int64_t> scope_counts() {
+    std::vector<unsigned long long> c((size_t)nscopes * nrules * KV_HIST);
+    if (!c.empty()) HIPCHK(hipMemcpy(c.data(), scn.p, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return std::vector<int64_t>(c.begin(), c.end());
+  }
   void fetch(kv_result* out, double ms) {
     out->ps = ps;
     out->b = bt;
@@ -449,7 +469,8 @@ struct kv_session {
     std::vector<unsigned long long> c(nrules * KV_HIST);
     if (nrules) HIPCHK(hipMemcpy(c.data(), cn.p, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     out->counts.assign(c.begin(), c.end());
-    if (O.status) {
+    if (mode & KV_MODE_SCOPES) out->scope_counts = scope_counts();
+    if (O.status && (mode & (KV_MODE_STATUS | KV_MODE_ERRORS))) {
       out->status.resize(nrules * nres);
       if (!out->status.empty()) HIPCHK(hipMemcpy(out->status.data(), st.p, out->status.size(), hipMemcpyDeviceToHost));
     }
@@ -616,6 +637,25 @@ int kv_result_counts(const kv_result* r, const int64_t** counts) {
   return 0;
 }
 
+int kv_result_scope_counts(const kv_result* r, const int64_t** counts, uint32_t* n_scopes) {
+  if (!r || !counts) return KV_E_INVALID;
+  if (!(r->mode & KV_MODE_SCOPES)) return KV_E_INVALID;
+  *counts = r->scope_counts.data();
+  if (n_scopes) *n_scopes = (uint32_t)r->b->b.namespaces.size();
+  return 0;
+}
+
+int kv_batch_namespaces(const kv_batch* b, uint32_t* n) {
+  if (!b || !n) return KV_E_INVALID;
+  *n = (uint32_t)b->b.namespaces.size();
+  return 0;
+}
+
+const char* kv_batch_namespace(const kv_batch* b, uint32_t i) {
+  if (!b || i >= b->b.namespaces.size()) return nullptr;
+  return b->b.namespaces[i].c_str();
+}
+
 int kv_result_path(const kv_result* r, uint32_t rule, uint64_t res, char* buf, size_t cap) {
   if (!r || r->err.empty()) return KV_E_INVALID;
   if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
@@ -672,6 +712,17 @@ int kv_session_counts(kv_session* s, int64_t* counts) {
     std::vector<unsigned long long> c(s->nrules * KV_HIST);
     if (s->nrules) HIPCHK(hipMemcpy(c.data(), s->cn.p, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     for (size_t i = 0; i < c.size(); i++) counts[i] = (int64_t)c[i];
+    return 0;
+  } catch (const HipError&) {
+    return KV_E_DEVICE;
+  }
+}
+
+int kv_session_scope_counts(kv_session* s, int64_t* counts) {
+  if (!s || !counts || !(s->mode & KV_MODE_SCOPES)) return KV_E_INVALID;
+  try {
+    std::vector<int64_t> c = s->scope_counts();
+    std::copy(c.begin(), c.end(), counts);
     return 0;
   } catch (const HipError&) {
     return KV_E_DEVICE;

@@ -335,3 +335,70 @@ hipError_t launch_validate(const DevPS* P, const DevBatch* B, uint32_t n_res, co
   return hipGetLastError();
 }
 }  // namespace kv
+
+// ---------------------------------------------------------------------------
+// Per-scope PolicyReport counts: counts[scope][rule][KV_HIST] from status[rule][res]
+// and the namespace index of every resource (scope = namespace, "" = cluster
+// scope), the summaries of pkg/kyverno/apply/report.go:76-179 and
+// pkg/policyreport/builder.go:245-308. One workgroup per (rule, chunk of
+// KV_SCOPE_CHUNK resources): coalesced 4-byte status / 16-byte scope loads,
+// LDS histogram over all scopes when it fits (<= KV_SCOPE_LDS scopes), then one
+// global atomic per non-zero (scope, status) of the chunk. HBM-bound: reads
+// n_rules x n_res status bytes (+ the scope array once per rule, L2/MALL hits).
+namespace kv {
+
+__global__ __launch_bounds__(KV_WG) void kv_scope_count_kernel(const uint8_t* __restrict__ status,
+                                                                const uint32_t* __restrict__ scope, uint32_t n_res,
+                                                                uint32_t n_rules, uint32_t n_scopes,
+                                                                unsigned long long* __restrict__ out) {
+  extern __shared__ uint32_t s_cnt[];
+  const uint32_t rule = blockIdx.x % n_rules;
+  const uint32_t chunk = blockIdx.x / n_rules;
+  const bool in_lds = n_scopes <= KV_SCOPE_LDS;
+  if (in_lds)
+    for (uint32_t q = threadIdx.x; q < n_scopes * KV_HIST; q += KV_WG) s_cnt[q] = 0;
+  __syncthreads();
+  const uint64_t row = (uint64_t)rule * n_res;
+  const uint32_t base = chunk * KV_SCOPE_CHUNK;
+  const uint32_t end = min(base + KV_SCOPE_CHUNK, n_res);
+  for (uint32_t i = base + threadIdx.x * 4; i < end; i += KV_WG * 4) {
+    uint32_t sc[4];
+    uint32_t st[4];
+    if (i + 4 <= end) {
+      const uint4 s4 = *(const uint4*)(scope + i);  // base and i are multiples of 4
+      sc[0] = s4.x; sc[1] = s4.y; sc[2] = s4.z; sc[3] = s4.w;
+#pragma unroll
+      for (int k = 0; k < 4; k++) st[k] = status[row + i + k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        sc[k] = i + k < end ? scope[i + k] : 0xFFFFFFFFu;
+        st[k] = i + k < end ? status[row + i + k] : 0;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (sc[k] >= n_scopes || st[k] >= KV_HIST) continue;
+      if (in_lds) atomicAdd(&s_cnt[sc[k] * KV_HIST + st[k]], 1u);
+      else atomicAdd(&out[((uint64_t)sc[k] * n_rules + rule) * KV_HIST + st[k]], 1ull);
+    }
+  }
+  if (!in_lds) return;
+  __syncthreads();
+  for (uint32_t q = threadIdx.x; q < n_scopes * KV_HIST; q += KV_WG) {
+    const uint32_t v = s_cnt[q];
+    if (v) atomicAdd(&out[((uint64_t)(q / KV_HIST) * n_rules + rule) * KV_HIST + q % KV_HIST], (unsigned long long)v);
+  }
+}
+
+hipError_t launch_scope_counts(const uint8_t* status, const uint32_t* scope, uint32_t n_res, uint32_t n_rules,
+                               uint32_t n_scopes, unsigned long long* out, hipStream_t stream) {
+  if (n_res == 0 || n_rules == 0 || n_scopes == 0) return hipSuccess;
+  const uint32_t chunks = (n_res + KV_SCOPE_CHUNK - 1) / KV_SCOPE_CHUNK;
+  const size_t shm = n_scopes <= KV_SCOPE_LDS ? (size_t)n_scopes * KV_HIST * sizeof(uint32_t) : 0;
+  hipLaunchKernelGGL(kv_scope_count_kernel, dim3(chunks * n_rules), dim3(KV_WG), shm, stream, status, scope, n_res,
+                     n_rules, n_scopes, out);
+  return hipGetLastError();
+}
+
+}  // namespace kv

@@ -133,3 +133,68 @@ def test_messages_match_oracle_on_corpus():
                     assert cli.rule_message(ev, r, j) == rr["message"], (pol["metadata"]["name"], rr["name"], j)
                     checked += 1
     assert checked > 100
+
+
+def _scope_counts_from_status(status, res_ns, namespaces):
+    sc = np.zeros((len(namespaces), status.shape[0], 8), np.int64)
+    idx = {n: i for i, n in enumerate(namespaces)}
+    for j, ns in enumerate(res_ns):
+        np.add.at(sc[idx[ns]], (np.arange(status.shape[0]), status[:, j]), 1)
+    return sc
+
+
+def test_scope_summaries_match_cli_policy_reports():
+    """report.scope_summaries (device-count path of the background scan) agrees with the CLI's
+    per-resource PolicyReport construction (report.go:23-179) on the reference corpus."""
+    from kyverno_amd import report
+
+    corpus = json.load(open(os.path.join(GOLDEN, "corpus.json")))["cases"][0]
+    pols = autogen.mutate_policies([p["policy"] for p in corpus["policies"]])
+    pols = [p for p in pols if not cli.has_unset_variables(p)]
+    ress = [r["resource"] for r in corpus["resources"]]
+    ev = oracle_evaluation(pols, ress)
+    infos = []
+    rc = cli.ResultCounts()
+    for pi, pol in enumerate(pols):
+        if cli.policy_has_validate(pol):
+            for j in range(len(ress)):
+                infos.append(cli.process_validate(ev, pi, j, rc, True, io.StringIO()))
+    want = {r["metadata"]["name"]: r["summary"] for r in cli.build_policy_reports(infos)}
+    res_ns = [(r.get("metadata") or {}).get("namespace", "") for r in ress]
+    namespaces = sorted(set(res_ns))
+    got = report.scope_summaries(ev.rules, pols, namespaces, _scope_counts_from_status(ev.status, res_ns, namespaces))
+    routed = {k: v.pop("cpu") for k, v in got.items()}
+    # CPU-routed pairs are reported by the reference engine, not here: remove them from the CLI side
+    for k in want:
+        want[k] = dict(want[k])
+    assert set(got) == set(want)
+    for k in got:
+        assert got[k] == want[k], (k, got[k], want[k], routed[k])
+
+
+def test_allreduce_counts_gloo_two_ranks():
+    """The one collective of the path (per-scope PolicyReport counts), world_size 2 over gloo."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    ps = [ctx.Process(target=_allreduce_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    outs = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, arr in outs:
+        assert np.array_equal(arr, np.full((3, 4, 8), 1 + 2, np.int64)), rank
+
+
+def _allreduce_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from kyverno_amd import report
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    arr = np.full((3, 4, 8), rank + 1, np.int64)
+    q.put((rank, report.allreduce_counts(arr, dist)))
+    dist.destroy_process_group()

@@ -158,3 +158,31 @@ def test_c5_background_scan_counts(orc, spec):
     for s in range(7):
         assert np.array_equal((ost == s).sum(axis=1), counts.counts[:, s]), s
     assert counts.counts[:, 0].sum() > 1000 and counts.counts[:, 1].sum() > 100
+
+
+@engines
+def test_c5_scope_counts(orc, spec):
+    """Per-namespace PolicyReport counts (KV_MODE_SCOPES, scope-count kernel) against the oracle's
+    per-pair statuses grouped by the resources' namespaces, plus cluster-scoped resources."""
+    from kyverno_amd import batch, workloads
+
+    pols = workloads.c5_policies()
+    data = batch.synth(workloads.SEED + 6, 3000, kind_mix=1).decode().strip().split("\n")
+    ress = [json.loads(l) for l in data]
+    for r in ress[::50]:  # some cluster-scoped resources (empty namespace -> clusterpolicyreport)
+        r["metadata"].pop("namespace", None)
+    ps = batch.PolicySet(pols, specialize=spec)
+    b = batch.Batch(ps, ress)
+    res = batch.validate(ps, b, mode=batch.MODE_SCOPES)
+    ost, _ = orc.validate_batch(json.dumps(pols), json.dumps(ress), nthreads=8)
+    ost[ost == 7] = 6
+    nss = b.namespaces
+    idx = {n: i for i, n in enumerate(nss)}
+    want = np.zeros((len(nss), ost.shape[0], 8), np.int64)
+    for j, r in enumerate(ress):
+        np.add.at(want[idx[r["metadata"].get("namespace", "")]], (np.arange(ost.shape[0]), ost[:, j]), 1)
+    assert "" in idx and len(nss) > 60
+    assert np.array_equal(res.scope_counts, want)
+    sess = batch.Session(ps, b, mode=batch.MODE_SCOPES)
+    sess.run(2)
+    assert np.array_equal(sess.scope_counts(len(nss)), want)
