@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _header_symbols():
     with open(os.path.join(ROOT, "include", "kvgpu.h")) as f:
         src = f.read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|double)\s+(kv_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void|double|const char\s*\*)\s*(kv_\w+)\s*\(", src, re.M)))
 
 
 def test_library_exports_header_symbols():
