@@ -9,7 +9,7 @@ GPU, each evaluates its own shard of resources (weak scaling, no data-path
 collective); per-rule pass/fail/... counts are all-reduced over RCCL once after
 the timed region (PolicyReport summary), outside the timing.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n-res R] [--mode full|counts]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n-res R] [--mode full|counts|scopes] [--config c2|c3|c4|c5]
 """
 from __future__ import annotations
 
@@ -51,13 +51,19 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n-res", type=int, default=1_000_000, help="resources per GPU")
-    ap.add_argument("--mode", choices=["full", "counts"], default="full")
+    ap.add_argument("--mode", choices=["full", "counts", "scopes"], default=None,
+                    help="full: status + failing-path records per pair; counts: per-rule histogram only; "
+                         "scopes: per-namespace PolicyReport counts (status kept on device). "
+                         "Default: full, scopes for c5")
     ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2: Pods x 100 pattern rules; c3: mixed kinds x 1000 policies with match/exclude; "
                          "c4: anchor-heavy chart + test/policy/validate (138 rules) x Pods; "
                          "c5: background scan, chart after autogen (105 rules) x mixed kinds, counts")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=40_000)
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default=None,
+                    help="torch.distributed backend for N>1 (default: nccl = RCCL when GPUs are visible); "
+                         "gloo lets several ranks share one GPU for a rehearsal")
     ap.add_argument("--rule-filter", default="", help="diagnostics: regex over C2 rule names")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_v4", "traffic.json"),
                     help="PMC-derived HBM bytes per pass of this same command (tools/collect_profile.py)")
@@ -73,12 +79,13 @@ def main():
         import torch
         import torch.distributed as dist  # noqa: F811
 
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = args.backend or ("nccl" if torch.cuda.device_count() > 0 else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
+        local = local % max(1, torch.cuda.device_count())
 
-    from kyverno_amd import batch, workloads
+    from kyverno_amd import batch, report, workloads
 
     if args.config == "c2":
         pols = workloads.c2_policies()
@@ -102,8 +109,8 @@ def main():
         pols = workloads.c5_policies()
         kind_mix = 1
         workload = "C5: background scan, kyverno-policies chart (restricted) after autogen x Pods/Deployments/Services"
-        if args.mode == "full" and "--mode" not in " ".join(sys.argv):
-            args.mode = "counts"
+    if args.mode is None:
+        args.mode = "scopes" if args.config == "c5" else "full"
     t0 = time.time()
     ps = batch.PolicySet(pols, specialize=args.engine == "specialized")
     jit = ps.jit_info
@@ -117,7 +124,8 @@ def main():
     t2 = time.time()
     log(f"[rank {rank}] compile+synth {t1 - t0:.2f}s ingest {t2 - t1:.2f}s store {b.store_bytes / 1e6:.1f} MB "
         f"({b.store_bytes / b.n_res:.0f} B/resource), rules {ps.n_rules}")
-    mode = batch.MODE_STATUS | batch.MODE_ERRORS if args.mode == "full" else batch.MODE_COUNTS
+    mode = {"full": batch.MODE_STATUS | batch.MODE_ERRORS, "counts": batch.MODE_COUNTS,
+            "scopes": batch.MODE_COUNTS | batch.MODE_SCOPES}[args.mode]
 
     # device-resident session: inputs uploaded and output buffers allocated once (untimed)
     sess = batch.Session(ps, b, device=local, mode=mode)
@@ -140,22 +148,28 @@ def main():
         import torch
 
         t = torch.tensor([wall], dtype=torch.float64)
-        if torch.cuda.is_available():
+        if dist.get_backend() == "nccl":
             t = t.cuda()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         t_max = float(t.item())
-        # PolicyReport summary: per-rule pass/fail/warn/error/skip counts over RCCL
-        c = torch.tensor(counts, dtype=torch.int64)
-        if torch.cuda.is_available():
-            c = c.cuda()
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        counts = c.cpu().numpy()
+    # PolicyReport summaries (outside the timed region): per-rule counts, and in scopes mode the
+    # per-namespace counts, summed over the ranks with one all-reduce each (RCCL / gloo)
+    counts = report.allreduce_counts(counts, dist)
+    scopes = None
+    if args.mode == "scopes":
+        names, sc = report.allreduce_scope_counts(b.namespaces, sess.scope_counts(len(b.namespaces)), dist)
+        summ = report.scope_summaries(ps.rules, pols, names, sc)
+        scopes = {"reports": len(summ), "fail": sum(v["fail"] for v in summ.values()),
+                  "pass": sum(v["pass"] for v in summ.values())}
 
     n_pairs_rank = b.n_res * ps.n_rules
     value = world * n_pairs_rank * args.steps / t_max
     # algorithmic bytes per launch: projected store read once + program tables + outputs
     prog_bytes = 0  # program/predicate tables are KB-scale (<0.01%)
-    out_bytes = n_pairs_rank * (1 if args.mode == "full" else 0) + (32 * n_fail if args.mode == "full" else 0)
+    # full: 1 B status + 32 B record per FAIL/ERROR/SKIP pair; scopes: status written and read back
+    # by the scope-count kernel (2 B per pair) + the 4 B scope index of every resource
+    out_bytes = {"full": n_pairs_rank + 32 * n_fail, "counts": 0,
+                 "scopes": 2 * n_pairs_rank + 4 * b.n_res}[args.mode]
     b_alg = b.store_bytes + prog_bytes + out_bytes
     achieved = b_alg / (kernel_ms / 1e3) / 1e9
     traffic, traffic_src = None, None
@@ -188,6 +202,8 @@ def main():
                      "bytes_per_launch": b_alg, "bytes_per_eval": b_alg / n_pairs_rank},
         "status_counts": {n: int(counts[:, i].sum()) for i, n in enumerate(batch.STATUS_NAMES)},
     }
+    if scopes is not None:
+        out["policy_reports"] = scopes
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
         out["cpu_baseline"] = cpu_baseline(pols, args.cpu_sample, threads, kind_mix, args.config.upper())

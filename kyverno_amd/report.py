@@ -63,3 +63,19 @@ def allreduce_counts(counts: np.ndarray, dist=None) -> np.ndarray:
         t = t.cuda()
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t.cpu().numpy()
+
+
+def allreduce_scope_counts(namespaces: list[str], scope_counts: np.ndarray, dist=None) -> tuple[list[str], np.ndarray]:
+    """Per-scope counts of resource shards → node-wide counts. Every rank's batch numbers its
+    namespaces in first-seen order, so the scope axis is first re-indexed onto the sorted union of
+    all ranks' namespaces (one all_gather_object of the names), then summed with one all-reduce."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        order = sorted(range(len(namespaces)), key=lambda i: namespaces[i])
+        return [namespaces[i] for i in order], scope_counts[order]
+    names: list = [None] * dist.get_world_size()
+    dist.all_gather_object(names, list(namespaces))
+    universe = sorted(set().union(*names))
+    pos = {n: i for i, n in enumerate(universe)}
+    full = np.zeros((len(universe),) + scope_counts.shape[1:], np.int64)
+    full[[pos[n] for n in namespaces]] = scope_counts
+    return universe, allreduce_counts(full, dist)

@@ -185,8 +185,11 @@ def test_allreduce_counts_gloo_two_ranks():
     outs = [q.get(timeout=120) for _ in ps]
     for p in ps:
         p.join(timeout=60)
-    for rank, arr in outs:
+    for rank, arr, names, scoped in outs:
         assert np.array_equal(arr, np.full((3, 4, 8), 1 + 2, np.int64)), rank
+        # rank 0 saw [b, a], rank 1 saw [c, a]: merged onto the sorted union [a, b, c]
+        assert names == ["a", "b", "c"]
+        assert scoped[:, 0, 0].tolist() == [10 + 1, 20, 2], scoped[:, 0, 0]
 
 
 def _allreduce_worker(rank, world, port, q):
@@ -196,5 +199,10 @@ def _allreduce_worker(rank, world, port, q):
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     arr = np.full((3, 4, 8), rank + 1, np.int64)
-    q.put((rank, report.allreduce_counts(arr, dist)))
+    nss = ["b", "a"] if rank == 0 else ["c", "a"]
+    sc = np.zeros((2, 4, 8), np.int64)
+    sc[0, 0, 0] = 20 if rank == 0 else 2   # b / c
+    sc[1, 0, 0] = 10 if rank == 0 else 1   # a
+    names, scoped = report.allreduce_scope_counts(nss, sc, dist)
+    q.put((rank, report.allreduce_counts(arr, dist), names, scoped))
     dist.destroy_process_group()
