@@ -75,6 +75,8 @@ struct DevPolicySet {
   // specialized kernels (KV_COMPILE_SPECIALIZE): one function per rule chunk
   hipModule_t mod = nullptr;
   std::vector<hipFunction_t> fns;
+  hipFunction_t ptab_fn = nullptr;  // value-predicate table builder (kvj_ptab)
+  uint32_t memo_words = 0;
   int dev = -1;
   ~DevPolicySet() {
     if (mod) {
@@ -189,6 +191,10 @@ DevPolicySet& dev_ps(kv_policyset* s, int device) {
         fprintf(stderr, "[kvgpu] %s: %zu rules, %d VGPRs, %d B scratch/lane\n", ch.name.c_str(),
                 ch.rules.empty() ? (size_t)(ch.rule_end - ch.rule_begin) : ch.rules.size(), regs, local);
       }
+    }
+    if (s->jit->memo_words) {
+      HIPCHK(hipModuleGetFunction(&d->ptab_fn, d->mod, "kvj_ptab"));
+      d->memo_words = s->jit->memo_words;
     }
   }
   auto& ref = *d;
@@ -366,8 +372,8 @@ struct kv_session {
   int device = 0;
   uint32_t mode = 0;
   uint64_t nrules = 0, nres = 0;
-  DevBuf fflags, pview, st, er, cn, scope, scn;
-  uint32_t nscopes = 0;
+  DevBuf fflags, pview, st, er, cn, scope, scn, ptab;
+  uint32_t nscopes = 0, nvals = 0;
   DevOut O{};
   const DevBatch* bview = nullptr;
   const DevBatch* bhost = nullptr;  // host copy of the batch view (device pointers)
@@ -387,6 +393,12 @@ struct kv_session {
     fflags.upload(fold_filters(ps->ps, ai), device);
     DevPS P = dp.view;
     P.fflags = (const uint32_t*)fflags.p;
+    if (dp.ptab_fn) {  // value-predicate table of the specialized kernels: memo_words per distinct value
+      nvals = (uint32_t)bt->b.vals.size();
+      ptab.alloc(std::max<size_t>((size_t)dp.memo_words * nvals, 1) * sizeof(uint32_t), device);
+      P.ptab = (const uint32_t*)ptab.p;
+      P.n_vals = nvals;
+    }
     pview.upload_raw(&P, sizeof(DevPS), device);  // read through a uniform pointer (scalar loads)
     nrules = ps->ps.rules.size();
     nres = bt->b.res.size();
@@ -449,6 +461,13 @@ struct kv_session {
     const Node* N = bhost->nodes;
     const Val* V = bhost->vals;
     const uint8_t* S = bhost->bstr;
+    if (dps->ptab_fn && nvals) {  // every leaf predicate once per distinct value, before the rule kernels
+      uint32_t NV = nvals;
+      uint32_t* PT = (uint32_t*)ptab.p;
+      void* targs[] = {(void*)&P, (void*)&V, (void*)&S, (void*)&NV, (void*)&PT};
+      HIPCHK(hipModuleLaunchKernel(dps->ptab_fn, (NV + KV_WG - 1) / KV_WG, 1, 1, KV_WG, 1, 1, 0, stream, targs,
+                                   nullptr));
+    }
     DevOut Ov = O;
     void* args[] = {(void*)&P, (void*)&bview, (void*)&N, (void*)&V, (void*)&S, (void*)&Ov};
     for (hipFunction_t f : dps->fns)

@@ -34,6 +34,12 @@ struct DevPS {
   const uint8_t* pstr;
   uint32_t star_id;
   uint32_t n_rules;
+  // value-predicate table of the specialized kernels (per launch configuration):
+  // ptab[word * n_vals + val] bit b = leaf predicate of memo slot 32*word+b on
+  // the scalar Val `val` (built each pass by kvj_ptab before the rule kernels)
+  const uint32_t* ptab;
+  uint32_t n_vals;
+  uint32_t pad_;
 };
 
 struct DevBatch {

@@ -54,7 +54,18 @@ struct Gen {
   const PolicySet& ps;
   std::ostringstream o;
   std::set<uint32_t> preds_done, atoms_done;
+  // value-predicate memo: a leaf predicate on a scalar is a pure function of the
+  // (deduplicated) Val it reads, so each one is evaluated once per distinct value
+  // of the batch (kvj_ptab) and the rule kernels test one bit of the table
+  bool memo = true;
+  std::vector<uint32_t> mpreds;  // memo slot -> pred
   explicit Gen(const PolicySet& p) : ps(p) {}
+
+  // call of leaf predicate `pi` on node `n` of type `t`
+  std::string pred_call(uint32_t pi, const std::string& t, const std::string& n) {
+    return std::string(memo ? "m_pred_" : "g_pred_") + std::to_string(pi) +
+           (memo ? "(P, V, S, pstr, " : "(V, S, pstr, ") + t + ", " + n + ")";
+  }
 
   // ---------------------------------------------------------------- globs
   // word compare of segment `sg` against value bytes [k, k + len) (base 4-byte aligned)
@@ -244,6 +255,44 @@ struct Gen {
       default: o << "  return false;\n"; break;
     }
     o << "}\n";
+    if (memo) {
+      const uint32_t slot = (uint32_t)mpreds.size();
+      mpreds.push_back(pi);
+      // scalars (BOOL/INT/FLOAT/STR carry a Val id in n.a): one bit of the table;
+      // null / map / array: the predicate itself (no value loads on those paths)
+      o << "__device__ __forceinline__ bool m_pred_" << pi
+        << "(const DevPS& P, const Val* __restrict__ V, const uint8_t* __restrict__ S, const uint8_t* __restrict__ pstr, "
+           "uint32_t type, const Node& n) {\n"
+        << "  if (type - 1u < 4u) return (P.ptab[(size_t)" << (slot / 32) << "u * P.n_vals + n.a] >> " << (slot % 32)
+        << "u) & 1u;\n"
+        << "  return g_pred_" << pi << "(V, S, pstr, type, n);\n}\n";
+    }
+  }
+
+  // kvj_ptab: one lane per distinct scalar Val of the batch; evaluates every memo
+  // slot's predicate on the scalar node ingest builds for that value
+  // (kvingest.cpp scalar(): a = val id, b = e_off, c = e_len | NC_* flags)
+  void ptab_kernel() {
+    o << "extern \"C\" __global__ __launch_bounds__(KV_WG) void kvj_ptab(const DevPS* __restrict__ Pp, "
+         "const Val* __restrict__ V, const uint8_t* __restrict__ S, uint32_t NV, uint32_t* __restrict__ PT) {\n"
+      << "  const uint32_t v = blockIdx.x * KV_WG + threadIdx.x;\n"
+      << "  if (v >= NV) return;\n"
+      << "  const uint8_t* __restrict__ pstr = Pp->pstr;\n"
+      << "  const Val& val = V[v];\n"
+      << "  const uint32_t type = val.type;\n"
+      << "  Node n{type, v, val.e_off, val.e_len};\n"
+      << "  if (val.flags & VF_ASCII_E) n.c |= NC_ASCII_E;\n"
+      << "  if (val.flags & VF_BOOLV) n.c |= NC_BOOLV;\n"
+      << "  if (val.flags & VF_NILLIKE) n.c |= NC_NILLIKE;\n"
+      << "  uint32_t w = 0u;\n";
+    for (uint32_t k = 0; k < mpreds.size(); k++) {
+      o << "  if (g_pred_" << mpreds[k] << "(V, S, pstr, type, n)) w |= " << u32(1u << (k % 32)) << ";\n";
+      if (k % 32 == 31 || k + 1 == mpreds.size()) {
+        o << "  PT[(size_t)" << (k / 32) << "u * NV + v] = w;\n";
+        if (k + 1 < mpreds.size()) o << "  w = 0u;\n";
+      }
+    }
+    o << "}\n\n";
   }
 
   // ---------------------------------------------------------------- match / exclude
@@ -403,8 +452,8 @@ struct Gen {
           o << "  { Node vn_{0u, 0u, 0u, 0u}; if (" << cd << " != ABSENT) vn_ = N[" << cd << "];\n"
             << "    const uint32_t vt_ = node_type(vn_.kt); bool ok_;\n"
             << "    if (vt_ == NT_ARR) { ok_ = true; for (uint32_t k_ = 0; k_ < vn_.b && ok_; k_++) { const Node en_ = N[ni(vn_.a + k_)]; "
-            << "ok_ = g_pred_" << in.a << "(V, S, pstr, node_type(en_.kt), en_); } }\n"
-            << "    else ok_ = g_pred_" << in.a << "(V, S, pstr, vt_, vn_);\n"
+            << "ok_ = " << pred_call(in.a, "node_type(en_.kt)", "en_") << "; } }\n"
+            << "    else ok_ = " << pred_call(in.a, "vt_", "vn_") << ";\n"
             << "    if (!ok_) " << raise("E_VALUE", in.b, cd, in.c) << " }\n";
           break;
         case OP_RAISE:
@@ -704,9 +753,9 @@ struct Gen {
           else w << "  { Node vn_{0u, 0u, 0u, 0u}; if (" << cd << " != ABSENT) vn_ = N[" << cd << "];\n";
           w << "    const uint32_t vt_ = node_type(vn_.kt); bool ok_;\n"
             << "    if (vt_ == NT_ARR) { ok_ = true; for (uint32_t k_ = 0; k_ < vn_.b && ok_; k_++) { const Node en_ = "
-               "N[ni(vn_.a + k_)]; ok_ = g_pred_"
-            << in.a << "(V, S, pstr, node_type(en_.kt), en_); } }\n"
-            << "    else ok_ = g_pred_" << in.a << "(V, S, pstr, vt_, vn_);\n"
+               "N[ni(vn_.a + k_)]; ok_ = "
+            << pred_call(in.a, "node_type(en_.kt)", "en_") << "; } }\n"
+            << "    else ok_ = " << pred_call(in.a, "vt_", "vn_") << ";\n"
             << "    if (!ok_) " << raise("E_VALUE", in.b, in.c) << " }\n";
           break;
         case OP_RAISE:
@@ -1060,6 +1109,9 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   // KVGPU_JIT_FUSE=0: one device function per rule (no cross-rule sharing), for A/B runs
   const char* fz = getenv("KVGPU_JIT_FUSE");
   const bool fused = !(fz && fz[0] == '0');
+  // KVGPU_JIT_MEMO=0: evaluate every leaf predicate per pair (no value-predicate table), for A/B runs
+  const char* mz = getenv("KVGPU_JIT_MEMO");
+  g.memo = !(mz && mz[0] == '0');
   for (uint32_t ri = 0; ri < ps.rules.size(); ri++) {
     g.match_fn(ri);
     if (!fused && ps.rules[ri].route == 0) g.rule_fn(ri);
@@ -1089,6 +1141,13 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
       g.chunk_kernel_fused(ch);
       out->chunks.push_back(ch);
     }
+  }
+  out->memo_preds.clear();
+  out->memo_words = 0;
+  if (g.memo && !g.mpreds.empty()) {
+    g.ptab_kernel();
+    out->memo_preds = g.mpreds;
+    out->memo_words = (uint32_t)((g.mpreds.size() + 31) / 32);
   }
   out->source = g.o.str();
   out->gen_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

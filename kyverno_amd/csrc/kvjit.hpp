@@ -22,6 +22,10 @@ struct JitImage {
   std::string source;       // generated HIP source (kept for diagnostics)
   std::vector<JitChunk> chunks;
   std::vector<char> code;   // gfx950 code object
+  // leaf predicates memoized per distinct scalar value: slot k = memo_preds[k];
+  // kernel "kvj_ptab" fills DevPS::ptab (memo_words words per value)
+  std::vector<uint32_t> memo_preds;
+  uint32_t memo_words = 0;
   double gen_ms = 0, compile_ms = 0;
 };
 
