@@ -465,7 +465,7 @@ struct kv_session {
       uint32_t NV = nvals;
       uint32_t* PT = (uint32_t*)ptab.p;
       void* targs[] = {(void*)&P, (void*)&V, (void*)&S, (void*)&NV, (void*)&PT};
-      HIPCHK(hipModuleLaunchKernel(dps->ptab_fn, (NV + KV_WG - 1) / KV_WG, 1, 1, KV_WG, 1, 1, 0, stream, targs,
+      HIPCHK(hipModuleLaunchKernel(dps->ptab_fn, (NV + KV_WG - 1) / KV_WG, dps->memo_words, 1, KV_WG, 1, 1, 0, stream, targs,
                                    nullptr));
     }
     DevOut Ov = O;

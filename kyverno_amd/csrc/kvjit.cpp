@@ -284,15 +284,15 @@ struct Gen {
       << "  if (val.flags & VF_ASCII_E) n.c |= NC_ASCII_E;\n"
       << "  if (val.flags & VF_BOOLV) n.c |= NC_BOOLV;\n"
       << "  if (val.flags & VF_NILLIKE) n.c |= NC_NILLIKE;\n"
-      << "  uint32_t w = 0u;\n";
+      << "  uint32_t w = 0u;\n"
+      << "  switch (blockIdx.y) {  // one table word (32 predicates) per grid row\n";
     for (uint32_t k = 0; k < mpreds.size(); k++) {
-      o << "  if (g_pred_" << mpreds[k] << "(V, S, pstr, type, n)) w |= " << u32(1u << (k % 32)) << ";\n";
-      if (k % 32 == 31 || k + 1 == mpreds.size()) {
-        o << "  PT[(size_t)" << (k / 32) << "u * NV + v] = w;\n";
-        if (k + 1 < mpreds.size()) o << "  w = 0u;\n";
-      }
+      if (k % 32 == 0) o << "    case " << (k / 32) << "u:\n";
+      o << "      if (g_pred_" << mpreds[k] << "(V, S, pstr, type, n)) w |= " << u32(1u << (k % 32)) << ";\n";
+      if (k % 32 == 31 || k + 1 == mpreds.size()) o << "      break;\n";
     }
-    o << "}\n\n";
+    o << "    default: break;\n  }\n"
+      << "  PT[(size_t)blockIdx.y * NV + v] = w;\n}\n\n";
   }
 
   // ---------------------------------------------------------------- match / exclude
@@ -859,7 +859,9 @@ struct Gen {
     return g;
   }
 
-  void chunk_kernel_fused(const JitChunk& ch) {
+  // Code block of one fused chunk inside a kernel body (its own C++ scope); the
+  // chunk's histogram rows are s_hist[hbase, hbase + rules).
+  std::string fused_block(const JitChunk& ch, uint32_t hbase) {
     const uint32_t nr = (uint32_t)ch.rules.size();
     std::vector<RGen> gs;
     HoistTable global;
@@ -969,11 +971,79 @@ struct Gen {
                                          std::to_string(g.ri) + " is not in a segment");
       }
 
-    // kernel (rule ids of the chunk's histogram rows in a device table)
-    o << "__device__ const uint32_t " << ch.name << "_rules[" << nr << "] = {";
-    for (uint32_t q = 0; q < nr; q++) o << (q ? ", " : "") << u32(ch.rules[q]);
+    std::ostringstream k;
+    // per-rule state (rules of other routes only carry rs = FIN | status)
+    for (uint32_t ri : ch.rules) k << "  uint32_t rs_" << ri << " = FIN_ | ST_NOMATCH;\n";
+    for (const RGen& g : gs) {
+      const std::string& s = g.s;
+      k << "  uint32_t ek" << s << " = 0u";
+      for (uint32_t lv = 0; lv <= g.max_level && lv < 4; lv++) k << ", ei" << lv << s << " = 0u";
+      if (g.uses_keyglob) k << ", kn" << s << " = ABSENT, ekn" << s << " = ABSENT";
+      k << ";\n";
+      if (g.uses_anchor) k << "  uint64_t areg" << s << " = 0ull, apres" << s << " = 0ull;\n";
+      k << "  uint32_t c0" << s << " = root";
+      for (uint32_t d = 1; d < g.maxd; d++) k << ", c" << d << s << " = ABSENT";
+      k << ";\n";
+      k << "  uint32_t";
+      for (uint32_t l = 0; l <= g.max_level && l < 4; l++)
+        k << (l ? "," : "") << " li" << l << s << " = 0u, lf" << l << s << " = 0u, ll" << l << s << " = 0u";
+      k << ";\n";
+    }
+    // match / route
+    for (uint32_t ri : ch.rules) {
+      const RuleRec& rr = ps.rules[ri];
+      const std::string s = "_" + std::to_string(ri);
+      k << "  if (valid && g_match_" << ri << "(P, B, R, rkind, rflags)) {\n";
+      switch (rr.route) {
+        case 1: k << "    rs" << s << " = FIN_ | ST_CPU;\n"; break;
+        case 2: k << "    rs" << s << " = FIN_ | ST_NOMATCH;\n"; break;
+        case 3: k << "    rs" << s << " = FIN_ | " << u32(rr.const_status) << ";\n"; break;
+        default:
+          k << "    if (rflags & RF_MAGIC) rs" << s << " = FIN_ | ST_CPU;\n";
+          if (rr.flags & RR_META_EXPAND) k << "    else if (rflags & RF_BAD_META) rs" << s << " = FIN_ | ST_CPU;\n";
+          k << "    else rs" << s << " = " << u32(rr.prog) << ";\n";
+          break;
+      }
+      k << "  }\n";
+    }
+    k << body.str();
+    std::set<uint32_t> gpu;
+    for (const RGen& g : gs) gpu.insert(g.ri);
+    for (uint32_t q = 0; q < ch.rules.size(); q++) {
+      const uint32_t ri = ch.rules[q];
+      const std::string s = "_" + std::to_string(ri);
+      if (gpu.count(ri)) {
+        const RGen* g = nullptr;
+        for (const RGen& x : gs)
+          if (x.ri == ri) g = &x;
+        k << "  { EState e_{ek" << s << " & 15u, (ek" << s << " >> 4) & 15u, ek" << s << " >> 8, "
+          << (g->uses_keyglob ? "ekn" + s : std::string("ABSENT")) << ", ABSENT";
+        for (uint32_t lv = 0; lv < 4; lv++) k << ", " << (lv <= g->max_level ? "ei" + std::to_string(lv) + s : "0u");
+        k << "};\n";
+      } else {
+        k << "  { EState e_{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u};\n";
+      }
+      k << "    store_result2(O, " << ri << "u, n_res, r, valid, rs" << s << " & 0xFFu, e_, &s_hist[" << (hbase + q)
+        << "][0]); }\n";
+    }
+    return k.str();
+  }
+
+  // One kernel running the fused chunks `chs` one after the other for each
+  // resource: a workgroup re-reads its resources' node rows per chunk while they
+  // are still cache-resident, instead of one grid-wide pass per chunk.
+  void group_kernel(const std::string& name, const std::vector<const JitChunk*>& chs) {
+    std::vector<std::string> blocks;
+    std::vector<uint32_t> rules;
+    for (const JitChunk* c : chs) {
+      blocks.push_back(fused_block(*c, (uint32_t)rules.size()));
+      rules.insert(rules.end(), c->rules.begin(), c->rules.end());
+    }
+    const uint32_t nr = (uint32_t)rules.size();
+    o << "__device__ const uint32_t " << name << "_rules[" << nr << "] = {";
+    for (uint32_t q = 0; q < nr; q++) o << (q ? ", " : "") << u32(rules[q]);
     o << "};\n";
-    o << "extern \"C\" __global__ __launch_bounds__(KV_WG) void " << ch.name
+    o << "extern \"C\" __global__ __launch_bounds__(KV_WG) void " << name
       << "(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp, const Node* __restrict__ N, "
          "const Val* __restrict__ V, const uint8_t* __restrict__ S, DevOut O) {\n"
       << "  constexpr uint32_t FIN_ = " << u32(FIN) << ", ACT_ = " << u32(ACT) << ";\n"
@@ -988,65 +1058,11 @@ struct Gen {
       << "  uint32_t root = ABSENT, rkind = KEY_NONE, rflags = 0u;\n"
       << "  if (valid) { root = ni(R->root); rkind = R->kind; rflags = R->flags; }\n"
       << "  Node rootn{0u, 0u, 0u, 0u};\n  if (valid) rootn = N[root];\n";
-    // per-rule state (rules of other routes only carry rs = FIN | status)
-    for (uint32_t ri : ch.rules) o << "  uint32_t rs_" << ri << " = FIN_ | ST_NOMATCH;\n";
-    for (const RGen& g : gs) {
-      const std::string& s = g.s;
-      o << "  uint32_t ek" << s << " = 0u";
-      for (uint32_t lv = 0; lv <= g.max_level && lv < 4; lv++) o << ", ei" << lv << s << " = 0u";
-      if (g.uses_keyglob) o << ", kn" << s << " = ABSENT, ekn" << s << " = ABSENT";
-      o << ";\n";
-      if (g.uses_anchor) o << "  uint64_t areg" << s << " = 0ull, apres" << s << " = 0ull;\n";
-      o << "  uint32_t c0" << s << " = root";
-      for (uint32_t d = 1; d < g.maxd; d++) o << ", c" << d << s << " = ABSENT";
-      o << ";\n";
-      if (g.max_level > 0 || !g.loops.empty() || true) {
-        o << "  uint32_t";
-        for (uint32_t l = 0; l <= g.max_level && l < 4; l++)
-          o << (l ? "," : "") << " li" << l << s << " = 0u, lf" << l << s << " = 0u, ll" << l << s << " = 0u";
-        o << ";\n";
-      }
-    }
-    // match / route
-    for (uint32_t ri : ch.rules) {
-      const RuleRec& rr = ps.rules[ri];
-      const std::string s = "_" + std::to_string(ri);
-      o << "  if (valid && g_match_" << ri << "(P, B, R, rkind, rflags)) {\n";
-      switch (rr.route) {
-        case 1: o << "    rs" << s << " = FIN_ | ST_CPU;\n"; break;
-        case 2: o << "    rs" << s << " = FIN_ | ST_NOMATCH;\n"; break;
-        case 3: o << "    rs" << s << " = FIN_ | " << u32(rr.const_status) << ";\n"; break;
-        default:
-          o << "    if (rflags & RF_MAGIC) rs" << s << " = FIN_ | ST_CPU;\n";
-          if (rr.flags & RR_META_EXPAND) o << "    else if (rflags & RF_BAD_META) rs" << s << " = FIN_ | ST_CPU;\n";
-          o << "    else rs" << s << " = " << u32(rr.prog) << ";\n";
-          break;
-      }
-      o << "  }\n";
-    }
-    o << body.str();
-    std::set<uint32_t> gpu;
-    for (const RGen& g : gs) gpu.insert(g.ri);
-    for (uint32_t q = 0; q < nr; q++) {
-      const uint32_t ri = ch.rules[q];
-      const std::string s = "_" + std::to_string(ri);
-      if (gpu.count(ri)) {
-        const RGen* g = nullptr;
-        for (const RGen& x : gs)
-          if (x.ri == ri) g = &x;
-        o << "  { EState e_{ek" << s << " & 15u, (ek" << s << " >> 4) & 15u, ek" << s << " >> 8, "
-          << (g->uses_keyglob ? "ekn" + s : std::string("ABSENT")) << ", ABSENT";
-        for (uint32_t lv = 0; lv < 4; lv++) o << ", " << (lv <= g->max_level ? "ei" + std::to_string(lv) + s : "0u");
-        o << "};\n";
-      } else {
-        o << "  { EState e_{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u};\n";
-      }
-      o << "    store_result2(O, " << ri << "u, n_res, r, valid, rs" << s << " & 0xFFu, e_, &s_hist[" << q << "][0]); }\n";
-    }
+    for (const std::string& b : blocks) o << "  {\n" << b << "  }\n";
     o << "  __syncthreads();\n"
       << "  for (uint32_t q = threadIdx.x; q < " << nr << "u * KV_HIST; q += KV_WG) {\n"
       << "    const uint32_t v = (&s_hist[0][0])[q];\n"
-      << "    if (v) atomicAdd(&O.counts[(size_t)" << ch.name << "_rules[q / KV_HIST] * KV_HIST + q % KV_HIST], "
+      << "    if (v) atomicAdd(&O.counts[(size_t)" << name << "_rules[q / KV_HIST] * KV_HIST + q % KV_HIST], "
          "(unsigned long long)v);\n"
       << "  }\n}\n\n";
   }
@@ -1134,12 +1150,25 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
     for (uint32_t ri = 0; ri < n; ri++)
       order.push_back({ps.rules[ri].route == 0 ? "0" + rule_signature(ps, ri) : "1", ri});
     std::stable_sort(order.begin(), order.end());
+    // KVGPU_JIT_GROUP: fused chunks run back to back inside one kernel (default 3)
+    const char* gz = getenv("KVGPU_JIT_GROUP");
+    const uint32_t group = gz ? std::max(1, atoi(gz)) : 3u;
+    std::vector<JitChunk> chs;
     for (uint32_t b = 0; b < n; b += chunk_rules) {
       JitChunk ch;
       for (uint32_t q = b; q < std::min(n, b + chunk_rules); q++) ch.rules.push_back(order[q].second);
-      ch.name = "kvj_chunk_" + std::to_string(out->chunks.size());
-      g.chunk_kernel_fused(ch);
-      out->chunks.push_back(ch);
+      chs.push_back(ch);
+    }
+    for (size_t b = 0; b < chs.size(); b += group) {
+      JitChunk kc;
+      kc.name = "kvj_chunk_" + std::to_string(out->chunks.size());
+      std::vector<const JitChunk*> part;
+      for (size_t q = b; q < std::min(chs.size(), b + group); q++) {
+        part.push_back(&chs[q]);
+        kc.rules.insert(kc.rules.end(), chs[q].rules.begin(), chs[q].rules.end());
+      }
+      g.group_kernel(kc.name, part);
+      out->chunks.push_back(kc);
     }
   }
   out->memo_preds.clear();
