@@ -45,6 +45,16 @@ constexpr uint32_t NC_BOOLV = 1u << 30;
 constexpr uint32_t NC_NILLIKE = 1u << 29;  // validateValueWithNilPattern true (0, 0.0, "", false)
 constexpr uint32_t NC_LEN_MASK = 0x1FFFFFFFu;
 KV_HD inline uint32_t node_type(uint32_t kt) { return kt & 15u; }
+// Position classes of stored values (value-predicate table pruning): a value's
+// position is its projection-trie node, or for an array element the trie's
+// element node (kv_pos_elem: a pseudo id when the trie has none); -1 = a child
+// of a keep-all map or an element of an unknown position. Both ingest and the
+// specialized-kernel generator derive the same ids from the same trie.
+KV_HD inline int32_t kv_pos_elem(int32_t pos, int32_t trie_node) {
+  (void)trie_node;
+  return pos < 0 ? -1 : (int32_t)(0x100000 + pos);
+}
+KV_HD inline uint32_t kv_tcls(int32_t pos) { return 1u << (pos < 0 ? 31u : (uint32_t)pos % 31u); }
 KV_HD inline uint32_t node_key(uint32_t kt) { return kt >> 4; }
 
 constexpr uint32_t KEY_NONE = 0xFFFFFFFFu;
@@ -59,7 +69,8 @@ struct Val {
   uint32_t e_off, e_len;  // validateString form: FormatFloat 'E' / decimal / raw / "true"|"false"
   uint32_t n_off, n_len;  // validateNumberWithStr form: %f / decimal / raw (invalid for bool)
   int32_t q_exp;          // quantity of the n-form: order of magnitude (digits + exp10)
-  uint32_t q_pad;
+  uint32_t cls;           // position classes referencing this value: bit kv_tcls(trie node) of every node
+                          // holding it (value-predicate table pruning, kvjit.cpp ptab_kernel)
   uint64_t q_hi, q_lo;    // 38 left-aligned significant decimal digits (19 + 19)
   double f;               // FLOAT: value; STR: ParseFloat(value) when VF_PF_OK
   int64_t i;              // INT: value

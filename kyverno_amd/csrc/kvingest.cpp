@@ -205,8 +205,9 @@ struct Ingest {
     for (auto& e : s.elems) assign(e, next);
   }
 
-  Node scalar(const JDoc& d, const JNode& n, uint32_t type, uint32_t key) {
+  Node scalar(const JDoc& d, const JNode& n, uint32_t type, uint32_t key, int32_t pos) {
     const uint32_t vid = val(d, n);
+    b.vals[vid].cls |= kv_tcls(pos);
     const Val& v = b.vals[vid];
     Node out{(key & KEY_NONE28) << 4 | type, vid, v.e_off, v.e_len};
     if (v.e_len > NC_LEN_MASK) throw std::runtime_error("ingest: string value too long");
@@ -220,15 +221,16 @@ struct Ingest {
   Node& cell(uint32_t row, uint32_t lane) { return b.nodes[(size_t)(base_row + row) * KV_LANES + lane]; }
 
   // Write lane's value at shape position s (key = key id in the parent map)
-  void put(const Shape& s, const JDoc& d, uint32_t jn, uint32_t lane, uint32_t key) {
+  // pos: position class id of this value (kv_pos_*; Val::cls)
+  void put(const Shape& s, const JDoc& d, uint32_t jn, uint32_t lane, uint32_t key, int32_t pos) {
     const JNode& n = d.at(jn);
     Node out{(key & KEY_NONE28) << 4 | NT_NULL, 0, 0, 0};
     switch (n.t) {
       case J_NULL: break;
-      case J_BOOL: out = scalar(d, n, NT_BOOL, key); break;
-      case J_INT: out = scalar(d, n, NT_INT, key); break;
-      case J_FLOAT: out = scalar(d, n, NT_FLOAT, key); break;
-      case J_STR: out = scalar(d, n, NT_STR, key); break;
+      case J_BOOL: out = scalar(d, n, NT_BOOL, key, pos); break;
+      case J_INT: out = scalar(d, n, NT_INT, key, pos); break;
+      case J_FLOAT: out = scalar(d, n, NT_FLOAT, key, pos); break;
+      case J_STR: out = scalar(d, n, NT_STR, key, pos); break;
       case J_MAP: {
         out.kt = (key & KEY_NONE28) << 4 | NT_MAP;
         if (s.t < 0) break;
@@ -238,7 +240,7 @@ struct Ingest {
           out.b = n.count;
           std::vector<uint32_t> ch;
           sorted_children(d, n, &ch);
-          for (size_t i = 0; i < ch.size(); i++) put(s.kids[i], d, ch[i], lane, key_of(d.key(d.at(ch[i]))));
+          for (size_t i = 0; i < ch.size(); i++) put(s.kids[i], d, ch[i], lane, key_of(d.key(d.at(ch[i]))), -1);
         } else {
           const uint32_t K = (uint32_t)tn.slot_keys.size();
           out.b = K;
@@ -247,7 +249,7 @@ struct Ingest {
           for (uint32_t i = 0; i < K; i++) cell(s.map_row + i, lane) = Node{(ids[i] & KEY_NONE28) << 4 | NT_ABSENT, 0, 0, 0};
           for (uint32_t c = n.first; c < n.first + n.count; c++) {
             auto it = tn.slot.find(std::string(d.key(d.at(c))));
-            if (it != tn.slot.end()) put(s.kids[it->second], d, c, lane, ids[it->second]);
+            if (it != tn.slot.end()) put(s.kids[it->second], d, c, lane, ids[it->second], s.kids[it->second].t);
           }
         }
         break;
@@ -256,7 +258,7 @@ struct Ingest {
         out.kt = (key & KEY_NONE28) << 4 | NT_ARR;
         out.a = (uint32_t)(base_row + s.arr_row);
         out.b = n.count;
-        for (uint32_t j = 0; j < n.count; j++) put(s.elems[j], d, n.first + j, lane, KEY_NONE);
+        for (uint32_t j = 0; j < n.count; j++) put(s.elems[j], d, n.first + j, lane, KEY_NONE, kv_pos_elem(pos, s.t));
         break;
       }
     }
@@ -279,7 +281,7 @@ struct Ingest {
     if (b.n_rows * KV_LANES >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: batch too large for 32-bit node indices");
     b.nodes.resize((size_t)b.n_rows * KV_LANES, Node{NT_NULL, 0, 0, 0});
     for (uint32_t l = 0; l < group_n; l++) {
-      put(root, group[l], group[l].root, l, KEY_NONE);
+      put(root, group[l], group[l].root, l, KEY_NONE, 0);
       b.res[b.res.size() - group_n + l].root = (uint32_t)base_row;
     }
     for (size_t c = (size_t)base_row * KV_LANES; c < b.nodes.size(); c++)

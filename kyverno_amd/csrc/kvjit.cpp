@@ -269,6 +269,54 @@ struct Gen {
     }
   }
 
+  // Position classes of every leaf predicate: the projection-trie node of each
+  // cursor is followed through the rule program (KEY: slot child, LOOP/EXIST/
+  // INDEX: element node, keep-all scans: leaf-only positions, KEYGLOB: unknown),
+  // and a predicate gets the class bit of every position it tests (its cursor,
+  // and the element position when the value is an array). Ingest marks each
+  // value with the class bits of the positions holding it (Val::cls), so the
+  // table bit of (pred, value) is computed exactly when some node could read it.
+  std::map<uint32_t, uint32_t> pmask;
+  void leaf_classes(uint32_t ri) {
+    // per cursor depth: projection-trie node (child lookups) and position id (value classes,
+    // kv_pos_elem); -2 = unknown (every class)
+    std::vector<int32_t> tn(8, -2), pos(8, -2);
+    tn[0] = 0;
+    pos[0] = 0;
+    auto cls = [&](int32_t p) -> uint32_t { return p == -2 ? 0xFFFFFFFFu : kv_tcls(p); };
+    auto epos = [&](int32_t p) -> int32_t { return p == -2 ? -2 : kv_pos_elem(p, 0); };
+    for (uint32_t pc = ps.rules[ri].prog; pc < ps.prog.size(); pc++) {
+      const Inst& in = ps.prog[pc];
+      const uint32_t op = in.op & 0xFF, d = (in.op >> 8) & 0xFF, aux = (in.op >> 16) & 0xFF;
+      if (op == OP_DONE) break;
+      if (d + 2 > tn.size()) { tn.resize(d + 2, -2); pos.resize(d + 2, -2); }
+      switch (op) {
+        case OP_KEY:
+        case OP_KEYV: {
+          const int32_t t = tn[d];
+          if (aux & AUX_SCAN) {  // children of keep-all maps: leaf-only positions
+            tn[d + 1] = t == -2 ? -2 : -1;
+            pos[d + 1] = t == -2 ? -2 : -1;
+          } else if (t >= 0 && in.a < ps.trie.nodes[t].slot_keys.size()) {
+            tn[d + 1] = pos[d + 1] = (int32_t)ps.trie.nodes[t].kids.at(ps.trie.nodes[t].slot_keys[in.a]);
+          } else {
+            tn[d + 1] = pos[d + 1] = -2;
+          }
+          break;
+        }
+        case OP_KEYGLOB: tn[d + 1] = pos[d + 1] = -2; break;
+        case OP_LOOP_BEGIN:
+        case OP_EXIST_BEGIN:
+        case OP_INDEX:
+          tn[d + 1] = tn[d] >= 0 ? ps.trie.nodes[tn[d]].elem : tn[d];
+          pos[d + 1] = epos(pos[d]);
+          break;
+        case OP_LEAF: pmask[in.a] |= cls(pos[d]) | cls(epos(pos[d])); break;
+        default: break;
+      }
+    }
+  }
+
   // kvj_ptab: one lane per distinct scalar Val of the batch; evaluates every memo
   // slot's predicate on the scalar node ingest builds for that value
   // (kvingest.cpp scalar(): a = val id, b = e_off, c = e_len | NC_* flags)
@@ -284,11 +332,18 @@ struct Gen {
       << "  if (val.flags & VF_ASCII_E) n.c |= NC_ASCII_E;\n"
       << "  if (val.flags & VF_BOOLV) n.c |= NC_BOOLV;\n"
       << "  if (val.flags & VF_NILLIKE) n.c |= NC_NILLIKE;\n"
+      << "  const uint32_t vc = val.cls;\n"
       << "  uint32_t w = 0u;\n"
       << "  switch (blockIdx.y) {  // one table word (32 predicates) per grid row\n";
+    auto pm = [&](uint32_t k) { auto it = pmask.find(mpreds[k]); return it == pmask.end() ? 0xFFFFFFFFu : it->second; };
     for (uint32_t k = 0; k < mpreds.size(); k++) {
-      if (k % 32 == 0) o << "    case " << (k / 32) << "u:\n";
-      o << "      if (g_pred_" << mpreds[k] << "(V, S, pstr, type, n)) w |= " << u32(1u << (k % 32)) << ";\n";
+      if (k % 32 == 0) {
+        uint32_t wm = 0;
+        for (uint32_t q = k; q < std::min<size_t>(k + 32, mpreds.size()); q++) wm |= pm(q);
+        o << "    case " << (k / 32) << "u:\n      if (!(vc & " << u32(wm) << ")) break;\n";
+      }
+      o << "      if ((vc & " << u32(pm(k)) << ") && g_pred_" << mpreds[k] << "(V, S, pstr, type, n)) w |= "
+        << u32(1u << (k % 32)) << ";\n";
       if (k % 32 == 31 || k + 1 == mpreds.size()) o << "      break;\n";
     }
     o << "    default: break;\n  }\n"
@@ -1128,6 +1183,8 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   // KVGPU_JIT_MEMO=0: evaluate every leaf predicate per pair (no value-predicate table), for A/B runs
   const char* mz = getenv("KVGPU_JIT_MEMO");
   g.memo = !(mz && mz[0] == '0');
+  for (uint32_t ri = 0; ri < ps.rules.size(); ri++)
+    if (ps.rules[ri].route == 0) g.leaf_classes(ri);
   for (uint32_t ri = 0; ri < ps.rules.size(); ri++) {
     g.match_fn(ri);
     if (!fused && ps.rules[ri].route == 0) g.rule_fn(ri);
