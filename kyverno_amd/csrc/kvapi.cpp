@@ -176,7 +176,10 @@ DevPolicySet& dev_ps(kv_policyset* s, int device) {
   v.gwords = (const GWord*)d->gwords.p;
   v.n_rules = (uint32_t)ps.rules.size();
   v.pstr = (const uint8_t*)d->pstr.p;
+  // resource version "*" (checkKind, pkg/engine/utils.go:49): when "*" is not in the key dictionary no
+  // resource can carry it, and an unknown version (KEY_NONE) must not compare equal to it
   v.star_id = ps.lookup("*");
+  if (v.star_id == KEY_NONE) v.star_id = KEY_NONE - 1;
   d->dev = device;
   if (s->jit) {
     HIPCHK(hipModuleLoadData(&d->mod, s->jit->code.data()));
