@@ -1098,7 +1098,14 @@ struct Gen {
     o << "__device__ const uint32_t " << name << "_rules[" << nr << "] = {";
     for (uint32_t q = 0; q < nr; q++) o << (q ? ", " : "") << u32(rules[q]);
     o << "};\n";
-    o << "extern \"C\" __global__ __launch_bounds__(KV_WG) void " << name
+    // Occupancy over registers: the rule kernels are latency-bound on dependent
+    // tree loads, so ask for 8 waves per SIMD (<= 64 VGPRs, a few spilled cursor
+    // registers) — measured faster on C2-C5 than the unconstrained 86-102 VGPRs.
+    // KVGPU_JIT_WAVES=w overrides (0: no bound).
+    const char* wz = getenv("KVGPU_JIT_WAVES");
+    const int waves = wz ? atoi(wz) : 8;
+    const std::string lb = waves > 0 ? "KV_WG, " + std::to_string(waves) : "KV_WG";
+    o << "extern \"C\" __global__ __launch_bounds__(" << lb << ") void " << name
       << "(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp, const Node* __restrict__ N, "
          "const Val* __restrict__ V, const uint8_t* __restrict__ S, DevOut O) {\n"
       << "  constexpr uint32_t FIN_ = " << u32(FIN) << ", ACT_ = " << u32(ACT) << ";\n"
