@@ -76,7 +76,7 @@ struct DevPolicySet {
   hipModule_t mod = nullptr;
   std::vector<hipFunction_t> fns;
   hipFunction_t ptab_fn = nullptr;  // value-predicate table builder (kvj_ptab)
-  uint32_t memo_words = 0;
+  uint32_t memo_words = 0, ptab_rows = 0;
   int dev = -1;
   ~DevPolicySet() {
     if (mod) {
@@ -198,6 +198,7 @@ DevPolicySet& dev_ps(kv_policyset* s, int device) {
     if (s->jit->memo_words) {
       HIPCHK(hipModuleGetFunction(&d->ptab_fn, d->mod, "kvj_ptab"));
       d->memo_words = s->jit->memo_words;
+      d->ptab_rows = (uint32_t)((s->jit->memo_preds.size() + 15) / 16);  // kvjit.cpp kPtabRow
     }
   }
   auto& ref = *d;
@@ -468,7 +469,7 @@ struct kv_session {
       uint32_t NV = nvals;
       uint32_t* PT = (uint32_t*)ptab.p;
       void* targs[] = {(void*)&P, (void*)&V, (void*)&S, (void*)&NV, (void*)&PT};
-      HIPCHK(hipModuleLaunchKernel(dps->ptab_fn, (NV + KV_WG - 1) / KV_WG, dps->memo_words, 1, KV_WG, 1, 1, 0, stream, targs,
+      HIPCHK(hipModuleLaunchKernel(dps->ptab_fn, (NV + KV_WG - 1) / KV_WG, dps->ptab_rows, 1, KV_WG, 1, 1, 0, stream, targs,
                                    nullptr));
     }
     DevOut Ov = O;

@@ -64,7 +64,7 @@ struct Gen {
   // call of leaf predicate `pi` on node `n` of type `t`
   std::string pred_call(uint32_t pi, const std::string& t, const std::string& n) {
     return std::string(memo ? "m_pred_" : "g_pred_") + std::to_string(pi) +
-           (memo ? "(P, V, S, pstr, " : "(V, S, pstr, ") + t + ", " + n + ")";
+           (memo ? "(P, V, S, pstr, " : "(V, S, S + (" + n + ").b, pstr, ") + t + ", " + n + ")";
   }
 
   // ---------------------------------------------------------------- globs
@@ -172,19 +172,19 @@ struct Gen {
     const Atom& A = ps.atoms[ai];
     if (A.kind == AT_GLOB_E || A.kind == AT_GLOB_N) glob_fn(ai);
     o << "__device__ __forceinline__ bool g_atom_" << ai
-      << "(const Val* __restrict__ V, const uint8_t* __restrict__ S, const uint8_t* __restrict__ pstr, uint32_t type, "
-         "const Node& n) {\n";
+      << "(const Val* __restrict__ V, const uint8_t* __restrict__ S, const uint8_t* __restrict__ E, "
+         "const uint8_t* __restrict__ pstr, uint32_t type, const Node& n) {\n";
     switch (A.kind) {
       case AT_FALSE: o << "  return false;\n"; break;
       case AT_GLOB_E:
         o << "  if (type == NT_MAP || type == NT_ARR || type == NT_NULL) return false;\n"
-          << "  const bool r = g_glob_" << ai << "(S + n.b, n.c & NC_LEN_MASK, (n.c & NC_ASCII_E) != 0u, pstr);\n"
+          << "  const bool r = g_glob_" << ai << "(E, n.c & NC_LEN_MASK, (n.c & NC_ASCII_E) != 0u, pstr);\n"
           << "  return " << (A.op == CO_NE ? "!r" : "r") << ";\n";
         break;
       case AT_GLOB_N:
         o << "  if (type == NT_MAP || type == NT_ARR || type == NT_BOOL) return false;\n"
           << "  if (type == NT_NULL) return g_glob_" << ai << "(S, 1u, true, pstr);\n"
-          << "  if (type != NT_FLOAT) return g_glob_" << ai << "(S + n.b, n.c & NC_LEN_MASK, (n.c & NC_ASCII_E) != 0u, pstr);\n"
+          << "  if (type != NT_FLOAT) return g_glob_" << ai << "(E, n.c & NC_LEN_MASK, (n.c & NC_ASCII_E) != 0u, pstr);\n"
           << "  const Val& v = V[n.a];\n"
           << "  return g_glob_" << ai << "(S + v.n_off, v.n_len, (v.flags & VF_ASCII_N) != 0u, pstr);\n";
         break;
@@ -219,9 +219,10 @@ struct Gen {
         }
       }
     }
+    // E: the validateString (e-form) bytes of the value, S + n.b in the rule kernels (a staged copy in kvj_ptab)
     o << "__device__ __forceinline__ bool g_pred_" << pi
-      << "(const Val* __restrict__ V, const uint8_t* __restrict__ S, const uint8_t* __restrict__ pstr, uint32_t type, "
-         "const Node& n) {\n";
+      << "(const Val* __restrict__ V, const uint8_t* __restrict__ S, const uint8_t* __restrict__ E, "
+         "const uint8_t* __restrict__ pstr, uint32_t type, const Node& n) {\n";
     switch (pr.kind) {
       case PK_BOOL: o << "  return type == NT_BOOL && ((n.c & NC_BOOLV) != 0u) == " << (pr.flags ? "true" : "false") << ";\n"; break;
       case PK_FLOAT:
@@ -242,7 +243,7 @@ struct Gen {
           o << "  if (true";
           for (uint32_t c = al.first; c < al.first + al.count; c++) {
             const Conj& cj = ps.conjs[c];
-            auto call = [&](uint32_t at) { return "g_atom_" + std::to_string(at) + "(V, S, pstr, type, n)"; };
+            auto call = [&](uint32_t at) { return "g_atom_" + std::to_string(at) + "(V, S, E, pstr, type, n)"; };
             if (cj.kind == CJ_INRANGE) o << " && (" << call(cj.a0) << " && " << call(cj.a1) << ")";
             else if (cj.kind == CJ_NOTINRANGE) o << " && (" << call(cj.a0) << " || " << call(cj.a1) << ")";
             else o << " && " << call(cj.a0);
@@ -265,7 +266,7 @@ struct Gen {
            "uint32_t type, const Node& n) {\n"
         << "  if (type - 1u < 4u) return (P.ptab[(size_t)" << (slot / 32) << "u * P.n_vals + n.a] >> " << (slot % 32)
         << "u) & 1u;\n"
-        << "  return g_pred_" << pi << "(V, S, pstr, type, n);\n}\n";
+        << "  return g_pred_" << pi << "(V, S, S + n.b, pstr, type, n);\n}\n";
     }
   }
 
@@ -320,6 +321,10 @@ struct Gen {
   // kvj_ptab: one lane per distinct scalar Val of the batch; evaluates every memo
   // slot's predicate on the scalar node ingest builds for that value
   // (kvingest.cpp scalar(): a = val id, b = e_off, c = e_len | NC_* flags)
+  // One grid row per 16 predicates (half a table word, stored as a u16 half):
+  // keeps the code of a row (16 inlined globs / compares) within the
+  // instruction cache — 32-predicate rows stalled on instruction fetch.
+  static constexpr uint32_t kPtabRow = 16;
   void ptab_kernel() {
     o << "extern \"C\" __global__ __launch_bounds__(KV_WG) void kvj_ptab(const DevPS* __restrict__ Pp, "
          "const Val* __restrict__ V, const uint8_t* __restrict__ S, uint32_t NV, uint32_t* __restrict__ PT) {\n"
@@ -333,21 +338,23 @@ struct Gen {
       << "  if (val.flags & VF_BOOLV) n.c |= NC_BOOLV;\n"
       << "  if (val.flags & VF_NILLIKE) n.c |= NC_NILLIKE;\n"
       << "  const uint32_t vc = val.cls;\n"
+      << "  const uint8_t* __restrict__ E = S + val.e_off;\n"
       << "  uint32_t w = 0u;\n"
-      << "  switch (blockIdx.y) {  // one table word (32 predicates) per grid row\n";
+      << "  switch (blockIdx.y) {\n";
     auto pm = [&](uint32_t k) { auto it = pmask.find(mpreds[k]); return it == pmask.end() ? 0xFFFFFFFFu : it->second; };
-    for (uint32_t k = 0; k < mpreds.size(); k++) {
-      if (k % 32 == 0) {
-        uint32_t wm = 0;
-        for (uint32_t q = k; q < std::min<size_t>(k + 32, mpreds.size()); q++) wm |= pm(q);
-        o << "    case " << (k / 32) << "u:\n      if (!(vc & " << u32(wm) << ")) break;\n";
-      }
-      o << "      if ((vc & " << u32(pm(k)) << ") && g_pred_" << mpreds[k] << "(V, S, pstr, type, n)) w |= "
-        << u32(1u << (k % 32)) << ";\n";
-      if (k % 32 == 31 || k + 1 == mpreds.size()) o << "      break;\n";
+    for (uint32_t k0 = 0; k0 < mpreds.size(); k0 += kPtabRow) {
+      const uint32_t k1 = (uint32_t)std::min<size_t>(k0 + kPtabRow, mpreds.size());
+      uint32_t wm = 0;
+      for (uint32_t q = k0; q < k1; q++) wm |= pm(q);
+      o << "    case " << (k0 / kPtabRow) << "u:\n      if (!(vc & " << u32(wm) << ")) break;\n";
+      for (uint32_t k = k0; k < k1; k++)
+        o << "      if ((vc & " << u32(pm(k)) << ") && g_pred_" << mpreds[k] << "(V, S, E, pstr, type, n)) w |= "
+          << u32(1u << (k % kPtabRow)) << ";\n";
+      o << "      break;\n";
     }
     o << "    default: break;\n  }\n"
-      << "  PT[(size_t)blockIdx.y * NV + v] = w;\n}\n\n";
+      << "  // row y = bits [16 (y % 2), +16) of table word y / 2 (little-endian u16 halves)\n"
+      << "  ((uint16_t*)PT)[((size_t)(blockIdx.y >> 1) * NV + v) * 2u + (blockIdx.y & 1u)] = (uint16_t)w;\n}\n\n";
   }
 
   // ---------------------------------------------------------------- match / exclude
