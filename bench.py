@@ -118,6 +118,7 @@ def main():
         log(f"[rank {rank}] specialized kernels: {jit['kernels']} ({jit['code_bytes'] / 1e3:.0f} KB code), "
             f"hiprtc {jit['compile_ms'] / 1e3:.1f}s")
     data = batch.synth(workloads.SEED + rank, args.n_res, kind_mix)
+    ndjson_bytes = len(data)
     t1 = time.time()
     b = batch.Batch(ps, data)
     del data
@@ -204,6 +205,10 @@ def main():
     }
     if scopes is not None:
         out["policy_reports"] = scopes
+    # host ingest (NDJSON -> projected columnar store, kv_ingest; multi-threaded), outside `value`
+    out["ingest"] = {"seconds": t2 - t1, "resources_per_s": b.n_res / (t2 - t1),
+                     "MB_per_s": ndjson_bytes / (t2 - t1) / 1e6,
+                     "threads": int(os.environ.get("KVGPU_INGEST_THREADS", min(16, os.cpu_count() or 1)))}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
         out["cpu_baseline"] = cpu_baseline(pols, args.cpu_sample, threads, kind_mix, args.config.upper())

@@ -10,8 +10,13 @@
 // Resource identity for match/exclude follows unstructured accessors
 // (GetKind/GetName/GetNamespace/GetLabels/GetAnnotations, GroupVersionKind).
 #include <algorithm>
+#include <array>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
+#include <thread>
 #include <unordered_map>
 
 #include "kvinternal.hpp"
@@ -400,10 +405,214 @@ struct Ingest {
 
 }  // namespace
 
+namespace {
+
+unsigned ingest_threads() {
+  if (const char* e = getenv("KVGPU_INGEST_THREADS")) return (unsigned)std::max(1, atoi(e));
+  return std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+}
+
+// Start offsets of the top-level values of a JSON value stream (NDJSON, one or
+// more values per line). The stream is cut at newlines followed by '{' and each
+// piece is scanned in parallel (string / escape / depth tracking); a cut that
+// fell inside a value (pretty-printed input) shows up as a piece not ending at
+// depth 0, and the caller then ingests serially.
+bool scan_values(const char* p, size_t n, unsigned T, std::vector<size_t>* starts) {
+  std::vector<size_t> cut{0};
+  for (unsigned k = 1; k < T; k++) {
+    size_t x = std::max(cut.back() + 1, n / T * k);
+    while (x < n && !(p[x - 1] == '\n' && p[x] == '{')) x++;
+    if (x >= n) break;
+    cut.push_back(x);
+  }
+  cut.push_back(n);
+  const size_t P = cut.size() - 1;
+  std::vector<std::vector<size_t>> part(P);
+  std::vector<char> ok(P, 0);
+  std::vector<std::thread> th;
+  for (size_t k = 0; k < P; k++)
+    th.emplace_back([&, k]() {
+      // byte classes: 0 plain, 1 quote, 2 backslash, 3 open, 4 close
+      static const auto cls = []() {
+        std::array<uint8_t, 256> t{};
+        t['"'] = 1; t['\\'] = 2; t['{'] = 3; t['['] = 3; t['}'] = 4; t[']'] = 4;
+        return t;
+      }();
+      int depth = 0;
+      const uint8_t* q = (const uint8_t*)p;
+      size_t i = cut[k];
+      const size_t e = cut[k + 1];
+      while (i < e) {
+        const uint8_t c = cls[q[i]];
+        if (c == 0) { i++; continue; }
+        if (c == 1) {  // string: skip to the closing quote
+          if (depth == 0) return;  // top-level scalar: not a resource stream
+          i++;
+          while (i < e) {
+            const uint8_t d = cls[q[i]];
+            if (d == 1) break;
+            i += d == 2 ? 2 : 1;
+          }
+          if (i >= e) return;  // unterminated string in this piece
+          i++;
+          continue;
+        }
+        if (c == 3) {
+          if (depth == 0) part[k].push_back(i);
+          depth++;
+        } else if (c == 4) {
+          if (--depth < 0) return;
+        }
+        i++;
+      }
+      ok[k] = depth == 0;
+    });
+  for (auto& t : th) t.join();
+  for (size_t k = 0; k < P; k++)
+    if (!ok[k]) return false;
+  for (auto& v : part) starts->insert(starts->end(), v.begin(), v.end());
+  return true;
+}
+
+// Concatenate per-thread batches (each a whole number of 64-resource wave
+// groups, in input order): heaps, values, KV pairs and rows are appended with
+// their offsets rebased; batch-local key ids and namespace indices are remapped
+// onto tables built in thread order (= the serial first-seen order).
+void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
+  const size_t P = parts.size();
+  std::unordered_map<std::string, uint32_t> dyn, nsi;
+  std::vector<std::vector<uint32_t>> dmap(P), nmap(P);
+  std::vector<uint64_t> hb(P), vb(P), kb(P), rb(P), nb(P), resb(P);
+  uint64_t H = 0, V = 0, K = 0, R = 0, N = 0, RS = 0;
+  for (size_t k = 0; k < P; k++) {  // offsets and id remaps (serial, small)
+    Batch& q = parts[k];
+    H = (H + 3) & ~3ull;
+    hb[k] = H; vb[k] = V; kb[k] = K; rb[k] = R; nb[k] = N; resb[k] = RS;
+    H += q.strs.size(); V += q.vals.size(); K += q.kvs.size(); R += q.n_rows; N += q.nodes.size(); RS += q.res.size();
+    for (const std::string& s : q.dyn_keys) {
+      auto it = dyn.find(s);
+      if (it == dyn.end()) {
+        it = dyn.emplace(s, nstatic + (uint32_t)b.dyn_keys.size()).first;
+        b.dyn_keys.push_back(s);
+      }
+      dmap[k].push_back(it->second);
+    }
+    for (const std::string& s : q.namespaces) {
+      auto it = nsi.find(s);
+      if (it == nsi.end()) {
+        it = nsi.emplace(s, (uint32_t)b.namespaces.size()).first;
+        b.namespaces.push_back(s);
+      }
+      nmap[k].push_back(it->second);
+    }
+    b.cells_used += q.cells_used;
+  }
+  if (H >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: string heap exceeds 4 GiB");
+  if (R * KV_LANES >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: batch too large for 32-bit node indices");
+  b.strs.assign(H, '\0');
+  b.vals.resize(V);
+  b.kvs.resize(K);
+  b.nodes.resize(N);
+  b.res.resize(RS);
+  b.n_rows = R;
+  std::vector<std::thread> th;
+  for (size_t k = 0; k < P; k++)
+    th.emplace_back([&, k]() {  // each part fills its own disjoint ranges
+      Batch& q = parts[k];
+      const uint32_t h = (uint32_t)hb[k], v0 = (uint32_t)vb[k], k0 = (uint32_t)kb[k], r0 = (uint32_t)rb[k];
+      memcpy(&b.strs[h], q.strs.data(), q.strs.size());
+      for (size_t i = 0; i < q.vals.size(); i++) {
+        Val v = q.vals[i];
+        v.e_off += h;
+        if (v.flags & VF_N_VALID) v.n_off += h;
+        b.vals[vb[k] + i] = v;
+      }
+      for (size_t i = 0; i < q.kvs.size(); i++) {
+        KV x = q.kvs[i];
+        x.k_off += h;
+        x.v_off += h;
+        b.kvs[kb[k] + i] = x;
+      }
+      Node* out = &b.nodes[nb[k]];
+      for (size_t i = 0; i < q.nodes.size(); i++) {
+        Node nd = q.nodes[i];
+        const uint32_t t = node_type(nd.kt);
+        uint32_t key = node_key(nd.kt);
+        if (key >= nstatic && key != KEY_NONE28) key = dmap[k][key - nstatic];
+        nd.kt = key << 4 | t;
+        if (t == NT_MAP || t == NT_ARR) nd.a += r0;
+        else if (t == NT_BOOL || t == NT_INT || t == NT_FLOAT || t == NT_STR) { nd.a += v0; nd.b += h; }
+        out[i] = nd;
+      }
+      for (size_t i = 0; i < q.res.size(); i++) {
+        Res r = q.res[i];
+        r.root += r0;
+        r.name_off += h;
+        r.ns_off += h;
+        r.labels_first += k0;
+        r.annot_first += k0;
+        r.ns_index = nmap[k][r.ns_index];
+        b.res[resb[k] + i] = r;
+      }
+      Batch().nodes.swap(q.nodes);
+    });
+  for (auto& t : th) t.join();
+}
+
+}  // namespace
+
 void ingest_resources(const PolicySet& ps, const char* json, size_t len, const char* ns_labels_json, Batch* b) {
-  Ingest in(ps, *b);
-  parse_json_stream(json, len, NUM_UNSTRUCTURED, [&](JDoc& d) { in.take(d); });
-  in.flush_group();
+  const unsigned T = ingest_threads();
+  size_t first = 0;
+  while (first < len && (json[first] == ' ' || json[first] == '\t' || json[first] == '\n' || json[first] == '\r')) first++;
+  std::vector<size_t> starts;
+  bool parallel = false;
+  std::unordered_map<std::string, uint32_t> ns_index;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto ms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+  const bool verbose = getenv("KVGPU_VERBOSE") != nullptr;
+  if (T > 1 && len >= (1u << 20) && first < len && json[first] == '{' && scan_values(json, len, T, &starts)) {
+    if (verbose) fprintf(stderr, "[kvgpu] ingest: scan %.1f ms (%zu values)\n", ms(), starts.size());
+    // whole wave groups per thread, so lane = resource index % 64 holds in the merged batch
+    const size_t nres = starts.size(), groups = (nres + KV_LANES - 1) / KV_LANES;
+    const size_t per = (groups + T - 1) / T * KV_LANES;
+    const size_t P = (nres + per - 1) / per;
+    std::vector<Batch> parts(P);
+    std::vector<std::string> errs(P);
+    std::vector<std::thread> th;
+    for (size_t k = 0; k < P; k++)
+      th.emplace_back([&, k]() {
+        try {
+          Ingest in(ps, parts[k]);
+          JDoc doc;
+          const size_t e = std::min(nres, (k + 1) * per);
+          for (size_t i = k * per; i < e; i++) {
+            const size_t end = i + 1 < nres ? starts[i + 1] : len;
+            doc.nodes.clear();
+            doc.strs.clear();
+            parse_one(json + starts[i], end - starts[i], NUM_UNSTRUCTURED, &doc);
+            in.take(doc);
+          }
+          in.flush_group();
+        } catch (const std::exception& ex) {
+          errs[k] = ex.what();
+        }
+      });
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+      if (!e.empty()) throw std::runtime_error(e);
+    if (verbose) fprintf(stderr, "[kvgpu] ingest: %zu threads %.1f ms\n", P, ms());
+    merge_batches(parts, *b, (uint32_t)ps.keys.size());
+    if (verbose) fprintf(stderr, "[kvgpu] ingest: merge %.1f ms\n", ms());
+    for (size_t i = 0; i < b->namespaces.size(); i++) ns_index.emplace(b->namespaces[i], (uint32_t)i);
+    parallel = true;
+  }
+  if (!parallel) {
+    Ingest in(ps, *b);
+    parse_json_stream(json, len, NUM_UNSTRUCTURED, [&](JDoc& d) { in.take(d); });
+    in.flush_group();
+    ns_index = std::move(in.ns_index);
+  }
   // namespace labels (CLI --values-file namespaceSelector map / cluster namespaces)
   b->ns_labels.assign(b->namespaces.size(), {});
   if (ns_labels_json && *ns_labels_json) {
@@ -413,8 +622,8 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
     if (r.t == J_MAP) {
       for (uint32_t c = r.first; c < r.first + r.count; c++) {
         std::string nsn(d.key(d.at(c)));
-        auto it = in.ns_index.find(nsn);
-        if (it == in.ns_index.end()) continue;
+        auto it = ns_index.find(nsn);
+        if (it == ns_index.end()) continue;
         const JNode& m = d.at(c);
         if (m.t != J_MAP) continue;
         for (uint32_t g = m.first; g < m.first + m.count; g++)

@@ -186,3 +186,27 @@ def test_c5_scope_counts(orc, spec):
     sess = batch.Session(ps, b, mode=batch.MODE_SCOPES)
     sess.run(2)
     assert np.array_equal(sess.scope_counts(len(nss)), want)
+
+
+def test_parallel_ingest_matches_serial():
+    """Multi-threaded NDJSON ingest (per-thread wave groups merged with rebased offsets) gives the
+    same statuses and failing paths as the serial ingest."""
+    import os
+
+    from kyverno_amd import batch, workloads
+
+    pols = workloads.c2_policies() + workloads.c5_policies()
+    ps = batch.PolicySet(pols, specialize=True)
+    data = batch.synth(workloads.SEED + 7, 20000, kind_mix=1)
+    out = {}
+    for t in ("1", "16"):
+        os.environ["KVGPU_INGEST_THREADS"] = t
+        try:
+            b = batch.Batch(ps, data)
+        finally:
+            os.environ.pop("KVGPU_INGEST_THREADS", None)
+        r = batch.validate(ps, b)
+        fails = np.argwhere(r.status == 1)[:300]
+        out[t] = (r.status, b.namespaces, [r.path(int(a), int(c)) for a, c in fails])
+    assert np.array_equal(out["1"][0], out["16"][0])
+    assert out["1"][1] == out["16"][1] and out["1"][2] == out["16"][2]

@@ -102,3 +102,22 @@ def test_ingest_rejects_malformed():
         batch.Batch(ps, b'{"kind": "Pod", ')
     with pytest.raises(KvError):
         batch.PolicySet(b"[{]")
+
+
+def test_parallel_ingest_host_tables():
+    """Serial and multi-threaded ingest agree on resource count and the first-seen namespace order."""
+    import os
+
+    from kyverno_amd import batch, workloads
+
+    ps = batch.PolicySet(workloads.c2_policies())
+    data = batch.synth(workloads.SEED + 3, 6000, kind_mix=1)
+    got = []
+    for t in ("1", "4"):
+        os.environ["KVGPU_INGEST_THREADS"] = t
+        try:
+            b = batch.Batch(ps, data)
+        finally:
+            os.environ.pop("KVGPU_INGEST_THREADS", None)
+        got.append((b.n_res, b.namespaces))
+    assert got[0] == got[1] and got[0][0] == 6000
