@@ -478,6 +478,60 @@ bool scan_values(const char* p, size_t n, unsigned T, std::vector<size_t>* start
 // groups, in input order): heaps, values, KV pairs and rows are appended with
 // their offsets rebased; batch-local key ids and namespace indices are remapped
 // onto tables built in thread order (= the serial first-seen order).
+// Val order: the value-predicate table kernel (kvj_ptab) runs one lane per Val and
+// one grid row per 16 leaf predicates, each row gated by the position classes of
+// the value (Val.cls). Numbering the Vals grouped by (cls, type) makes its waves
+// class-homogeneous: a wave whose values no predicate of the row applies to
+// exits after one load, and the rest run the same predicate code without
+// divergence. Buckets are ordered by key and stable inside (ingest order).
+// KVGPU_VAL_ORDER=0 keeps ingest order (A/B runs)
+const bool g_val_order = [] { const char* e = getenv("KVGPU_VAL_ORDER"); return !(e && e[0] == '0'); }();
+inline uint64_t val_order_key(const Val& v) { return g_val_order ? ((uint64_t)v.cls << 8 | v.type) : 0u; }
+
+using KeyCount = std::unordered_map<uint64_t, uint32_t>;
+
+// per-bucket first new id for each of `hists` (parts in order), buckets by ascending key
+std::vector<KeyCount> val_order_cursors(const std::vector<KeyCount>& hists) {
+  std::vector<uint64_t> keys;
+  KeyCount total;
+  for (const KeyCount& h : hists)
+    for (const auto& kv : h)
+      if (total.emplace(kv.first, 0).second) keys.push_back(kv.first);
+  std::sort(keys.begin(), keys.end());
+  std::vector<KeyCount> cur(hists.size());
+  uint32_t next = 0;
+  for (uint64_t key : keys)
+    for (size_t k = 0; k < hists.size(); k++) {
+      auto it = hists[k].find(key);
+      if (it == hists[k].end()) continue;
+      cur[k][key] = next;
+      next += it->second;
+    }
+  return cur;
+}
+
+KeyCount val_hist(const std::vector<Val>& vals) {
+  KeyCount h;
+  for (const Val& v : vals) h[val_order_key(v)]++;
+  return h;
+}
+
+// serial ingest: renumber the Vals in place and remap the scalar cells
+void order_vals(Batch& b) {
+  std::vector<KeyCount> cur = val_order_cursors({val_hist(b.vals)});
+  std::vector<uint32_t> perm(b.vals.size());
+  std::vector<Val> out(b.vals.size());
+  for (size_t i = 0; i < b.vals.size(); i++) {
+    perm[i] = cur[0][val_order_key(b.vals[i])]++;
+    out[perm[i]] = b.vals[i];
+  }
+  b.vals.swap(out);
+  for (Node& nd : b.nodes) {
+    const uint32_t t = node_type(nd.kt);
+    if (t == NT_BOOL || t == NT_INT || t == NT_FLOAT || t == NT_STR) nd.a = perm[nd.a];
+  }
+}
+
 void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
   const size_t P = parts.size();
   std::unordered_map<std::string, uint32_t> dyn, nsi;
@@ -515,17 +569,24 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
   b.nodes.resize(N);
   b.res.resize(RS);
   b.n_rows = R;
+  std::vector<KeyCount> hists(P);
   std::vector<std::thread> th;
+  for (size_t k = 0; k < P; k++) th.emplace_back([&, k]() { hists[k] = val_hist(parts[k].vals); });
+  for (auto& t : th) t.join();
+  th.clear();
+  std::vector<KeyCount> cur = val_order_cursors(hists);
   for (size_t k = 0; k < P; k++)
-    th.emplace_back([&, k]() {  // each part fills its own disjoint ranges
+    th.emplace_back([&, k]() {  // each part fills its own disjoint ranges (Vals: its share of every bucket)
       Batch& q = parts[k];
-      const uint32_t h = (uint32_t)hb[k], v0 = (uint32_t)vb[k], k0 = (uint32_t)kb[k], r0 = (uint32_t)rb[k];
+      const uint32_t h = (uint32_t)hb[k], k0 = (uint32_t)kb[k], r0 = (uint32_t)rb[k];
       memcpy(&b.strs[h], q.strs.data(), q.strs.size());
+      std::vector<uint32_t> perm(q.vals.size());
       for (size_t i = 0; i < q.vals.size(); i++) {
         Val v = q.vals[i];
         v.e_off += h;
         if (v.flags & VF_N_VALID) v.n_off += h;
-        b.vals[vb[k] + i] = v;
+        perm[i] = cur[k][val_order_key(v)]++;
+        b.vals[perm[i]] = v;
       }
       for (size_t i = 0; i < q.kvs.size(); i++) {
         KV x = q.kvs[i];
@@ -541,7 +602,7 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
         if (key >= nstatic && key != KEY_NONE28) key = dmap[k][key - nstatic];
         nd.kt = key << 4 | t;
         if (t == NT_MAP || t == NT_ARR) nd.a += r0;
-        else if (t == NT_BOOL || t == NT_INT || t == NT_FLOAT || t == NT_STR) { nd.a += v0; nd.b += h; }
+        else if (t == NT_BOOL || t == NT_INT || t == NT_FLOAT || t == NT_STR) { nd.a = perm[nd.a]; nd.b += h; }
         out[i] = nd;
       }
       for (size_t i = 0; i < q.res.size(); i++) {
@@ -603,7 +664,9 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
       if (!e.empty()) throw std::runtime_error(e);
     if (verbose) fprintf(stderr, "[kvgpu] ingest: %zu threads %.1f ms\n", P, ms());
     merge_batches(parts, *b, (uint32_t)ps.keys.size());
-    if (verbose) fprintf(stderr, "[kvgpu] ingest: merge %.1f ms\n", ms());
+    if (verbose)
+      fprintf(stderr, "[kvgpu] ingest: merge %.1f ms (%zu vals, %llu rows, %zu string bytes)\n", ms(), b->vals.size(),
+              (unsigned long long)b->n_rows, b->strs.size());
     for (size_t i = 0; i < b->namespaces.size(); i++) ns_index.emplace(b->namespaces[i], (uint32_t)i);
     parallel = true;
   }
@@ -612,6 +675,7 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
     parse_json_stream(json, len, NUM_UNSTRUCTURED, [&](JDoc& d) { in.take(d); });
     in.flush_group();
     ns_index = std::move(in.ns_index);
+    order_vals(*b);
   }
   // namespace labels (CLI --values-file namespaceSelector map / cluster namespaces)
   b->ns_labels.assign(b->namespaces.size(), {});

@@ -59,6 +59,11 @@ struct Gen {
   // of the batch (kvj_ptab) and the rule kernels test one bit of the table
   bool memo = true;
   std::vector<uint32_t> mpreds;  // memo slot -> pred
+  std::map<uint32_t, uint32_t> pslot;  // pred -> memo slot
+  // leaves on a hoisted scalar read their table word(s) through a load hoisted
+  // with the cursor (issued with the other lookups of the region instead of one
+  // dependent load per rule); KVGPU_JIT_PW=0 disables, for A/B runs
+  bool pw = true;
   explicit Gen(const PolicySet& p) : ps(p) {}
 
   // call of leaf predicate `pi` on node `n` of type `t`
@@ -259,6 +264,7 @@ struct Gen {
     if (memo) {
       const uint32_t slot = (uint32_t)mpreds.size();
       mpreds.push_back(pi);
+      pslot[pi] = slot;
       // scalars (BOOL/INT/FLOAT/STR carry a Val id in n.a): one bit of the table;
       // null / map / array: the predicate itself (no value loads on those paths)
       o << "__device__ __forceinline__ bool m_pred_" << pi
@@ -330,6 +336,21 @@ struct Gen {
          "const Val* __restrict__ V, const uint8_t* __restrict__ S, uint32_t NV, uint32_t* __restrict__ PT) {\n"
       << "  const uint32_t v = blockIdx.x * KV_WG + threadIdx.x;\n"
       << "  if (v >= NV) return;\n"
+      << "  // Vals are numbered grouped by class (kvingest.cpp val_order_key): most waves\n"
+      << "  // are uniform in vc, and a wave no predicate of its row applies to stops here\n"
+      << "  const uint32_t vc = V[v].cls;\n"
+      << "  uint32_t rm = 0u;\n"
+      << "  switch (blockIdx.y) {\n";
+    auto pm = [&](uint32_t k) { auto it = pmask.find(mpreds[k]); return it == pmask.end() ? 0xFFFFFFFFu : it->second; };
+    for (uint32_t k0 = 0; k0 < mpreds.size(); k0 += kPtabRow) {
+      const uint32_t k1 = (uint32_t)std::min<size_t>(k0 + kPtabRow, mpreds.size());
+      uint32_t wm = 0;
+      for (uint32_t q = k0; q < k1; q++) wm |= pm(q);
+      o << "    case " << (k0 / kPtabRow) << "u: rm = " << u32(wm) << "; break;\n";
+    }
+    o << "    default: break;\n  }\n"
+      << "  uint32_t w = 0u;\n"
+      << "  if (" << (getenv("KVGPU_PTAB_EARLY") && getenv("KVGPU_PTAB_EARLY")[0] == '0' ? "true" : "vc & rm") << ") {\n"
       << "  const uint8_t* __restrict__ pstr = Pp->pstr;\n"
       << "  const Val& val = V[v];\n"
       << "  const uint32_t type = val.type;\n"
@@ -337,22 +358,17 @@ struct Gen {
       << "  if (val.flags & VF_ASCII_E) n.c |= NC_ASCII_E;\n"
       << "  if (val.flags & VF_BOOLV) n.c |= NC_BOOLV;\n"
       << "  if (val.flags & VF_NILLIKE) n.c |= NC_NILLIKE;\n"
-      << "  const uint32_t vc = val.cls;\n"
       << "  const uint8_t* __restrict__ E = S + val.e_off;\n"
-      << "  uint32_t w = 0u;\n"
       << "  switch (blockIdx.y) {\n";
-    auto pm = [&](uint32_t k) { auto it = pmask.find(mpreds[k]); return it == pmask.end() ? 0xFFFFFFFFu : it->second; };
     for (uint32_t k0 = 0; k0 < mpreds.size(); k0 += kPtabRow) {
       const uint32_t k1 = (uint32_t)std::min<size_t>(k0 + kPtabRow, mpreds.size());
-      uint32_t wm = 0;
-      for (uint32_t q = k0; q < k1; q++) wm |= pm(q);
-      o << "    case " << (k0 / kPtabRow) << "u:\n      if (!(vc & " << u32(wm) << ")) break;\n";
+      o << "    case " << (k0 / kPtabRow) << "u:\n";
       for (uint32_t k = k0; k < k1; k++)
         o << "      if ((vc & " << u32(pm(k)) << ") && g_pred_" << mpreds[k] << "(V, S, E, pstr, type, n)) w |= "
           << u32(1u << (k % kPtabRow)) << ";\n";
       o << "      break;\n";
     }
-    o << "    default: break;\n  }\n"
+    o << "    default: break;\n  }\n  }\n"
       << "  // row y = bits [16 (y % 2), +16) of table word y / 2 (little-endian u16 halves)\n"
       << "  ((uint16_t*)PT)[((size_t)(blockIdx.y >> 1) * NV + v) * 2u + (blockIdx.y & 1u)] = (uint16_t)w;\n}\n\n";
   }
@@ -637,6 +653,7 @@ struct Gen {
     std::string prefix;
     std::map<std::string, HVar> vars;
     std::vector<std::string> code;  // one statement group per entry, dependency order
+    std::set<std::string> words;    // hoisted table-word loads (Gen::pw)
     size_t flushed = 0;
     uint32_t n = 0;
     std::string flush() {
@@ -810,16 +827,32 @@ struct Gen {
           else w << "  if (" << cn << " == ABSENT || node_type(N[" << cn << "].kt) == NT_NULL) ";
           w << raise("E_STAR", in.b, in.c) << "\n";
           break;
-        case OP_LEAF:
-          if (known(d)) w << "  { const Node vn_ = " << NODE(d) << ";\n";
-          else w << "  { Node vn_{0u, 0u, 0u, 0u}; if (" << cd << " != ABSENT) vn_ = N[" << cd << "];\n";
+        case OP_LEAF: {
+          std::string scalar = pred_call(in.a, "vt_", "vn_");
+          if (known(d)) {
+            w << "  { const Node vn_ = " << NODE(d) << ";\n";
+            auto sl = pslot.find(in.a);
+            HoistTable* T = table_for(d);
+            if (memo && pw && sl != pslot.end() && T) {
+              const uint32_t word = sl->second / 32;
+              const std::string wv = g.hv[d].node + "_w" + std::to_string(word);
+              if (T->words.insert(wv).second)
+                T->code.push_back("  const uint32_t " + wv + " = node_type(" + g.hv[d].node + ".kt) - 1u < 4u ? P.ptab[(size_t)" +
+                                  std::to_string(word) + "u * P.n_vals + " + g.hv[d].node + ".a] : 0u;\n");
+              scalar = "(vt_ - 1u < 4u ? ((" + wv + " >> " + std::to_string(sl->second % 32) + "u) & 1u) != 0u : " +
+                       "g_pred_" + std::to_string(in.a) + "(V, S, S + vn_.b, pstr, vt_, vn_))";
+            }
+          } else {
+            w << "  { Node vn_{0u, 0u, 0u, 0u}; if (" << cd << " != ABSENT) vn_ = N[" << cd << "];\n";
+          }
           w << "    const uint32_t vt_ = node_type(vn_.kt); bool ok_;\n"
             << "    if (vt_ == NT_ARR) { ok_ = true; for (uint32_t k_ = 0; k_ < vn_.b && ok_; k_++) { const Node en_ = "
                "N[ni(vn_.a + k_)]; ok_ = "
             << pred_call(in.a, "node_type(en_.kt)", "en_") << "; } }\n"
-            << "    else ok_ = " << pred_call(in.a, "vt_", "vn_") << ";\n"
+            << "    else ok_ = " << scalar << ";\n"
             << "    if (!ok_) " << raise("E_VALUE", in.b, in.c) << " }\n";
           break;
+        }
         case OP_RAISE:
           w << "  " << raise(u32(in.b), in.a, in.c) << "\n";
           break;
@@ -1197,6 +1230,8 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   // KVGPU_JIT_MEMO=0: evaluate every leaf predicate per pair (no value-predicate table), for A/B runs
   const char* mz = getenv("KVGPU_JIT_MEMO");
   g.memo = !(mz && mz[0] == '0');
+  const char* pz = getenv("KVGPU_JIT_PW");
+  g.pw = !(pz && pz[0] == '0');
   for (uint32_t ri = 0; ri < ps.rules.size(); ri++)
     if (ps.rules[ri].route == 0) g.leaf_classes(ri);
   for (uint32_t ri = 0; ri < ps.rules.size(); ri++) {

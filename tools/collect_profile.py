@@ -21,7 +21,7 @@ def per_pass(csv_path, counter):
     agg = collections.defaultdict(float)
     for r in csv.DictReader(open(csv_path)):
         k = r.get("Kernel_Name", "")
-        if r["Counter_Name"] == counter and ("kv_validate" in k or "kvj_chunk" in k):
+        if r["Counter_Name"] == counter and k.startswith(("kv_", "kvj_")):
             agg[(k, r["Dispatch_Id"])] += float(r["Counter_Value"])
     per_k = collections.defaultdict(list)
     for (k, _), v in agg.items():
