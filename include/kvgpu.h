@@ -114,6 +114,15 @@ int kv_result_scope_counts(const kv_result* r, const int64_t** counts, uint32_t*
 int kv_result_path(const kv_result* r, uint32_t rule, uint64_t res, char* buf, size_t cap);
 /* raw error record: kind (validate.go/anchor.go error form) and anchor-wrap flags */
 int kv_result_error(const kv_result* r, uint32_t rule, uint64_t res, uint32_t* kind, uint32_t* flags);
+/* err.Error() of the PatternError behind a FAIL / ERROR / SKIP pair — the SKIP
+ * message and the "execution error: %s" operand of the ERROR message
+ * (pkg/engine/validation.go:421-439,510-527; error forms of
+ * pkg/engine/validate/validate.go:62-172 and pkg/engine/anchor/anchor.go:61-261).
+ * The caller passes the resource document (JSON) it ingested, from which the
+ * Go '%v' / %T operands are formatted. Returns the message length, KV_E_INVALID
+ * for other statuses or constant (compile-time) statuses, KV_E_PARSE for bad JSON. */
+int kv_result_error_message(const kv_result* r, uint32_t rule, uint64_t res, const char* resource_json, size_t len,
+                            char* buf, size_t cap);
 double kv_result_kernel_ms(const kv_result* r);
 
 /* Benchmark entry: device-resident inputs, `iters` timed launches on one stream

@@ -166,6 +166,23 @@ class Result:
             return None
         return buf.value.decode("utf-8")
 
+    def error_message(self, rule: int, res: int, resource) -> str | None:
+        """err.Error() of the pattern error behind a FAIL / ERROR / SKIP pair (``kv_result_error_message``):
+        the SKIP message, and the operand of the ERROR message. ``resource`` is the ingested document
+        (dict or JSON text), from which the Go '%v' operands are formatted."""
+        doc = resource if isinstance(resource, (bytes, str)) else _dumps(resource)
+        if isinstance(doc, str):
+            doc = doc.encode("utf-8")
+        cap = 1 << 16
+        while True:
+            buf = ctypes.create_string_buffer(cap)
+            n = lib().kv_result_error_message(self._h, rule, res, doc, len(doc), buf, cap)
+            if n < 0:
+                return None
+            if n < cap:
+                return buf.raw[:n].decode("utf-8", "replace")
+            cap = n + 1
+
     def error(self, rule: int, res: int):
         k, f = ctypes.c_uint32(), ctypes.c_uint32()
         if lib().kv_result_error(self._h, rule, res, ctypes.byref(k), ctypes.byref(f)) != 0:

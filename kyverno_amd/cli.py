@@ -98,6 +98,7 @@ class Evaluation:
     rules: list             # batch.Rule per compiled rule (policy order)
     status: np.ndarray      # u8 [n_rules][n_res]
     paths: dict = field(default_factory=dict)   # (rule, res) -> failing path (FAIL pairs)
+    errors: dict = field(default_factory=dict)  # (rule, res) -> err.Error() of ERROR / SKIP pairs
     anypattern: dict = field(default_factory=dict)  # (rule, res) -> [(status, path)] per pattern
 
     def policy_rules(self, pi: int) -> list:
@@ -105,11 +106,13 @@ class Evaluation:
 
 
 def evaluate(policies: list[dict], resources: list[dict], device: int = 0, messages: bool = True,
-             namespace_labels: dict | None = None) -> Evaluation:
-    """All (rule, resource) pairs on the GPU (``kv_compile`` → ``kv_ingest`` → ``kv_validate``)."""
+             namespace_labels: dict | None = None, specialize: bool = False) -> Evaluation:
+    """All (rule, resource) pairs on the GPU (``kv_compile`` → ``kv_ingest`` → ``kv_validate``).
+    ``specialize`` selects the per-policy-set specialized kernels (worth their hiprtc compile on
+    large batches) over the bytecode interpreter; both write the same statuses and error records."""
     from . import batch
 
-    ps = batch.PolicySet(policies)
+    ps = batch.PolicySet(policies, specialize=specialize)
     b = batch.Batch(ps, resources, namespace_labels)
     r = batch.validate(ps, b, device=device)
     ev = Evaluation(policies, resources, ps.rules, r.status)
@@ -117,11 +120,16 @@ def evaluate(policies: list[dict], resources: list[dict], device: int = 0, messa
         for ri, res in zip(*np.nonzero(r.status == FAIL)):
             if not ps.rules[ri].any_pattern:
                 ev.paths[(int(ri), int(res))] = r.path(int(ri), int(res))
-        _evaluate_anypatterns(ev, device)
+        for ri, res in zip(*np.nonzero((r.status == ERROR) | (r.status == SKIP))):
+            if not ps.rules[ri].any_pattern:
+                m = r.error_message(int(ri), int(res), resources[int(res)])
+                if m is not None:
+                    ev.errors[(int(ri), int(res))] = m
+        _evaluate_anypatterns(ev, device, specialize)
     return ev
 
 
-def _evaluate_anypatterns(ev: Evaluation, device: int) -> None:
+def _evaluate_anypatterns(ev: Evaluation, device: int, specialize: bool = False) -> None:
     """Per-pattern outcomes of anyPattern rules, for the pass index and the failure message of
     validatePatterns (pkg/engine/validation.go:446-484): every pattern of the rule is compiled as a
     pattern rule of its own (same match/exclude) and run on the device over the resources where
@@ -145,7 +153,7 @@ def _evaluate_anypatterns(ev: Evaluation, device: int) -> None:
             sub_rules.append(sr)
         sub = {"apiVersion": src.get("apiVersion", "kyverno.io/v1"), "kind": src.get("kind", "ClusterPolicy"),
                "metadata": src.get("metadata", {}), "spec": {"rules": sub_rules}}
-        ps = batch.PolicySet([sub])
+        ps = batch.PolicySet([sub], specialize=specialize)
         ress = [ev.resources[i] for i in idx]
         b = batch.Batch(ps, ress)
         r = batch.validate(ps, b, device=device)
@@ -153,7 +161,12 @@ def _evaluate_anypatterns(ev: Evaluation, device: int) -> None:
             outs = []
             for j in range(len(pats)):
                 st = int(r.status[j, k])
-                outs.append((st, r.path(j, k) if st == FAIL else None))
+                if st == FAIL:
+                    outs.append((st, r.path(j, k)))
+                elif st in (ERROR, SKIP):  # PatternError with an empty path: its text
+                    outs.append((st, r.error_message(j, k, ress[k])))
+                else:
+                    outs.append((st, None))
             ev.anypattern[(rule.index, int(res))] = outs
 
 
@@ -165,8 +178,9 @@ def _with_dot(s: str) -> str:
 
 
 def rule_message(ev: Evaluation, rule, res: int) -> str:
-    """RuleResponse.Message for pass / fail (validatePatterns, buildErrorMessage,
-    buildAnyPatternErrorMessage: pkg/engine/validation.go:421-547)."""
+    """RuleResponse.Message (validatePatterns, buildErrorMessage, buildAnyPatternErrorMessage:
+    pkg/engine/validation.go:421-547): pass / fail from the status and failing path, skip / error
+    from the device's error record rendered by ``kv_result_error_message``."""
     st = int(ev.status[rule.index, res])
     if rule.any_pattern:
         outs = ev.anypattern.get((rule.index, res), [])
@@ -174,11 +188,11 @@ def rule_message(ev: Evaluation, rule, res: int) -> str:
             j = next((j for j, (s, _) in enumerate(outs) if s == PASS), 0)
             return f"validation rule '{rule.name}' anyPattern[{j}] passed."
         errs = []
-        for j, (s, path) in enumerate(outs):
-            if s == FAIL and path:
-                errs.append(f"Rule {rule.name}[{j}] failed at path {path}.")
-            elif s != PASS:
-                errs.append(f"Rule {rule.name}[{j}] failed: {REPORT_STATUS.get(s, 'error')}.")
+        for j, (s, detail) in enumerate(outs):
+            if s == FAIL and detail:
+                errs.append(f"Rule {rule.name}[{j}] failed at path {detail}.")
+            elif s in (ERROR, SKIP) and detail is not None:
+                errs.append(f"Rule {rule.name}[{j}] failed: {detail}.")
         es = " ".join(errs)
         if not rule.message:
             return f"validation error: {es}"
@@ -190,6 +204,13 @@ def rule_message(ev: Evaluation, rule, res: int) -> str:
         if not rule.message:
             return f"validation error: rule {rule.name} failed at path {path}"
         return f"validation error: {_with_dot(rule.message)} Rule {rule.name} failed at path {path}"
+    if st in (ERROR, SKIP) and (rule.index, res) in ev.errors:
+        err = ev.errors[(rule.index, res)]
+        if st == SKIP:  # ruleResponse(..., pe.Error(), RuleStatusSkip)
+            return err
+        if not rule.message:  # buildErrorMessage(err, "")
+            return f"validation error: rule {rule.name} execution error: {err}"
+        return f"validation error: {_with_dot(rule.message)} Rule {rule.name} execution error: {err}"
     if rule.const_message:
         return rule.const_message
     return ""
@@ -232,7 +253,7 @@ def process_validate(ev: Evaluation, pi: int, res: int, rc: ResultCounts, policy
                 rc.routed += 1
                 violated.append({"name": r.name, "status": "cpu", "message": ""})
                 continue
-            msg = rule_message(ev, r, res) if st in (PASS, FAIL) or r.const_message else ""
+            msg = rule_message(ev, r, res)
             if st == PASS:
                 rc.pass_ += 1
             elif st == FAIL:

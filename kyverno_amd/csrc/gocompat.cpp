@@ -107,6 +107,51 @@ std::string go_format_E(double v) {
   return mant + "E" + sign + digs;
 }
 
+// fmt's %v of a float64: strconv.FormatFloat(v, 'g', -1, 64) — shortest
+// round-trip digits; strconv/ftoa.go %g rule with shortest precision: eprec = 6,
+// exponent form when exp < -4 || exp >= eprec, exponent written e±dd.
+std::string go_format_g(double v) {
+  if (std::isnan(v)) return "NaN";
+  if (std::isinf(v)) return v > 0 ? "+Inf" : "-Inf";
+  if (v == 0) return std::signbit(v) ? "-0" : "0";
+  char buf[64];
+  auto r = std::to_chars(buf, buf + sizeof buf, v, std::chars_format::scientific);
+  std::string s(buf, r.ptr);
+  bool neg = s[0] == '-';
+  if (neg) s.erase(0, 1);
+  size_t e = s.find('e');
+  std::string digs;
+  for (size_t i = 0; i < e; i++)
+    if (s[i] != '.') digs += s[i];
+  while (digs.size() > 1 && digs.back() == '0') digs.pop_back();
+  const int exp = std::stoi(s.substr(e + 1));  // value = d.ddd x 10^exp
+  const int nd = (int)digs.size(), dp = exp + 1;
+  std::string out = neg ? "-" : "";
+  if (exp < -4 || exp >= 6) {
+    out += digs[0];
+    if (nd > 1) { out += '.'; out += digs.substr(1); }
+    out += 'e';
+    out += exp < 0 ? '-' : '+';
+    int ax = exp < 0 ? -exp : exp;
+    if (ax < 10) out += '0';
+    out += std::to_string(ax);
+    return out;
+  }
+  if (dp <= 0) {
+    out += "0.";
+    out += std::string((size_t)-dp, '0');
+    out += digs;
+  } else if (dp >= nd) {
+    out += digs;
+    out += std::string((size_t)(dp - nd), '0');
+  } else {
+    out += digs.substr(0, (size_t)dp);
+    out += '.';
+    out += digs.substr((size_t)dp);
+  }
+  return out;
+}
+
 std::string go_format_f6(double v) {
   if (std::isnan(v)) return "NaN";
   if (std::isinf(v)) return v > 0 ? "+Inf" : "-Inf";

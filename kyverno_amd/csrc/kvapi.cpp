@@ -340,31 +340,178 @@ std::vector<uint32_t> fold_filters(const PolicySet& ps, const AdmissionCtx& ai) 
   return out;
 }
 
-std::string render_path(const PolicySet& ps, const Batch& b, const ErrRec& e) {
-  std::vector<std::string> segs;
-  uint32_t p = e.pnode;
+// Path segments from the pattern root to pnode p: keys (resolved wildcard keys
+// from the record's key node) and array indices (loop counters of the record).
+struct PathSeg {
+  bool index;
+  std::string key;
+};
+std::vector<PathSeg> path_segs(const PolicySet& ps, const Batch& b, const ErrRec& e, uint32_t p) {
+  std::vector<PathSeg> segs;
   while (p != 0xFFFFFFFFu && p < ps.pnodes.size()) {
     const PNodeInfo& n = ps.pnodes[p];
     switch (n.seg) {
       case SEG_ROOT: break;
-      case SEG_KEY: segs.push_back(n.key); break;
-      case SEG_LOOP: segs.push_back(std::to_string(e.idx[n.level & 3])); break;
-      case SEG_CONST_INDEX: segs.push_back(std::to_string(n.level)); break;
+      case SEG_KEY: segs.push_back({false, n.key}); break;
+      case SEG_LOOP: segs.push_back({true, std::to_string(e.idx[n.level & 3])}); break;
+      case SEG_CONST_INDEX: segs.push_back({true, std::to_string(n.level)}); break;
       case SEG_RESOLVED: {
         if (e.keynode != ABSENT && e.keynode < b.nodes.size()) {
           uint32_t k = node_key(b.nodes[e.keynode].kt);
-          segs.push_back(k < ps.keys.size() ? ps.keys[k] : b.dyn_keys[k - ps.keys.size()]);
+          segs.push_back({false, k < ps.keys.size() ? ps.keys[k] : b.dyn_keys[k - ps.keys.size()]});
         } else {
-          segs.push_back(n.key);
+          segs.push_back({false, n.key});
         }
         break;
       }
     }
     p = n.parent;
   }
+  std::reverse(segs.begin(), segs.end());
+  return segs;
+}
+
+std::string join_path(const std::vector<PathSeg>& segs) {
   std::string out = "/";
-  for (size_t i = segs.size(); i-- > 0;) out += segs[i] + "/";
+  for (const PathSeg& s : segs) out += s.key + "/";
   return out;
+}
+
+uint32_t err_kind(const ErrRec& e) { return e.kind_flags & 0xFFFF; }
+
+// pnode whose path is the PatternError path: the "*" shortcut reports its parent
+// map (anchor.go:139), every other form the node it was raised at
+uint32_t path_pnode(const PolicySet& ps, const ErrRec& e) {
+  if (err_kind(e) == E_STAR && e.pnode < ps.pnodes.size()) return ps.pnodes[e.pnode].parent;
+  return e.pnode;
+}
+
+std::string render_path(const PolicySet& ps, const Batch& b, const ErrRec& e) {
+  return join_path(path_segs(ps, b, e, path_pnode(ps, e)));
+}
+
+// ---- Go fmt of resource values (unstructured typing: int64 / float64 / string /
+// bool / nil / map[string]interface{} / []interface{}), for '%v' and %T operands
+std::string res_T(const JDoc& d, int64_t n) {
+  if (n < 0) return "<nil>";
+  switch (d.at((uint32_t)n).t) {
+    case J_MAP: return "map[string]interface {}";
+    case J_ARR: return "[]interface {}";
+    case J_STR: return "string";
+    case J_BOOL: return "bool";
+    case J_INT: return "int64";
+    case J_FLOAT: return "float64";
+    default: return "<nil>";
+  }
+}
+
+std::string res_v(const JDoc& d, int64_t n) {
+  if (n < 0) return "<nil>";
+  const JNode& x = d.at((uint32_t)n);
+  switch (x.t) {
+    case J_MAP: {  // fmt prints maps with sorted keys
+      std::vector<uint32_t> ix;
+      for (uint32_t c = x.first; c < x.first + x.count; c++) ix.push_back(c);
+      std::sort(ix.begin(), ix.end(), [&](uint32_t a, uint32_t b) { return d.key(d.at(a)) < d.key(d.at(b)); });
+      std::string o = "map[";
+      for (size_t k = 0; k < ix.size(); k++) {
+        if (k) o += ' ';
+        o += d.key(d.at(ix[k]));
+        o += ':';
+        o += res_v(d, ix[k]);
+      }
+      return o + "]";
+    }
+    case J_ARR: {
+      std::string o = "[";
+      for (uint32_t c = x.first; c < x.first + x.count; c++) {
+        if (c > x.first) o += ' ';
+        o += res_v(d, c);
+      }
+      return o + "]";
+    }
+    case J_STR: return std::string(d.sval(x));
+    case J_BOOL: return x.b ? "true" : "false";
+    case J_INT: return std::to_string(x.i);
+    case J_FLOAT: return go_format_g(x.f);
+    default: return "<nil>";
+  }
+}
+
+// resource element at a pattern path (-1 when absent)
+int64_t res_at(const JDoc& d, const std::vector<PathSeg>& segs) {
+  int64_t n = d.root;
+  for (const PathSeg& s : segs) {
+    if (n < 0) return -1;
+    const JNode& x = d.at((uint32_t)n);
+    if (x.t == J_MAP) {
+      n = d.get((uint32_t)n, s.key);
+    } else if (x.t == J_ARR && s.index) {
+      uint64_t i = std::stoull(s.key);
+      n = i < x.count ? (int64_t)(x.first + i) : -1;
+    } else {
+      return -1;
+    }
+  }
+  return n;
+}
+
+// err.Error() of the PatternError behind a FAIL / ERROR / SKIP record
+// (pkg/engine/validate/validate.go:62-172, pkg/engine/anchor/anchor.go:61-261;
+// condition / global anchor handlers wrap what propagates through them,
+// anchor.go:72-95 with common/anchorKey.go:21-40)
+std::string error_message(const PolicySet& ps, const Batch& b, const ErrRec& e, const JDoc& doc) {
+  const uint32_t kind = err_kind(e);
+  if (e.pnode >= ps.pnodes.size()) return "";
+  const PNodeInfo& P = ps.pnodes[e.pnode];
+  const std::vector<PathSeg> segs = path_segs(ps, b, e, e.pnode);
+  const std::string path = join_path(segs);
+  std::string m;
+  switch (kind) {
+    case E_TYPE_MAP:
+      m = "pattern and resource have different structures. Path: " + path + ". Expected " + P.pat_t + ", found " +
+          res_T(doc, res_at(doc, segs));
+      break;
+    case E_TYPE_ARR:
+      m = "validation rule Failed at path " + path + ", resource does not satisfy the expected overlay pattern";
+      break;
+    case E_VALUE:
+      m = "resource value '" + res_v(doc, res_at(doc, segs)) + "' does not match '" + P.pat_v + "' at path " + path;
+      break;
+    case E_EMPTY_PATARR: m = "pattern Array empty"; break;
+    case E_LEN: {
+      int64_t n = res_at(doc, segs);
+      uint32_t rl = n >= 0 && doc.at((uint32_t)n).t == J_ARR ? doc.at((uint32_t)n).count : 0;
+      m = "validate Array failed, array length mismatch, resource Array len is " + std::to_string(rl) +
+          " and pattern Array len is " + std::to_string(P.pat_len);
+      break;
+    }
+    case E_NEG: m = path + "/" + (segs.empty() ? std::string() : segs.back().key) + " is not allowed"; break;
+    case E_STAR: {
+      std::vector<PathSeg> ps_ = segs;
+      std::string key = ps_.empty() ? std::string() : ps_.back().key;
+      if (!ps_.empty()) ps_.pop_back();
+      m = join_path(ps_) + "/" + key + " not found";
+      break;
+    }
+    case E_EXIST_PATLIST:
+      m = "invalid pattern type " + P.pat_t + ": Pattern has to be of list to compare against resource";
+      break;
+    case E_EXIST_PATMAP:
+      m = "invalid pattern type " + P.pat_t + ": Pattern has to be of type map to compare against items in resource";
+      break;
+    case E_EXIST_RESTYPE:
+      m = "invalid resource type " + res_T(doc, res_at(doc, segs)) +
+          ": Existence ^ () anchor can be used only on list/array type resource";
+      break;
+    case E_EXIST_FAIL: m = "existence anchor validation failed at path " + path; break;
+    default: return "";
+  }
+  for (uint32_t q = e.pnode; q != 0xFFFFFFFFu && q < ps.pnodes.size(); q = ps.pnodes[q].parent) {
+    if (ps.pnodes[q].wrap == 1) m = "conditional anchor mismatch: " + m;
+    else if (ps.pnodes[q].wrap == 2) m = "global anchor mismatch: " + m;
+  }
+  return m;
 }
 
 }  // namespace
@@ -597,6 +744,9 @@ int kv_ingest(const kv_policyset* ps, const char* resources_json, size_t len, co
       delete b;
       throw;
     }
+    if (getenv("KVGPU_VERBOSE"))
+      fprintf(stderr, "[kvgpu] ingest: %zu resources, %zu nodes, %zu vals, %zu string bytes\n", b->b.res.size(),
+              b->b.nodes.size(), b->b.vals.size(), b->b.strs.size());
     *out = b;
     return 0;
   } catch (const std::exception& e) {
@@ -700,6 +850,30 @@ int kv_result_error(const kv_result* r, uint32_t rule, uint64_t res, uint32_t* k
   if (kind) *kind = e.kind_flags & 0xFFFF;
   if (flags) *flags = e.kind_flags >> 16;
   return 0;
+}
+
+int kv_result_error_message(const kv_result* r, uint32_t rule, uint64_t res, const char* resource_json, size_t len,
+                            char* buf, size_t cap) {
+  if (!r || r->err.empty() || !resource_json) return KV_E_INVALID;
+  if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
+  size_t o = (size_t)rule * r->n_res + res;
+  const uint8_t st = r->status[o];
+  if (st != ST_FAIL && st != ST_ERROR && st != ST_SKIP) return KV_E_INVALID;
+  std::string m;
+  try {
+    JDoc doc;
+    parse_json(resource_json, len, NUM_UNSTRUCTURED, &doc);
+    m = error_message(r->ps->ps, r->b->b, r->err[o], doc);
+  } catch (const std::exception&) {
+    return KV_E_PARSE;
+  }
+  if (m.empty()) return KV_E_INVALID;  // a compile-time constant status: no pattern error record
+  if (buf && cap) {
+    size_t n = std::min(cap - 1, m.size());
+    memcpy(buf, m.data(), n);
+    buf[n] = 0;
+  }
+  return (int)m.size();
 }
 
 double kv_result_kernel_ms(const kv_result* r) { return r ? r->kernel_ms : -1.0; }

@@ -51,6 +51,42 @@ std::string remove_anchor(const std::string& key, std::string* prefix) {
 
 static bool has_wild(const std::string& s) { return s.find_first_of("*?") != std::string::npos; }
 
+// Go fmt of a decoded pattern value (encoding/json into interface{}), for the
+// error messages of validate.go / anchor.go: %T and %v (map keys sorted).
+static std::string go_T(const PV& p) {
+  switch (p.t) {
+    case J_MAP: return "map[string]interface {}";
+    case J_ARR: return "[]interface {}";
+    case J_STR: return "string";
+    case J_BOOL: return "bool";
+    case J_INT: return "int64";
+    case J_FLOAT: return "float64";
+    default: return "<nil>";
+  }
+}
+static std::string go_v(const PV& p) {
+  switch (p.t) {
+    case J_MAP: {
+      std::vector<size_t> ix(p.mk.size());
+      for (size_t i = 0; i < ix.size(); i++) ix[i] = i;
+      std::sort(ix.begin(), ix.end(), [&](size_t a, size_t b) { return p.mk[a] < p.mk[b]; });
+      std::string o = "map[";
+      for (size_t k = 0; k < ix.size(); k++) o += (k ? " " : "") + p.mk[ix[k]] + ":" + go_v(p.mv[ix[k]]);
+      return o + "]";
+    }
+    case J_ARR: {
+      std::string o = "[";
+      for (size_t k = 0; k < p.a.size(); k++) o += (k ? " " : "") + go_v(p.a[k]);
+      return o + "]";
+    }
+    case J_STR: return p.s;
+    case J_BOOL: return p.b ? "true" : "false";
+    case J_INT: return std::to_string((long long)p.f);
+    case J_FLOAT: return go_format_g(p.f);
+    default: return "<nil>";
+  }
+}
+
 // ---------------------------------------------------------------- glob compilation
 void PolicySet::compile_glob(Atom& a, const std::string& p) {
   a.gflags = 0;
@@ -746,8 +782,17 @@ struct Compiler {
   void lookup_fix(uint32_t pc, uint32_t t, const std::string& k) { slot_fix.emplace_back(pc, t, k); }
 
   // validateResourceElement(cur[d], P); t = projection-trie node of cur[d]
+  // message operands of the pattern value compared at pnode pn
+  void note_pattern(uint32_t pn, const PV& P) {
+    PNodeInfo& n = ps.pnodes[pn];
+    n.pat_t = go_T(P);
+    n.pat_len = (uint32_t)P.a.size();
+    n.pat_v = go_v(P.t == J_ARR && !P.a.empty() ? P.a[0] : P);
+  }
+
   void elem(const PV& P, uint32_t d, uint32_t pn, uint32_t cs, uint32_t t, int expand_tag = 0) {
     if (d >= 30) { cpu_reason = "pattern too deep"; return; }
+    note_pattern(pn, P);
     if (P.t == J_MAP) {
       emit(OP_MAPCHK, d, 0, pn, 0, cs);
       // CheckAnchorInResource: condition / existence / negation keys of this map
@@ -866,6 +911,7 @@ struct Compiler {
         bool global = !is_condition_anchor(k);
         std::string ak = remove_anchor(k, nullptr);
         uint32_t cpn = pnode(pn, wildkey ? SEG_RESOLVED : SEG_KEY, 0, ak);
+        ps.pnodes[cpn].wrap = global ? 2 : 1;
         uint32_t s = new_scope();
         uint32_t kpc = key_op(d, ak, wildkey, true, t);
         skip_fix.push_back({kpc, s});
@@ -876,6 +922,7 @@ struct Compiler {
         std::string ak = remove_anchor(k, nullptr);
         if (wildkey) { cpu_reason = "anchored wildcard metadata key"; break; }
         uint32_t cpn = pnode(pn, SEG_KEY, 0, ak);
+        note_pattern(cpn, Pk);
         uint32_t s = new_scope();
         uint32_t kpc = key_op(d, ak, false, true, t);
         skip_fix.push_back({kpc, s});
@@ -926,13 +973,13 @@ struct Compiler {
           uint32_t s = new_scope();
           uint32_t kpc = key_op(d, k, wildkey, false, t);
           skip_fix.push_back({kpc, s});
-          if (Pk.t == J_STR && Pk.s == "*") emit(OP_STAR, d, 0, 0, pn, cs);
+          if (Pk.t == J_STR && Pk.s == "*") emit(OP_STAR, d, 0, 0, cpn, cs);  // path: parent of cpn
           else elem(Pk, d + 1, cpn, cs, ps.trie.child(t, k), child_tag);
           uint32_t e = emit(OP_SCOPE_END, d, 0, 0, 0, 0xFFFFFFFFu);
           end_scope(s, e);
         } else {
           lookup_fix(emit(OP_KEYV, d, 0, key(k), 0, 0xFFFFFFFFu), t, k);
-          if (Pk.t == J_STR && Pk.s == "*") emit(OP_STAR, d, 0, 0, pn, cs);
+          if (Pk.t == J_STR && Pk.s == "*") emit(OP_STAR, d, 0, 0, cpn, cs);  // path: parent of cpn
           else elem(Pk, d + 1, cpn, cs, ps.trie.child(t, k), child_tag);
         }
       }

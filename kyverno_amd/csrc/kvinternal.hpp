@@ -36,6 +36,11 @@ struct PNodeInfo {
   uint8_t seg;       // SegKind
   uint32_t level;    // SEG_LOOP: loop level; SEG_CONST_INDEX: index
   std::string key;   // SEG_KEY text; SEG_RESOLVED: literal fallback (anchor-free pattern key)
+  // Error-message operands of the pattern value at this node (kv_result_error_message):
+  uint8_t wrap = 0;      // 1: condition-anchor key, 2: global-anchor key (anchor.go:72-95 wraps errors below)
+  std::string pat_t;     // Go %T of the pattern value ("map[string]interface {}", "[]interface {}", ...)
+  std::string pat_v;     // Go %v of the compared scalar (the value, or element 0 of a scalar list)
+  uint32_t pat_len = 0;  // pattern array length (validate.go:172)
 };
 
 // Projection trie over resource key paths referenced by any compiled pattern
