@@ -167,9 +167,10 @@ def main():
     value = world * n_pairs_rank * args.steps / t_max
     # algorithmic bytes per launch: projected store read once + program tables + outputs
     prog_bytes = 0  # program/predicate tables are KB-scale (<0.01%)
-    # full: 1 B status + 32 B record per FAIL/ERROR/SKIP pair; scopes: status written and read back
+    # full: 1 B status + 8 B compact error record per FAIL/ERROR/SKIP pair (kvdevtypes.h ErrRec8;
+    # the rare records that do not fit also write 32 B, not counted); scopes: status written and read back
     # by the scope-count kernel (2 B per pair) + the 4 B scope index of every resource
-    out_bytes = {"full": n_pairs_rank + 32 * n_fail, "counts": 0,
+    out_bytes = {"full": n_pairs_rank + 8 * n_fail, "counts": 0,
                  "scopes": 2 * n_pairs_rank + 4 * b.n_res}[args.mode]
     b_alg = b.store_bytes + prog_bytes + out_bytes
     achieved = b_alg / (kernel_ms / 1e3) / 1e9

@@ -116,7 +116,23 @@ struct kv_result {
   const kv_batch* b = nullptr;
   uint64_t n_rules = 0, n_res = 0;
   std::vector<uint8_t> status;
-  std::vector<ErrRec> err;
+  std::vector<ErrRec8> err8;  // compact records of FAIL / ERROR / SKIP pairs
+  std::vector<ErrRec> errw;   // full records (only those flagged ERR8_WIDE are meaningful)
+  bool has_err() const { return !err8.empty(); }
+  ErrRec err(size_t o) const {
+    const ErrRec8 c = err8[o];
+    if ((c.w0 & ERR8_WIDE) && o < errw.size()) return errw[o];
+    ErrRec e{};
+    e.kind_flags = (c.w0 & 15u) | (((c.w0 >> 4) & 3u) << 16);
+    e.pnode = c.w0 >> 7;
+    e.keynode = ABSENT;
+    e.resnode = ABSENT;
+    e.idx[0] = c.w1 & 4095u;
+    e.idx[1] = (c.w1 >> 12) & 1023u;
+    e.idx[2] = c.w1 >> 22;
+    e.idx[3] = 0;
+    return e;
+  }
   std::vector<int64_t> counts;
   std::vector<int64_t> scope_counts;  // [scope][rule][KV_HIST] (KV_MODE_SCOPES)
   double kernel_ms = 0;
@@ -523,7 +539,7 @@ struct kv_session {
   int device = 0;
   uint32_t mode = 0;
   uint64_t nrules = 0, nres = 0;
-  DevBuf fflags, pview, st, er, cn, scope, scn, ptab;
+  DevBuf fflags, pview, st, er8, er, cn, scope, scn, ptab;
   uint32_t nscopes = 0, nvals = 0;
   DevOut O{};
   const DevBatch* bview = nullptr;
@@ -560,7 +576,9 @@ struct kv_session {
       O.full |= 1;
     }
     if (mode & KV_MODE_ERRORS) {
-      er.alloc(nrules * nres * sizeof(ErrRec), device);
+      er8.alloc(nrules * nres * sizeof(ErrRec8), device);
+      O.err8 = (ErrRec8*)er8.p;
+      er.alloc(nrules * nres * sizeof(ErrRec), device);  // full records: only a re-run pass writes them
       O.err = (ErrRec*)er.p;
       O.full |= 2;
     }
@@ -644,10 +662,22 @@ struct kv_session {
       out->status.resize(nrules * nres);
       if (!out->status.empty()) HIPCHK(hipMemcpy(out->status.data(), st.p, out->status.size(), hipMemcpyDeviceToHost));
     }
-    if (O.err) {
-      out->err.resize(nrules * nres);
-      if (!out->err.empty())
-        HIPCHK(hipMemcpy(out->err.data(), er.p, out->err.size() * sizeof(ErrRec), hipMemcpyDeviceToHost));
+    if (O.err8) {
+      out->err8.resize(nrules * nres);
+      if (!out->err8.empty())
+        HIPCHK(hipMemcpy(out->err8.data(), er8.p, out->err8.size() * sizeof(ErrRec8), hipMemcpyDeviceToHost));
+      bool wide = false;
+      for (size_t o = 0; o < out->err8.size() && !wide; o++) {
+        const uint8_t s_ = out->status[o];
+        wide = (s_ == ST_FAIL || s_ == ST_ERROR || s_ == ST_SKIP) && (out->err8[o].w0 & ERR8_WIDE);
+      }
+      if (wide) {  // re-run the pass once writing full records (same statuses), keep those
+        O.full |= 4;
+        run(1);
+        O.full &= ~4u;
+        out->errw.resize(nrules * nres);
+        HIPCHK(hipMemcpy(out->errw.data(), er.p, out->errw.size() * sizeof(ErrRec), hipMemcpyDeviceToHost));
+      }
     }
   }
 };
@@ -830,11 +860,11 @@ const char* kv_batch_namespace(const kv_batch* b, uint32_t i) {
 }
 
 int kv_result_path(const kv_result* r, uint32_t rule, uint64_t res, char* buf, size_t cap) {
-  if (!r || r->err.empty()) return KV_E_INVALID;
+  if (!r || !r->has_err()) return KV_E_INVALID;
   if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
   size_t o = (size_t)rule * r->n_res + res;
   if (r->status[o] != ST_FAIL) return KV_E_INVALID;
-  std::string p = render_path(r->ps->ps, r->b->b, r->err[o]);
+  std::string p = render_path(r->ps->ps, r->b->b, r->err(o));
   if (buf && cap) {
     size_t n = std::min(cap - 1, p.size());
     memcpy(buf, p.data(), n);
@@ -844,9 +874,9 @@ int kv_result_path(const kv_result* r, uint32_t rule, uint64_t res, char* buf, s
 }
 
 int kv_result_error(const kv_result* r, uint32_t rule, uint64_t res, uint32_t* kind, uint32_t* flags) {
-  if (!r || r->err.empty()) return KV_E_INVALID;
+  if (!r || !r->has_err()) return KV_E_INVALID;
   if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
-  const ErrRec& e = r->err[(size_t)rule * r->n_res + res];
+  const ErrRec e = r->err((size_t)rule * r->n_res + res);
   if (kind) *kind = e.kind_flags & 0xFFFF;
   if (flags) *flags = e.kind_flags >> 16;
   return 0;
@@ -854,7 +884,7 @@ int kv_result_error(const kv_result* r, uint32_t rule, uint64_t res, uint32_t* k
 
 int kv_result_error_message(const kv_result* r, uint32_t rule, uint64_t res, const char* resource_json, size_t len,
                             char* buf, size_t cap) {
-  if (!r || r->err.empty() || !resource_json) return KV_E_INVALID;
+  if (!r || !r->has_err() || !resource_json) return KV_E_INVALID;
   if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
   size_t o = (size_t)rule * r->n_res + res;
   const uint8_t st = r->status[o];
@@ -863,7 +893,7 @@ int kv_result_error_message(const kv_result* r, uint32_t rule, uint64_t res, con
   try {
     JDoc doc;
     parse_json(resource_json, len, NUM_UNSTRUCTURED, &doc);
-    m = error_message(r->ps->ps, r->b->b, r->err[o], doc);
+    m = error_message(r->ps->ps, r->b->b, r->err(o), doc);
   } catch (const std::exception&) {
     return KV_E_PARSE;
   }

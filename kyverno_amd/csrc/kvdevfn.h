@@ -469,6 +469,26 @@ struct EState {
   uint32_t kind, flags, pn, key, res, i0, i1, i2, i3;
 };
 
+// error record of a FAIL / ERROR / SKIP pair (kvdevtypes.h ErrRec8): the 8 B
+// compact form, flagged `wide` when the indices / key do not fit. Passes with
+// O.full bit 2 (re-run by the host only when some record was wide) write the
+// full 32 B form instead; the flag is uniform, so this is a scalar branch.
+__device__ __forceinline__ void store_err(const DevOut& O, size_t o, uint32_t kind, uint32_t flags, uint32_t pn,
+                                          uint32_t key, uint32_t res, uint32_t i0, uint32_t i1, uint32_t i2,
+                                          uint32_t i3) {
+  if (O.full & 4) {
+    uint4* x = (uint4*)(O.err + o);
+    x[0] = make_uint4(kind | (flags << 16), pn, key, res);
+    x[1] = make_uint4(i0, i1, i2, i3);
+    return;
+  }
+  const uint32_t fits = (i0 < 4096u) & (i1 < 1024u) & (i2 < 1024u) & (i3 == 0u) & (key == ABSENT) & (pn < (1u << 25));
+  uint2 w;
+  w.x = kind | (flags << 4) | ((fits ^ 1u) << 6) | (pn << 7);
+  w.y = i0 | (i1 << 12) | (i2 << 22);
+  *(uint2*)(O.err8 + o) = w;
+}
+
 // status + error record (FAIL/ERROR/SKIP) + per-rule histogram with the
 // common statuses counted by one ballot each (fused specialized kernels)
 __device__ __forceinline__ void store_result2(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, bool valid,
@@ -476,11 +496,8 @@ __device__ __forceinline__ void store_result2(const DevOut& O, uint32_t ri, uint
   if (valid && (O.full & 1)) {
     const size_t o = (size_t)ri * n_res + r;
     O.status[o] = (uint8_t)st;
-    if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP)) {
-      uint4* x = (uint4*)(O.err + o);
-      x[0] = make_uint4(e.kind | (e.flags << 16), e.pn, e.key, e.res);
-      x[1] = make_uint4(e.i0, e.i1, e.i2, e.i3);
-    }
+    if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP))
+      store_err(O, o, e.kind, e.flags, e.pn, e.key, e.res, e.i0, e.i1, e.i2, e.i3);
   }
   const uint64_t m_pass = __ballot(valid && st == ST_PASS), m_fail = __ballot(valid && st == ST_FAIL);
   const uint64_t m_nm = __ballot(valid && st == ST_NOMATCH);
@@ -506,15 +523,8 @@ __device__ __forceinline__ void store_result(const DevOut& O, uint32_t ri, uint3
   if (valid && (O.full & 1)) {
     const size_t o = (size_t)ri * n_res + r;
     O.status[o] = (uint8_t)st;
-    if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP)) {
-      ErrRec x;
-      x.kind_flags = e.kind | (e.flags << 16);
-      x.pnode = e.pn;
-      x.keynode = e.key;
-      x.resnode = e.res;
-      x.idx[0] = e.i0; x.idx[1] = e.i1; x.idx[2] = e.i2; x.idx[3] = e.i3;
-      O.err[o] = x;
-    }
+    if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP))
+      store_err(O, o, e.kind, e.flags, e.pn, e.key, e.res, e.i0, e.i1, e.i2, e.i3);
   }
   for (uint32_t s = 0; s < 7; s++) {
     const uint64_t bm = __ballot(valid && st == s);

@@ -13,6 +13,17 @@ struct ErrRec {
   uint32_t idx[4];
 };
 
+// Compact error record (8 B per FAIL / ERROR / SKIP pair, the one written per pass):
+//   w0 = kind | flags << 4 | wide << 6 | pnode << 7          (pnode < 2^25)
+//   w1 = idx0 | idx1 << 12 | idx2 << 22    (idx0 < 4096, idx1 / idx2 < 1024, idx3 == 0)
+// A record that does not fit (larger loop indices, a fourth loop level, a resolved
+// wildcard key) sets `wide`; the host then re-runs the pass with full records
+// (DevOut::full bit 2) into the 32 B ErrRec array.
+struct ErrRec8 {
+  uint32_t w0, w1;
+};
+constexpr uint32_t ERR8_WIDE = 1u << 6;
+
 struct DevPS {
   const Inst* prog;
   const Pred* preds;
@@ -58,9 +69,10 @@ struct DevBatch {
 
 struct DevOut {
   uint8_t* status;             // [rule][res]
-  ErrRec* err;                 // [rule][res] (written for fail/error/skip)
+  ErrRec8* err8;               // [rule][res] (written for fail/error/skip)
+  ErrRec* err;                 // [rule][res] (only records flagged ERR8_WIDE)
   unsigned long long* counts;  // [rule][8]
-  uint32_t full;               // bit0 status, bit1 error records
+  uint32_t full;               // bit0 status, bit1 error records, bit2 full 32 B records (not 8 B)
 };
 
 constexpr int KV_WG = 256;

@@ -291,15 +291,8 @@ extern "C" __global__ __launch_bounds__(KV_WG) __attribute__((amdgpu_waves_per_e
       if (valid && (O.full & 1)) {
         const size_t o = (size_t)ri * n_res + r;
         O.status[o] = (uint8_t)st;
-        if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP)) {
-          ErrRec e;
-          e.kind_flags = ekind | (eflags << 16);
-          e.pnode = epn;
-          e.keynode = ekey;
-          e.resnode = eres;
-          e.idx[0] = eidx0; e.idx[1] = eidx1; e.idx[2] = eidx2; e.idx[3] = eidx3;
-          O.err[o] = e;
-        }
+        if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP))
+          store_err(O, o, ekind, eflags, epn, ekey, eres, eidx0, eidx1, eidx2, eidx3);
       }
       // histogram: one LDS atomic per (wave, status) via ballot popcount
       for (uint32_t s = 0; s < 7; s++) {

@@ -14,7 +14,7 @@ import random
 KEYS_SCALAR = ["image", "name", "imagePullPolicy", "cpu", "memory", "port", "privileged", "level", "mode"]
 KEYS_MAP = ["securityContext", "resources", "limits", "requests", "meta"]
 KEYS_LIST = ["containers", "ports", "volumes", "add"]
-STRINGS = ["nginx", "nginx:latest", "nginx:1.19", "gcr.io/app:v1", "a", "", "Always", "Never", "IfNotPresent",
+STRINGS = ["it's", "a b", "nginx", "nginx:latest", "nginx:1.19", "gcr.io/app:v1", "a", "", "Always", "Never", "IfNotPresent",
            "100m", "1", "2", "0.5", "512Mi", "1Gi", "2Gi", "true", "false", "null", "-1", "1e3", "abc*",
            "*", "NET_ADMIN", "SYS_TIME", " ", "10", "0", "1.5", "ab?c", "Ki", "01"]
 GLOBS = ["*", "?*", "*:*", "*:latest", "!*:latest", "nginx*", "gcr.io/*", "?", "a?c", "*a*", "", "**", "N*_*"]
@@ -75,6 +75,9 @@ def pattern(r: random.Random, depth: int = 0):
                 m[k] = [_leaf_pattern(r)]
             elif r.random() < 0.05:
                 m[k] = []
+            elif r.random() < 0.08:  # nested lists: positional compare, length check (validate.go:160-172)
+                m[k] = [[pattern(r, depth + 1)] if r.random() < 0.5 else [_leaf_pattern(r)]
+                        for _ in range(r.randint(1, 2))]
             else:
                 m[_anchor(r, k, r.random() < 0.3)] = [pattern(r, depth + 1)]
         else:
@@ -107,6 +110,9 @@ def value(r: random.Random, depth: int = 0):
             k = r.choice(KEYS_LIST)
             if r.random() < 0.2:
                 m[k] = [_leaf_value(r) for _ in range(r.randint(0, 3))]
+            elif r.random() < 0.1:
+                m[k] = [[value(r, depth + 1)] if r.random() < 0.5 else [_leaf_value(r)]
+                        for _ in range(r.randint(0, 3))]
             elif r.random() < 0.9:
                 m[k] = [value(r, depth + 1) for _ in range(r.randint(0, 3))]
             else:

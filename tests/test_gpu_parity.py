@@ -210,3 +210,39 @@ def test_parallel_ingest_matches_serial():
         out[t] = (r.status, b.namespaces, [r.path(int(a), int(c)) for a, c in fails])
     assert np.array_equal(out["1"][0], out["16"][0])
     assert out["1"][1] == out["16"][1] and out["1"][2] == out["16"][2]
+
+
+@engines
+def test_wide_error_records(orc, spec):
+    """Failing paths whose loop indices overflow the compact 8 B error record (index >= 4096 at
+    level 0, >= 1024 at levels 1-2, a fourth loop level) or name a resolved wildcard label key:
+    the device writes the full record beside the compact one (kvdevtypes.h ErrRec8)."""
+    def pod(n0, n1, bad0, bad1, labels):
+        cs = [{"name": f"c{i}", "image": "nginx:1.0", "ports": [{"containerPort": 80}] * (n1 if i == bad0 else 1)}
+              for i in range(n0)]
+        cs[bad0]["ports"] = [dict(p) for p in cs[bad0]["ports"]]
+        cs[bad0]["ports"][bad1]["containerPort"] = 81
+        return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p", "labels": labels}, "spec": {"containers": cs}}
+
+    def deep(k):  # four loop levels, the failing element at index 1 of each
+        x = {"v": "bad" if k else "ok"}
+        for _ in range(4):
+            x = {"l": [{"v": "ok", "l": []}, x]}
+        return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "d"}, "spec": x}
+
+    ress = [pod(5000, 1, 4500, 0, {"app-x": "no"}), pod(3, 2000, 1, 1500, {"app-y": "web"}),
+            pod(10, 3, 2, 1, {"tier": "x"}), deep(1), deep(0)]
+    pol = {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "wide"},
+           "spec": {"rules": [
+               {"name": "port", "match": {"resources": {"kinds": ["Pod"]}},
+                "validate": {"pattern": {"spec": {"containers": [{"ports": [{"containerPort": 80}]}]}}}},
+               {"name": "label", "match": {"resources": {"kinds": ["Pod"]}},
+                "validate": {"pattern": {"metadata": {"labels": {"app-*": "web"}}}}},
+               {"name": "deep", "match": {"resources": {"kinds": ["Pod"]}},
+                "validate": {"pattern": {"spec": {"l": [{"l": [{"l": [{"l": [{"v": "ok"}]}]}]}]}}}}]}}
+    mism, r, ost = compare(orc, [pol], ress, check_paths=True, specialize=spec)
+    assert not mism, "\n".join(mism)
+    assert r.path(0, 0) == "/spec/containers/4500/ports/0/containerPort/"
+    assert r.path(0, 1) == "/spec/containers/1/ports/1500/containerPort/"
+    assert r.path(1, 0) == "/metadata/labels/app-x/"
+    assert r.path(2, 3) == "/spec/l/1/l/1/l/1/l/1/v/"

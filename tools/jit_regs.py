@@ -19,6 +19,8 @@ os.environ["KVGPU_JIT_SKIP_COMPILE"] = "1"
 from kyverno_amd import batch, workloads  # noqa: E402
 if wl == "c2":
     pols = workloads.c2_policies()
+elif wl == "c4":
+    pols = workloads.c4_policies()
 elif wl == "c3":
     pols = workloads.c3_policies(int(os.environ.get("NPOL", "60")))
 else:
