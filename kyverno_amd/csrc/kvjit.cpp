@@ -64,6 +64,9 @@ struct Gen {
   // with the cursor (issued with the other lookups of the region instead of one
   // dependent load per rule); KVGPU_JIT_PW=0 disables, for A/B runs
   bool pw = true;
+  // kvj_ptab stages each value's bytes in LDS before its row of predicates;
+  // KVGPU_PTAB_LDS=0 reads them from global memory per glob, for A/B runs
+  bool ptab_lds = !(getenv("KVGPU_PTAB_LDS") && getenv("KVGPU_PTAB_LDS")[0] == '0');
   explicit Gen(const PolicySet& p) : ps(p) {}
 
   // call of leaf predicate `pi` on node `n` of type `t`
@@ -358,8 +361,21 @@ struct Gen {
       << "  if (val.flags & VF_ASCII_E) n.c |= NC_ASCII_E;\n"
       << "  if (val.flags & VF_BOOLV) n.c |= NC_BOOLV;\n"
       << "  if (val.flags & VF_NILLIKE) n.c |= NC_NILLIKE;\n"
-      << "  const uint8_t* __restrict__ E = S + val.e_off;\n"
-      << "  switch (blockIdx.y) {\n";
+      << "  const uint8_t* __restrict__ E = S + val.e_off;\n";
+    if (ptab_lds) {
+      // Stage the value's bytes (<= 64 B, plus the one word the word-wise globs read
+      // past the end) in LDS once: the row's predicates then re-read them from LDS
+      // instead of re-issuing global loads per glob. Odd word stride: no bank conflicts.
+      o << "  __shared__ uint32_t lds_e[KV_WG * 17];\n"
+        << "  if (val.e_len <= 64u) {\n"
+        << "    const uint32_t* __restrict__ src = (const uint32_t*)E;\n"
+        << "    uint32_t* dst = lds_e + threadIdx.x * 17u;\n"
+        << "    const uint32_t nw = (val.e_len + 3u) / 4u + 1u;\n"
+        << "    for (uint32_t i = 0; i < nw; i++) dst[i] = src[i];\n"
+        << "    E = (const uint8_t*)dst;\n"
+        << "  }\n";
+    }
+    o << "  switch (blockIdx.y) {\n";
     for (uint32_t k0 = 0; k0 < mpreds.size(); k0 += kPtabRow) {
       const uint32_t k1 = (uint32_t)std::min<size_t>(k0 + kPtabRow, mpreds.size());
       o << "    case " << (k0 / kPtabRow) << "u:\n";
