@@ -314,7 +314,11 @@ struct Gen {
           }
           break;
         }
-        case OP_KEYGLOB: tn[d + 1] = pos[d + 1] = -2; break;
+        case OP_KEYGLOB: {  // a resolved label / annotation key: a child of a keep-all map (pos -1)
+          const int32_t t = tn[d];
+          tn[d + 1] = pos[d + 1] = t >= 0 && ps.trie.nodes[t].keep_all ? -1 : -2;
+          break;
+        }
         case OP_LOOP_BEGIN:
         case OP_EXIST_BEGIN:
         case OP_INDEX:
