@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 import fuzz_gen
+import fuzz_match
 from parity_util import compare, oracle_status
 
 SEEDS = list(range(8))
@@ -70,3 +71,32 @@ def test_fuzz_messages(orc, seed, spec):
             bad.append(f"rule {rule} res {res} [{rr['status']}]\n  device {got!r}\n  oracle {rr['message']!r}\n"
                        f"  pattern {json.dumps(pols[0]['spec']['rules'][rule]['validate'])[:300]}")
     assert not bad, f"seed {seed}: {len(bad)} of {len(pairs)} differ\n" + "\n".join(bad[:10])
+
+
+# admission info of the batch: none (background scan / CLI), or a request by a cluster admin, a
+# namespaced role holder, or a service account (folded on the host, validation.go:383-398)
+ADMISSIONS = [None,
+              {"admission": {"clusterRoles": ["admin"], "groups": [], "roles": [], "username": ""}},
+              {"admission": {"clusterRoles": [], "groups": ["devs"], "roles": ["dev:editor"], "username": "alice"}},
+              {"admission": {"clusterRoles": ["view"], "groups": [], "roles": [],
+                             "username": "system:serviceaccount:prod:sa"}}]
+
+
+def test_match_fuzz_generator_reach(orc):
+    seen = set()
+    for seed in range(3):
+        pols, ress = fuzz_match.policies(seed, 80), fuzz_match.resources(seed, 400)
+        seen |= set(np.unique(oracle_status(orc, pols, ress)).tolist())
+    assert {0, 1, 5} <= seen, seen
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", [False, True], ids=["vm", "specialized"])
+@pytest.mark.parametrize("seed", range(4))
+def test_match_exclude_fuzz(orc, seed, spec):
+    """Random match / exclude blocks (kinds, names, namespaces, annotations, selectors, any / all,
+    user info) x resources of several kinds, statuses vs oracle under each admission context."""
+    pols, ress = fuzz_match.policies(seed, 80), fuzz_match.resources(seed, 400)
+    for ctx in ADMISSIONS:
+        mism, r, ost = compare(orc, pols, ress, ctx=ctx, check_paths=False, specialize=spec)
+        assert not mism, f"seed {seed} ctx {ctx}: " + "\n".join(mism[:20])
