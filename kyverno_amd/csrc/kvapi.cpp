@@ -214,7 +214,7 @@ DevPolicySet& dev_ps(kv_policyset* s, int device) {
     if (s->jit->memo_words) {
       HIPCHK(hipModuleGetFunction(&d->ptab_fn, d->mod, "kvj_ptab"));
       d->memo_words = s->jit->memo_words;
-      d->ptab_rows = (uint32_t)((s->jit->memo_preds.size() + 15) / 16);  // kvjit.cpp kPtabRow
+      d->ptab_rows = (uint32_t)((s->jit->memo_preds.size() + s->jit->ptab_row - 1) / s->jit->ptab_row);
     }
   }
   auto& ref = *d;

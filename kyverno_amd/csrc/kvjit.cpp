@@ -337,7 +337,8 @@ struct Gen {
   // One grid row per 16 predicates (half a table word, stored as a u16 half):
   // keeps the code of a row (16 inlined globs / compares) within the
   // instruction cache — 32-predicate rows stalled on instruction fetch.
-  static constexpr uint32_t kPtabRow = 16;
+  // KVGPU_PTAB_ROW=32: one row per table word (A/B runs)
+  const uint32_t kPtabRow = getenv("KVGPU_PTAB_ROW") && atoi(getenv("KVGPU_PTAB_ROW")) == 32 ? 32u : 16u;
   void ptab_kernel() {
     o << "extern \"C\" __global__ __launch_bounds__(KV_WG) void kvj_ptab(const DevPS* __restrict__ Pp, "
          "const Val* __restrict__ V, const uint8_t* __restrict__ S, uint32_t NV, uint32_t* __restrict__ PT) {\n"
@@ -389,8 +390,9 @@ struct Gen {
       o << "      break;\n";
     }
     o << "    default: break;\n  }\n  }\n"
-      << "  // row y = bits [16 (y % 2), +16) of table word y / 2 (little-endian u16 halves)\n"
-      << "  ((uint16_t*)PT)[((size_t)(blockIdx.y >> 1) * NV + v) * 2u + (blockIdx.y & 1u)] = (uint16_t)w;\n}\n\n";
+      << (kPtabRow == 32 ? "  PT[(size_t)blockIdx.y * NV + v] = w;\n}\n\n"
+                         : "  // row y = bits [16 (y % 2), +16) of table word y / 2 (little-endian u16 halves)\n"
+                           "  ((uint16_t*)PT)[((size_t)(blockIdx.y >> 1) * NV + v) * 2u + (blockIdx.y & 1u)] = (uint16_t)w;\n}\n\n");
   }
 
   // ---------------------------------------------------------------- match / exclude
@@ -1303,6 +1305,7 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
     g.ptab_kernel();
     out->memo_preds = g.mpreds;
     out->memo_words = (uint32_t)((g.mpreds.size() + 31) / 32);
+    out->ptab_row = g.kPtabRow;
   }
   out->source = g.o.str();
   out->gen_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -26,6 +26,7 @@ struct JitImage {
   // kernel "kvj_ptab" fills DevPS::ptab (memo_words words per value)
   std::vector<uint32_t> memo_preds;
   uint32_t memo_words = 0;
+  uint32_t ptab_row = 16;   // predicates per kvj_ptab grid row (16: u16 halves of a word, 32: whole words)
   double gen_ms = 0, compile_ms = 0;
 };
 
