@@ -60,6 +60,7 @@ def main():
                          "c4: anchor-heavy chart + test/policy/validate (138 rules) x Pods; "
                          "c5: background scan, chart after autogen (105 rules) x mixed kinds, counts")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive kv_validate timing")
     ap.add_argument("--cpu-sample", type=int, default=40_000)
     ap.add_argument("--backend", choices=["nccl", "gloo"], default=None,
                     help="torch.distributed backend for N>1 (default: nccl = RCCL when GPUs are visible); "
@@ -210,6 +211,18 @@ def main():
     out["ingest"] = {"seconds": t2 - t1, "resources_per_s": b.n_res / (t2 - t1),
                      "MB_per_s": ndjson_bytes / (t2 - t1) / 1e6,
                      "threads": int(os.environ.get("KVGPU_INGEST_THREADS", min(16, os.cpu_count() or 1)))}
+    if rank == 0 and world == 1 and args.mode == "full" and not args.no_e2e:
+        # PCIe-inclusive rate of the host boundary: kv_validate on a freshly ingested
+        # batch = H2D upload of the projected store + one pass + D2H of statuses and error records
+        del sess
+        b2 = batch.Batch(ps, batch.synth(workloads.SEED + rank, args.n_res, kind_mix))
+        te0 = time.perf_counter()
+        r2 = batch.validate(ps, b2, device=local)
+        te1 = time.perf_counter()
+        out["e2e_kv_validate"] = {"seconds": te1 - te0, "evals_per_s": n_pairs_rank / (te1 - te0),
+                                  "kernel_ms": r2.kernel_ms,
+                                  "includes": "H2D store upload + 1 pass + D2H status/error records"}
+        del r2, b2
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
         out["cpu_baseline"] = cpu_baseline(pols, args.cpu_sample, threads, kind_mix, args.config.upper())

@@ -578,8 +578,7 @@ struct kv_session {
     if (mode & KV_MODE_ERRORS) {
       er8.alloc(nrules * nres * sizeof(ErrRec8), device);
       O.err8 = (ErrRec8*)er8.p;
-      er.alloc(nrules * nres * sizeof(ErrRec), device);  // full records: only a re-run pass writes them
-      O.err = (ErrRec*)er.p;
+      O.err = nullptr;  // full records: allocated by fetch() for the re-run pass, if some record is wide
       O.full |= 2;
     }
     cn.alloc(std::max<uint64_t>(nrules, 1) * KV_HIST * sizeof(unsigned long long), device);
@@ -672,6 +671,8 @@ struct kv_session {
         wide = (s_ == ST_FAIL || s_ == ST_ERROR || s_ == ST_SKIP) && (out->err8[o].w0 & ERR8_WIDE);
       }
       if (wide) {  // re-run the pass once writing full records (same statuses), keep those
+        if (!er.p) er.alloc(nrules * nres * sizeof(ErrRec), device);
+        O.err = (ErrRec*)er.p;
         O.full |= 4;
         run(1);
         O.full &= ~4u;
