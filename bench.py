@@ -66,7 +66,7 @@ def main():
                     help="torch.distributed backend for N>1 (default: nccl = RCCL when GPUs are visible); "
                          "gloo lets several ranks share one GPU for a rehearsal")
     ap.add_argument("--rule-filter", default="", help="diagnostics: regex over C2 rule names")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_v9", "traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_v10", "traffic.json"),
                     help="PMC-derived HBM bytes per pass of this same command (tools/collect_profile.py)")
     ap.add_argument("--engine", choices=["vm", "specialized"], default="specialized",
                     help="bytecode interpreter kernel, or per-policy-set specialized kernels (hiprtc)")
