@@ -35,7 +35,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from . import autogen, yamlio
+from . import autogen, msgvars, yamlio
 
 PASS, FAIL, WARN, ERROR, SKIP, NOMATCH, CPU = range(7)  # kv status codes (include/kvgpu.h)
 ROUTE_NORESPONSE = 2  # KV_ROUTE_NORESPONSE: not a validate rule, never in the validate response
@@ -203,14 +203,16 @@ def rule_message(ev: Evaluation, rule, res: int) -> str:
         path = ev.paths.get((rule.index, res), "")
         if not rule.message:
             return f"validation error: rule {rule.name} failed at path {path}"
-        return f"validation error: {_with_dot(rule.message)} Rule {rule.name} failed at path {path}"
+        msg = msgvars.substitute_message(rule.message, ev.resources[res])
+        return f"validation error: {_with_dot(msg)} Rule {rule.name} failed at path {path}"
     if st in (ERROR, SKIP) and (rule.index, res) in ev.errors:
         err = ev.errors[(rule.index, res)]
         if st == SKIP:  # ruleResponse(..., pe.Error(), RuleStatusSkip)
             return err
         if not rule.message:  # buildErrorMessage(err, "")
             return f"validation error: rule {rule.name} execution error: {err}"
-        return f"validation error: {_with_dot(rule.message)} Rule {rule.name} execution error: {err}"
+        msg = msgvars.substitute_message(rule.message, ev.resources[res])
+        return f"validation error: {_with_dot(msg)} Rule {rule.name} execution error: {err}"
     if rule.const_message:
         return rule.const_message
     return ""

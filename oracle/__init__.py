@@ -58,6 +58,8 @@ class Oracle:
         L.orc_substitute.argtypes = [ctypes.c_char_p]
         L.orc_substitute.restype = ctypes.c_void_p
         L.orc_validate.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
+        L.orc_substitute_message.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.orc_substitute_message.restype = ctypes.c_void_p
         L.orc_validate.restype = ctypes.c_void_p
         L.orc_last_error.restype = ctypes.c_char_p
         L.orc_validate_batch.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
@@ -117,6 +119,12 @@ class Oracle:
 
     def substitute(self, pattern_json: str) -> dict:
         return json.loads(self._take(self.lib.orc_substitute(pattern_json.encode())))
+
+    def substitute_message(self, msg: str, resource: dict | str):
+        """buildErrorMessage's message substitution; None where the reference panics."""
+        r = resource if isinstance(resource, str) else json.dumps(resource)
+        p = self.lib.orc_substitute_message(msg.encode(), r.encode())
+        return None if not p else self._take(p)
 
     def validate(self, policy: dict | str, resource: dict | str, ctx: dict | None = None) -> dict:
         p = policy if isinstance(policy, str) else json.dumps(policy)

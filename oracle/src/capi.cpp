@@ -158,6 +158,23 @@ char* orc_substitute(const char* pattern_json) {
   }
 }
 
+// buildErrorMessage's SubstituteAll of a validate message against request.object = resource
+// (validation.go:518-524). Returns nullptr where the reference panics.
+char* orc_substitute_message(const char* msg, const char* resource_json) {
+  try {
+    Value rv = parse_json(resource_json, NumMode::Unstructured);
+    std::string out;
+    if (!SubstituteMessage(msg, rv, &out)) {
+      g_err = "reference panics";
+      return nullptr;
+    }
+    return dup(out);
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return nullptr;
+  }
+}
+
 // engine.Validate for one policy x one resource.
 // ctx_json: {"admission": {"roles":[],"clusterRoles":[],"groups":[],"username":""},
 //            "excludeGroupRole": [], "namespaceLabels": {"ns": {"k":"v"}}}

@@ -529,7 +529,7 @@ struct RuleResult {
   std::string message;
   std::string path;      // failing path (FAIL) — "" otherwise
   std::string reason;    // CPU route reason
-  bool message_needs_vars = false;
+  bool message_panics = false;  // the reference panics building the message (validation.go:519-524)
 };
 
 static std::string with_dot(const std::string& m) {
@@ -537,20 +537,20 @@ static std::string with_dot(const std::string& m) {
   return m + ".";
 }
 
-// message substitution: references/escapes on the message document itself
-static std::string subst_message(const std::string& msg) {
-  Value v = Value::mk_str(msg);
-  std::string err;
-  if (!SubstituteReferences(v, &err)) return msg;
-  return v.s;
-}
-
-static std::string build_error_message(const Rule& rule, const std::string& err, const std::string& path) {
+// message substitution (buildErrorMessage, validation.go:518-524): SubstituteAll of the message
+// with request.object = the resource. *panics is set where the reference panics.
+static std::string build_error_message(const Rule& rule, const std::string& err, const std::string& path,
+                                       const Value& resource, bool* panics) {
   if (rule.message.empty()) {
     if (!path.empty()) return "validation error: rule " + rule.name + " failed at path " + path;
     return "validation error: rule " + rule.name + " execution error: " + err;
   }
-  std::string msg = with_dot(subst_message(rule.message));
+  std::string sub;
+  if (!SubstituteMessage(rule.message, resource, &sub)) {
+    *panics = true;
+    return "";
+  }
+  std::string msg = with_dot(sub);
   if (!path.empty()) return "validation error: " + msg + " Rule " + rule.name + " failed at path " + path;
   return "validation error: " + msg + " Rule " + rule.name + " execution error: " + err;
 }
@@ -560,10 +560,10 @@ static void validate_patterns(const Rule& rule, Value pattern, Value anyPattern,
     PatternError pe = MatchPattern(&resource, pattern);
     if (pe.set) {
       if (pe.skip) { out->status = SKIP; out->message = pe.msg; return; }
-      if (pe.path.empty()) { out->status = ERROR; out->message = build_error_message(rule, pe.msg, ""); return; }
+      if (pe.path.empty()) { out->status = ERROR; out->message = build_error_message(rule, pe.msg, "", resource, &out->message_panics); return; }
       out->status = FAIL;
       out->path = pe.path;
-      out->message = build_error_message(rule, pe.msg, pe.path);
+      out->message = build_error_message(rule, pe.msg, pe.path, resource, &out->message_panics);
       return;
     }
     out->status = PASS;
@@ -623,7 +623,6 @@ RuleResult evaluate_rule(const Rule& rule, const Value& resource) {
   std::string reason = route_reason(rule);
   if (!reason.empty()) { rr.status = CPU; rr.reason = reason; return rr; }
   if (!rule.patternP && !rule.anyPatternP) { rr.status = NOMATCH; return rr; }  // validate() returns nil
-  rr.message_needs_vars = HasVariable(rule.message);
   Value pattern, anyPattern;
   std::string err;
   if (rule.patternP) {
@@ -719,7 +718,7 @@ std::string ValidateToJSON(const Value& policy, const Value& resource, const Val
     if (k) out += ",";
     out += "{\"name\":" + js(r.name) + ",\"status\":" + js(status_name(r.status)) + ",\"message\":" + js(r.message) +
            ",\"path\":" + js(r.path) + ",\"reason\":" + js(r.reason) +
-           ",\"message_needs_vars\":" + (r.message_needs_vars ? "true" : "false") + "}";
+           ",\"message_panics\":" + (r.message_panics ? "true" : "false") + "}";
   }
   out += "]}";
   return out;

@@ -75,6 +75,7 @@ void ExpandInMetadata(Value& patternMap, const Value& resourceMap);
 // $() references: pkg/engine/variables/vars.go:253-309,450-554
 // Returns false with *err set on failure (message as the reference formats it).
 bool SubstituteReferences(Value& document, std::string* err);
+bool SubstituteMessage(const std::string& msg, const Value& resource, std::string* out);
 // True if the string contains an unescaped {{...}} (RegexVariables, vars.go:20)
 bool HasVariable(const std::string& s);
 bool DocHasVariable(const Value& v);

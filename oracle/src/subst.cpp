@@ -326,4 +326,212 @@ bool SubstituteReferences(Value& document, std::string* err) {
   return true;
 }
 
+
+// ---------------------------------------------------------------- message variables
+// buildErrorMessage (pkg/engine/validation.go:510-532) -> variables.SubstituteAll on the
+// message: substituteReferences, then substituteVariablesIfAny (vars.go:319-398) with the
+// CLI context {"request":{"object": resource}} read back by encoding/json (float64 numbers),
+// then RegexEscpVariables unescaping. Returns false where the reference panics (an
+// unresolvable variable or a non-string whole-message value: msgRaw.(string), :519-524).
+namespace {
+
+// RegexVariables.FindAllString: ^\{\{[^{}]*\}\}|[^\\]\{\{[^{}]*\}\}, leftmost-first
+std::vector<std::string> find_vars(const std::string& s) {
+  std::vector<std::string> out;
+  auto close = [&](size_t j) -> size_t {
+    if (s.compare(j, 2, "{{") != 0) return std::string::npos;
+    size_t k = j + 2;
+    while (k < s.size() && s[k] != '{' && s[k] != '}') k++;
+    return s.compare(k, 2, "}}") == 0 ? k + 2 : std::string::npos;
+  };
+  size_t i = 0;
+  while (i < s.size()) {
+    if (i == 0) {
+      size_t e = close(0);
+      if (e != std::string::npos) { out.push_back(s.substr(0, e)); i = e; continue; }
+    }
+    if (s[i] != '\\' && i + 1 < s.size()) {
+      size_t e = close(i + 1);
+      if (e != std::string::npos) { out.push_back(s.substr(i, e - i)); i = e; continue; }
+    }
+    i++;
+  }
+  return out;
+}
+
+// encoding/json float64: strconv 'f' -1, or 'e' -1 outside [1e-6, 1e21) with "e-07" -> "e-7"
+std::string json_float(double f) {
+  char buf[64];
+  int p = 1;
+  for (; p <= 17; p++) {
+    snprintf(buf, sizeof buf, "%.*e", p - 1, f);
+    if (strtod(buf, nullptr) == f) break;
+  }
+  std::string e(buf);  // d.ddde[+-]XX
+  size_t ep = e.find('e');
+  std::string mant = e.substr(0, ep);
+  int ex = atoi(e.c_str() + ep + 1);
+  double a = f < 0 ? -f : f;
+  if (a != 0 && (a < 1e-6 || a >= 1e21)) {
+    char eb[16];
+    snprintf(eb, sizeof eb, "e%c%02d", ex < 0 ? '-' : '+', ex < 0 ? -ex : ex);
+    std::string es(eb);
+    if (es.size() == 4 && es[1] == '-' && es[2] == '0') es.erase(2, 1);
+    return mant + es;
+  }
+  bool neg = mant[0] == '-';
+  std::string digs;
+  for (char c : mant) if (c >= '0' && c <= '9') digs += c;
+  while (digs.size() > 1 && digs.back() == '0') digs.pop_back();
+  // value = 0.digs * 10^(ex+1)
+  int point = ex + 1;
+  std::string out;
+  if (point <= 0) out = "0." + std::string(-point, '0') + digs;
+  else if ((size_t)point >= digs.size()) out = digs + std::string(point - digs.size(), '0');
+  else out = digs.substr(0, point) + "." + digs.substr(point);
+  if (out == "0" || f == 0) out = "0";
+  return (neg ? "-" : "") + out;
+}
+
+std::string json_string(const std::string& s) {
+  std::string o = "\"";
+  for (size_t i = 0; i < s.size(); i++) {
+    unsigned char c = (unsigned char)s[i];
+    if (c == '"') o += "\\\"";
+    else if (c == '\\') o += "\\\\";
+    else if (c == '\n') o += "\\n";
+    else if (c == '\r') o += "\\r";
+    else if (c == '\t') o += "\\t";
+    else if (c < 0x20 || c == '<' || c == '>' || c == '&') {
+      char b[8];
+      snprintf(b, sizeof b, "\\u%04x", c);
+      o += b;
+    } else if (c == 0xE2 && i + 2 < s.size() && (unsigned char)s[i + 1] == 0x80 &&
+               ((unsigned char)s[i + 2] == 0xA8 || (unsigned char)s[i + 2] == 0xA9)) {
+      o += (unsigned char)s[i + 2] == 0xA8 ? "\\u2028" : "\\u2029";
+      i += 2;
+    } else {
+      o += (char)c;
+    }
+  }
+  return o + "\"";
+}
+
+std::string json_marshal(const Value* v) {
+  if (!v) return "null";
+  switch (v->t) {
+    case T::Null: return "null";
+    case T::Bool: return v->b ? "true" : "false";
+    case T::Int: return json_float((double)v->i);
+    case T::Float: return json_float(v->f);
+    case T::Str: return json_string(v->s);
+    case T::Arr: {
+      std::string o = "[";
+      for (size_t k = 0; k < v->a.size(); k++) o += (k ? "," : "") + json_marshal(v->a[k]);
+      return o + "]";
+    }
+    case T::Map: {
+      std::vector<const Value::Entry*> es;
+      for (const auto& e : v->m) es.push_back(&e);
+      std::sort(es.begin(), es.end(), [](const Value::Entry* x, const Value::Entry* y) { return x->key < y->key; });
+      std::string o = "{";
+      for (size_t k = 0; k < es.size(); k++) o += (k ? "," : "") + json_string(es[k]->key) + ":" + json_marshal(es[k]->val);
+      return o + "}";
+    }
+  }
+  return "null";
+}
+
+// ctx.Query (context/evaluate.go:15-50) for request.object field / "quoted" / [index] chains.
+// Returns false on an unknown key or an unsupported expression.
+bool query_object(const std::string& q, const Value& resource, const Value** out) {
+  const std::string root = "request.object";
+  if (q.compare(0, root.size(), root) != 0) return false;
+  const Value* cur = &resource;
+  size_t i = root.size();
+  while (i < q.size()) {
+    if (q[i] == '[') {
+      size_t e = q.find(']', i);
+      if (e == std::string::npos || e == i + 1) return false;
+      std::string num = q.substr(i + 1, e - i - 1);
+      for (size_t k = 0; k < num.size(); k++)
+        if (!(isdigit((unsigned char)num[k]) || (k == 0 && num[k] == '-' && num.size() > 1))) return false;
+      long idx = atol(num.c_str());
+      if (cur && cur->t == T::Arr) {
+        long n = (long)cur->a.size();
+        if (idx < 0) idx += n;
+        cur = (idx >= 0 && idx < n) ? cur->a[idx] : nullptr;
+      } else {
+        cur = nullptr;
+      }
+      i = e + 1;
+      continue;
+    }
+    if (q[i] != '.') return false;
+    i++;
+    std::string key;
+    if (i < q.size() && q[i] == '"') {
+      i++;
+      while (i < q.size() && q[i] != '"') {
+        if (q[i] == '\\' && i + 1 < q.size()) i++;
+        key += q[i++];
+      }
+      if (i >= q.size()) return false;
+      i++;
+    } else {
+      size_t s = i;
+      while (i < q.size() && (isalnum((unsigned char)q[i]) || q[i] == '_')) i++;
+      if (i == s || isdigit((unsigned char)q[s])) return false;
+      key = q.substr(s, i - s);
+    }
+    if (cur && cur->t == T::Map) {
+      cur = cur->get(key);
+      if (!cur) return false;  // NotFoundError: Unknown key
+    } else {
+      cur = nullptr;
+    }
+  }
+  *out = cur;
+  return true;
+}
+
+}  // namespace
+
+bool SubstituteMessage(const std::string& msg, const Value& resource, std::string* out) {
+  Value doc = Value::mk_str(msg);
+  {
+    Value original = doc;
+    Ctx cx{&original};
+    std::string err;
+    if (!traverse(cx, doc, "", &err)) return false;
+  }
+  std::string value = doc.s;
+  auto vars = find_vars(value);
+  while (!vars.empty()) {
+    std::string original = value;
+    for (std::string v : vars) {
+      bool initial = v.compare(0, 2, "{{") == 0;
+      std::string old = v;
+      if (!initial) v = v.substr(1);
+      std::string var = replace_n(replace_n(v, "{{", "", -1), "}}", "", -1);
+      size_t b = var.find_first_not_of(" \t\n\r\v\f"), e = var.find_last_not_of(" \t\n\r\v\f");
+      var = b == std::string::npos ? "" : var.substr(b, e - b + 1);
+      const Value* got = nullptr;
+      if (!query_object(var, resource, &got)) return false;
+      if (original == v) {
+        if (!got || got->t != T::Str) return false;
+        *out = got->s;
+        return true;
+      }
+      std::string prefix = initial ? "" : old.substr(0, 1);
+      std::string sub = got && got->t == T::Str ? got->s : json_marshal(got);
+      value = replace_n(original, prefix + v, prefix + sub, 1);
+    }
+    vars = find_vars(value);
+  }
+  for (const auto& e : find_escaped_vars(value)) value = replace_n(value, e, e.substr(1), -1);
+  *out = value;
+  return true;
+}
+
 }  // namespace orc

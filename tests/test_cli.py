@@ -129,7 +129,7 @@ def test_messages_match_oracle_on_corpus():
             assert [r.name for r in resp] == [rr["name"] for rr in orules]
             for r, rr in zip(resp, orules):
                 st = int(ev.status[r.index, j])
-                if st in (cli.PASS, cli.FAIL) and not rr.get("message_needs_vars"):
+                if st in (cli.PASS, cli.FAIL) and not rr.get("message_panics"):
                     assert cli.rule_message(ev, r, j) == rr["message"], (pol["metadata"]["name"], rr["name"], j)
                     checked += 1
     assert checked > 100

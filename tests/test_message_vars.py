@@ -1,0 +1,70 @@
+"""`{{request.object.*}}` variables in validate messages: host substitution vs oracle.
+
+buildErrorMessage (pkg/engine/validation.go:510-532) runs variables.SubstituteAll on the message
+with the resource as request.object (vars.go:319-398). The host (kyverno_amd/msgvars.py, used by
+cli.rule_message) and the oracle (oracle/src/subst.cpp SubstituteMessage) restate it separately.
+The reference's tests hold no known answer for a substituted validate message (the cases in
+validation_test.go:1933-1992 are deny rules): parity unpinned beyond the oracle, and the
+null / out-of-range-index results depend on kyverno's go-jmespath fork, which is absent.
+"""
+import json
+
+import pytest
+
+import oracle
+from kyverno_amd import msgvars
+
+RES = {
+    "apiVersion": "v1", "kind": "Pod",
+    "metadata": {"name": "web-0", "namespace": "prod",
+                 "labels": {"app": "web", "app.kubernetes.io/name": "frontend"},
+                 "annotations": {"note": "a<b & c>d"}},
+    "spec": {"replicas": 3, "ratio": 0.5, "big": 1.5e22, "tiny": 2.5e-7, "huge": 12345678901234567890,
+             "flag": True, "none": None, "neg": -0.0, "mid": 123456.789,
+             "containers": [{"name": "c0", "image": "nginx:latest", "ports": [{"containerPort": 80}]},
+                            {"name": "c1", "image": "redis", "env": {"b": 1, "a": "x\ty"}}]},
+}
+
+MESSAGES = [
+    "plain message",
+    "Pod {{request.object.metadata.name}} uses a latest tag",
+    "{{request.object.metadata.name}}",
+    "{{ request.object.metadata.namespace }}/{{request.object.metadata.name}}",
+    "replicas={{request.object.spec.replicas}} ratio={{request.object.spec.ratio}}",
+    "big={{request.object.spec.big}} tiny={{request.object.spec.tiny}} huge={{request.object.spec.huge}}",
+    "neg={{request.object.spec.neg}} mid={{request.object.spec.mid}} flag={{request.object.spec.flag}}",
+    "none={{request.object.spec.none}}",
+    "labels {{request.object.metadata.labels}}",
+    "ann {{request.object.metadata.annotations}}",
+    "c {{request.object.spec.containers[1]}}",
+    "first {{request.object.spec.containers[0].image}} last {{request.object.spec.containers[-1].name}}",
+    'quoted {{request.object.metadata.labels."app.kubernetes.io/name"}}',
+    "escaped \\{{request.object.metadata.name}} and {{request.object.kind}}",
+    "escaped ref \\$(./x) ok",
+    "{{request.object.kind}}{{request.object.metadata.name}}",
+    "x{{request.object.spec.containers[0].ports[0].containerPort}}y",
+    "twice {{request.object.kind}} {{request.object.kind}}",
+    # the reference panics on these (msgRaw.(string) of nil or a non-string)
+    "missing {{request.object.metadata.nothere}}",
+    "{{request.object.spec.replicas}}",
+]
+
+
+@pytest.mark.parametrize("msg", MESSAGES)
+def test_message_substitution_matches_oracle(msg):
+    want = oracle.get().substitute_message(msg, RES)
+    try:
+        got = msgvars.substitute_message(msg, json.loads(json.dumps(RES)))
+    except msgvars.MessageVariableError:
+        got = None
+    assert got == want
+
+
+def test_message_substitution_known_forms():
+    s = msgvars.substitute_message
+    assert s("Pod {{request.object.metadata.name}} bad", RES) == "Pod web-0 bad"
+    assert s("n={{request.object.spec.replicas}}", RES) == "n=3"
+    assert s("{{request.object.spec.tiny}}|", RES) == "2.5e-7|"
+    assert s("a {{request.object.metadata.annotations}}", RES) == 'a {"note":"a\\u003cb \\u0026 c\\u003ed"}'
+    with pytest.raises(msgvars.MessageVariableError):
+        s("{{request.object.spec.replicas}}", RES)
