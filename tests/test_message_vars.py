@@ -68,3 +68,65 @@ def test_message_substitution_known_forms():
     assert s("a {{request.object.metadata.annotations}}", RES) == 'a {"note":"a\\u003cb \\u0026 c\\u003ed"}'
     with pytest.raises(msgvars.MessageVariableError):
         s("{{request.object.spec.replicas}}", RES)
+
+
+def _rand_value(rng, depth):
+    k = rng.randrange(9 if depth < 3 else 6)
+    if k == 0:
+        return rng.choice(["", "a", "nginx:1.2", "x<y>&z", 'q"uote', "back\\slash", "tab\tnl\n", "ünï",
+                           "{{brace}}", "$(ref)", " "])
+    if k == 1:
+        return rng.randrange(-10**6, 10**6)
+    if k == 2:
+        return rng.choice([0.5, -0.25, 1e-7, 3.0e21, 1e21, 123456.789, 1e-6, 9.999e20, 2.0**60, -0.0])
+    if k == 3:
+        return rng.choice([True, False])
+    if k == 4:
+        return None
+    if k == 5:
+        return rng.randrange(2**63, 2**64)  # float64 in the unstructured / encoding/json views
+    if k in (6, 7):
+        return {rng.choice(["a", "b", "name", "x.y", "Z", "k_1"]): _rand_value(rng, depth + 1)
+                for _ in range(rng.randrange(4))}
+    return [_rand_value(rng, depth + 1) for _ in range(rng.randrange(4))]
+
+
+def _paths(v, prefix, out):
+    out.append(prefix)
+    if isinstance(v, dict):
+        for k, x in v.items():
+            seg = f'."{k}"' if not k.replace("_", "a").isalnum() or k[0].isdigit() else f".{k}"
+            _paths(x, prefix + seg, out)
+    elif isinstance(v, list):
+        for i, x in enumerate(v):
+            _paths(x, f"{prefix}[{i}]", out)
+            _paths(x, f"{prefix}[{i - len(v)}]", out)
+
+
+def test_message_substitution_fuzz_vs_oracle():
+    """Seeded random resources x message templates (existing, missing and out-of-range paths,
+    escapes, whole-message variables): host vs oracle, including where the reference panics."""
+    import random
+
+    rng = random.Random(0x6D736776)
+    orc = oracle.get()
+    n_sub = 0
+    for case in range(400):
+        res = {"kind": "Pod", "metadata": {"name": f"p{case}"}, "spec": _rand_value(rng, 0)}
+        paths = []
+        _paths(res, "request.object", paths)
+        paths += ["request.object.nothere", "request.object.spec[7]", "request.object.metadata.name.x"]
+        parts = []
+        for _ in range(rng.randrange(1, 4)):
+            p = rng.choice(paths)
+            sp = rng.choice(["", " "])
+            parts.append(rng.choice(["", "msg ", "\\", "x", "}"]) + "{{" + sp + p + sp + "}}")
+        msg = rng.choice(["", "Pod: "]) + rng.choice([" ", "-", ""]).join(parts) + rng.choice(["", ".", " end"])
+        want = orc.substitute_message(msg, json.dumps(res))
+        try:
+            got = msgvars.substitute_message(msg, json.loads(json.dumps(res)))
+        except msgvars.MessageVariableError:
+            got = None
+        assert got == want, (msg, res)
+        n_sub += got is not None
+    assert n_sub > 100
