@@ -419,7 +419,13 @@ def main(argv: list[str] | None = None) -> int:
     t.add_argument("--device", type=int, default=0)
     args = ap.parse_args(argv)
     if args.cmd == "apply":
-        rc, _ = apply(args.policies, args.resource, args.policy_report, args.device)
+        try:
+            rc, _ = apply(args.policies, args.resource, args.policy_report, args.device)
+        except msgvars.MessageVariableError as e:
+            # the Go CLI dies in buildErrorMessage (msgRaw.(string), validation.go:519-524): a
+            # panic, exit status 2
+            print(f"panic: validate message substitution: {e}", file=sys.stderr)
+            return 2
         return 1 if rc.fail > 0 or rc.error > 0 else 0
     import yaml
 
