@@ -206,3 +206,29 @@ def _allreduce_worker(rank, world, port, q):
     names, scoped = report.allreduce_scope_counts(nss, sc, dist)
     q.put((rank, report.allreduce_counts(arr, dist), names, scoped))
     dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_apply_substitutes_message_variables(tmp_path):
+    """`kyverno apply` prints a failing rule's message with its {{request.object.*}} variables
+    resolved per resource (buildErrorMessage, validation.go:518-532); an unknown key in the
+    message is the reference's panic (exit 2)."""
+    import yaml as _yaml
+
+    pol = {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "msgvars"},
+           "spec": {"rules": [{"name": "no-latest", "match": {"resources": {"kinds": ["Pod"]}},
+                               "validate": {"message": "Pod {{request.object.metadata.name}} uses "
+                                                       "{{request.object.spec.containers[0].image}}",
+                                            "pattern": {"spec": {"containers": [{"image": "!*:latest"}]}}}}]}}
+    pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "web", "namespace": "prod"},
+           "spec": {"containers": [{"name": "c", "image": "nginx:latest"}]}}
+    (tmp_path / "p.yaml").write_text(_yaml.safe_dump(pol))
+    (tmp_path / "r.yaml").write_text(_yaml.safe_dump(pod))
+    assert cli.main(["apply", str(tmp_path / "p.yaml"), "-r", str(tmp_path / "r.yaml")]) == 1
+    ev = cli.evaluate(autogen.mutate_policies([pol]), [pod])
+    rule = next(r for r in ev.rules if r.name == "no-latest")
+    assert cli.rule_message(ev, rule, 0) == ("validation error: Pod web uses nginx:latest. "
+                                             "Rule no-latest failed at path /spec/containers/0/image/")
+    pol["spec"]["rules"][0]["validate"]["message"] = "Pod {{request.object.metadata.nothere}}"
+    (tmp_path / "p.yaml").write_text(_yaml.safe_dump(pol))
+    assert cli.main(["apply", str(tmp_path / "p.yaml"), "-r", str(tmp_path / "r.yaml")]) == 2
