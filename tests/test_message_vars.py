@@ -130,3 +130,18 @@ def test_message_substitution_fuzz_vs_oracle():
         assert got == want, (msg, res)
         n_sub += got is not None
     assert n_sub > 100
+
+
+def test_go_json_float_forms():
+    """encoding/json floatEncoder (Go 1.16 encode.go:573-606): 'f' inside [1e-6, 1e21), else 'e'
+    with a one-digit negative exponent; documented behaviour, no reference test holds it."""
+    m = msgvars.go_json_marshal
+    assert m(1e21) == "1e+21"
+    assert m(1e20) == "100000000000000000000"
+    assert m(1e-7) == "1e-7"
+    assert m(0.000001) == "0.000001"
+    assert m(123456789.0) == "123456789"
+    assert m(3) == "3"
+    assert m(-2.5) == "-2.5"
+    assert m(1.5e-10) == "1.5e-10"
+    assert m({"b": [1, None, True], "a": "<&>"}) == '{"a":"\\u003c\\u0026\\u003e","b":[1,null,true]}'
