@@ -100,6 +100,7 @@ class Evaluation:
     paths: dict = field(default_factory=dict)   # (rule, res) -> failing path (FAIL pairs)
     errors: dict = field(default_factory=dict)  # (rule, res) -> err.Error() of ERROR / SKIP pairs
     anypattern: dict = field(default_factory=dict)  # (rule, res) -> [(status, path)] per pattern
+    warnings: list = field(default_factory=list)    # host-side limits met while rendering messages
 
     def policy_rules(self, pi: int) -> list:
         return [r for r in self.rules if r.policy == pi]
@@ -125,11 +126,12 @@ def evaluate(policies: list[dict], resources: list[dict], device: int = 0, messa
                 m = r.error_message(int(ri), int(res), resources[int(res)])
                 if m is not None:
                     ev.errors[(int(ri), int(res))] = m
-        _evaluate_anypatterns(ev, device, specialize)
+        _evaluate_anypatterns(ev, device, specialize, namespace_labels)
     return ev
 
 
-def _evaluate_anypatterns(ev: Evaluation, device: int, specialize: bool = False) -> None:
+def _evaluate_anypatterns(ev: Evaluation, device: int, specialize: bool = False,
+                          namespace_labels: dict | None = None) -> None:
     """Per-pattern outcomes of anyPattern rules, for the pass index and the failure message of
     validatePatterns (pkg/engine/validation.go:446-484): every pattern of the rule is compiled as a
     pattern rule of its own (same match/exclude) and run on the device over the resources where
@@ -155,7 +157,7 @@ def _evaluate_anypatterns(ev: Evaluation, device: int, specialize: bool = False)
                "metadata": src.get("metadata", {}), "spec": {"rules": sub_rules}}
         ps = batch.PolicySet([sub], specialize=specialize)
         ress = [ev.resources[i] for i in idx]
-        b = batch.Batch(ps, ress)
+        b = batch.Batch(ps, ress, namespace_labels)
         r = batch.validate(ps, b, device=device)
         for k, res in enumerate(idx):
             outs = []
@@ -175,6 +177,19 @@ def _evaluate_anypatterns(ev: Evaluation, device: int, specialize: bool = False)
 
 def _with_dot(s: str) -> str:
     return s if s.endswith(".") else s + "."
+
+
+def _message(ev: Evaluation, rule, res: int) -> str:
+    """The rule's message after SubstituteAll (msgvars). A JMESPath form the host does not evaluate
+    leaves the message as written and is reported in ``ev.warnings``; a form on which the reference
+    panics raises ``msgvars.MessageVariableError``."""
+    try:
+        return msgvars.substitute_message(rule.message, ev.resources[res])
+    except msgvars.UnsupportedMessageVariable as e:
+        w = f"rule {rule.name}: message variables not rendered: {e}"
+        if w not in ev.warnings:
+            ev.warnings.append(w)
+        return rule.message
 
 
 def rule_message(ev: Evaluation, rule, res: int) -> str:
@@ -203,7 +218,7 @@ def rule_message(ev: Evaluation, rule, res: int) -> str:
         path = ev.paths.get((rule.index, res), "")
         if not rule.message:
             return f"validation error: rule {rule.name} failed at path {path}"
-        msg = msgvars.substitute_message(rule.message, ev.resources[res])
+        msg = _message(ev, rule, res)
         return f"validation error: {_with_dot(msg)} Rule {rule.name} failed at path {path}"
     if st in (ERROR, SKIP) and (rule.index, res) in ev.errors:
         err = ev.errors[(rule.index, res)]
@@ -211,7 +226,7 @@ def rule_message(ev: Evaluation, rule, res: int) -> str:
             return err
         if not rule.message:  # buildErrorMessage(err, "")
             return f"validation error: rule {rule.name} execution error: {err}"
-        msg = msgvars.substitute_message(rule.message, ev.resources[res])
+        msg = _message(ev, rule, res)
         return f"validation error: {_with_dot(msg)} Rule {rule.name} execution error: {err}"
     if rule.const_message:
         return rule.const_message
@@ -319,6 +334,8 @@ def apply_docs(policies: list[dict], resources: list[dict], policy_report: bool 
                 continue
             for res in range(len(resources)):
                 infos.append(process_validate(ev, pi, res, rc, policy_report, out))
+        for w in ev.warnings:
+            print(f"warning: {w}", file=sys.stderr)
     if skipped:
         out.write(DIVIDER + "\n")
         out.write("Policies Skipped (as required variables are not provided by the user):\n")

@@ -237,15 +237,7 @@ DevBatchRes& dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
   // key string table: static dictionary then batch-dynamic keys
   std::vector<uint32_t> off, len;
   std::string ks;
-  auto addk = [&](const std::string& k) {  // 4-byte aligned (word-granular glob)
-    while (ks.size() & 3) ks.push_back('\0');
-    off.push_back((uint32_t)ks.size());
-    len.push_back((uint32_t)k.size());
-    ks += k;
-  };
-  for (auto& k : ps.keys) addk(k);
-  for (auto& k : b.dyn_keys) addk(k);
-  ks.append(16, '\0');
+  key_table(ps, b, &off, &len, &ks);
   d->koff.upload(off, device);
   d->klen.upload(len, device);
   d->kstr.upload_raw(ks.data(), ks.size(), device);
@@ -265,95 +257,6 @@ DevBatchRes& dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
   auto& ref = *d;
   bt->dev[device] = std::move(d);
   return ref;
-}
-
-struct AdmissionCtx {
-  std::vector<std::string> roles, clusterRoles, groups, dyn;
-  std::string username;
-  bool empty() const { return roles.empty() && clusterRoles.empty() && groups.empty() && username.empty(); }
-};
-
-AdmissionCtx parse_ctx(const char* ctx_json) {
-  AdmissionCtx c;
-  if (!ctx_json || !*ctx_json) return c;
-  JDoc d;
-  parse_json(ctx_json, strlen(ctx_json), NUM_FLOAT, &d);
-  auto list = [&](int64_t n, std::vector<std::string>* out) {
-    if (n < 0 || d.at((uint32_t)n).t != J_ARR) return;
-    const JNode& a = d.at((uint32_t)n);
-    for (uint32_t k = a.first; k < a.first + a.count; k++)
-      if (d.at(k).t == J_STR) out->push_back(std::string(d.sval(d.at(k))));
-  };
-  int64_t a = d.get(d.root, "admission");
-  if (a >= 0 && d.at((uint32_t)a).t == J_MAP) {
-    list(d.get((uint32_t)a, "roles"), &c.roles);
-    list(d.get((uint32_t)a, "clusterRoles"), &c.clusterRoles);
-    list(d.get((uint32_t)a, "groups"), &c.groups);
-    int64_t u = d.get((uint32_t)a, "username");
-    if (u >= 0 && d.at((uint32_t)u).t == J_STR) c.username = std::string(d.sval(d.at((uint32_t)u)));
-  }
-  list(d.get(d.root, "excludeGroupRole"), &c.dyn);
-  return c;
-}
-
-bool slice_contains(const std::vector<std::string>& s, const std::vector<std::string>& v) {
-  for (auto& x : v)
-    if (std::find(s.begin(), s.end(), x) != s.end()) return true;
-  return false;
-}
-
-// user-info part of doesResourceMatchConditionBlock (pkg/engine/utils.go:183-229):
-// true if it appends errors (every checked criterion failed)
-bool ui_fails(const UserInfoSpec& ui, const AdmissionCtx& ai) {
-  std::vector<std::string> keys = ai.groups;
-  keys.push_back(ai.username);
-  int checked = 0, uerr = 0;
-  if (!ui.roles.empty() && !slice_contains(keys, ai.dyn)) {
-    checked++;
-    if (!slice_contains(ui.roles, ai.roles)) uerr++;
-    else return false;
-  }
-  if (!ui.clusterRoles.empty() && !slice_contains(keys, ai.dyn)) {
-    checked++;
-    if (!slice_contains(ui.clusterRoles, ai.clusterRoles)) uerr++;
-    else return false;
-  }
-  if (!ui.subjects.empty()) {
-    checked++;
-    const std::string sa = "system:serviceaccount:";
-    std::vector<UserInfoSpec::Subj> subs = ui.subjects;
-    for (auto& e : ai.dyn) subs.push_back({"Group", e, ""});
-    bool m = false;
-    for (auto& s : subs) {
-      if (s.kind == "ServiceAccount") {
-        if (ai.username.size() <= sa.size()) continue;
-        if (ai.username.substr(sa.size()) == s.ns + ":" + s.name) { m = true; break; }
-      } else if (s.kind == "User" || s.kind == "Group") {
-        if (std::find(keys.begin(), keys.end(), s.name) != keys.end()) { m = true; break; }
-      }
-    }
-    if (!m) uerr++;
-    else return false;
-  }
-  return checked == uerr && uerr > 0;
-}
-
-std::vector<uint32_t> fold_filters(const PolicySet& ps, const AdmissionCtx& ai) {
-  std::vector<uint32_t> out(ps.filters.size());
-  size_t f = 0;
-  for (size_t r = 0; r < ps.rules.size(); r++) {
-    const RuleHost& rh = ps.rhost[r];
-    for (size_t k = 0; k < rh.filter_ui.size(); k++, f++) {
-      uint32_t fl = ps.filters[f].flags & ~(MF_EMPTY | MF_UI_FAIL);
-      bool rd_empty = ps.filters[f].flags & MF_EMPTY;
-      UserInfoSpec ui = rh.filter_ui[k];
-      if (rh.filter_is_match[k] && ai.empty()) ui = UserInfoSpec();
-      if (rd_empty && !ui.present) fl |= MF_EMPTY;
-      if (ui.present && ui_fails(ui, ai)) fl |= MF_UI_FAIL;
-      out[f] = fl;
-    }
-  }
-  return out;
 }
 
 // Path segments from the pattern root to pnode p: keys (resolved wildcard keys
@@ -556,8 +459,7 @@ struct kv_session {
     bview = (const DevBatch*)db.view_dev.p;
     bhost = &db.view;
     dps = &dp;
-    AdmissionCtx ai = parse_ctx(ctx_json);
-    fflags.upload(fold_filters(ps->ps, ai), device);
+    fflags.upload(fold_filters(ps->ps, ctx_json), device);
     DevPS P = dp.view;
     P.fflags = (const uint32_t*)fflags.p;
     if (dp.ptab_fn) {  // value-predicate table of the specialized kernels: memo_words per distinct value
@@ -716,6 +618,12 @@ int kv_compile(const char* policies_json, size_t len, uint32_t flags, kv_policys
           }
         }
         if (!getenv("KVGPU_JIT_SKIP_COMPILE")) jit_compile(s->jit.get());  // dump-only analysis runs
+        if (const char* dump = getenv("KVGPU_JIT_DUMP_CO")) {  // the gfx950 code object (llvm-objdump / readelf)
+          if (FILE* f = fopen(dump, "wb")) {
+            fwrite(s->jit->code.data(), 1, s->jit->code.size(), f);
+            fclose(f);
+          }
+        }
       }
     } catch (...) {
       delete s;

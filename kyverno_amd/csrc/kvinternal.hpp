@@ -175,6 +175,13 @@ struct Batch {
 
 void ingest_resources(const PolicySet& ps, const char* json, size_t len, const char* ns_labels_json, Batch* b);
 
+// Launch-time folding (kvfold.cpp): per-filter flags with the batch-constant
+// user-info criteria folded in (ctx_json: AdmissionInfo / ExcludeGroupRole, or
+// NULL), and the batch key string table (4-byte aligned entries).
+std::vector<uint32_t> fold_filters(const PolicySet& ps, const char* ctx_json);
+void key_table(const PolicySet& ps, const Batch& b, std::vector<uint32_t>* off, std::vector<uint32_t>* len,
+               std::string* ks);
+
 // Go-semantics helpers shared by compiler and ingest
 bool wildcard_match_host(std::string_view pattern, std::string_view name);
 bool valid_label_key(const std::string& k);

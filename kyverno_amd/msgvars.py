@@ -8,21 +8,32 @@ context in ``buildErrorMessage`` (pkg/engine/validation.go:510-532): ``variables
 ``{"request": {"object": <resource>}}`` re-read with encoding/json, so numbers are float64.
 
 Supported variables: JMESPath field / quoted-field / index chains rooted at ``request.object``
-(the only ones ``kyverno apply`` evaluates without ``--set``: common.go:76-80). Anything else, a
-missing key, or a whole-message variable whose value is not a string makes the reference panic
-(``msgRaw.(string)`` on a nil / non-string interface, validation.go:519-524); here that raises
-``MessageVariableError``.
+(the only ones ``kyverno apply`` evaluates without ``--set``: common.go:76-80). A missing key, or a
+whole-message variable whose value is not a string, makes the reference panic (``msgRaw.(string)``
+on a nil / non-string interface, validation.go:519-524); here that raises ``MessageVariableError``.
+Other JMESPath forms (projections, pipes, filters, functions) are valid for the reference but not
+evaluated here: they raise ``UnsupportedMessageVariable`` (not a reference panic).
+
+``$()`` references in a message resolve against the message string itself (vars.go:253-309,
+450-475): the lookup never finds a value, so a plain reference makes SubstituteAll return the
+message unchanged together with an error that buildErrorMessage only logs (variables are then not
+substituted at all), while an empty or operator-prefixed reference returns nil and panics.
 """
 from __future__ import annotations
 
 import decimal
 import re
 
-__all__ = ["MessageVariableError", "substitute_message", "has_variable", "go_json_marshal"]
+__all__ = ["MessageVariableError", "UnsupportedMessageVariable", "substitute_message", "has_variable",
+           "go_json_marshal"]
 
 
 class MessageVariableError(ValueError):
     """The reference engine panics on this message (unresolvable or non-string substitution)."""
+
+
+class UnsupportedMessageVariable(ValueError):
+    """A message variable the reference evaluates (general JMESPath) that this host does not."""
 
 
 def _find_vars(s: str) -> list[str]:
@@ -72,7 +83,7 @@ def _query(expr: str, context) -> object:
     while pos < len(expr):
         m = _TOKEN.match(expr, pos)
         if not m or (pos == 0 and expr[0] in ".["):
-            raise MessageVariableError(f"unsupported JMESPath expression in message: {expr!r}")
+            raise UnsupportedMessageVariable(f"JMESPath expression not evaluated here: {expr!r}")
         steps.append(m)
         pos = m.end()
     if not steps:
@@ -93,6 +104,21 @@ def _query(expr: str, context) -> object:
         else:
             cur = None
     return cur
+
+
+def _operator(p: str) -> str:
+    """operator.GetOperatorFromStringPattern (pkg/engine/operator/operator.go:33-67)."""
+    if len(p) < 2:
+        return ""
+    for op in (">=", "<=", ">", "<", "!"):
+        if p.startswith(op):
+            return op
+    # RE2: \d is ASCII, $ is the end of the text
+    if re.match(r"([0-9]+(\.[0-9]+)?)([^-]*)!-([0-9]+(\.[0-9]+)?)([^-]*)\Z", p):
+        return "!-"
+    if re.match(r"([0-9]+(\.[0-9]+)?)([^-]*)-([0-9]+(\.[0-9]+)?)([^-]*)\Z", p):
+        return "-"
+    return ""
 
 
 def _go_float(f: float) -> str:
@@ -160,11 +186,25 @@ def substitute_message(msg: str, resource: dict) -> str:
     """The message after SubstituteAll with context ``request.object = resource``: references
     (vars.go:253-309), then substituteVariablesIfAny (vars.go:319-398), then ``\\{{`` unescaping."""
     context = {"request": {"object": resource}}
-    # substituteReferencesIfAny on the message document (vars.go:253-309): a $() reference has
-    # nothing to resolve against in a string document (an error: the reference panics); \$( is
-    # unescaped
-    if _REF.search(msg):
-        raise MessageVariableError(f"$() reference in message {msg!r}")
+    # substituteReferencesIfAny on the message document (vars.go:253-309): the first reference
+    # decides. resolveReference (vars.go:450-475) looks the path up in the message string itself,
+    # whose only leaf sits at path "", so nothing is ever found: an empty path errors (nil element:
+    # panic), an operator fails valFromReferenceToString(nil) (nil element: panic), a plain
+    # reference resolves to nil and returns the original string with an error that
+    # buildErrorMessage only logs (validation.go:519-522) -- no variable substitution follows
+    m = _REF.search(msg)
+    if m:
+        v = m.group(0)
+        if not v.startswith("$("):
+            v = v[1:]
+        path = v.strip("$()")
+        op = _operator(path)
+        path = path[len(op):]
+        if not path:
+            raise MessageVariableError(f"empty $() reference in message {msg!r}")
+        if op:
+            raise MessageVariableError(f"$() reference with operator {op!r} in message {msg!r} resolves to nil")
+        return msg
     value = _ESC_REF.sub(lambda m: m.group(0)[1:], msg)
     vs = _find_vars(value)
     while vs:

@@ -172,8 +172,12 @@ struct Ctx {
   const Value* doc;
 };
 
-// Returns 0 ok (value updated), else error message.
-bool subst_string(const Ctx& cx, std::string& value, const std::string& dpath, std::string* err) {
+// Returns true (value updated), else false with the error message. *keep (optional) is set
+// when the reference's action returns the unchanged element together with the error
+// (vars.go:278-279,292-295: a reference resolving to nil, or to a non-string without an
+// operator) rather than nil (an empty path or an operator on a missing value).
+bool subst_string(const Ctx& cx, std::string& value, const std::string& dpath, std::string* err,
+                  bool* keep = nullptr) {
   std::string orig = value;
   for (const auto& m : find_references(orig)) {
     std::string v = orig.substr(m.b, m.e - m.b);
@@ -198,15 +202,12 @@ bool subst_string(const Ctx& cx, std::string& value, const std::string& dpath, s
     std::string resolved;
     bool resolved_is_string = false;
     if (op.empty()) {
-      if (!found) {
+      if (!found || found->t == T::Null) {
         *err = "failed to resolve " + v + " at path " + dpath + ": <nil>";
+        if (keep) *keep = true;
         return false;
       }
       if (found->t == T::Str) { resolved = found->s; resolved_is_string = true; }
-      else if (found->t == T::Null) {
-        *err = "failed to resolve " + v + " at path " + dpath + ": <nil>";
-        return false;
-      }
     } else {
       std::string fv;
       if (found && found->t == T::Str) fv = found->s;
@@ -227,6 +228,7 @@ bool subst_string(const Ctx& cx, std::string& value, const std::string& dpath, s
       continue;
     }
     *err = "NotResolvedReferenceErr,reference " + v + " not resolved at path " + dpath;
+    if (keep) *keep = true;
     return false;
   }
   for (const auto& e : find_escaped_references(value)) value = replace_n(value, e, e.substr(1), -1);
@@ -498,14 +500,21 @@ bool query_object(const std::string& q, const Value& resource, const Value** out
 }  // namespace
 
 bool SubstituteMessage(const std::string& msg, const Value& resource, std::string* out) {
-  Value doc = Value::mk_str(msg);
+  // substituteReferences over the string document (its only leaf, at path ""): a reference that
+  // returns the element with an error leaves the message as it is (SubstituteAll returns it,
+  // buildErrorMessage logs the error, validation.go:519-522); one that returns nil panics
+  std::string value = msg;
   {
-    Value original = doc;
+    const Value original = Value::mk_str(msg);
     Ctx cx{&original};
     std::string err;
-    if (!traverse(cx, doc, "", &err)) return false;
+    bool keep = false;
+    if (!subst_string(cx, value, "", &err, &keep)) {
+      if (!keep) return false;
+      *out = msg;
+      return true;
+    }
   }
-  std::string value = doc.s;
   auto vars = find_vars(value);
   while (!vars.empty()) {
     std::string original = value;

@@ -44,9 +44,15 @@ MESSAGES = [
     "{{request.object.kind}}{{request.object.metadata.name}}",
     "x{{request.object.spec.containers[0].ports[0].containerPort}}y",
     "twice {{request.object.kind}} {{request.object.kind}}",
+    # a plain $() reference resolves to nil against the message string: the message comes back
+    # unchanged, variables not substituted (vars.go:278-279, validation.go:519-522)
+    "bad $(ref) {{request.object.kind}}",
+    "$(./x) {{request.object.kind}} \\{{request.object.kind}}",
     # the reference panics on these (msgRaw.(string) of nil or a non-string)
     "missing {{request.object.metadata.nothere}}",
     "{{request.object.spec.replicas}}",
+    "bad $(<x) {{request.object.kind}}",
+    "bad $(>=) here",
 ]
 
 
@@ -68,6 +74,30 @@ def test_message_substitution_known_forms():
     assert s("a {{request.object.metadata.annotations}}", RES) == 'a {"note":"a\\u003cb \\u0026 c\\u003ed"}'
     with pytest.raises(msgvars.MessageVariableError):
         s("{{request.object.spec.replicas}}", RES)
+
+
+def test_message_reference_forms():
+    """Message references (vars.go:253-309,450-475 on a string document): plain -> unchanged,
+    empty path / operator -> the reference panics."""
+    s = msgvars.substitute_message
+    assert s("bad $(ref) {{request.object.kind}}", RES) == "bad $(ref) {{request.object.kind}}"
+    assert s("x $(a/b) \\$(c) {{request.object.kind}}", RES) == "x $(a/b) \\$(c) {{request.object.kind}}"
+    assert s("esc \\$(c) {{request.object.kind}}", RES) == "esc $(c) Pod"
+    assert s("$() and $(<)", RES) == "$() and $(<)"  # no reference / a plain one
+    for bad in ("bad $(<x) m", "$(!x)", "$(>=)", "$(1-2)"):
+        with pytest.raises(msgvars.MessageVariableError):
+            s(bad, RES)
+
+
+def test_unsupported_jmespath_is_not_a_panic():
+    """Projections / functions are valid JMESPath for the reference (ctx.Query); the host does not
+    evaluate them and says so with a distinct exception, never the panic one."""
+    for msg in ("images {{request.object.spec.containers[*].image}}",
+                "n {{length(request.object.spec.containers)}}",
+                "p {{request.object.spec.containers[0] | name}}"):
+        with pytest.raises(msgvars.UnsupportedMessageVariable):
+            msgvars.substitute_message(msg, RES)
+        assert not issubclass(msgvars.UnsupportedMessageVariable, msgvars.MessageVariableError)
 
 
 def _rand_value(rng, depth):

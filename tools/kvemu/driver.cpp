@@ -1,0 +1,210 @@
+// kvemu driver: runs the generated specialized kernels (kvjit.cpp output for one
+// policy set, compiled for the host with shim.h) over an ingested batch, lane by
+// lane, and writes the status matrix and error records. Test / debugging
+// infrastructure only (sanitizer runs of the generated code, CPU-side checks of
+// the generator against the oracle); the product path is libkvgpu on a GPU.
+//
+//   kvemu <policies.json> <resources.ndjson> <ctx.json|-> <out-prefix>
+//     -> <out-prefix>.status  u8 [rule][res]
+//        <out-prefix>.err     ErrRec (32 B) [rule][res], records of FAIL/ERROR/SKIP pairs
+//        <out-prefix>.meta    "n_rules n_res wide"
+// Environment: the KVGPU_JIT_* settings the source was generated with.
+#include <dlfcn.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../kyverno_amd/csrc/kv_layout.h"
+#include "../../kyverno_amd/csrc/kvdevtypes.h"
+#include "../../kyverno_amd/csrc/kvinternal.hpp"
+#include "../../kyverno_amd/csrc/kvjit.hpp"
+
+using namespace kv;
+using namespace kvh;
+
+struct kvemu_dim3 {
+  uint32_t x, y, z;
+};
+thread_local kvemu_dim3 threadIdx, blockIdx;
+
+typedef void (*ptab_fn)(const DevPS*, const Val*, const uint8_t*, uint32_t, uint32_t*);
+typedef void (*chunk_fn)(const DevPS*, const DevBatch*, const Node*, const Val*, const uint8_t*, DevOut);
+
+static std::string slurp(const char* p) {
+  std::ifstream f(p, std::ios::binary);
+  if (!f) throw std::runtime_error(std::string("cannot read ") + p);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  return ss.str();
+}
+
+static uint64_t fnv1a(const std::string& s) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+  return h;
+}
+
+#ifndef KVEMU_SRC_HASH
+#define KVEMU_SRC_HASH 0
+#endif
+
+// every (block, lane) of a grid, blocks spread over host threads
+template <class F>
+static void grid(uint32_t bx, uint32_t by, F f) {
+  const uint32_t T = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  std::atomic<uint64_t> next{0};
+  const uint64_t total = (uint64_t)bx * by;
+  std::vector<std::thread> th;
+  for (uint32_t t = 0; t < T; t++)
+    th.emplace_back([&]() {
+      for (uint64_t i; (i = next++) < total;) {
+        blockIdx = {(uint32_t)(i % bx), (uint32_t)(i / bx), 0};
+        for (uint32_t x = 0; x < (uint32_t)KV_WG; x++) {
+          threadIdx = {x, 0, 0};
+          f();
+        }
+      }
+    });
+  for (auto& t : th) t.join();
+}
+
+int main(int argc, char** argv) {
+  if (argc != 5) {
+    fprintf(stderr, "usage: kvemu policies.json resources.ndjson ctx.json|- out-prefix\n");
+    return 2;
+  }
+  try {
+    const std::string pol = slurp(argv[1]), res = slurp(argv[2]);
+    std::string ctx = strcmp(argv[3], "-") ? slurp(argv[3]) : std::string();
+    PolicySet ps;
+    compile_policies(pol.data(), pol.size(), &ps);
+    Batch b;
+    ingest_resources(ps, res.data(), res.size(), nullptr, &b);
+    JitImage img;
+    const char* ch = getenv("KVGPU_JIT_CHUNK");
+    jit_generate(ps, ch ? (uint32_t)atoi(ch) : 8u, &img);
+    if (KVEMU_SRC_HASH && fnv1a(img.source) != (uint64_t)KVEMU_SRC_HASH)
+      throw std::runtime_error("generated source differs from the one this binary was built from");
+
+    const std::vector<uint32_t> fflags = fold_filters(ps, ctx.empty() ? nullptr : ctx.c_str());
+    std::vector<uint32_t> koff, klen;
+    std::string ks;
+    key_table(ps, b, &koff, &klen, &ks);
+    const uint32_t NV = (uint32_t)b.vals.size();
+    std::vector<uint32_t> ptab((size_t)std::max<uint32_t>(img.memo_words, 1) * std::max<uint32_t>(NV, 1), 0u);
+    DevPS P{};
+    P.prog = ps.prog.data();
+    P.preds = ps.preds.data();
+    P.alts = ps.alts.data();
+    P.conjs = ps.conjs.data();
+    P.atoms = ps.atoms.data();
+    P.rules = ps.rules.data();
+    P.filters = ps.filters.data();
+    P.fflags = fflags.data();
+    P.kinds = ps.kinds.data();
+    P.strrefs = ps.strrefs.data();
+    P.strpairs = ps.strpairs.data();
+    P.sels = ps.selectors.data();
+    P.sellabels = ps.sellabels.data();
+    P.selexprs = ps.selexprs.data();
+    P.kg_specs = ps.kg_specs.data();
+    P.gsegs = ps.gsegs.data();
+    P.gwords = ps.gwords.data();
+    P.pstr = (const uint8_t*)ps.strs.data();
+    P.star_id = ps.lookup("*");
+    if (P.star_id == KEY_NONE) P.star_id = KEY_NONE - 1;
+    P.n_rules = (uint32_t)ps.rules.size();
+    P.ptab = ptab.data();
+    P.n_vals = NV;
+    DevBatch B{};
+    B.nodes = b.nodes.data();
+    B.vals = b.vals.data();
+    B.res = b.res.data();
+    B.kvs = b.kvs.data();
+    B.bstr = (const uint8_t*)b.strs.data();
+    B.ns_bits = b.ns_bits.data();
+    B.key_off = koff.data();
+    B.key_len = klen.data();
+    B.kstr = (const uint8_t*)ks.data();
+    B.ns_words = b.ns_words;
+    B.n_res = (uint32_t)b.res.size();
+    const uint64_t nr = ps.rules.size(), nres = b.res.size();
+
+    if (img.memo_words && NV) {
+      auto f = (ptab_fn)dlsym(RTLD_DEFAULT, "kvj_ptab");
+      if (!f) throw std::runtime_error("kvj_ptab not linked in");
+      const uint32_t rows = (uint32_t)((img.memo_preds.size() + img.ptab_row - 1) / img.ptab_row);
+      grid((NV + KV_WG - 1) / KV_WG, rows, [&]() { f(&P, B.vals, B.bstr, NV, ptab.data()); });
+    }
+    std::vector<uint8_t> status(nr * nres, 0xEE);
+    std::vector<ErrRec8> err8(nr * nres);
+    std::vector<ErrRec> errw;
+    std::vector<unsigned long long> counts(std::max<uint64_t>(nr, 1) * KV_HIST, 0);
+    DevOut O{};
+    O.status = status.data();
+    O.err8 = err8.data();
+    O.counts = counts.data();
+    O.full = 3;
+    std::vector<chunk_fn> fns;
+    for (const JitChunk& c : img.chunks) {
+      auto f = (chunk_fn)dlsym(RTLD_DEFAULT, c.name.c_str());
+      if (!f) throw std::runtime_error(c.name + " not linked in");
+      fns.push_back(f);
+    }
+    const uint32_t blocks = (uint32_t)((nres + KV_WG - 1) / KV_WG);
+    auto pass = [&]() {
+      for (chunk_fn f : fns) grid(blocks, 1, [&]() { f(&P, &B, B.nodes, B.vals, B.bstr, O); });
+    };
+    if (nres) pass();
+    bool wide = false;
+    for (size_t o = 0; o < status.size() && !wide; o++) {
+      const uint8_t s = status[o];
+      wide = (s == ST_FAIL || s == ST_ERROR || s == ST_SKIP) && (err8[o].w0 & ERR8_WIDE);
+    }
+    // KVEMU_NO_ERR=1: statuses only (large batches); the wide re-pass still runs
+    const bool want_err = !getenv("KVEMU_NO_ERR");
+    if (want_err || wide) errw.assign(nr * nres, ErrRec{});
+    if (wide) {  // as kv_session::fetch: one more pass writing full records
+      O.err = errw.data();
+      O.full |= 4;
+      pass();
+    }
+    for (size_t o = 0; o < status.size() && want_err; o++) {
+      const uint8_t s = status[o];
+      if (!(s == ST_FAIL || s == ST_ERROR || s == ST_SKIP) || (err8[o].w0 & ERR8_WIDE)) continue;
+      const ErrRec8 c = err8[o];
+      ErrRec e{};
+      e.kind_flags = (c.w0 & 15u) | (((c.w0 >> 4) & 3u) << 16);
+      e.pnode = c.w0 >> 7;
+      e.keynode = ABSENT;
+      e.resnode = ABSENT;
+      e.idx[0] = c.w1 & 4095u;
+      e.idx[1] = (c.w1 >> 12) & 1023u;
+      e.idx[2] = c.w1 >> 22;
+      errw[o] = e;
+    }
+    const std::string out = argv[4];
+    FILE* fs = fopen((out + ".status").c_str(), "wb");
+    FILE* fe = fopen((out + ".err").c_str(), "wb");
+    FILE* fm = fopen((out + ".meta").c_str(), "w");
+    if (!fs || !fe || !fm) throw std::runtime_error("cannot write outputs");
+    fwrite(status.data(), 1, status.size(), fs);
+    fwrite(errw.data(), sizeof(ErrRec), errw.size(), fe);
+    fprintf(fm, "%llu %llu %d\n", (unsigned long long)nr, (unsigned long long)nres, wide ? 1 : 0);
+    fclose(fs);
+    fclose(fe);
+    fclose(fm);
+    return 0;
+  } catch (const std::exception& e) {
+    fprintf(stderr, "kvemu: %s\n", e.what());
+    return 1;
+  }
+}
