@@ -29,20 +29,50 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(policies, n_sample: int, threads: int, kind_mix: int = 0, label: str = "C2") -> dict:
-    """Oracle (CPU restatement of the reference engine) on a bounded sample."""
+def host_cpu() -> dict:
+    """Host core count (all cores, and those this process may run on) and the CPU model (lscpu)."""
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 1
+    quota = None
+    try:  # cgroup v2 CPU quota ("max" = none)
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    usable = min(avail, quota) if quota else avail
+    return {"nproc": os.cpu_count() or 1, "affinity": avail, "cgroup_quota_cores": quota, "available": usable,
+            "model": model}
+
+
+def cpu_baseline(policies, pairs: float, threads: int, kind_mix: int = 0, label: str = "C2") -> dict:
+    """Oracle (CPU restatement of the reference engine) on a bounded sample of the same workload:
+    the first resources of the benchmark's synthetic stream, about `pairs` resource x rule pairs."""
     import oracle
     from kyverno_amd import batch, workloads
 
     orc = oracle.get()
-    data = batch.synth(workloads.SEED + 999, n_sample, kind_mix).decode()
-    ress = "[" + ",".join(data.strip().split("\n")) + "]"
-    st, secs = orc.validate_batch(json.dumps(policies), ress, nthreads=threads)
+    n_rules = sum(len(p["spec"]["rules"]) for p in policies)
+    n_sample = max(1000, int(pairs // max(1, n_rules)))
+    data = batch.synth(workloads.SEED, n_sample, kind_mix).strip()
+    st, secs = orc.validate_ndjson(json.dumps(policies), data, nthreads=threads, preparse=True)
     n_rules = st.shape[0]
     return {"value": n_sample * n_rules / secs, "unit": "resource×rule evals/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{n_sample} synthetic resources x {n_rules} rules ({label} rule set), evaluation only "
-                      f"(inputs pre-parsed), oracle/ C++ restatement on {threads} host threads, {secs:.2f} s"}
+            "host": host_cpu(), "kind": "port",
+            "sample": f"first {n_sample} resources of the benchmark stream x {n_rules} rules ({label} rule set), "
+                      f"evaluation only (inputs pre-parsed), oracle/ C++ restatement on {threads} host threads, "
+                      f"{secs:.2f} s"}
 
 
 def main():
@@ -50,7 +80,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n-res", type=int, default=1_000_000, help="resources per GPU")
+    ap.add_argument("--n-res", type=int, default=None,
+                    help="resources per GPU (default: the config's per-GPU share at 8 GPUs: C2/C4 1M, "
+                         "C3 10M/8, C5 50M/8)")
     ap.add_argument("--mode", choices=["full", "counts", "scopes"], default=None,
                     help="full: status + failing-path records per pair; counts: per-rule histogram only; "
                          "scopes: per-namespace PolicyReport counts (status kept on device). "
@@ -61,7 +93,8 @@ def main():
                          "c5: background scan, chart after autogen (105 rules) x mixed kinds, counts")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive kv_validate timing")
-    ap.add_argument("--cpu-sample", type=int, default=40_000)
+    ap.add_argument("--cpu-pairs", type=float, default=6e7,
+                    help="resource x rule pairs of the CPU baseline sample (~10 s on 16 EPYC cores at C2)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default=None,
                     help="torch.distributed backend for N>1 (default: nccl = RCCL when GPUs are visible); "
                          "gloo lets several ranks share one GPU for a rehearsal")
@@ -112,13 +145,16 @@ def main():
         workload = "C5: background scan, kyverno-policies chart (restricted) after autogen x Pods/Deployments/Services"
     if args.mode is None:
         args.mode = "scopes" if args.config == "c5" else "full"
+    if args.n_res is None:
+        args.n_res = {"c2": 1_000_000, "c3": 10_000_000 // 8, "c4": 1_000_000, "c5": 50_000_000 // 8}[args.config]
     t0 = time.time()
     ps = batch.PolicySet(pols, specialize=args.engine == "specialized")
     jit = ps.jit_info
     if jit["kernels"]:
         log(f"[rank {rank}] specialized kernels: {jit['kernels']} ({jit['code_bytes'] / 1e3:.0f} KB code), "
             f"hiprtc {jit['compile_ms'] / 1e3:.1f}s")
-    data = batch.synth(workloads.SEED + rank, args.n_res, kind_mix)
+    # rank r evaluates the contiguous shard [r * N, (r + 1) * N) of one synthetic stream
+    data = batch.synth(workloads.SEED, args.n_res, kind_mix, first=rank * args.n_res)
     ndjson_bytes = len(data)
     t1 = time.time()
     b = batch.Batch(ps, data)
@@ -176,11 +212,13 @@ def main():
     b_alg = b.store_bytes + prog_bytes + out_bytes
     achieved = b_alg / (kernel_ms / 1e3) / 1e9
     traffic, traffic_src = None, None
-    try:  # HBM bytes from the PMC passes of the same workload (rocprofv3 cannot run inside this process)
+    try:  # HBM bytes per pass from an OFFLINE rocprofv3 PMC run of this workload (rocprofv3 cannot run
+        # inside this process): reported only when that run's workload matches, labelled with its run id
         tj = json.load(open(args.traffic_json))
         if (tj["workload"], tj["resources_per_gpu"], tj["rules"], tj["output"], tj["engine"]) == \
                 (workload, b.n_res, ps.n_rules, args.mode, args.engine):
-            traffic, traffic_src = tj["bytes_per_pass"], tj["source"]
+            traffic = tj["bytes_per_pass"]
+            traffic_src = f"offline PMC, {os.path.relpath(args.traffic_json, ROOT)} (run {tj.get('run_id', '?')})"
     except (OSError, ValueError, KeyError):
         pass
     out = {
@@ -195,7 +233,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (kv_synth, seed 0x6B79766E + rank)",
+        "data": f"synthetic (kv_synth_range, seed 0x6B79766E, rank shard [r*N, (r+1)*N), N={args.n_res})",
         "config": {"workload": workload, "resources_per_gpu": b.n_res, "rules": ps.n_rules,
                    "pairs_per_gpu": n_pairs_rank, "output": args.mode, "parallelism": f"resource-shard x{world}",
                    "engine": args.engine},
@@ -215,7 +253,7 @@ def main():
         # PCIe-inclusive rate of the host boundary: kv_validate on a freshly ingested
         # batch = H2D upload of the projected store + one pass + D2H of statuses and error records
         del sess
-        b2 = batch.Batch(ps, batch.synth(workloads.SEED + rank, args.n_res, kind_mix))
+        b2 = batch.Batch(ps, batch.synth(workloads.SEED, args.n_res, kind_mix, first=rank * args.n_res))
         te0 = time.perf_counter()
         r2 = batch.validate(ps, b2, device=local)
         te1 = time.perf_counter()
@@ -224,8 +262,10 @@ def main():
                                   "includes": "H2D store upload + 1 pass + D2H status/error records"}
         del r2, b2
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(pols, args.cpu_sample, threads, kind_mix, args.config.upper())
+        # every core this process may run on (the GPU box grants a share of the machine's cores;
+        # nproc and the CPU model are recorded beside it)
+        threads = host_cpu()["available"]
+        out["cpu_baseline"] = cpu_baseline(pols, args.cpu_pairs, threads, kind_mix, args.config.upper())
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -147,6 +147,8 @@ void kv_free_session(kv_session* s);
  * kind_mix 0 = Pods; 1 = Pods/Deployments/Services 60/25/15. Returns NDJSON
  * (free with kv_free_buffer). */
 int kv_synth(uint64_t seed, uint64_t n, uint32_t kind_mix, char** json_out, size_t* len);
+/* resources [first, first + n) of the same stream (a rank's contiguous shard) */
+int kv_synth_range(uint64_t seed, uint64_t first, uint64_t n, uint32_t kind_mix, char** json_out, size_t* len);
 
 void kv_free_policyset(kv_policyset* ps);
 void kv_free_batch(kv_batch* b);

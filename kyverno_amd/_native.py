@@ -79,6 +79,7 @@ def lib():
         L.kv_result_kernel_ms.restype = ctypes.c_double
         L.kv_bench.argtypes = [vp, vp, ctypes.c_char_p, i32, u32, i32, i32, ctypes.POINTER(ctypes.c_double), errpp]
         L.kv_synth.argtypes = [u64, u64, u32, ctypes.POINTER(vp), ctypes.POINTER(sz)]
+        L.kv_synth_range.argtypes = [u64, u64, u64, u32, ctypes.POINTER(vp), ctypes.POINTER(sz)]
         L.kv_session_create.argtypes = [vp, vp, ctypes.c_char_p, i32, u32, ctypes.POINTER(vp), errpp]
         L.kv_session_run.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_double), errpp]
         L.kv_session_counts.argtypes = [vp, vp]
@@ -100,7 +101,7 @@ EXPORTED_SYMBOLS = [
     "kv_compile", "kv_policyset_info", "kv_policyset_jit_info", "kv_rule_info_get", "kv_ingest", "kv_batch_info", "kv_validate",
     "kv_result_status", "kv_result_counts", "kv_result_path", "kv_result_error", "kv_result_error_message",
     "kv_result_kernel_ms",
-    "kv_bench", "kv_synth", "kv_free_policyset", "kv_free_batch", "kv_free_result", "kv_free_error",
+    "kv_bench", "kv_synth", "kv_synth_range", "kv_free_policyset", "kv_free_batch", "kv_free_result", "kv_free_error",
     "kv_free_buffer", "kv_session_create", "kv_session_run", "kv_session_counts", "kv_free_session",
     "kv_session_scope_counts", "kv_result_scope_counts", "kv_batch_namespaces", "kv_batch_namespace",
 ]

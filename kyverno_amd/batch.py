@@ -267,10 +267,11 @@ class Session:
             self._h = None
 
 
-def synth(seed: int, n: int, kind_mix: int = 0) -> bytes:
+def synth(seed: int, n: int, kind_mix: int = 0, first: int = 0) -> bytes:
+    """NDJSON of resources [first, first + n) of the synthetic stream `seed` (kv_synth_range)."""
     p = ctypes.c_void_p()
     ln = ctypes.c_size_t()
-    rc = lib().kv_synth(seed, n, kind_mix, ctypes.byref(p), ctypes.byref(ln))
+    rc = lib().kv_synth_range(seed, first, n, kind_mix, ctypes.byref(p), ctypes.byref(ln))
     if rc != 0:
         raise _native.KvError(rc, "kv_synth failed")
     data = ctypes.string_at(p.value, ln.value)

@@ -89,17 +89,28 @@ enum ValFlags : uint32_t {
 };
 
 // Per-resource header used by the match/exclude prefilter and as the tree root.
+// The match inputs that repeat across resources are interned per batch and
+// referenced by id, so the match tables (DevPS::mt_*) evaluate each glob /
+// selector / annotation filter once per distinct input (kv_mtab):
+//   nsm  = the string checkNameSpace globs (the namespace; the name for kind
+//          Namespace, pkg/engine/utils.go:62-75), Batch::nsms
+//   lset = the resource's label list (selector + wildcard expansion, utils.go:99-107)
+//   aset = the resource's annotation list (checkAnnotations, utils.go:77-97)
 struct Res {
   uint32_t root;          // ROW of the root node (node index root * KV_LANES + r % KV_LANES)
   uint32_t kind;          // key-dictionary id of .kind (KEY_NONE if not in dictionary)
   uint32_t group, version;// dictionary ids of the apiVersion group / version
   uint32_t name_off, name_len;
-  uint32_t ns_off, ns_len;      // namespace used by checkNameSpace (name for kind Namespace)
-  uint32_t labels_first, labels_count;  // KV pairs (sorted by key bytes); count 0 if not a string map
-  uint32_t annot_first, annot_count;
-  uint32_t ns_index;      // index into the batch namespace table (namespaceSelector bits)
+  uint32_t nsm, lset, aset;
+  uint32_t ns_index;      // index into the batch namespace table (namespaceSelector bits, report scope)
   uint32_t flags;         // RF_*
-  uint32_t pad0, pad1;
+  uint32_t pad[5];
+};
+
+// a label / annotation list of a batch: kvs[first, first + count), sorted by key bytes
+// (count 0 when the field is not a string map: NestedStringMap error -> nil map)
+struct KVSet {
+  uint32_t first, count;
 };
 
 enum ResFlags : uint32_t {
@@ -107,6 +118,7 @@ enum ResFlags : uint32_t {
   RF_KIND_EMPTY = 1u << 1,      // kind == ""
   RF_BAD_META = 1u << 2,        // some metadata/labels/annotations shape would make ExpandInMetadata panic
   RF_MAGIC = 1u << 3,           // a string/key contains "conditional anchor mismatch" / "global anchor mismatch"
+  RF_NAME_ASCII = 1u << 4,      // metadata.name is ASCII (word globs exact for '?')
 };
 
 struct KV {
@@ -230,9 +242,10 @@ struct MFilter {          // one ResourceFilter / condition block
   uint32_t names_first, names_count;       // StrRef[] globs
   uint32_t nss_first, nss_count;           // StrRef[] namespace globs
   uint32_t ann_first, ann_count;           // StrPair[] annotation globs
-  uint32_t sel;                            // Selector index (MF_SEL)
+  uint32_t sel;                            // Selector index (MF_SEL): bit of the label-set match table
   uint32_t nssel_bit;                      // bit in the per-namespace table (MF_NSSEL)
-  uint32_t pad;
+  uint32_t nss_bit;                        // bit of the namespace-glob match table (MF_NSS)
+  uint32_t ann_bit;                        // bit of the annotation match table (MF_ANN)
 };
 enum MFilterFlags : uint32_t {
   MF_EMPTY = 1u << 0,     // ResourceDescription and UserInfo empty ("match cannot be empty")

@@ -72,18 +72,20 @@ struct DevPolicySet {
   DevBuf prog, preds, alts, conjs, atoms, rules, filters, kinds, strrefs, strpairs, sels, sellabels, selexprs, kgs,
       gsegs, gwords, pstr;
   DevPS view{};
-  // specialized kernels (KV_COMPILE_SPECIALIZE): one function per rule chunk
-  hipModule_t mod = nullptr;
+  // specialized kernels (KV_COMPILE_SPECIALIZE): one module per kernel program, one
+  // function per rule chunk
+  std::vector<hipModule_t> mods;
   std::vector<hipFunction_t> fns;
   hipFunction_t ptab_fn = nullptr;  // value-predicate table builder (kvj_ptab)
   uint32_t memo_words = 0, ptab_rows = 0;
   int dev = -1;
+  bool specialized() const { return !mods.empty(); }
   ~DevPolicySet() {
-    if (mod) {
+    if (!mods.empty()) {
       int cur;
       if (hipGetDevice(&cur) == hipSuccess) {
         (void)hipSetDevice(dev);
-        (void)hipModuleUnload(mod);
+        for (hipModule_t m : mods) (void)hipModuleUnload(m);
         (void)hipSetDevice(cur);
       }
     }
@@ -91,7 +93,7 @@ struct DevPolicySet {
 };
 
 struct DevBatchRes {
-  DevBuf nodes, vals, res, kvs, bstr, nsbits, koff, klen, kstr, view_dev;
+  DevBuf nodes, vals, res, kvs, bstr, nsbits, koff, klen, kstr, nsms, lsets, asets, view_dev;
   DevBatch view{};
 };
 
@@ -191,6 +193,8 @@ DevPolicySet& dev_ps(kv_policyset* s, int device) {
   v.gsegs = (const GSeg*)d->gsegs.p;
   v.gwords = (const GWord*)d->gwords.p;
   v.n_rules = (uint32_t)ps.rules.size();
+  v.n_filters = (uint32_t)ps.filters.size();
+  v.n_sels = (uint32_t)ps.selectors.size();
   v.pstr = (const uint8_t*)d->pstr.p;
   // resource version "*" (checkKind, pkg/engine/utils.go:49): when "*" is not in the key dictionary no
   // resource can carry it, and an unknown version (KEY_NONE) must not compare equal to it
@@ -198,10 +202,20 @@ DevPolicySet& dev_ps(kv_policyset* s, int device) {
   if (v.star_id == KEY_NONE) v.star_id = KEY_NONE - 1;
   d->dev = device;
   if (s->jit) {
-    HIPCHK(hipModuleLoadData(&d->mod, s->jit->code.data()));
-    for (auto& ch : s->jit->chunks) {
+    const JitImage& J = *s->jit;
+    std::map<std::string, hipFunction_t> byname;
+    for (size_t i = 0; i < J.codes.size(); i++) {
+      hipModule_t m;
+      HIPCHK(hipModuleLoadData(&m, J.codes[i].data()));
+      d->mods.push_back(m);
       hipFunction_t f;
-      HIPCHK(hipModuleGetFunction(&f, d->mod, ch.name.c_str()));
+      HIPCHK(hipModuleGetFunction(&f, m, J.kernel_name[i].c_str()));
+      byname[J.kernel_name[i]] = f;
+    }
+    for (auto& ch : J.chunks) {
+      auto it = byname.find(ch.name);
+      if (it == byname.end()) throw std::runtime_error("specialized kernel " + ch.name + " missing");
+      hipFunction_t f = it->second;
       d->fns.push_back(f);
       if (getenv("KVGPU_VERBOSE")) {  // register / scratch use of each specialized kernel
         int regs = 0, local = 0;
@@ -211,10 +225,10 @@ DevPolicySet& dev_ps(kv_policyset* s, int device) {
                 ch.rules.empty() ? (size_t)(ch.rule_end - ch.rule_begin) : ch.rules.size(), regs, local);
       }
     }
-    if (s->jit->memo_words) {
-      HIPCHK(hipModuleGetFunction(&d->ptab_fn, d->mod, "kvj_ptab"));
-      d->memo_words = s->jit->memo_words;
-      d->ptab_rows = (uint32_t)((s->jit->memo_preds.size() + s->jit->ptab_row - 1) / s->jit->ptab_row);
+    if (J.memo_words) {
+      d->ptab_fn = byname.at("kvj_ptab");
+      d->memo_words = J.memo_words;
+      d->ptab_rows = (uint32_t)((J.memo_preds.size() + J.ptab_row - 1) / J.ptab_row);
     }
   }
   auto& ref = *d;
@@ -241,6 +255,9 @@ DevBatchRes& dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
   d->koff.upload(off, device);
   d->klen.upload(len, device);
   d->kstr.upload_raw(ks.data(), ks.size(), device);
+  d->nsms.upload(b.nsms, device);
+  d->lsets.upload(b.lsets, device);
+  d->asets.upload(b.asets, device);
   DevBatch& v = d->view;
   v.nodes = (const Node*)d->nodes.p;
   v.vals = (const Val*)d->vals.p;
@@ -251,6 +268,12 @@ DevBatchRes& dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
   v.key_off = (const uint32_t*)d->koff.p;
   v.key_len = (const uint32_t*)d->klen.p;
   v.kstr = (const uint8_t*)d->kstr.p;
+  v.nsms = (const StrRef*)d->nsms.p;
+  v.lsets = (const KVSet*)d->lsets.p;
+  v.asets = (const KVSet*)d->asets.p;
+  v.n_nsm = (uint32_t)b.nsms.size();
+  v.n_lsets = (uint32_t)b.lsets.size();
+  v.n_asets = (uint32_t)b.asets.size();
   v.ns_words = b.ns_words;
   v.n_res = (uint32_t)b.res.size();
   d->view_dev.upload_raw(&d->view, sizeof(DevBatch), device);
@@ -442,7 +465,9 @@ struct kv_session {
   int device = 0;
   uint32_t mode = 0;
   uint64_t nrules = 0, nres = 0;
-  DevBuf fflags, pview, st, er8, er, cn, scope, scn, ptab;
+  DevBuf fflags, pview, st, er8, er, cn, scope, scn, ptab, mtab;
+  uint32_t mt_words = 0, mt_entities = 0;
+  uint32_t *mt_ns = nullptr, *mt_ann = nullptr, *mt_sel = nullptr;
   uint32_t nscopes = 0, nvals = 0;
   DevOut O{};
   const DevBatch* bview = nullptr;
@@ -467,6 +492,24 @@ struct kv_session {
       ptab.alloc(std::max<size_t>((size_t)dp.memo_words * nvals, 1) * sizeof(uint32_t), device);
       P.ptab = (const uint32_t*)ptab.p;
       P.n_vals = nvals;
+    }
+    {  // match tables: one allocation, three [word][entity] tables
+      const PolicySet& pp = ps->ps;
+      const Batch& bb = bt->b;
+      P.mt_ns_words = (pp.n_nss_bits + 31) / 32;
+      P.mt_ann_words = (pp.n_ann_bits + 31) / 32;
+      P.mt_sel_words = (uint32_t)((pp.selectors.size() + 31) / 32);
+      const size_t n_ns = (size_t)P.mt_ns_words * bb.nsms.size(), n_an = (size_t)P.mt_ann_words * bb.asets.size(),
+                   n_sl = (size_t)P.mt_sel_words * bb.lsets.size();
+      mtab.alloc(std::max<size_t>(n_ns + n_an + n_sl, 1) * sizeof(uint32_t), device);
+      mt_ns = (uint32_t*)mtab.p;
+      mt_ann = mt_ns + n_ns;
+      mt_sel = mt_ann + n_an;
+      P.mt_ns = mt_ns;
+      P.mt_ann = mt_ann;
+      P.mt_sel = mt_sel;
+      mt_words = P.mt_ns_words + P.mt_ann_words + P.mt_sel_words;
+      mt_entities = (uint32_t)std::max({bb.nsms.size(), bb.asets.size(), bb.lsets.size()});
     }
     pview.upload_raw(&P, sizeof(DevPS), device);  // read through a uniform pointer (scalar loads)
     nrules = ps->ps.rules.size();
@@ -509,7 +552,8 @@ struct kv_session {
     HIPCHK(hipEventRecord(e0, stream));
     for (int i = 0; i < iters; i++) {
       HIPCHK(hipMemsetAsync(cn.p, 0, cn.n, stream));
-      if (dps->mod) launch_specialized();
+      HIPCHK(launch_mtab((const DevPS*)pview.p, bview, mt_words, mt_entities, mt_ns, mt_ann, mt_sel, stream));
+      if (dps->specialized()) launch_specialized();
       else HIPCHK(launch_validate((const DevPS*)pview.p, bview, (uint32_t)nres, O, 0, (uint32_t)nrules, stream));
       if (mode & KV_MODE_SCOPES) {
         HIPCHK(hipMemsetAsync(scn.p, 0, scn.n, stream));
@@ -618,10 +662,12 @@ int kv_compile(const char* policies_json, size_t len, uint32_t flags, kv_policys
           }
         }
         if (!getenv("KVGPU_JIT_SKIP_COMPILE")) jit_compile(s->jit.get());  // dump-only analysis runs
-        if (const char* dump = getenv("KVGPU_JIT_DUMP_CO")) {  // the gfx950 code object (llvm-objdump / readelf)
-          if (FILE* f = fopen(dump, "wb")) {
-            fwrite(s->jit->code.data(), 1, s->jit->code.size(), f);
-            fclose(f);
+        if (const char* dump = getenv("KVGPU_JIT_DUMP_CO")) {  // gfx950 code objects (llvm-objdump / readelf)
+          for (size_t i = 0; i < s->jit->codes.size(); i++) {
+            if (FILE* f = fopen((std::string(dump) + "." + s->jit->kernel_name[i] + ".co").c_str(), "wb")) {
+              fwrite(s->jit->codes[i].data(), 1, s->jit->codes[i].size(), f);
+              fclose(f);
+            }
           }
         }
       }
@@ -650,7 +696,7 @@ int kv_policyset_jit_info(const kv_policyset* ps, uint32_t* n_kernels, double* g
   if (n_kernels) *n_kernels = j ? (uint32_t)j->chunks.size() : 0;
   if (gen_ms) *gen_ms = j ? j->gen_ms : 0;
   if (compile_ms) *compile_ms = j ? j->compile_ms : 0;
-  if (code_bytes) *code_bytes = j ? j->code.size() : 0;
+  if (code_bytes) *code_bytes = j ? kvh::code_bytes(*j) : 0;
   return 0;
 }
 

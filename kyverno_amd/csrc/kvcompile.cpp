@@ -1103,6 +1103,7 @@ static void compile_filter(Compiler& C, const JDoc& d, int64_t fnode, int64_t rd
     ui.present = r || c || s;
   }
   bool rd_empty = true;
+  std::vector<uint32_t> name_atoms;
   if (rdnode >= 0 && d.at((uint32_t)rdnode).t == J_MAP) {
     uint32_t rn = (uint32_t)rdnode;
     std::vector<std::string> kinds, names, nss;
@@ -1147,22 +1148,27 @@ static void compile_filter(Compiler& C, const JDoc& d, int64_t fnode, int64_t rd
       }
       f.kinds_count = (uint32_t)kinds.size();
     }
+    // name globs are per resource (no interning): compiled word globs for the
+    // specialized kernels (filter_name_atoms), strings for the bytecode VM
     if (!name.empty()) {
       f.flags |= MF_NAME;
       f.name_off = ps.add_str(name);
       f.name_len = (uint32_t)name.size();
+      name_atoms.push_back(C.glob_atom(name));
     }
     if (!names.empty()) {
       f.flags |= MF_NAMES;
       f.names_first = (uint32_t)ps.strrefs.size();
       for (auto& n : names) ps.strrefs.push_back({ps.add_str(n), (uint32_t)n.size()});
       f.names_count = (uint32_t)names.size();
+      for (auto& n : names) name_atoms.push_back(C.glob_atom(n));
     }
     if (!nss.empty()) {
       f.flags |= MF_NSS;
       f.nss_first = (uint32_t)ps.strrefs.size();
       for (auto& n : nss) ps.strrefs.push_back({ps.add_str(n), (uint32_t)n.size()});
       f.nss_count = (uint32_t)nss.size();
+      f.nss_bit = ps.n_nss_bits++;
     }
     if (!ann.empty()) {
       f.flags |= MF_ANN;
@@ -1170,6 +1176,7 @@ static void compile_filter(Compiler& C, const JDoc& d, int64_t fnode, int64_t rd
       for (auto& kv : ann)
         ps.strpairs.push_back({ps.add_str(kv.first), (uint32_t)kv.first.size(), ps.add_str(kv.second), (uint32_t)kv.second.size()});
       f.ann_count = (uint32_t)ann.size();
+      f.ann_bit = ps.n_ann_bits++;
     }
     auto parse_sel = [&](uint32_t sn, SelectorHost* sh) {
       jstrmap(d, d.get(sn, "matchLabels"), &sh->matchLabels);
@@ -1250,6 +1257,7 @@ static void compile_filter(Compiler& C, const JDoc& d, int64_t fnode, int64_t rd
   }
   if (rd_empty) f.flags |= MF_EMPTY;  // refined with user info at launch time
   ps.filters.push_back(f);
+  ps.filter_name_atoms.push_back(name_atoms);
   rh.filter_ui.push_back(ui);
   rh.filter_is_match.push_back(is_match);
 }

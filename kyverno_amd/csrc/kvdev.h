@@ -14,6 +14,11 @@ namespace kv {
 hipError_t launch_validate(const DevPS* P, const DevBatch* B, uint32_t n_res, const DevOut& O, uint32_t rule_begin,
                            uint32_t rule_end, hipStream_t stream);
 
+// Match tables of a pass (DevPS::mt_*): `words` = mt_ns_words + mt_ann_words +
+// mt_sel_words rows, max_entities = max(n_nsm, n_asets, n_lsets).
+hipError_t launch_mtab(const DevPS* P, const DevBatch* B, uint32_t words, uint32_t max_entities, uint32_t* ns,
+                       uint32_t* an, uint32_t* sl, hipStream_t stream);
+
 constexpr uint32_t KV_SCOPE_CHUNK = 65536;  // resources per workgroup of the scope-count kernel
 constexpr uint32_t KV_SCOPE_LDS = 2048;     // scopes held in LDS (2048 x 8 x 4 B = 64 KB)
 

@@ -5,6 +5,18 @@
 
 #define KV_SENT 0xFFFFFFFFu
 
+// Linkage of the shared helpers: the bytecode VM (kvkernel.hip) keeps the
+// generic ones out of line; the specialized kernels' prelude (kvjit.cpp)
+// defines KV_JIT_PRELUDE so everything is inlined and the rule kernels make no
+// calls (calls under the 8-wave register bound spill caller-saved registers).
+#ifdef KV_JIT_PRELUDE
+#define KV_FN __device__ __forceinline__
+#define KV_GLOB_FN __device__ __forceinline__
+#else
+#define KV_FN __device__
+#define KV_GLOB_FN __device__ __noinline__
+#endif
+
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -18,7 +30,7 @@ __device__ __forceinline__ uint32_t rune_len(uint8_t c) {
 // minio/pkg v1.1.3 wildcard.Match over valid UTF-8: '*' any run of runes,
 // '?' exactly one rune; star backtracking advances by whole runes.
 // General path (non-ASCII value with '?' in the pattern, selector/label globs).
-__device__ __noinline__ bool kv_glob(const uint8_t* p, uint32_t pl, const uint8_t* s, uint32_t sl) {
+KV_GLOB_FN bool kv_glob(const uint8_t* p, uint32_t pl, const uint8_t* s, uint32_t sl) {
   if (pl == 0) return sl == 0;
   if (pl == 1 && p[0] == '*') return true;
   uint32_t si = 0, pi = 0, star = KV_SENT, mark = 0;
@@ -61,7 +73,7 @@ __device__ __forceinline__ bool seg_at(const GWord* __restrict__ wd, uint32_t le
 }
 
 // compiled glob over a 4-byte aligned value string (see kv_layout.h GlobFlags)
-__device__ bool glob_fast(const DevPS& P, const Atom& A, const uint8_t* s, uint32_t sl) {
+KV_FN bool glob_fast(const DevPS& P, const Atom& A, const uint8_t* s, uint32_t sl) {
   const uint32_t fl = uni(A.gflags);
   if (fl & G_ALL) return true;
   if (fl & G_EMPTY) return sl == 0;
@@ -134,7 +146,7 @@ __device__ __forceinline__ bool cmp_ok(uint32_t op, int r) {
 }
 
 // one atom of a string pattern against a scalar/absent node (type NT_NULL == Go nil)
-__device__ bool atom_eval(const DevPS& P, const DevBatch& B, uint32_t ai, uint32_t type, const Node& n) {
+KV_FN bool atom_eval(const DevPS& P, const DevBatch& B, uint32_t ai, uint32_t type, const Node& n) {
   const Atom& A = P.atoms[ai];
   const uint32_t kind = uni(A.kind);
   if (kind == AT_FALSE) return false;
@@ -165,7 +177,7 @@ __device__ bool atom_eval(const DevPS& P, const DevBatch& B, uint32_t ai, uint32
 
 // ValidateValueWithPattern(value, pattern) for a scalar-pattern leaf; n = the
 // value node (ignored when type == NT_NULL, which also stands for absent)
-__device__ bool pred_eval(const DevPS& P, const DevBatch& B, uint32_t pi, uint32_t type, const Node& n) {
+KV_FN bool pred_eval(const DevPS& P, const DevBatch& B, uint32_t pi, uint32_t type, const Node& n) {
   const Pred& pr = P.preds[pi];
   const uint32_t kind = uni(pr.kind);
   switch (kind) {
@@ -234,7 +246,7 @@ __device__ __forceinline__ uint32_t lookup_op(const Node* __restrict__ N, uint32
 }
 
 // Resolved result key of sibling spec entry (OP_KEYGLOB): returns key id and node.
-__device__ void kg_resolve(const DevPS& P, const DevBatch& B, const Node* __restrict__ N, uint32_t m, uint32_t w,
+KV_FN void kg_resolve(const DevPS& P, const DevBatch& B, const Node* __restrict__ N, uint32_t m, uint32_t w,
                            uint32_t ref, uint32_t* key, uint32_t* node) {
   if (!w) {  // literal sibling: key id is the key
     *key = ref;
@@ -287,13 +299,15 @@ __device__ __forceinline__ bool keyglob_op(const DevPS& P, const DevBatch& B, co
 }
 
 // ------------------------------------------------------------------ match/exclude
-__device__ bool selector_match(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t si) {
+// LabelSelectorAsSelector(ReplaceInSelector(selector, labels)).Matches(labels)
+// (pkg/engine/utils.go:99-107, pkg/engine/wildcards/wildcards.go:13-63) on one
+// label list; `si` must be uniform across the wave (selector fields via uni()).
+KV_FN bool selector_match(const DevPS& P, const DevBatch& B, const KV* __restrict__ labels, uint32_t nl,
+                               uint32_t si) {
   const Selector& S = P.sels[si];
   const uint32_t fl = uni(S.flags);
   if (fl & SF_STATIC_INVALID) return false;
   if (fl & SF_EVERYTHING) return true;
-  const KV* labels = B.kvs + R->labels_first;
-  const uint32_t nl = R->labels_count;
   const uint32_t mf = uni(S.ml_first), mc = uni(S.ml_count);
   auto resolve = [&](const SelLabel& E, const uint8_t** ok, uint32_t* okl, const uint8_t** ov, uint32_t* ovl,
                      bool* val) {
@@ -361,9 +375,80 @@ __device__ bool selector_match(const DevPS& P, const DevBatch& B, const Res* __r
   return true;
 }
 
+// checkAnnotations (pkg/engine/utils.go:77-97): every pattern pair is matched
+// (key and value globs) by some annotation of the list
+KV_FN bool annotations_match(const DevPS& P, const DevBatch& B, const KV* __restrict__ ann, uint32_t na,
+                                  uint32_t first, uint32_t count) {
+  for (uint32_t k = first; k < first + count; k++) {
+    const StrPair sp = P.strpairs[k];
+    bool m = false;
+    for (uint32_t q = 0; q < na && !m; q++) {
+      const KV kv = ann[q];
+      m = kv_glob(P.pstr + sp.k_off, sp.k_len, B.bstr + kv.k_off, kv.k_len & KV_LEN_MASK) &&
+          kv_glob(P.pstr + sp.v_off, sp.v_len, B.bstr + kv.v_off, kv.v_len & KV_LEN_MASK);
+    }
+    if (!m) return false;
+  }
+  return true;
+}
+
+// checkNameSpace (pkg/engine/utils.go:62-75): some namespace glob matches
+KV_FN bool namespaces_match(const DevPS& P, const uint8_t* __restrict__ s, uint32_t sl, uint32_t first,
+                                 uint32_t count) {
+  for (uint32_t k = first; k < first + count; k++)
+    if (kv_glob(P.pstr + P.strrefs[k].off, P.strrefs[k].len, s, sl)) return true;
+  return false;
+}
+
+// bit `bit` of a match table [word][n_entities] for entity e
+__device__ __forceinline__ bool mt_bit(const uint32_t* __restrict__ t, uint32_t bit, uint32_t n_entities, uint32_t e) {
+  return (t[(size_t)(bit >> 5) * n_entities + e] >> (bit & 31u)) & 1u;
+}
+
+// One word of the match tables (kv_mtab grid: y = table word, uniform per
+// workgroup, so the 32 criteria of the word are uniform across the wave; x =
+// entity). Rows y enumerate the namespace words, then the annotation words, then
+// the selector words.
+KV_FN void mtab_word(const DevPS& P, const DevBatch& B, uint32_t y, uint32_t e, uint32_t* __restrict__ ns,
+                          uint32_t* __restrict__ an, uint32_t* __restrict__ sl) {
+  uint32_t w = 0;
+  if (y < P.mt_ns_words) {
+    if (e >= B.n_nsm) return;
+    const StrRef s = B.nsms[e];
+    for (uint32_t f = 0; f < P.n_filters; f++) {  // filters whose nss_bit falls in this word
+      const MFilter& F = P.filters[f];
+      if (!(uni(F.flags) & MF_NSS) || (uni(F.nss_bit) >> 5) != y) continue;
+      if (namespaces_match(P, B.bstr + s.off, s.len, uni(F.nss_first), uni(F.nss_count))) w |= 1u << (F.nss_bit & 31u);
+    }
+    ns[(size_t)y * B.n_nsm + e] = w;
+    return;
+  }
+  y -= P.mt_ns_words;
+  if (y < P.mt_ann_words) {
+    if (e >= B.n_asets) return;
+    const KVSet a = B.asets[e];
+    for (uint32_t f = 0; f < P.n_filters; f++) {
+      const MFilter& F = P.filters[f];
+      if (!(uni(F.flags) & MF_ANN) || (uni(F.ann_bit) >> 5) != y) continue;
+      if (annotations_match(P, B, B.kvs + a.first, a.count, uni(F.ann_first), uni(F.ann_count)))
+        w |= 1u << (F.ann_bit & 31u);
+    }
+    an[(size_t)y * B.n_asets + e] = w;
+    return;
+  }
+  y -= P.mt_ann_words;
+  if (e >= B.n_lsets) return;
+  const KVSet l = B.lsets[e];
+  const uint32_t s1 = P.n_sels < (y + 1) * 32u ? P.n_sels : (y + 1) * 32u;
+  for (uint32_t si = y * 32u; si < s1; si++)
+    if (selector_match(P, B, B.kvs + l.first, l.count, si)) w |= 1u << (si & 31u);
+  sl[(size_t)y * B.n_lsets + e] = w;
+}
+
 // doesResourceMatchConditionBlock: number of failed criteria (0 == block matches)
-// (criteria restricted to the flag bits in `mask`)
-__device__ uint32_t block_errs_masked(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t rkind,
+// (criteria restricted to the flag bits in `mask`). Namespace globs, annotations
+// and label selectors are bits of the pass's match tables.
+KV_FN uint32_t block_errs_masked(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t rkind,
                                       uint32_t rflags, uint32_t f, uint32_t mask) {
   const MFilter& F = P.filters[f];
   const uint32_t fl = uni(P.fflags[f]) & mask;
@@ -390,27 +475,9 @@ __device__ uint32_t block_errs_masked(const DevPS& P, const DevBatch& B, const R
       any = kv_glob(P.pstr + P.strrefs[k].off, P.strrefs[k].len, B.bstr + R->name_off, R->name_len);
     errs += any ? 0 : 1;
   }
-  if (fl & MF_NSS) {
-    bool any = false;
-    for (uint32_t k = F.nss_first; k < F.nss_first + F.nss_count && !any; k++)
-      any = kv_glob(P.pstr + P.strrefs[k].off, P.strrefs[k].len, B.bstr + R->ns_off, R->ns_len);
-    errs += any ? 0 : 1;
-  }
-  if (fl & MF_ANN) {
-    bool all = true;
-    for (uint32_t k = F.ann_first; k < F.ann_first + F.ann_count && all; k++) {
-      const StrPair sp = P.strpairs[k];
-      bool m = false;
-      for (uint32_t q = 0; q < R->annot_count && !m; q++) {
-        const KV kv = B.kvs[R->annot_first + q];
-        m = kv_glob(P.pstr + sp.k_off, sp.k_len, B.bstr + kv.k_off, kv.k_len & KV_LEN_MASK) &&
-            kv_glob(P.pstr + sp.v_off, sp.v_len, B.bstr + kv.v_off, kv.v_len & KV_LEN_MASK);
-      }
-      all = m;
-    }
-    errs += all ? 0 : 1;
-  }
-  if (fl & MF_SEL) errs += selector_match(P, B, R, F.sel) ? 0 : 1;
+  if (fl & MF_NSS) errs += mt_bit(P.mt_ns, uni(F.nss_bit), B.n_nsm, R->nsm) ? 0 : 1;
+  if (fl & MF_ANN) errs += mt_bit(P.mt_ann, uni(F.ann_bit), B.n_asets, R->aset) ? 0 : 1;
+  if (fl & MF_SEL) errs += mt_bit(P.mt_sel, uni(F.sel), B.n_lsets, R->lset) ? 0 : 1;
   if ((fl & MF_NSSEL) && !(rflags & (RF_KIND_NAMESPACE | RF_KIND_EMPTY))) {
     const uint32_t bit = F.nssel_bit;
     errs += (B.ns_bits[R->ns_index * B.ns_words + bit / 32] >> (bit % 32)) & 1 ? 0 : 1;
@@ -424,7 +491,7 @@ __device__ __forceinline__ uint32_t block_errs(const DevPS& P, const DevBatch& B
   return block_errs_masked(P, B, R, rkind, rflags, f, 0xFFFFFFFFu);
 }
 
-__device__ bool rule_matches(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t rkind,
+KV_FN bool rule_matches(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t rkind,
                              uint32_t rflags, const RuleRec& rr) {
   const uint32_t mm = uni(rr.m_mode), mf = uni(rr.m_first), mc = uni(rr.m_count);
   bool ok;

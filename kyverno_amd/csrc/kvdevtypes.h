@@ -45,12 +45,21 @@ struct DevPS {
   const uint8_t* pstr;
   uint32_t star_id;
   uint32_t n_rules;
+  uint32_t n_filters, n_sels;
   // value-predicate table of the specialized kernels (per launch configuration):
   // ptab[word * n_vals + val] bit b = leaf predicate of memo slot 32*word+b on
   // the scalar Val `val` (built each pass by kvj_ptab before the rule kernels)
   const uint32_t* ptab;
   uint32_t n_vals;
-  uint32_t pad_;
+  // match tables (per launch configuration, built each pass by kv_mtab before the rule
+  // kernels): bit b of word w at [w * n_entities + e] = filter criterion b on entity e
+  //   mt_ns  [nss_bit]  namespace globs   x distinct checkNameSpace strings (DevBatch::nsms)
+  //   mt_ann [ann_bit]  annotation globs  x distinct annotation lists       (DevBatch::asets)
+  //   mt_sel [sel]      label selectors   x distinct label lists            (DevBatch::lsets)
+  uint32_t mt_ns_words, mt_ann_words, mt_sel_words;
+  const uint32_t* mt_ns;
+  const uint32_t* mt_ann;
+  const uint32_t* mt_sel;
 };
 
 struct DevBatch {
@@ -63,6 +72,10 @@ struct DevBatch {
   const uint32_t* key_off;
   const uint32_t* key_len;
   const uint8_t* kstr;
+  const StrRef* nsms;   // distinct checkNameSpace strings (bstr offsets)
+  const KVSet* lsets;   // distinct label lists
+  const KVSet* asets;   // distinct annotation lists
+  uint32_t n_nsm, n_lsets, n_asets;
   uint32_t ns_words;
   uint32_t n_res;
 };

@@ -319,15 +319,30 @@ struct Ingest {
     return false;
   }
 
-  void kvs(const JDoc& d, int64_t mapnode, uint32_t* first, uint32_t* count, bool labels) {
-    *first = (uint32_t)b.kvs.size();
-    *count = 0;
-    if (mapnode < 0) return;
-    const JNode& m = d.at((uint32_t)mapnode);
-    if (!is_str_map(d, m)) return;  // NestedStringMap error -> nil map
+  // Interned label / annotation list of a resource: identical lists (same pairs, same
+  // validity bits) share one KVSet, so the match tables evaluate a selector or an
+  // annotation filter once per distinct list.
+  std::unordered_map<std::string, uint32_t> lset_id, aset_id, nsm_id;
+  uint32_t kvset(const JDoc& d, int64_t mapnode, bool labels) {
     std::vector<std::pair<std::string_view, std::string_view>> pairs;
-    for (uint32_t c = m.first; c < m.first + m.count; c++) pairs.push_back({d.key(d.at(c)), d.sval(d.at(c))});
+    if (mapnode >= 0) {
+      const JNode& m = d.at((uint32_t)mapnode);
+      if (is_str_map(d, m))  // else NestedStringMap error -> nil map
+        for (uint32_t c = m.first; c < m.first + m.count; c++) pairs.push_back({d.key(d.at(c)), d.sval(d.at(c))});
+    }
     std::sort(pairs.begin(), pairs.end());
+    std::string key;
+    for (auto& p : pairs) {
+      key.append(p.first.data(), p.first.size());
+      key.push_back('\0');
+      key.append(p.second.data(), p.second.size());
+      key.push_back('\0');
+    }
+    auto& ids = labels ? lset_id : aset_id;
+    auto& sets = labels ? b.lsets : b.asets;
+    auto it = ids.find(key);
+    if (it != ids.end()) return it->second;
+    KVSet set{(uint32_t)b.kvs.size(), (uint32_t)pairs.size()};
     for (auto& p : pairs) {
       KV kv{};
       kv.k_off = str(p.first);
@@ -340,7 +355,22 @@ struct Ingest {
       }
       b.kvs.push_back(kv);
     }
-    *count = (uint32_t)pairs.size();
+    const uint32_t id = (uint32_t)sets.size();
+    sets.push_back(set);
+    (labels ? b.lset_keys : b.aset_keys).push_back(key);
+    ids.emplace(std::move(key), id);
+    return id;
+  }
+
+  uint32_t nsm(std::string_view s) {
+    std::string k(s);
+    auto it = nsm_id.find(k);
+    if (it != nsm_id.end()) return it->second;
+    const uint32_t id = (uint32_t)b.nsms.size();
+    b.nsms.push_back(StrRef{str(s), (uint32_t)s.size()});
+    b.nsm_keys.push_back(k);
+    nsm_id.emplace(std::move(k), id);
+    return id;
   }
 
   void add(const JDoc& d) {  // per-resource header (match/exclude inputs)
@@ -373,14 +403,13 @@ struct Ingest {
     r.version = ps.lookup(ver);
     r.name_off = str(name);
     r.name_len = (uint32_t)name.size();
+    if (utf8_ascii(std::string(name))) r.flags |= RF_NAME_ASCII;
     bool isns = kind == "Namespace";
-    std::string_view nsm = isns ? name : ns;
-    r.ns_off = str(nsm);
-    r.ns_len = (uint32_t)nsm.size();
+    r.nsm = nsm(isns ? name : ns);
     if (isns) r.flags |= RF_KIND_NAMESPACE;
     if (kind.empty()) r.flags |= RF_KIND_EMPTY;
-    kvs(d, labels, &r.labels_first, &r.labels_count, true);
-    kvs(d, ann, &r.annot_first, &r.annot_count, false);
+    r.lset = kvset(d, labels, true);
+    r.aset = kvset(d, ann, false);
     std::string nss(ns);
     auto it = ns_index.find(nss);
     if (it == ns_index.end()) {
@@ -534,8 +563,8 @@ void order_vals(Batch& b) {
 
 void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
   const size_t P = parts.size();
-  std::unordered_map<std::string, uint32_t> dyn, nsi;
-  std::vector<std::vector<uint32_t>> dmap(P), nmap(P);
+  std::unordered_map<std::string, uint32_t> dyn, nsi, gnsm, glset, gaset;
+  std::vector<std::vector<uint32_t>> dmap(P), nmap(P), nsmmap(P), lmap(P), amap(P);
   std::vector<uint64_t> hb(P), vb(P), kb(P), rb(P), nb(P), resb(P);
   uint64_t H = 0, V = 0, K = 0, R = 0, N = 0, RS = 0;
   for (size_t k = 0; k < P; k++) {  // offsets and id remaps (serial, small)
@@ -558,6 +587,31 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
         b.namespaces.push_back(s);
       }
       nmap[k].push_back(it->second);
+    }
+    // interned match inputs: first occurrence (in part order) is kept, offsets rebased
+    for (size_t i = 0; i < q.nsm_keys.size(); i++) {
+      auto it = gnsm.find(q.nsm_keys[i]);
+      if (it == gnsm.end()) {
+        it = gnsm.emplace(q.nsm_keys[i], (uint32_t)b.nsms.size()).first;
+        b.nsms.push_back(StrRef{q.nsms[i].off + (uint32_t)hb[k], q.nsms[i].len});
+      }
+      nsmmap[k].push_back(it->second);
+    }
+    for (size_t i = 0; i < q.lset_keys.size(); i++) {
+      auto it = glset.find(q.lset_keys[i]);
+      if (it == glset.end()) {
+        it = glset.emplace(q.lset_keys[i], (uint32_t)b.lsets.size()).first;
+        b.lsets.push_back(KVSet{q.lsets[i].first + (uint32_t)kb[k], q.lsets[i].count});
+      }
+      lmap[k].push_back(it->second);
+    }
+    for (size_t i = 0; i < q.aset_keys.size(); i++) {
+      auto it = gaset.find(q.aset_keys[i]);
+      if (it == gaset.end()) {
+        it = gaset.emplace(q.aset_keys[i], (uint32_t)b.asets.size()).first;
+        b.asets.push_back(KVSet{q.asets[i].first + (uint32_t)kb[k], q.asets[i].count});
+      }
+      amap[k].push_back(it->second);
     }
     b.cells_used += q.cells_used;
   }
@@ -609,9 +663,9 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
         Res r = q.res[i];
         r.root += r0;
         r.name_off += h;
-        r.ns_off += h;
-        r.labels_first += k0;
-        r.annot_first += k0;
+        r.nsm = nsmmap[k][r.nsm];
+        r.lset = lmap[k][r.lset];
+        r.aset = amap[k][r.aset];
         r.ns_index = nmap[k][r.ns_index];
         b.res[resb[k] + i] = r;
       }
@@ -704,9 +758,14 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
       if (selector_eval_host(ps.nsselectors[s], b->ns_labels[n]) == 1) b->ns_bits[n * b->ns_words + s / 32] |= 1u << (s % 32);
   // word-granular readers may touch up to 8 bytes past the last string
   b->strs.append(16, '\0');
+  // interning keys are only needed while ingesting
+  std::vector<std::string>().swap(b->nsm_keys);
+  std::vector<std::string>().swap(b->lset_keys);
+  std::vector<std::string>().swap(b->aset_keys);
   // algorithmic bytes: populated cells only (row padding of the wave-group layout excluded)
   b->bytes_referenced = b->cells_used * sizeof(Node) + b->vals.size() * sizeof(Val) + b->res.size() * sizeof(Res) +
-                        b->kvs.size() * sizeof(KV) + b->strs.size();
+                        b->kvs.size() * sizeof(KV) + b->strs.size() + b->nsms.size() * sizeof(StrRef) +
+                        (b->lsets.size() + b->asets.size()) * sizeof(KVSet);
 }
 
 }  // namespace kvh

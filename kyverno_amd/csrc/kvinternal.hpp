@@ -145,6 +145,9 @@ struct PolicySet {
   std::vector<kv::SelLabel> sellabels;
   std::vector<kv::SelExpr> selexprs;
   std::vector<SelectorHost> nsselectors;  // bit i of the namespace table
+  uint32_t n_nss_bits = 0, n_ann_bits = 0;  // rows of the namespace-glob / annotation match tables
+  // per filter: compiled glob atoms of `name` (first, if MF_NAME) then `names` (specialized kernels)
+  std::vector<std::vector<uint32_t>> filter_name_atoms;
   std::vector<PNodeInfo> pnodes;
   Trie trie;
   std::vector<std::tuple<uint32_t, uint32_t, std::string>> slot_fix;  // (pc, trie node, key)
@@ -167,6 +170,10 @@ struct Batch {
   std::string strs;                  // string heap
   std::vector<std::string> dyn_keys; // key ids >= ps.keys.size()
   std::vector<std::string> namespaces;
+  std::vector<kv::StrRef> nsms;      // distinct checkNameSpace strings (Res::nsm)
+  std::vector<kv::KVSet> lsets;      // distinct label lists (Res::lset)
+  std::vector<kv::KVSet> asets;      // distinct annotation lists (Res::aset)
+  std::vector<std::string> nsm_keys, lset_keys, aset_keys;  // interning keys (ingest only)
   std::vector<std::vector<std::pair<std::string, std::string>>> ns_labels;
   std::vector<uint32_t> ns_bits;     // [n_ns][ceil(n_nssel/32)]
   uint32_t ns_words = 1;

@@ -12,6 +12,10 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -20,6 +24,7 @@
 #include <set>
 #include <sstream>
 #include <stdexcept>
+#include <thread>
 
 #include "kvjit.hpp"
 
@@ -102,6 +107,11 @@ struct Gen {
     return e.str();
   }
 
+  std::set<uint32_t> globs_done;
+  void glob_once(uint32_t ai) {
+    if (globs_done.insert(ai).second) glob_fn(ai);
+  }
+
   void glob_fn(uint32_t ai) {
     const Atom& A = ps.atoms[ai];
     o << "__device__ __forceinline__ bool g_glob_" << ai
@@ -178,7 +188,7 @@ struct Gen {
   void atom_fn(uint32_t ai) {
     if (!atoms_done.insert(ai).second) return;
     const Atom& A = ps.atoms[ai];
-    if (A.kind == AT_GLOB_E || A.kind == AT_GLOB_N) glob_fn(ai);
+    if (A.kind == AT_GLOB_E || A.kind == AT_GLOB_N) glob_once(ai);
     o << "__device__ __forceinline__ bool g_atom_" << ai
       << "(const Val* __restrict__ V, const uint8_t* __restrict__ S, const uint8_t* __restrict__ E, "
          "const uint8_t* __restrict__ pstr, uint32_t type, const Node& n) {\n";
@@ -339,7 +349,22 @@ struct Gen {
   // instruction cache — 32-predicate rows stalled on instruction fetch.
   // KVGPU_PTAB_ROW=32: one row per table word (A/B runs)
   const uint32_t kPtabRow = getenv("KVGPU_PTAB_ROW") && atoi(getenv("KVGPU_PTAB_ROW")) == 32 ? 32u : 16u;
+  // kernel texts (name, source): each one is compiled as its own hiprtc program
+  // after the helpers every kernel may use (Gen::o, the common part)
+  std::vector<std::pair<std::string, std::string>> kernels;
+  struct KernelText {  // redirects Gen::o into a kernel's own text for its lifetime
+    Gen& g;
+    std::string name;
+    std::ostringstream saved;
+    KernelText(Gen& gg, std::string n) : g(gg), name(std::move(n)) { std::swap(g.o, saved); }
+    ~KernelText() {
+      std::swap(g.o, saved);
+      g.kernels.push_back({name, saved.str()});
+    }
+  };
+
   void ptab_kernel() {
+    KernelText kt(*this, "kvj_ptab");
     o << "extern \"C\" __global__ __launch_bounds__(KV_WG) void kvj_ptab(const DevPS* __restrict__ Pp, "
          "const Val* __restrict__ V, const uint8_t* __restrict__ S, uint32_t NV, uint32_t* __restrict__ PT) {\n"
       << "  const uint32_t v = blockIdx.x * KV_WG + threadIdx.x;\n"
@@ -403,6 +428,7 @@ struct Gen {
   void blk_fn(uint32_t f) {
     if (!blks_done.insert(f).second) return;
     const MFilter& F = ps.filters[f];
+    for (uint32_t a : ps.filter_name_atoms.at(f)) glob_once(a);  // before this function's text
     o << "__device__ __forceinline__ bool g_blk_" << f
       << "(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t rkind, uint32_t rflags) {\n"
       << "  if (uni(P.fflags[" << f << "]) & (MF_EMPTY | MF_UI_FAIL)) return false;\n";
@@ -424,20 +450,22 @@ struct Gen {
       }
       if (!any_star) o << "  if (!(" << k.str() << ")) return false;\n";
     }
-    auto glob_any = [&](uint32_t first, uint32_t count, const char* off, const char* len) {
-      o << "  if (!(false";
-      for (uint32_t i = first; i < first + count; i++)
-        o << " || kv_glob(P.pstr + " << u32(ps.strrefs[i].off) << ", " << u32(ps.strrefs[i].len) << ", B.bstr + R->" << off
-          << ", R->" << len << ")";
-      o << ")) return false;\n";
+    // name / names: compiled word globs over the resource name (no calls)
+    const std::vector<uint32_t>& na = ps.filter_name_atoms.at(f);
+    auto name_glob = [&](uint32_t a) {
+      return "g_glob_" + std::to_string(a) + "(B.bstr + R->name_off, R->name_len, (rflags & RF_NAME_ASCII) != 0u, P.pstr)";
     };
-    if (F.flags & MF_NAME)
-      o << "  if (!kv_glob(P.pstr + " << u32(F.name_off) << ", " << u32(F.name_len)
-        << ", B.bstr + R->name_off, R->name_len)) return false;\n";
-    if (F.flags & MF_NAMES) glob_any(F.names_first, F.names_count, "name_off", "name_len");
-    if (F.flags & MF_NSS) glob_any(F.nss_first, F.nss_count, "ns_off", "ns_len");
-    if (F.flags & (MF_ANN | MF_SEL))  // rarer criteria: the generic evaluator, restricted to them
-      o << "  if (block_errs_masked(P, B, R, rkind, rflags, " << f << "u, MF_ANN | MF_SEL) != 0u) return false;\n";
+    size_t k = 0;
+    if (F.flags & MF_NAME) o << "  if (!" << name_glob(na.at(k++)) << ") return false;\n";
+    if (F.flags & MF_NAMES) {
+      o << "  if (!(false";
+      for (; k < na.size(); k++) o << " || " << name_glob(na[k]);
+      o << ")) return false;\n";
+    }
+    // namespace globs, annotations, label selectors: bits of the pass's match tables (kv_mtab)
+    if (F.flags & MF_NSS) o << "  if (!mt_bit(P.mt_ns, " << u32(F.nss_bit) << ", B.n_nsm, R->nsm)) return false;\n";
+    if (F.flags & MF_ANN) o << "  if (!mt_bit(P.mt_ann, " << u32(F.ann_bit) << ", B.n_asets, R->aset)) return false;\n";
+    if (F.flags & MF_SEL) o << "  if (!mt_bit(P.mt_sel, " << u32(F.sel) << ", B.n_lsets, R->lset)) return false;\n";
     if (F.flags & MF_NSSEL)
       o << "  if (!(rflags & (RF_KIND_NAMESPACE | RF_KIND_EMPTY)) && !((B.ns_bits[R->ns_index * B.ns_words + "
         << (F.nssel_bit / 32) << "u] >> " << (F.nssel_bit % 32) << "u) & 1u)) return false;\n";
@@ -612,6 +640,7 @@ struct Gen {
   }
 
   void chunk_kernel(const JitChunk& ch) {
+    KernelText kt(*this, ch.name);
     const uint32_t nr = ch.rule_end - ch.rule_begin;
     o << "extern \"C\" __global__ __launch_bounds__(KV_WG) void " << ch.name
       << "(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp, const Node* __restrict__ N, "
@@ -1157,6 +1186,7 @@ struct Gen {
       rules.insert(rules.end(), c->rules.begin(), c->rules.end());
     }
     const uint32_t nr = (uint32_t)rules.size();
+    KernelText kt(*this, name);
     o << "__device__ const uint32_t " << name << "_rules[" << nr << "] = {";
     for (uint32_t q = 0; q < nr; q++) o << (q ? ", " : "") << u32(rules[q]);
     o << "};\n";
@@ -1307,30 +1337,131 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
     out->memo_words = (uint32_t)((g.mpreds.size() + 31) / 32);
     out->ptab_row = g.kPtabRow;
   }
-  out->source = g.o.str();
+  out->common = g.o.str();
+  out->kernel_name.clear();
+  out->kernel_src.clear();
+  out->source = out->common;
+  for (auto& k : g.kernels) {
+    out->kernel_name.push_back(k.first);
+    out->kernel_src.push_back(k.second);
+    out->source += k.second;
+  }
   out->gen_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
-void jit_compile(JitImage* img) {
-  auto t0 = std::chrono::steady_clock::now();
+namespace {
+
+uint64_t fnv1a64(const std::string& a, uint64_t h = 1469598103934665603ull) {
+  for (unsigned char c : a) h = (h ^ c) * 1099511628211ull;
+  return h;
+}
+
+std::string cache_dir() {
+  const char* e = getenv("KVGPU_JIT_CACHE");
+  if (e && std::string(e) == "0") return "";
+  if (e && *e) return e;
+  if (const char* x = getenv("XDG_CACHE_HOME"); x && *x) return std::string(x) + "/kvgpu";
+  if (const char* h = getenv("HOME"); h && *h) return std::string(h) + "/.cache/kvgpu";
+  return "";
+}
+
+bool read_file(const std::string& path, std::vector<char>* out) {
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) return false;
+  fseek(f, 0, SEEK_END);
+  long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  out->resize(n > 0 ? (size_t)n : 0);
+  const bool ok = n > 0 && fread(out->data(), 1, (size_t)n, f) == (size_t)n;
+  fclose(f);
+  return ok;
+}
+
+void write_file_atomic(const std::string& dir, const std::string& path, const std::vector<char>& data) {
+  std::string cmd = dir;  // create the directory (one level under an existing parent is enough here)
+  for (size_t i = 1; i <= cmd.size(); i++)
+    if (i == cmd.size() || cmd[i] == '/') mkdir(cmd.substr(0, i).c_str(), 0755);
+  const std::string tmp = path + ".tmp." + std::to_string((unsigned long long)getpid()) + "." +
+                          std::to_string(std::hash<std::thread::id>()(std::this_thread::get_id()));
+  FILE* f = fopen(tmp.c_str(), "wb");
+  if (!f) return;
+  const bool ok = fwrite(data.data(), 1, data.size(), f) == data.size();
+  fclose(f);
+  if (!ok || rename(tmp.c_str(), path.c_str()) != 0) unlink(tmp.c_str());
+}
+
+const char* const kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-unused-label", "-Wno-unused-variable"};
+
+std::vector<char> compile_one(const std::string& src, const std::string& name) {
   hiprtcProgram prog;
-  if (hiprtcCreateProgram(&prog, img->source.c_str(), "kvjit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+  if (hiprtcCreateProgram(&prog, src.c_str(), (name + ".hip").c_str(), 0, nullptr, nullptr) != HIPRTC_SUCCESS)
     throw std::runtime_error("hiprtcCreateProgram failed");
-  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-unused-label", "-Wno-unused-variable"};
-  hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof opts[0]), opts);
+  hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof kOpts / sizeof kOpts[0]), kOpts);
   if (rc != HIPRTC_SUCCESS) {
     size_t ls = 0;
     hiprtcGetProgramLogSize(prog, &ls);
     std::string log(ls, '\0');
     if (ls) hiprtcGetProgramLog(prog, &log[0]);
     hiprtcDestroyProgram(&prog);
-    throw std::runtime_error("hiprtc compile failed: " + log.substr(0, 4000));
+    throw std::runtime_error("hiprtc compile of " + name + " failed: " + log.substr(0, 4000));
   }
   size_t cs = 0;
   hiprtcGetCodeSize(prog, &cs);
-  img->code.resize(cs);
-  hiprtcGetCode(prog, img->code.data());
+  std::vector<char> code(cs);
+  hiprtcGetCode(prog, code.data());
   hiprtcDestroyProgram(&prog);
+  return code;
+}
+
+}  // namespace
+
+uint64_t code_bytes(const JitImage& img) {
+  uint64_t n = 0;
+  for (auto& c : img.codes) n += c.size();
+  return n;
+}
+
+void jit_compile(JitImage* img) {
+  auto t0 = std::chrono::steady_clock::now();
+  const size_t K = img->kernel_src.size();
+  img->codes.assign(K, {});
+  img->cache_hits = 0;
+  const std::string dir = cache_dir();
+  std::string opt_key;
+  for (const char* o : kOpts) opt_key += std::string(o) + "\n";
+  int hv = 0;
+  (void)hiprtcVersion(&hv, &hv);
+  opt_key += "hiprtc " + std::to_string(hv) + "\n";
+  const uint64_t hcommon = fnv1a64(img->common, fnv1a64(opt_key));
+  unsigned T = std::thread::hardware_concurrency();
+  if (const char* e = getenv("KVGPU_JIT_THREADS")) T = (unsigned)std::max(1, atoi(e));
+  T = std::max(1u, std::min<unsigned>(T, (unsigned)K));
+  std::atomic<size_t> next{0};
+  std::atomic<uint32_t> hits{0};
+  std::vector<std::string> errs(T);
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < T; t++)
+    th.emplace_back([&, t]() {
+      try {
+        for (size_t i; (i = next++) < K;) {
+          char key[40];
+          snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a64(img->kernel_src[i], hcommon));
+          const std::string path = dir.empty() ? "" : dir + "/" + img->kernel_name[i] + "-" + key + ".co";
+          if (!path.empty() && read_file(path, &img->codes[i])) {
+            hits++;
+            continue;
+          }
+          img->codes[i] = compile_one(img->common + img->kernel_src[i], img->kernel_name[i]);
+          if (!path.empty()) write_file_atomic(dir, path, img->codes[i]);
+        }
+      } catch (const std::exception& e) {
+        errs[t] = e.what();
+      }
+    });
+  for (auto& x : th) x.join();
+  for (auto& e : errs)
+    if (!e.empty()) throw std::runtime_error(e);
+  img->cache_hits = hits;
   img->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 

@@ -19,9 +19,12 @@ struct JitChunk {
 };
 
 struct JitImage {
-  std::string source;       // generated HIP source (kept for diagnostics)
+  std::string source;       // generated HIP source, all of it (diagnostics, tools/kvemu)
+  std::string common;       // prelude + helper functions shared by the kernels
+  std::vector<std::string> kernel_name, kernel_src;  // one hiprtc program per kernel: common + kernel_src[i]
+  std::vector<std::vector<char>> codes;              // gfx950 code object per kernel program
+  uint32_t cache_hits = 0;  // programs loaded from the code-object cache
   std::vector<JitChunk> chunks;
-  std::vector<char> code;   // gfx950 code object
   // leaf predicates memoized per distinct scalar value: slot k = memo_preds[k];
   // kernel "kvj_ptab" fills DevPS::ptab (memo_words words per value)
   std::vector<uint32_t> memo_preds;
@@ -33,7 +36,12 @@ struct JitImage {
 // Generate the specialized source for every rule of `ps` (chunks of at most
 // `chunk_rules` rules per kernel).
 void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out);
-// Compile out->source with hiprtc for gfx950; throws std::runtime_error with the log on failure.
+// Compile every kernel program with hiprtc for gfx950, on parallel host threads
+// (KVGPU_JIT_THREADS, default: hardware threads), through the code-object cache
+// (KVGPU_JIT_CACHE directory, default $XDG_CACHE_HOME/kvgpu or ~/.cache/kvgpu;
+// "0" disables; entries keyed by a hash of compiler options + program text).
+// Throws std::runtime_error with the log on failure.
 void jit_compile(JitImage* img);
+uint64_t code_bytes(const JitImage& img);
 
 }  // namespace kvh

@@ -330,6 +330,28 @@ hipError_t launch_validate(const DevPS* P, const DevBatch* B, uint32_t n_res, co
 }  // namespace kv
 
 // ---------------------------------------------------------------------------
+// Match tables of one pass (both engines): every namespace glob set, annotation
+// filter and label selector of the policy set, once per distinct input of the
+// batch (DevPS::mt_*). grid.y = table word, grid.x = entities.
+namespace kv {
+
+__global__ __launch_bounds__(KV_WG) void kv_mtab_kernel(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp,
+                                                         uint32_t* __restrict__ ns, uint32_t* __restrict__ an,
+                                                         uint32_t* __restrict__ sl) {
+  mtab_word(*Pp, *Bp, blockIdx.y, blockIdx.x * KV_WG + threadIdx.x, ns, an, sl);
+}
+
+hipError_t launch_mtab(const DevPS* P, const DevBatch* B, uint32_t words, uint32_t max_entities, uint32_t* ns,
+                       uint32_t* an, uint32_t* sl, hipStream_t stream) {
+  if (words == 0 || max_entities == 0) return hipSuccess;
+  hipLaunchKernelGGL(kv_mtab_kernel, dim3((max_entities + KV_WG - 1) / KV_WG, words), dim3(KV_WG), 0, stream, P, B, ns,
+                     an, sl);
+  return hipGetLastError();
+}
+
+}  // namespace kv
+
+// ---------------------------------------------------------------------------
 // Per-scope PolicyReport counts: counts[scope][rule][KV_HIST] from status[rule][res]
 // and the namespace index of every resource (scope = namespace, "" = cluster
 // scope), the summaries of pkg/kyverno/apply/report.go:76-179 and

@@ -5,6 +5,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
+#include <vector>
+#include <algorithm>
 
 #include "../../include/kvgpu.h"
 
@@ -171,40 +174,65 @@ void metadata(std::string& o, Rng& r, const char* prefix, uint64_t i) {
   o += "}";
 }
 
+
+// resource i of stream `seed`: its own generator state, so any contiguous range
+// [first, first + n) of one stream is reproducible on its own (the shard of a rank)
+void resource(std::string& o, uint64_t seed, uint64_t i, uint32_t kind_mix) {
+  Rng r{seed};
+  r.s = r.next() ^ (i * 0xD1B54A32D192ED03ull);
+  (void)r.next();
+  double k = kind_mix == 1 ? r.u() : 0.0;
+  if (k < 0.60) {
+    o += "{\"apiVersion\":\"v1\",\"kind\":\"Pod\",";
+    metadata(o, r, "pod-", i);
+    o += ",\"spec\":";
+    pod_spec(o, r);
+    o += "}\n";
+  } else if (k < 0.85) {
+    o += "{\"apiVersion\":\"apps/v1\",\"kind\":\"Deployment\",";
+    metadata(o, r, "deploy-", i);
+    o += ",\"spec\":{\"replicas\":" + std::to_string(1 + r.n(5)) + ",\"template\":{\"metadata\":{";
+    labels(o, r);
+    o += "},\"spec\":";
+    pod_spec(o, r);
+    o += "}}}\n";
+  } else {
+    static const char* st[] = {"ClusterIP", "NodePort", "LoadBalancer"};
+    o += "{\"apiVersion\":\"v1\",\"kind\":\"Service\",";
+    metadata(o, r, "svc-", i);
+    o += std::string(",\"spec\":{\"type\":\"") + st[r.n(3)] + "\",\"ports\":[{\"port\":" + std::to_string(80 + r.n(1000)) + "}]}}\n";
+  }
+}
+
 }  // namespace
 
-extern "C" int kv_synth(uint64_t seed, uint64_t n, uint32_t kind_mix, char** json_out, size_t* len) {
+extern "C" int kv_synth_range(uint64_t seed, uint64_t first, uint64_t n, uint32_t kind_mix, char** json_out,
+                              size_t* len) {
   if (!json_out || !len) return KV_E_INVALID;
-  std::string o;
-  o.reserve(n * 900);
-  Rng r{seed};
-  for (uint64_t i = 0; i < n; i++) {
-    double k = kind_mix == 1 ? r.u() : 0.0;
-    if (k < 0.60) {
-      o += "{\"apiVersion\":\"v1\",\"kind\":\"Pod\",";
-      metadata(o, r, "pod-", i);
-      o += ",\"spec\":";
-      pod_spec(o, r);
-      o += "}\n";
-    } else if (k < 0.85) {
-      o += "{\"apiVersion\":\"apps/v1\",\"kind\":\"Deployment\",";
-      metadata(o, r, "deploy-", i);
-      o += ",\"spec\":{\"replicas\":" + std::to_string(1 + r.n(5)) + ",\"template\":{\"metadata\":{";
-      labels(o, r);
-      o += "},\"spec\":";
-      pod_spec(o, r);
-      o += "}}}\n";
-    } else {
-      static const char* st[] = {"ClusterIP", "NodePort", "LoadBalancer"};
-      o += "{\"apiVersion\":\"v1\",\"kind\":\"Service\",";
-      metadata(o, r, "svc-", i);
-      o += std::string(",\"spec\":{\"type\":\"") + st[r.n(3)] + "\",\"ports\":[{\"port\":" + std::to_string(80 + r.n(1000)) + "}]}}\n";
-    }
-  }
-  *json_out = (char*)malloc(o.size() + 1);
+  const unsigned T = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(16, n / 4096));
+  std::vector<std::string> parts(T);
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < T; t++)
+    th.emplace_back([&, t]() {
+      const uint64_t b = n * t / T, e = n * (t + 1) / T;
+      parts[t].reserve((e - b) * 900);
+      for (uint64_t i = b; i < e; i++) resource(parts[t], seed, first + i, kind_mix);
+    });
+  for (auto& x : th) x.join();
+  size_t total = 0;
+  for (auto& p : parts) total += p.size();
+  *json_out = (char*)malloc(total + 1);
   if (!*json_out) return KV_E_NOMEM;
-  memcpy(*json_out, o.data(), o.size());
-  (*json_out)[o.size()] = 0;
-  *len = o.size();
+  size_t at = 0;
+  for (auto& p : parts) {
+    memcpy(*json_out + at, p.data(), p.size());
+    at += p.size();
+  }
+  (*json_out)[total] = 0;
+  *len = total;
   return 0;
+}
+
+extern "C" int kv_synth(uint64_t seed, uint64_t n, uint32_t kind_mix, char** json_out, size_t* len) {
+  return kv_synth_range(seed, 0, n, kind_mix, json_out, len);
 }

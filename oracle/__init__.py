@@ -66,6 +66,11 @@ class Oracle:
                                          ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong),
                                          ctypes.POINTER(ctypes.c_longlong)]
         L.orc_validate_batch.restype = ctypes.c_double
+        L.orc_count_rules.argtypes = [ctypes.c_char_p]
+        L.orc_count_rules.restype = ctypes.c_longlong
+        L.orc_validate_ndjson.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                          ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        L.orc_validate_ndjson.restype = ctypes.c_double
 
     def _take(self, p) -> str:
         if not p:
@@ -146,6 +151,25 @@ class Oracle:
             raise RuntimeError(self.lib.orc_last_error().decode())
         out = np.full((nr.value, nn.value), 255, dtype=np.uint8)
         t = self.lib.orc_validate_batch(p, r, c, nthreads, out.ctypes.data, ctypes.byref(nr), ctypes.byref(nn))
+        if t < 0:
+            raise RuntimeError(self.lib.orc_last_error().decode())
+        return out, t
+
+
+    def validate_ndjson(self, policies_json: str, ndjson: bytes, ctx: dict | None = None, nthreads: int = 1,
+                        preparse: bool = False):
+        """Large batches: one resource per NDJSON line, parsed and evaluated on `nthreads` threads.
+        preparse=False streams (bounded memory; seconds include parsing); preparse=True parses every
+        line first and times the evaluation alone. Returns (status uint8 [n_rules, n_res], seconds)."""
+        import numpy as np
+
+        nr = self.lib.orc_count_rules(policies_json.encode())
+        if nr < 0:
+            raise RuntimeError(self.lib.orc_last_error().decode())
+        n_res = sum(1 for line in ndjson.split(b"\n") if line)
+        out = np.full((nr, n_res), 255, dtype=np.uint8)
+        t = self.lib.orc_validate_ndjson(policies_json.encode(), ndjson, len(ndjson), json.dumps(ctx or {}).encode(),
+                                         nthreads, out.ctypes.data, n_res, 1 if preparse else 0)
         if t < 0:
             raise RuntimeError(self.lib.orc_last_error().decode())
         return out, t

@@ -204,4 +204,23 @@ double orc_validate_batch(const char* policies_json, const char* resources_json,
   }
 }
 
+long long orc_count_rules(const char* policies_json) {
+  try {
+    return (long long)CountRules(policies_json);
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+double orc_validate_ndjson(const char* policies_json, const char* ndjson, size_t len, const char* ctx_json, int nthreads,
+                           unsigned char* status_out, size_t n_res, int preparse) {
+  try {
+    return BatchValidateNdjson(policies_json, ndjson, len, ctx_json, nthreads, status_out, n_res, preparse);
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1.0;
+  }
+}
+
 }  // extern "C"

@@ -12,6 +12,8 @@
 // Rules that need the reference CPU engine (context, preconditions, deny,
 // foreach, {{ }} variables in pattern/anyPattern) are reported with status
 // "cpu" — the same deterministic routing decision the GPU compiler makes.
+#include <atomic>
+#include <mutex>
 #include <algorithm>
 #include <cstring>
 #include <map>
@@ -755,6 +757,86 @@ double BatchValidate(const char* policies_json, const char* resources_json, cons
   }
   for (auto& t : th) t.join();
   auto t1 = std::chrono::steady_clock::now();
+  return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// NDJSON batch for the large parity tests: one resource per line, each thread
+// parses and evaluates its own contiguous range of lines (bounded memory, parse in
+// parallel). status_out [n_rules][n_res] must hold CountRules() x (lines) bytes.
+size_t CountRules(const char* policies_json) {
+  Value pl = parse_json(policies_json, NumMode::Float);
+  if (pl.t != T::Arr) throw std::runtime_error("batch: expected a list");
+  size_t n = 0;
+  for (auto* p : pl.a) n += parse_policy(*p).rules.size();
+  return n;
+}
+
+double BatchValidateNdjson(const char* policies_json, const char* ndjson, size_t len, const char* ctx_json,
+                           int nthreads, unsigned char* status_out, size_t n_res, int preparse) {
+  Value pl = parse_json(policies_json, NumMode::Float);
+  Value cv = parse_json(ctx_json && *ctx_json ? ctx_json : "{}", NumMode::Float);
+  if (pl.t != T::Arr) throw std::runtime_error("batch: expected a list");
+  std::vector<Policy> pols;
+  for (auto* p : pl.a) pols.push_back(parse_policy(*p));
+  EngineCtx cx = parse_ctx(cv);
+  std::vector<std::pair<size_t, size_t>> lines;
+  for (size_t i = 0; i < len;) {
+    size_t e = i;
+    while (e < len && ndjson[e] != '\n') e++;
+    if (e > i) lines.push_back({i, e - i});
+    i = e + 1;
+  }
+  if (lines.size() != n_res) throw std::runtime_error("batch: line count differs from n_res");
+  if (nthreads < 1) nthreads = 1;
+  std::vector<std::thread> th;
+  std::vector<std::string> errs(nthreads);
+  const size_t per = (n_res + nthreads - 1) / nthreads;
+  auto eval = [&](size_t r, const Value& v) {
+    size_t rule_base = 0;
+    for (const auto& pol : pols) {
+      std::vector<RuleResult> rs = validate_policy(pol, v, cx);
+      for (size_t k = 0; k < rs.size(); k++) status_out[(rule_base + k) * n_res + r] = (unsigned char)rs[k].status;
+      rule_base += pol.rules.size();
+    }
+  };
+  auto parse_line = [&](size_t r) {
+    return parse_json(std::string(ndjson + lines[r].first, lines[r].second), NumMode::Unstructured);
+  };
+  // preparse: every thread parses its range first; the timed region is the evaluation
+  // alone, from the moment all threads have parsed until the last one finishes
+  std::vector<std::vector<Value>> docs(preparse ? nthreads : 0);
+  std::atomic<int> parsed{0};
+  std::atomic<bool> go{!preparse};
+  std::chrono::steady_clock::time_point t0;
+  std::mutex mu;
+  for (int w = 0; w < nthreads; w++) {
+    th.emplace_back([&, w]() {
+      const size_t b = std::min(n_res, w * per), e = std::min(n_res, (w + 1) * per);
+      try {
+        if (preparse) {
+          for (size_t r = b; r < e; r++) docs[w].push_back(parse_line(r));
+          if (++parsed == nthreads) {
+            std::lock_guard<std::mutex> g(mu);
+            t0 = std::chrono::steady_clock::now();
+            go = true;
+          }
+          while (!go) std::this_thread::yield();
+          for (size_t r = b; r < e; r++) eval(r, docs[w][r - b]);
+        } else {
+          for (size_t r = b; r < e; r++) eval(r, parse_line(r));
+        }
+      } catch (const std::exception& ex) {
+        errs[w] = ex.what();
+        if (preparse && ++parsed == nthreads) go = true;
+      }
+    });
+  }
+  if (!preparse) t0 = std::chrono::steady_clock::now();
+  for (auto& t : th) t.join();
+  const auto t1 = std::chrono::steady_clock::now();
+  for (auto& e : errs)
+    if (!e.empty()) throw std::runtime_error(e);
+  std::lock_guard<std::mutex> g(mu);
   return std::chrono::duration<double>(t1 - t0).count();
 }
 

@@ -11,4 +11,7 @@ bool ValidateElementEntry(int entry, const Value& resource, Value& pattern, std:
 std::string ValidateToJSON(const Value& policy, const Value& resource, const Value& ctx);
 double BatchValidate(const char* policies_json, const char* resources_json, const char* ctx_json, int nthreads,
                      unsigned char* status_out, long long* n_rules_out, long long* n_res_out);
+size_t CountRules(const char* policies_json);
+double BatchValidateNdjson(const char* policies_json, const char* ndjson, size_t len, const char* ctx_json,
+                           int nthreads, unsigned char* status_out, size_t n_res, int preparse);
 }  // namespace orc

@@ -1,0 +1,95 @@
+"""Parity at the sizes and rule sets the benchmark times (BASELINE.json configs).
+
+Full status matrices of the specialized kernels (the engine bench.py times)
+against the oracle run on every host core, plus sampled failing paths and
+error messages:
+* C3: the whole 1 000-policy / 1 978-rule set on mixed Pods/Deployments/Services,
+  at the shipped kernel grouping and at five fused chunks per kernel;
+* C2: 1 M Pods x 100 rules (the headline workload);
+* C4: 1 M Pods x 138 anchor-heavy rules.
+Reference semantics: pkg/engine/validation.go:26-106 (oracle/src/engine.cpp).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from parity_util import rule_index
+
+pytestmark = pytest.mark.gpu
+
+
+def _threads():
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except OSError:
+        return os.cpu_count() or 1
+
+
+def _check(orc, pols, data, env=None, n_paths=300, n_msgs=100, min_fail=100):
+    from kyverno_amd import batch
+
+    old = {k: os.environ.get(k) for k in (env or {})}
+    os.environ.update(env or {})
+    try:
+        ps = batch.PolicySet(pols, specialize=True)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    b = batch.Batch(ps, data)
+    r = batch.validate(ps, b)
+    ost, _ = orc.validate_ndjson(json.dumps(pols), data, nthreads=_threads())
+    ost[ost == 7] = 6
+    bad = np.argwhere(r.status != ost)
+    assert not len(bad), [(int(a), ps.rules[a].name, int(c), int(r.status[a, c]), int(ost[a, c])) for a, c in bad[:20]]
+    assert (r.status == 1).sum() >= min_fail
+    # sampled failing paths and skip / error messages against the per-pair oracle
+    lines = data.split(b"\n")
+    ridx = rule_index(pols)
+    rng = np.random.default_rng(1)
+    fails = np.argwhere(r.status == 1)
+    for a, c in fails[rng.choice(len(fails), min(n_paths, len(fails)), replace=False)]:
+        if ps.rules[a].any_pattern:
+            continue
+        pi, ri = ridx[a]
+        want = orc.validate(pols[pi], lines[c].decode(), None)["rules"][ri]["path"]
+        assert r.path(int(a), int(c)) == want, (ps.rules[a].name, int(c))
+    errs = np.argwhere((r.status == 3) | (r.status == 4))
+    for a, c in errs[rng.choice(len(errs), min(n_msgs, len(errs)), replace=False)] if len(errs) else []:
+        pi, ri = ridx[a]
+        want = orc.validate(pols[pi], lines[c].decode(), None)["rules"][ri]["message"]
+        got = r.error_message(int(a), int(c), lines[c].decode())
+        assert got is not None and got in want, (ps.rules[a].name, int(c), got, want)
+    return r
+
+
+@pytest.mark.parametrize("group", ["3", "5"])
+def test_c3_full_policy_set(orc, group):
+    """1 000 policies / 1 978 rules (match/exclude: kinds, namespace globs, wildcard matchLabels,
+    matchExpressions, any-blocks, exclude blocks) x 2 000 mixed resources."""
+    from kyverno_amd import batch, workloads
+
+    pols = workloads.c3_policies(1000)
+    data = batch.synth(workloads.SEED + 11, 2000, 1).strip()
+    r = _check(orc, pols, data, env={"KVGPU_JIT_GROUP": group}, n_paths=200)
+    assert r.n_rules == 1978 and (r.status == 5).sum() > 0
+
+
+def test_c2_full_scale(orc):
+    """C2 at its benchmark size: 1 M synthetic Pods x 100 rules (bench.py's default workload)."""
+    from kyverno_amd import batch, workloads
+
+    data = batch.synth(workloads.SEED, 1_000_000).strip()
+    _check(orc, workloads.c2_policies(), data)
+
+
+def test_c4_full_scale(orc):
+    """C4 at its benchmark size: 1 M synthetic Pods x 138 anchor-heavy chart + test/policy/validate rules."""
+    from kyverno_amd import batch, workloads
+
+    data = batch.synth(workloads.SEED + 4, 1_000_000).strip()
+    _check(orc, workloads.c4_policies(), data)

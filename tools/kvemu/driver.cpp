@@ -11,6 +11,7 @@
 // Environment: the KVGPU_JIT_* settings the source was generated with.
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -34,6 +35,9 @@ struct kvemu_dim3 {
   uint32_t x, y, z;
 };
 thread_local kvemu_dim3 threadIdx, blockIdx;
+
+extern "C" void kvemu_mtab(const DevPS* P, const DevBatch* B, uint32_t words, uint32_t max_entities, uint32_t* ns,
+                           uint32_t* an, uint32_t* sl);
 
 typedef void (*ptab_fn)(const DevPS*, const Val*, const uint8_t*, uint32_t, uint32_t*);
 typedef void (*chunk_fn)(const DevPS*, const DevBatch*, const Node*, const Val*, const uint8_t*, DevOut);
@@ -122,6 +126,8 @@ int main(int argc, char** argv) {
     P.star_id = ps.lookup("*");
     if (P.star_id == KEY_NONE) P.star_id = KEY_NONE - 1;
     P.n_rules = (uint32_t)ps.rules.size();
+    P.n_filters = (uint32_t)ps.filters.size();
+    P.n_sels = (uint32_t)ps.selectors.size();
     P.ptab = ptab.data();
     P.n_vals = NV;
     DevBatch B{};
@@ -134,8 +140,26 @@ int main(int argc, char** argv) {
     B.key_off = koff.data();
     B.key_len = klen.data();
     B.kstr = (const uint8_t*)ks.data();
+    B.nsms = b.nsms.data();
+    B.lsets = b.lsets.data();
+    B.asets = b.asets.data();
+    B.n_nsm = (uint32_t)b.nsms.size();
+    B.n_lsets = (uint32_t)b.lsets.size();
+    B.n_asets = (uint32_t)b.asets.size();
     B.ns_words = b.ns_words;
     B.n_res = (uint32_t)b.res.size();
+    // match tables (as kv_session: one allocation, three [word][entity] tables)
+    P.mt_ns_words = (ps.n_nss_bits + 31) / 32;
+    P.mt_ann_words = (ps.n_ann_bits + 31) / 32;
+    P.mt_sel_words = (uint32_t)((ps.selectors.size() + 31) / 32);
+    const size_t n_ns = (size_t)P.mt_ns_words * B.n_nsm, n_an = (size_t)P.mt_ann_words * B.n_asets,
+                 n_sl = (size_t)P.mt_sel_words * B.n_lsets;
+    std::vector<uint32_t> mt(std::max<size_t>(n_ns + n_an + n_sl, 1), 0xA5A5A5A5u);
+    P.mt_ns = mt.data();
+    P.mt_ann = mt.data() + n_ns;
+    P.mt_sel = mt.data() + n_ns + n_an;
+    kvemu_mtab(&P, &B, P.mt_ns_words + P.mt_ann_words + P.mt_sel_words,
+               std::max({B.n_nsm, B.n_asets, B.n_lsets}), mt.data(), mt.data() + n_ns, mt.data() + n_ns + n_an);
     const uint64_t nr = ps.rules.size(), nres = b.res.size();
 
     if (img.memo_words && NV) {
