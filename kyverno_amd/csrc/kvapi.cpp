@@ -653,15 +653,25 @@ int kv_compile(const char* policies_json, size_t len, uint32_t flags, kv_policys
       compile_policies(policies_json, len, &s->ps);
       if (flags & KV_COMPILE_SPECIALIZE) {
         s->jit = std::make_unique<JitImage>();
-        const char* ch = getenv("KVGPU_JIT_CHUNK");  // rules per specialized kernel (experiments)
-        jit_generate(s->ps, ch ? (uint32_t)atoi(ch) : 8u, s->jit.get());
+        const char* ch = getenv("KVGPU_JIT_CHUNK");  // rules per fused chunk (experiments)
+        const uint32_t chunk = ch ? (uint32_t)atoi(ch) : 8u;
+        jit_generate(s->ps, chunk, s->jit.get());
         if (const char* dump = getenv("KVGPU_JIT_DUMP")) {
           if (FILE* f = fopen(dump, "w")) {
             fwrite(s->jit->source.data(), 1, s->jit->source.size(), f);
             fclose(f);
           }
         }
-        if (!getenv("KVGPU_JIT_SKIP_COMPILE")) jit_compile(s->jit.get());  // dump-only analysis runs
+        if (!getenv("KVGPU_JIT_SKIP_COMPILE")) {  // (dump-only analysis runs skip it)
+          double ms = 0;
+          for (int round = 0; round < 8; round++) {  // register budget: re-plan kernels that spill
+            jit_compile(s->jit.get());
+            ms += s->jit->compile_ms;
+            if (!jit_plan_spills(s->jit.get())) break;
+            jit_generate(s->ps, chunk, s->jit.get());
+          }
+          s->jit->compile_ms = ms;
+        }
         if (const char* dump = getenv("KVGPU_JIT_DUMP_CO")) {  // gfx950 code objects (llvm-objdump / readelf)
           for (size_t i = 0; i < s->jit->codes.size(); i++) {
             if (FILE* f = fopen((std::string(dump) + "." + s->jit->kernel_name[i] + ".co").c_str(), "wb")) {

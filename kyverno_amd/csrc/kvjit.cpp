@@ -15,6 +15,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -1022,6 +1023,27 @@ struct Gen {
       K = std::max(K, g.loops.size());
       gs.push_back(std::move(g));
     }
+    // status + error record + histogram of rule `ri` (chunk position q): emitted as
+    // soon as the rule's last segment has run, so its state registers die there
+    auto store = [&](uint32_t ri) {
+      const uint32_t q = (uint32_t)(std::find(ch.rules.begin(), ch.rules.end(), ri) - ch.rules.begin());
+      const std::string s = "_" + std::to_string(ri);
+      const RGen* g = nullptr;
+      for (const RGen& x : gs)
+        if (x.ri == ri) g = &x;
+      std::ostringstream k;
+      if (g) {
+        k << "  { EState e_{ek" << s << " & 15u, (ek" << s << " >> 4) & 15u, ek" << s << " >> 8, "
+          << (g->uses_keyglob ? "ekn" + s : std::string("ABSENT")) << ", ABSENT";
+        for (uint32_t lv = 0; lv < 4; lv++) k << ", " << (lv <= g->max_level ? "ei" + std::to_string(lv) + s : "0u");
+        k << "};\n";
+      } else {
+        k << "  { EState e_{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u};\n";
+      }
+      k << "    store_result2(O, " << ri << "u, n_res, r, valid, rs" << s << " & 0xFFu, e_, &s_hist[" << (hbase + q)
+        << "][0]); }\n";
+      return k.str();
+    };
     std::ostringstream body;  // everything after the per-rule declarations
     for (size_t k = 0; k <= K; k++) {
       for (RGen& g : gs) {
@@ -1042,6 +1064,7 @@ struct Gen {
         for (uint32_t t : g.resume)
           if (t >= sb && t < se) body << "    case " << u32(t) << ": goto R" << g.ri << "_L" << t << ";\n";
         body << "    default: goto " << R.se << ";\n  }\n" << w.str() << R.se << ":;\n";
+        if (k == g.loops.size()) body << store(g.ri);  // the rule has finished for every lane
       }
       if (k == K) break;
       // fused loops of stage k: group rules by the symbolic array cursor
@@ -1152,33 +1175,17 @@ struct Gen {
       }
       k << "  }\n";
     }
+    // rules of other routes are final after match / route
+    for (uint32_t ri : ch.rules)
+      if (ps.rules[ri].route != 0) k << store(ri);
     k << body.str();
-    std::set<uint32_t> gpu;
-    for (const RGen& g : gs) gpu.insert(g.ri);
-    for (uint32_t q = 0; q < ch.rules.size(); q++) {
-      const uint32_t ri = ch.rules[q];
-      const std::string s = "_" + std::to_string(ri);
-      if (gpu.count(ri)) {
-        const RGen* g = nullptr;
-        for (const RGen& x : gs)
-          if (x.ri == ri) g = &x;
-        k << "  { EState e_{ek" << s << " & 15u, (ek" << s << " >> 4) & 15u, ek" << s << " >> 8, "
-          << (g->uses_keyglob ? "ekn" + s : std::string("ABSENT")) << ", ABSENT";
-        for (uint32_t lv = 0; lv < 4; lv++) k << ", " << (lv <= g->max_level ? "ei" + std::to_string(lv) + s : "0u");
-        k << "};\n";
-      } else {
-        k << "  { EState e_{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u};\n";
-      }
-      k << "    store_result2(O, " << ri << "u, n_res, r, valid, rs" << s << " & 0xFFu, e_, &s_hist[" << (hbase + q)
-        << "][0]); }\n";
-    }
     return k.str();
   }
 
   // One kernel running the fused chunks `chs` one after the other for each
   // resource: a workgroup re-reads its resources' node rows per chunk while they
   // are still cache-resident, instead of one grid-wide pass per chunk.
-  void group_kernel(const std::string& name, const std::vector<const JitChunk*>& chs) {
+  void group_kernel(const std::string& name, const std::vector<const JitChunk*>& chs, int waves) {
     std::vector<std::string> blocks;
     std::vector<uint32_t> rules;
     for (const JitChunk* c : chs) {
@@ -1191,11 +1198,8 @@ struct Gen {
     for (uint32_t q = 0; q < nr; q++) o << (q ? ", " : "") << u32(rules[q]);
     o << "};\n";
     // Occupancy over registers: the rule kernels are latency-bound on dependent
-    // tree loads, so ask for 8 waves per SIMD (<= 64 VGPRs, a few spilled cursor
-    // registers) — measured faster on C2-C5 than the unconstrained 86-102 VGPRs.
-    // KVGPU_JIT_WAVES=w overrides (0: no bound).
-    const char* wz = getenv("KVGPU_JIT_WAVES");
-    const int waves = wz ? atoi(wz) : 8;
+    // tree loads, so they ask for 8 waves per SIMD (<= 64 VGPRs) unless the plan
+    // relaxes it for a kernel that would spill (jit_plan_spills).
     const std::string lb = waves > 0 ? "KV_WG, " + std::to_string(waves) : "KV_WG";
     o << "extern \"C\" __global__ __launch_bounds__(" << lb << ") void " << name
       << "(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp, const Node* __restrict__ N, "
@@ -1308,24 +1312,33 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
     for (uint32_t ri = 0; ri < n; ri++)
       order.push_back({ps.rules[ri].route == 0 ? "0" + rule_signature(ps, ri) : "1", ri});
     std::stable_sort(order.begin(), order.end());
-    // KVGPU_JIT_GROUP: fused chunks run back to back inside one kernel (default 3)
-    const char* gz = getenv("KVGPU_JIT_GROUP");
-    const uint32_t group = gz ? std::max(1, atoi(gz)) : 3u;
     std::vector<JitChunk> chs;
     for (uint32_t b = 0; b < n; b += chunk_rules) {
       JitChunk ch;
       for (uint32_t q = b; q < std::min(n, b + chunk_rules); q++) ch.rules.push_back(order[q].second);
       chs.push_back(ch);
     }
-    for (size_t b = 0; b < chs.size(); b += group) {
+    out->n_chunks = (uint32_t)chs.size();
+    if (out->plan.empty()) {
+      // KVGPU_JIT_GROUP: fused chunks run back to back inside one kernel (default 5);
+      // KVGPU_JIT_WAVES: launch bound in waves per SIMD (default 8, 0: none)
+      const char* gz = getenv("KVGPU_JIT_GROUP");
+      const uint32_t group = gz ? (uint32_t)std::max(1, atoi(gz)) : 5u;
+      const char* wz = getenv("KVGPU_JIT_WAVES");
+      const int waves = wz ? atoi(wz) : 8;
+      for (uint32_t b = 0; b < chs.size(); b += group)
+        out->plan.push_back({b, std::min<uint32_t>(group, (uint32_t)chs.size() - b), waves});
+    }
+    for (const JitKernelPlan& kp : out->plan) {
       JitChunk kc;
-      kc.name = "kvj_chunk_" + std::to_string(out->chunks.size());
+      // named by its first chunk and chunk count: stable when other groups are re-planned
+      kc.name = "kvj_c" + std::to_string(kp.first) + "_" + std::to_string(kp.count) + (kp.waves ? "" : "u");
       std::vector<const JitChunk*> part;
-      for (size_t q = b; q < std::min(chs.size(), b + group); q++) {
-        part.push_back(&chs[q]);
+      for (uint32_t q = kp.first; q < kp.first + kp.count; q++) {
+        part.push_back(&chs.at(q));
         kc.rules.insert(kc.rules.end(), chs[q].rules.begin(), chs[q].rules.end());
       }
-      g.group_kernel(kc.name, part);
+      g.group_kernel(kc.name, part, kp.waves);
       out->chunks.push_back(kc);
     }
   }
@@ -1414,6 +1427,86 @@ std::vector<char> compile_one(const std::string& src, const std::string& name) {
 }
 
 }  // namespace
+
+// Private (scratch) segment size and code size of kernel `name` in a gfx950 code
+// object: the kernel descriptor `<name>.kd` (offset 4: private_segment_fixed_size)
+// and the size of the function symbol. A non-zero private segment in these
+// kernels means register spills (they keep no arrays on the stack).
+bool co_kernel_info(const std::vector<char>& co, const std::string& name, uint32_t* private_seg, uint64_t* code) {
+  auto rd = [&](size_t off, size_t n, void* out) {
+    if (off + n > co.size()) return false;
+    memcpy(out, co.data() + off, n);
+    return true;
+  };
+  if (co.size() < 64 || memcmp(co.data(), "\x7f" "ELF", 4) != 0 || co[4] != 2) return false;
+  uint64_t shoff = 0;
+  uint16_t shentsize = 0, shnum = 0;
+  rd(0x28, 8, &shoff);
+  rd(0x3A, 2, &shentsize);
+  rd(0x3C, 2, &shnum);
+  struct Sh { uint32_t name, type; uint64_t flags, addr, off, size; uint32_t link, info; uint64_t align, entsize; };
+  std::vector<Sh> sh(shnum);
+  for (uint16_t i = 0; i < shnum; i++)
+    if (!rd(shoff + (uint64_t)i * shentsize, sizeof(Sh), &sh[i])) return false;
+  bool kd = false, fn = false;
+  for (const Sh& t : sh) {
+    if (t.type != 2 /* SHT_SYMTAB */ || t.link >= shnum) continue;
+    const Sh& strtab = sh[t.link];
+    for (uint64_t o = t.off; o + 24 <= t.off + t.size; o += 24) {
+      uint32_t nm = 0;
+      uint16_t shndx = 0;
+      uint64_t value = 0, size = 0;
+      rd(o, 4, &nm);
+      rd(o + 6, 2, &shndx);
+      rd(o + 8, 8, &value);
+      rd(o + 16, 8, &size);
+      if (strtab.off + nm >= co.size()) continue;
+      const char* sn = co.data() + strtab.off + nm;
+      const size_t maxlen = co.size() - (strtab.off + nm);
+      const std::string sym(sn, strnlen(sn, maxlen));
+      if (sym == name + ".kd" && shndx < shnum) {
+        const Sh& sec = sh[shndx];
+        kd = rd(sec.off + (value - sec.addr) + 4, 4, private_seg);
+      } else if (sym == name) {
+        *code = size;
+        fn = true;
+      }
+    }
+  }
+  return kd && fn;
+}
+
+bool jit_plan_spills(JitImage* img) {
+  if (getenv("KVGPU_JIT_SPILL_SPLIT") && getenv("KVGPU_JIT_SPILL_SPLIT")[0] == '0') return false;
+  std::vector<JitKernelPlan> next;
+  bool changed = false;
+  img->kernel_scratch.assign(img->plan.size(), 0);
+  for (size_t k = 0; k < img->plan.size(); k++) {
+    const JitKernelPlan& kp = img->plan[k];
+    const std::string& name = img->chunks[k].name;
+    uint32_t priv = 0;
+    uint64_t code = 0;
+    size_t ci = 0;
+    while (ci < img->kernel_name.size() && img->kernel_name[ci] != name) ci++;
+    if (ci == img->kernel_name.size() || !co_kernel_info(img->codes[ci], name, &priv, &code))
+      throw std::runtime_error("kvjit: no kernel descriptor for " + name);
+    img->kernel_scratch[k] = priv;
+    if (priv == 0 || kp.waves == 0) {
+      next.push_back(kp);
+      continue;
+    }
+    changed = true;
+    if (kp.count > 1) {  // split the group: fewer rules' state per kernel
+      const uint32_t h = kp.count / 2;
+      next.push_back({kp.first, h, kp.waves});
+      next.push_back({kp.first + h, kp.count - h, kp.waves});
+    } else {  // one fused chunk that still spills under the bound: let it take the registers it needs
+      next.push_back({kp.first, 1, 0});
+    }
+  }
+  if (changed) img->plan = next;
+  return changed;
+}
 
 uint64_t code_bytes(const JitImage& img) {
   uint64_t n = 0;

@@ -18,7 +18,17 @@ struct JitChunk {
   std::string name;
 };
 
+// One specialized rule kernel: fused chunks [first, first + count) of the
+// signature-sorted rule order, compiled with a `waves`-per-SIMD launch bound (0: none).
+struct JitKernelPlan {
+  uint32_t first, count;
+  int waves;
+};
+
 struct JitImage {
+  std::vector<JitKernelPlan> plan;     // kernel grouping (empty: default groups; kept across re-plans)
+  std::vector<uint32_t> kernel_scratch;  // private segment bytes per lane of each planned kernel
+  uint32_t n_chunks = 0;
   std::string source;       // generated HIP source, all of it (diagnostics, tools/kvemu)
   std::string common;       // prelude + helper functions shared by the kernels
   std::vector<std::string> kernel_name, kernel_src;  // one hiprtc program per kernel: common + kernel_src[i]
@@ -43,5 +53,11 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out);
 // Throws std::runtime_error with the log on failure.
 void jit_compile(JitImage* img);
 uint64_t code_bytes(const JitImage& img);
+// Register budget of the plan: a kernel that spills under its wave bound (non-zero
+// private segment) is split in two, or, as a single fused chunk, compiled without
+// the bound. Returns true when the plan changed (regenerate + compile again; the
+// kernels that did not change come from the code-object cache).
+bool jit_plan_spills(JitImage* img);
+bool co_kernel_info(const std::vector<char>& co, const std::string& name, uint32_t* private_seg, uint64_t* code);
 
 }  // namespace kvh
