@@ -103,6 +103,17 @@ const char* kv_batch_namespace(const kv_batch* b, uint32_t i);
 int kv_validate(const kv_policyset* ps, const kv_batch* b, const char* ctx_json, int device, uint32_t mode,
                 kv_result** out, kv_error** err);
 
+/* Evaluate on several devices (SURVEY.md §8b "Threading"): the batch's resources are
+ * split into contiguous ranges [k*N/G, (k+1)*N/G) (cut at 64-resource boundaries)
+ * over the G devices of device_mask (bit d = HIP device d), one host thread + HIP
+ * stream per device, the policy set replicated; per-rule counts (and per-scope
+ * counts with KV_MODE_SCOPES) are summed over the devices by one RCCL all-reduce
+ * (ncclUint64, ncclSum; communicators created per session). Statuses and error
+ * records come back in resource order in one result. Callers: the background
+ * scan (pkg/policy/apply.go:72) and kyverno apply (pkg/kyverno/apply/apply_command.go:270-310). */
+int kv_validate_devices(const kv_policyset* ps, const kv_batch* b, const char* ctx_json, uint32_t device_mask,
+                        uint32_t mode, kv_result** out, kv_error** err);
+
 /* status[rule * n_res + res] (rule-major) */
 int kv_result_status(const kv_result* r, const uint8_t** status, uint64_t* n_rules, uint64_t* n_res);
 /* counts[rule * 8 + status] */
@@ -125,6 +136,17 @@ int kv_result_error_message(const kv_result* r, uint32_t rule, uint64_t res, con
                             char* buf, size_t cap);
 double kv_result_kernel_ms(const kv_result* r);
 
+/* Bulk export of the failing pairs (KV_MODE_ERRORS): every FAIL / ERROR / SKIP pair,
+ * rule-major and in resource order: pair i = (rule[i], res[i]); path_id[i] names the
+ * failing path of a FAIL pair (KV_PATH_NONE for ERROR / SKIP), rendered once per
+ * distinct path by kv_path_string (e.g. "/spec/containers/0/image/"). The arrays and
+ * strings live as long as the result. This is what a Go caller builds
+ * RuleResponse.Message from without one call per pair (validation.go:510-547). */
+enum { KV_PATH_NONE = 0xFFFFFFFFu };
+int kv_result_failures(const kv_result* r, uint64_t* n, const uint32_t** rule, const uint64_t** res,
+                       const uint32_t** path_id);
+const char* kv_path_string(const kv_result* r, uint32_t path_id);
+
 /* Benchmark entry: device-resident inputs, `iters` timed launches on one stream
  * bracketed by HIP events. Returns mean kernel milliseconds per pass over all
  * rules of the batch. */
@@ -138,6 +160,12 @@ int kv_bench(const kv_policyset* ps, const kv_batch* b, const char* ctx_json, in
 typedef struct kv_session kv_session;
 int kv_session_create(const kv_policyset* ps, const kv_batch* b, const char* ctx_json, int device, uint32_t mode,
                       kv_session** out, kv_error** err);
+/* multi-device session (see kv_validate_devices); kv_session_counts / _scope_counts
+ * return the RCCL-reduced totals, kv_session_fetch the last pass as a result */
+int kv_session_create_devices(const kv_policyset* ps, const kv_batch* b, const char* ctx_json, uint32_t device_mask,
+                              uint32_t mode, kv_session** out, kv_error** err);
+int kv_session_parts(const kv_session* s, uint32_t* n_parts);
+int kv_session_fetch(kv_session* s, kv_result** out, kv_error** err);
 int kv_session_run(kv_session* s, int iters, double* event_ms, kv_error** err);
 int kv_session_counts(kv_session* s, int64_t* counts /* [n_rules][8], last pass */);
 int kv_session_scope_counts(kv_session* s, int64_t* counts /* [n_scopes][n_rules][8], last pass */);

@@ -88,6 +88,14 @@ def lib():
         L.kv_batch_namespaces.argtypes = [vp, ctypes.POINTER(u32)]
         L.kv_batch_namespace.argtypes = [vp, u32]
         L.kv_batch_namespace.restype = ctypes.c_char_p
+        L.kv_validate_devices.argtypes = [vp, vp, ctypes.c_char_p, u32, u32, ctypes.POINTER(vp), errpp]
+        L.kv_session_create_devices.argtypes = [vp, vp, ctypes.c_char_p, u32, u32, ctypes.POINTER(vp), errpp]
+        L.kv_session_parts.argtypes = [vp, ctypes.POINTER(u32)]
+        L.kv_session_fetch.argtypes = [vp, ctypes.POINTER(vp), errpp]
+        L.kv_result_failures.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                         ctypes.POINTER(vp)]
+        L.kv_path_string.argtypes = [vp, u32]
+        L.kv_path_string.restype = ctypes.c_char_p
         for fn in ("kv_free_policyset", "kv_free_batch", "kv_free_result", "kv_free_buffer", "kv_free_session"):
             getattr(L, fn).argtypes = [vp]
             getattr(L, fn).restype = None
@@ -104,6 +112,8 @@ EXPORTED_SYMBOLS = [
     "kv_bench", "kv_synth", "kv_synth_range", "kv_free_policyset", "kv_free_batch", "kv_free_result", "kv_free_error",
     "kv_free_buffer", "kv_session_create", "kv_session_run", "kv_session_counts", "kv_free_session",
     "kv_session_scope_counts", "kv_result_scope_counts", "kv_batch_namespaces", "kv_batch_namespace",
+    "kv_validate_devices", "kv_session_create_devices", "kv_session_parts", "kv_session_fetch", "kv_result_failures",
+    "kv_path_string",
 ]
 
 

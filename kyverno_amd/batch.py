@@ -183,6 +183,28 @@ class Result:
                 return buf.raw[:n].decode("utf-8", "replace")
             cap = n + 1
 
+    def failures(self):
+        """Every FAIL / ERROR / SKIP pair (``kv_result_failures``), rule-major in resource order:
+        (rule u32[n], res u64[n], path_id u32[n]) and ``paths`` (path_id -> string; FAIL only)."""
+        n = ctypes.c_uint64()
+        pr, pq, pp = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        rc = lib().kv_result_failures(self._h, ctypes.byref(n), ctypes.byref(pr), ctypes.byref(pq), ctypes.byref(pp))
+        if rc != 0:
+            raise _native.KvError(rc, "kv_result_failures failed")
+        k = n.value
+        if k == 0:
+            return np.zeros(0, np.uint32), np.zeros(0, np.uint64), np.zeros(0, np.uint32), []
+        rule = np.frombuffer((ctypes.c_uint32 * k).from_address(pr.value), np.uint32).copy()
+        res = np.frombuffer((ctypes.c_uint64 * k).from_address(pq.value), np.uint64).copy()
+        pid = np.frombuffer((ctypes.c_uint32 * k).from_address(pp.value), np.uint32).copy()
+        paths = []
+        while True:
+            p = lib().kv_path_string(self._h, len(paths))
+            if p is None:
+                break
+            paths.append(p.decode("utf-8"))
+        return rule, res, pid, paths
+
     def error(self, rule: int, res: int):
         k, f = ctypes.c_uint32(), ctypes.c_uint32()
         if lib().kv_result_error(self._h, rule, res, ctypes.byref(k), ctypes.byref(f)) != 0:
@@ -201,7 +223,9 @@ class Result:
 
 def validate(policyset: PolicySet, batch: Batch, admission: dict | None = None,
              exclude_group_role: list | None = None, device: int = 0,
-             mode: int = MODE_STATUS | MODE_ERRORS) -> Result:
+             mode: int = MODE_STATUS | MODE_ERRORS, device_mask: int | None = None) -> Result:
+    """kv_validate on `device`, or kv_validate_devices over the devices of `device_mask`
+    (contiguous resource shards, counts all-reduced over RCCL inside the library)."""
     ctx = {}
     if admission:
         ctx["admission"] = admission
@@ -209,8 +233,12 @@ def validate(policyset: PolicySet, batch: Batch, admission: dict | None = None,
         ctx["excludeGroupRole"] = list(exclude_group_role)
     h = ctypes.c_void_p()
     err = new_err()
-    check(lib().kv_validate(policyset._h, batch._h, _dumps(ctx), device, mode, ctypes.byref(h), ctypes.byref(err)),
-          err)
+    if device_mask is None:
+        rc = lib().kv_validate(policyset._h, batch._h, _dumps(ctx), device, mode, ctypes.byref(h), ctypes.byref(err))
+    else:
+        rc = lib().kv_validate_devices(policyset._h, batch._h, _dumps(ctx), device_mask, mode, ctypes.byref(h),
+                                       ctypes.byref(err))
+    check(rc, err)
     return Result(h, policyset, batch)
 
 
@@ -227,13 +255,29 @@ class Session:
     """Device-resident launch configuration: inputs and output buffers allocated once."""
 
     def __init__(self, policyset: PolicySet, batch: Batch, device: int = 0, mode: int = MODE_COUNTS,
-                 ctx: dict | None = None):
+                 ctx: dict | None = None, device_mask: int | None = None):
         h = ctypes.c_void_p()
         err = new_err()
-        check(lib().kv_session_create(policyset._h, batch._h, _dumps(ctx or {}), device, mode, ctypes.byref(h),
-                                      ctypes.byref(err)), err)
+        if device_mask is None:
+            rc = lib().kv_session_create(policyset._h, batch._h, _dumps(ctx or {}), device, mode, ctypes.byref(h),
+                                         ctypes.byref(err))
+        else:
+            rc = lib().kv_session_create_devices(policyset._h, batch._h, _dumps(ctx or {}), device_mask, mode,
+                                                 ctypes.byref(h), ctypes.byref(err))
+        check(rc, err)
         self._h = h
+        self.policyset, self.batch = policyset, batch
         self.n_rules = policyset.n_rules
+        n = ctypes.c_uint32()
+        lib().kv_session_parts(h, ctypes.byref(n))
+        self.n_parts = n.value
+
+    def fetch(self) -> "Result":
+        """The last pass as a result (statuses, compacted error records, reduced counts)."""
+        h = ctypes.c_void_p()
+        err = new_err()
+        check(lib().kv_session_fetch(self._h, ctypes.byref(h), ctypes.byref(err)), err)
+        return Result(h, self.policyset, self.batch)
 
     def run(self, iters: int) -> float:
         """Enqueue `iters` passes and wait; returns total HIP-event milliseconds."""

@@ -2,6 +2,7 @@
 // sets and ingested batches, launch-time folding of batch-constant user info,
 // result decoding (failing paths) on the host.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -11,7 +12,9 @@
 #include <memory>
 #include <mutex>
 #include <stdexcept>
+#include <thread>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/kvgpu.h"
@@ -113,17 +116,88 @@ struct kv_batch {
   std::map<int, std::unique_ptr<DevBatchRes>> dev;
 };
 
+namespace {
+
+// Host array without value-initialisation; page-locked (hipHostMalloc) unless
+// KVGPU_PINNED=0, so device-to-host copies of results are direct DMA.
+template <class T>
+struct HostArray {
+  T* p = nullptr;
+  size_t n = 0;
+  bool pinned = false;
+  HostArray() = default;
+  HostArray(const HostArray&) = delete;
+  HostArray& operator=(const HostArray&) = delete;
+  HostArray(HostArray&& o) noexcept : p(o.p), n(o.n), pinned(o.pinned) { o.p = nullptr; o.n = 0; }
+  ~HostArray() { release(); }
+  void alloc(size_t count) {
+    release();
+    n = count;
+    if (!count) return;
+    static const bool use_pinned = !(getenv("KVGPU_PINNED") && getenv("KVGPU_PINNED")[0] == '0');
+    if (use_pinned && hipHostMalloc((void**)&p, count * sizeof(T), hipHostMallocDefault) == hipSuccess) {
+      pinned = true;
+      return;
+    }
+    (void)hipGetLastError();
+    p = (T*)malloc(count * sizeof(T));
+    if (!p) throw std::bad_alloc();
+  }
+  void release() {
+    if (p) {
+      if (pinned) (void)hipHostFree(p);
+      else free(p);
+    }
+    p = nullptr;
+    n = 0;
+    pinned = false;
+  }
+  T* data() const { return p; }
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  T& operator[](size_t i) const { return p[i]; }
+};
+
+}  // namespace
+
+// Records of one device shard: FAIL / ERROR / SKIP pairs, rule-major and in
+// resource order (kv_rec_* kernels). Record of (rule, local res): base[rule] +
+// offs[rule][tile] + the record pairs before it in its tile (from the statuses).
+struct ResultPart {
+  std::shared_ptr<kv_batch> shard;  // the shard's batch (null: the result's own batch)
+  uint64_t lo = 0, n = 0;           // resources [lo, lo + n) of the result
+  uint32_t tiles = 0;
+  std::vector<uint32_t> offs;       // [rule][tile] exclusive record offsets within the rule
+  std::vector<uint64_t> base;       // [rule + 1] record offsets of the rules
+  HostArray<ErrRec8> rec;           // compact records
+  HostArray<ErrRec> recw;           // full records, parallel to rec (only when some record is wide)
+};
+
 struct kv_result {
   const kv_policyset* ps = nullptr;
   const kv_batch* b = nullptr;
   uint64_t n_rules = 0, n_res = 0;
-  std::vector<uint8_t> status;
-  std::vector<ErrRec8> err8;  // compact records of FAIL / ERROR / SKIP pairs
-  std::vector<ErrRec> errw;   // full records (only those flagged ERR8_WIDE are meaningful)
-  bool has_err() const { return !err8.empty(); }
-  ErrRec err(size_t o) const {
-    const ErrRec8 c = err8[o];
-    if ((c.w0 & ERR8_WIDE) && o < errw.size()) return errw[o];
+  HostArray<uint8_t> status;        // [rule][res]
+  std::vector<ResultPart> parts;    // by resource range
+  bool errors = false;              // KV_MODE_ERRORS: records fetched
+  std::vector<int64_t> counts;
+  std::vector<int64_t> scope_counts;  // [scope][rule][KV_HIST] (KV_MODE_SCOPES)
+  double kernel_ms = 0;
+  uint32_t mode = 0;
+  // bulk failure export (kv_result_failures), built on first use
+  std::once_flag fail_once;
+  std::vector<uint32_t> f_rule, f_path;
+  std::vector<uint64_t> f_res;
+  std::vector<std::string> f_paths;
+
+  bool has_err() const { return errors; }
+  const Batch& batch_of(const ResultPart& p) const { return p.shard ? p.shard->b : b->b; }
+  const ResultPart* part_of(uint64_t res) const {
+    for (const ResultPart& p : parts)
+      if (res >= p.lo && res < p.lo + p.n) return &p;
+    return nullptr;
+  }
+  static ErrRec decode(const ErrRec8& c) {
     ErrRec e{};
     e.kind_flags = (c.w0 & 15u) | (((c.w0 >> 4) & 3u) << 16);
     e.pnode = c.w0 >> 7;
@@ -135,10 +209,28 @@ struct kv_result {
     e.idx[3] = 0;
     return e;
   }
-  std::vector<int64_t> counts;
-  std::vector<int64_t> scope_counts;  // [scope][rule][KV_HIST] (KV_MODE_SCOPES)
-  double kernel_ms = 0;
-  uint32_t mode = 0;
+  // record index of pair (rule, res) within its part
+  uint64_t rec_index(const ResultPart& p, uint32_t rule, uint64_t res) const {
+    const uint64_t local = res - p.lo;
+    const uint64_t tile = local / KV_WG;
+    uint64_t idx = p.base[rule] + p.offs[(size_t)rule * p.tiles + tile];
+    const uint8_t* row = status.data() + (size_t)rule * n_res;
+    for (uint64_t q = p.lo + tile * KV_WG; q < res; q++) {
+      const uint8_t s = row[q];
+      idx += s == ST_FAIL || s == ST_ERROR || s == ST_SKIP;
+    }
+    return idx;
+  }
+  // error record of a FAIL / ERROR / SKIP pair, and the batch its node ids refer to
+  bool err(uint32_t rule, uint64_t res, ErrRec* e, const Batch** bt) const {
+    const ResultPart* p = part_of(res);
+    if (!p || !errors) return false;
+    const uint64_t i = rec_index(*p, rule, res);
+    if (i >= p->rec.size()) return false;
+    *e = (p->rec[i].w0 & ERR8_WIDE) && !p->recw.empty() ? p->recw[i] : decode(p->rec[i]);
+    *bt = &batch_of(*p);
+    return true;
+  }
 };
 
 namespace {
@@ -458,14 +550,18 @@ std::string error_message(const PolicySet& ps, const Batch& b, const ErrRec& e, 
 
 }  // namespace
 
-// A launch configuration with device-resident inputs and outputs.
-struct kv_session {
+namespace {
+
+// A launch configuration on one device over one batch (a whole batch or a
+// shard): device-resident inputs and output buffers.
+struct DevSession {
   kv_policyset* ps = nullptr;
   kv_batch* bt = nullptr;
   int device = 0;
   uint32_t mode = 0;
   uint64_t nrules = 0, nres = 0;
   DevBuf fflags, pview, st, er8, er, cn, scope, scn, ptab, mtab;
+  DevBuf r_offs, r_tot, r_base, r_out8, r_outw, r_wide;  // record compaction (fetch)
   uint32_t mt_words = 0, mt_entities = 0;
   uint32_t *mt_ns = nullptr, *mt_ann = nullptr, *mt_sel = nullptr;
   uint32_t nscopes = 0, nvals = 0;
@@ -476,7 +572,7 @@ struct kv_session {
   hipStream_t stream = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
 
-  kv_session(kv_policyset* p, kv_batch* b, const char* ctx_json, int dev, uint32_t m)
+  DevSession(kv_policyset* p, kv_batch* b, const char* ctx_json, int dev, uint32_t m)
       : ps(p), bt(b), device(dev), mode(m) {
     HIPCHK(hipSetDevice(device));
     DevPolicySet& dp = dev_ps(ps, device);
@@ -540,7 +636,7 @@ struct kv_session {
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
   }
-  ~kv_session() {
+  ~DevSession() {
     (void)hipSetDevice(device);
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
@@ -567,7 +663,7 @@ struct kv_session {
     HIPCHK(hipEventElapsedTime(&t, e0, e1));
     return t;
   }
-  // one launch per rule chunk of the specialized kernels, 256 resources per workgroup
+  // one launch per rule kernel of the specialized kernels, 256 resources per workgroup
   void launch_specialized() {
     if (nres == 0) return;
     const uint32_t blocks = (uint32_t)((nres + KV_WG - 1) / KV_WG);
@@ -587,10 +683,212 @@ struct kv_session {
     for (hipFunction_t f : dps->fns)
       HIPCHK(hipModuleLaunchKernel(f, blocks, 1, 1, KV_WG, 1, 1, 0, stream, args, nullptr));
   }
-  std::vector<int64_t> scope_counts() {
+  std::vector<int64_t> read_counts() {
+    HIPCHK(hipSetDevice(device));
+    std::vector<unsigned long long> c(nrules * KV_HIST);
+    if (!c.empty()) HIPCHK(hipMemcpy(c.data(), cn.p, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return std::vector<int64_t>(c.begin(), c.end());
+  }
+  std::vector<int64_t> read_scope_counts() {
+    HIPCHK(hipSetDevice(device));
     std::vector<unsigned long long> c((size_t)nscopes * nrules * KV_HIST);
     if (!c.empty()) HIPCHK(hipMemcpy(c.data(), scn.p, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return std::vector<int64_t>(c.begin(), c.end());
+  }
+  // statuses into rows [rule][lo, lo + nres) of the result's [rule][n_total] matrix, and
+  // the compacted error records of this shard
+  void fetch(kv_result* out, ResultPart* part, uint64_t lo, uint64_t n_total) {
+    HIPCHK(hipSetDevice(device));
+    if (O.status && (mode & (KV_MODE_STATUS | KV_MODE_ERRORS)) && nres && nrules)
+      HIPCHK(hipMemcpy2DAsync(out->status.data() + lo, n_total, st.p, nres, nres, nrules, hipMemcpyDeviceToHost,
+                              stream));
+    if (O.err8 && nres && nrules) {
+      const uint32_t tiles = (uint32_t)((nres + KV_WG - 1) / KV_WG);
+      part->tiles = tiles;
+      if (!r_offs.p) {
+        r_offs.alloc((size_t)nrules * tiles * sizeof(uint32_t), device);
+        r_tot.alloc(nrules * sizeof(unsigned long long), device);
+        r_base.alloc((nrules + 1) * sizeof(unsigned long long), device);
+        r_wide.alloc(sizeof(uint32_t), device);
+      }
+      HIPCHK(launch_rec_compact(O.status, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
+                                (unsigned long long*)r_tot.p, (unsigned long long*)r_base.p, nullptr, nullptr, nullptr,
+                                0, stream));
+      part->base.resize(nrules + 1);
+      part->offs.resize((size_t)nrules * tiles);
+      HIPCHK(hipMemcpyAsync(part->base.data(), r_base.p, part->base.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                            stream));
+      HIPCHK(hipMemcpyAsync(part->offs.data(), r_offs.p, part->offs.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                            stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      const uint64_t total = part->base[nrules];
+      if (r_out8.n < total * sizeof(ErrRec8)) r_out8.alloc(std::max<uint64_t>(total, 1) * sizeof(ErrRec8), device);
+      HIPCHK(hipMemsetAsync(r_wide.p, 0, sizeof(uint32_t), stream));
+      HIPCHK(launch_rec_compact(O.status, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
+                                nullptr, (unsigned long long*)r_base.p, (ErrRec8*)r_out8.p, nullptr,
+                                (uint32_t*)r_wide.p, 1, stream));
+      part->rec.alloc(total);
+      if (total)
+        HIPCHK(hipMemcpyAsync(part->rec.data(), r_out8.p, total * sizeof(ErrRec8), hipMemcpyDeviceToHost, stream));
+      uint32_t wide = 0;
+      HIPCHK(hipMemcpyAsync(&wide, r_wide.p, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      if (wide) {  // re-run the pass once writing full records (same statuses), compact those too
+        if (!er.p) er.alloc(nrules * nres * sizeof(ErrRec), device);
+        O.err = (ErrRec*)er.p;
+        O.full |= 4;
+        run(1);
+        O.full &= ~4u;
+        if (r_outw.n < total * sizeof(ErrRec)) r_outw.alloc(std::max<uint64_t>(total, 1) * sizeof(ErrRec), device);
+        HIPCHK(launch_rec_compact(O.status, O.err8, O.err, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
+                                  nullptr, (unsigned long long*)r_base.p, (ErrRec8*)r_out8.p, (ErrRec*)r_outw.p,
+                                  (uint32_t*)r_wide.p, 1, stream));
+        part->recw.alloc(total);
+        HIPCHK(hipMemcpyAsync(part->recw.data(), r_outw.p, total * sizeof(ErrRec), hipMemcpyDeviceToHost, stream));
+      }
+    }
+    HIPCHK(hipStreamSynchronize(stream));
+  }
+};
+
+// Sessions on the devices of a mask: contiguous resource shards, one host thread
+// + HIP stream per part, policy set replicated, per-rule (and per-scope) counts
+// summed over the parts by one RCCL all-reduce (distinct devices) when read.
+struct SessionSet {
+  kv_policyset* ps = nullptr;
+  kv_batch* bt = nullptr;
+  uint32_t mode = 0;
+  uint64_t nrules = 0, nres = 0;
+  std::vector<std::shared_ptr<kv_batch>> shards;           // empty: one part over the whole batch
+  std::vector<std::pair<uint64_t, uint64_t>> ranges;       // resource range of each part
+  std::vector<std::unique_ptr<DevSession>> parts;
+  std::vector<ncclComm_t> comms;                           // one per part (distinct devices only)
+  bool reduced = false;
+  std::vector<int64_t> counts_, scope_counts_;
+
+  SessionSet(kv_policyset* p, kv_batch* b, const char* ctx_json, const std::vector<int>& devices, uint32_t m)
+      : ps(p), bt(b), mode(m) {
+    nrules = ps->ps.rules.size();
+    nres = bt->b.res.size();
+    if (devices.size() == 1) {
+      ranges.push_back({0, nres});
+      parts.push_back(std::make_unique<DevSession>(ps, bt, ctx_json, devices[0], mode));
+      // KVGPU_RCCL_ALWAYS=1: reduce through a one-rank communicator too (exercises RCCL on one GPU)
+      if (getenv("KVGPU_RCCL_ALWAYS") && getenv("KVGPU_RCCL_ALWAYS")[0] == '1') {
+        comms.resize(1);
+        if (ncclCommInitAll(comms.data(), 1, devices.data()) != ncclSuccess) {
+          comms.clear();
+          throw HipError("ncclCommInitAll failed");
+        }
+      }
+      return;
+    }
+    ranges = shard_ranges(nres, (uint32_t)devices.size());
+    shards.resize(devices.size());
+    std::vector<std::thread> th;
+    std::vector<std::string> errs(devices.size());
+    for (size_t k = 0; k < devices.size(); k++)
+      th.emplace_back([&, k]() {
+        try {
+          auto sb = std::make_shared<kv_batch>();
+          sb->owner = ps;
+          make_shard(bt->b, ranges[k].first, ranges[k].second, &sb->b);
+          shards[k] = sb;
+        } catch (const std::exception& e) {
+          errs[k] = e.what();
+        }
+      });
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+      if (!e.empty()) throw std::runtime_error(e);
+    parts.resize(devices.size());
+    th.clear();
+    for (size_t k = 0; k < devices.size(); k++)
+      th.emplace_back([&, k]() {
+        try {
+          parts[k] = std::make_unique<DevSession>(ps, shards[k].get(), ctx_json, devices[k], mode);
+        } catch (const std::exception& e) {
+          errs[k] = e.what();
+        }
+      });
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+      if (!e.empty()) throw HipError(e);
+    std::vector<int> uniq(devices);
+    std::sort(uniq.begin(), uniq.end());
+    if (std::unique(uniq.begin(), uniq.end()) == uniq.end()) {  // RCCL needs one rank per device
+      comms.resize(devices.size());
+      if (ncclCommInitAll(comms.data(), (int)devices.size(), devices.data()) != ncclSuccess) {
+        comms.clear();
+        throw HipError("ncclCommInitAll failed");
+      }
+    }
+  }
+  ~SessionSet() {
+    for (ncclComm_t c : comms) (void)ncclCommDestroy(c);
+  }
+  template <class F>
+  void each(F f) {
+    if (parts.size() == 1) {
+      f(0);
+      return;
+    }
+    std::vector<std::thread> th;
+    std::vector<std::string> errs(parts.size());
+    for (size_t k = 0; k < parts.size(); k++)
+      th.emplace_back([&, k]() {
+        try {
+          f(k);
+        } catch (const std::exception& e) {
+          errs[k] = e.what();
+        }
+      });
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+      if (!e.empty()) throw HipError(e);
+  }
+  // `iters` passes on every part concurrently; the slowest part's HIP-event time
+  double run(int iters) {
+    std::vector<double> ms(parts.size(), 0.0);
+    each([&](size_t k) { ms[k] = parts[k]->run(iters); });
+    reduced = false;
+    return *std::max_element(ms.begin(), ms.end());
+  }
+  // counts of the last pass summed over the parts: RCCL all-reduce (ncclUint64, sum)
+  // of the device count arrays across distinct devices, else a host sum
+  void reduce() {
+    if (reduced) return;
+    counts_.assign(nrules * KV_HIST, 0);
+    scope_counts_.clear();
+    const bool scopes = (mode & KV_MODE_SCOPES) != 0;
+    if (!comms.empty()) {
+      if (ncclGroupStart() != ncclSuccess) throw HipError("ncclGroupStart failed");
+      for (size_t k = 0; k < parts.size(); k++) {
+        DevSession& d = *parts[k];
+        HIPCHK(hipSetDevice(d.device));
+        ncclAllReduce(d.cn.p, d.cn.p, nrules * KV_HIST, ncclUint64, ncclSum, comms[k], d.stream);
+        if (scopes)
+          ncclAllReduce(d.scn.p, d.scn.p, (size_t)d.nscopes * nrules * KV_HIST, ncclUint64, ncclSum, comms[k], d.stream);
+      }
+      if (ncclGroupEnd() != ncclSuccess) throw HipError("RCCL all-reduce failed");
+      for (auto& d : parts) {
+        HIPCHK(hipSetDevice(d->device));
+        HIPCHK(hipStreamSynchronize(d->stream));
+      }
+      counts_ = parts[0]->read_counts();
+      if (scopes) scope_counts_ = parts[0]->read_scope_counts();
+    } else {
+      for (auto& d : parts) {
+        std::vector<int64_t> c = d->read_counts();
+        for (size_t i = 0; i < c.size(); i++) counts_[i] += c[i];
+        if (scopes) {
+          std::vector<int64_t> sc = d->read_scope_counts();
+          if (scope_counts_.empty()) scope_counts_.assign(sc.size(), 0);
+          for (size_t i = 0; i < sc.size(); i++) scope_counts_[i] += sc[i];
+        }
+      }
+    }
+    reduced = true;
   }
   void fetch(kv_result* out, double ms) {
     out->ps = ps;
@@ -599,41 +897,40 @@ struct kv_session {
     out->n_res = nres;
     out->mode = mode;
     out->kernel_ms = ms;
-    std::vector<unsigned long long> c(nrules * KV_HIST);
-    if (nrules) HIPCHK(hipMemcpy(c.data(), cn.p, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    out->counts.assign(c.begin(), c.end());
-    if (mode & KV_MODE_SCOPES) out->scope_counts = scope_counts();
-    if (O.status && (mode & (KV_MODE_STATUS | KV_MODE_ERRORS))) {
-      out->status.resize(nrules * nres);
-      if (!out->status.empty()) HIPCHK(hipMemcpy(out->status.data(), st.p, out->status.size(), hipMemcpyDeviceToHost));
+    reduce();
+    out->counts = counts_;
+    if (mode & KV_MODE_SCOPES) out->scope_counts = scope_counts_;
+    if (parts[0]->O.status && (mode & (KV_MODE_STATUS | KV_MODE_ERRORS))) {
+      HIPCHK(hipSetDevice(parts[0]->device));
+      out->status.alloc(nrules * nres);
     }
-    if (O.err8) {
-      out->err8.resize(nrules * nres);
-      if (!out->err8.empty())
-        HIPCHK(hipMemcpy(out->err8.data(), er8.p, out->err8.size() * sizeof(ErrRec8), hipMemcpyDeviceToHost));
-      bool wide = false;
-      for (size_t o = 0; o < out->err8.size() && !wide; o++) {
-        const uint8_t s_ = out->status[o];
-        wide = (s_ == ST_FAIL || s_ == ST_ERROR || s_ == ST_SKIP) && (out->err8[o].w0 & ERR8_WIDE);
-      }
-      if (wide) {  // re-run the pass once writing full records (same statuses), keep those
-        if (!er.p) er.alloc(nrules * nres * sizeof(ErrRec), device);
-        O.err = (ErrRec*)er.p;
-        O.full |= 4;
-        run(1);
-        O.full &= ~4u;
-        out->errw.resize(nrules * nres);
-        HIPCHK(hipMemcpy(out->errw.data(), er.p, out->errw.size() * sizeof(ErrRec), hipMemcpyDeviceToHost));
-      }
+    out->errors = (mode & KV_MODE_ERRORS) != 0;
+    out->parts.resize(parts.size());
+    for (size_t k = 0; k < parts.size(); k++) {
+      out->parts[k].lo = ranges[k].first;
+      out->parts[k].n = ranges[k].second - ranges[k].first;
+      if (!shards.empty()) out->parts[k].shard = shards[k];
     }
+    each([&](size_t k) { parts[k]->fetch(out, &out->parts[k], ranges[k].first, nres); });
   }
 };
 
-namespace {
+// devices of a mask, each repeated KVGPU_SHARDS_PER_DEVICE times (logical shards: the
+// multi-device path on one GPU, for tests; counts are then summed on the host)
+std::vector<int> mask_devices(uint32_t mask) {
+  std::vector<int> d;
+  int per = 1;
+  if (const char* e = getenv("KVGPU_SHARDS_PER_DEVICE")) per = std::max(1, atoi(e));
+  for (int i = 0; i < 32; i++)
+    if (mask & (1u << i))
+      for (int k = 0; k < per; k++) d.push_back(i);
+  return d;
+}
 
-void run(kv_policyset* ps, kv_batch* bt, const char* ctx_json, int device, uint32_t mode, kv_result* out, int warmup,
-         int iters, double* ms) {
-  kv_session s(ps, bt, ctx_json, device, mode);
+void run(kv_policyset* ps, kv_batch* bt, const char* ctx_json, const std::vector<int>& devices, uint32_t mode,
+         kv_result* out, int warmup, int iters, double* ms) {
+  if (devices.empty()) throw std::runtime_error("empty device mask");
+  SessionSet s(ps, bt, ctx_json, devices, mode);
   if (warmup > 0) s.run(warmup);
   int n = std::max(iters, 1);
   double t = s.run(n) / n;
@@ -642,6 +939,12 @@ void run(kv_policyset* ps, kv_batch* bt, const char* ctx_json, int device, uint3
 }
 
 }  // namespace
+
+struct kv_session {
+  SessionSet set;
+  kv_session(kv_policyset* p, kv_batch* b, const char* ctx_json, const std::vector<int>& devices, uint32_t m)
+      : set(p, b, ctx_json, devices, m) {}
+};
 
 extern "C" {
 
@@ -763,7 +1066,29 @@ int kv_validate(const kv_policyset* ps, const kv_batch* b, const char* ctx_json,
   try {
     auto* r = new kv_result();
     try {
-      run(const_cast<kv_policyset*>(ps), const_cast<kv_batch*>(b), ctx_json, device, mode, r, 0, 1, nullptr);
+      run(const_cast<kv_policyset*>(ps), const_cast<kv_batch*>(b), ctx_json, {device}, mode, r, 0, 1, nullptr);
+    } catch (...) {
+      delete r;
+      throw;
+    }
+    *out = r;
+    return 0;
+  } catch (const HipError& e) {
+    return fail(err, KV_E_DEVICE, e.what());
+  } catch (const std::exception& e) {
+    return fail(err, KV_E_PARSE, e.what());
+  }
+}
+
+int kv_validate_devices(const kv_policyset* ps, const kv_batch* b, const char* ctx_json, uint32_t device_mask,
+                        uint32_t mode, kv_result** out, kv_error** err) {
+  if (!ps || !b || !out) return fail(err, KV_E_INVALID, "null argument");
+  if (b->owner != ps) return fail(err, KV_E_INVALID, "batch was ingested for a different policy set");
+  try {
+    auto* r = new kv_result();
+    try {
+      run(const_cast<kv_policyset*>(ps), const_cast<kv_batch*>(b), ctx_json, mask_devices(device_mask), mode, r, 0, 1,
+          nullptr);
     } catch (...) {
       delete r;
       throw;
@@ -781,7 +1106,7 @@ int kv_bench(const kv_policyset* ps, const kv_batch* b, const char* ctx_json, in
              int iters, double* ms_per_iter, kv_error** err) {
   if (!ps || !b || !ms_per_iter) return fail(err, KV_E_INVALID, "null argument");
   try {
-    run(const_cast<kv_policyset*>(ps), const_cast<kv_batch*>(b), ctx_json, device, mode, nullptr, warmup, iters,
+    run(const_cast<kv_policyset*>(ps), const_cast<kv_batch*>(b), ctx_json, {device}, mode, nullptr, warmup, iters,
         ms_per_iter);
     return 0;
   } catch (const HipError& e) {
@@ -829,7 +1154,10 @@ int kv_result_path(const kv_result* r, uint32_t rule, uint64_t res, char* buf, s
   if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
   size_t o = (size_t)rule * r->n_res + res;
   if (r->status[o] != ST_FAIL) return KV_E_INVALID;
-  std::string p = render_path(r->ps->ps, r->b->b, r->err(o));
+  ErrRec e;
+  const Batch* bt = nullptr;
+  if (!r->err(rule, res, &e, &bt)) return KV_E_INVALID;
+  std::string p = render_path(r->ps->ps, *bt, e);
   if (buf && cap) {
     size_t n = std::min(cap - 1, p.size());
     memcpy(buf, p.data(), n);
@@ -841,7 +1169,11 @@ int kv_result_path(const kv_result* r, uint32_t rule, uint64_t res, char* buf, s
 int kv_result_error(const kv_result* r, uint32_t rule, uint64_t res, uint32_t* kind, uint32_t* flags) {
   if (!r || !r->has_err()) return KV_E_INVALID;
   if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
-  const ErrRec e = r->err((size_t)rule * r->n_res + res);
+  const uint8_t st = r->status[(size_t)rule * r->n_res + res];
+  if (st != ST_FAIL && st != ST_ERROR && st != ST_SKIP) return KV_E_INVALID;
+  ErrRec e;
+  const Batch* bt = nullptr;
+  if (!r->err(rule, res, &e, &bt)) return KV_E_INVALID;
   if (kind) *kind = e.kind_flags & 0xFFFF;
   if (flags) *flags = e.kind_flags >> 16;
   return 0;
@@ -858,7 +1190,10 @@ int kv_result_error_message(const kv_result* r, uint32_t rule, uint64_t res, con
   try {
     JDoc doc;
     parse_json(resource_json, len, NUM_UNSTRUCTURED, &doc);
-    m = error_message(r->ps->ps, r->b->b, r->err(o), doc);
+    ErrRec e;
+    const Batch* bt = nullptr;
+    if (!r->err(rule, res, &e, &bt)) return KV_E_INVALID;
+    m = error_message(r->ps->ps, *bt, e, doc);
   } catch (const std::exception&) {
     return KV_E_PARSE;
   }
@@ -873,12 +1208,79 @@ int kv_result_error_message(const kv_result* r, uint32_t rule, uint64_t res, con
 
 double kv_result_kernel_ms(const kv_result* r) { return r ? r->kernel_ms : -1.0; }
 
+int kv_result_failures(const kv_result* cr, uint64_t* n, const uint32_t** rule, const uint64_t** res,
+                       const uint32_t** path_id) {
+  if (!cr || !cr->has_err() || !n) return KV_E_INVALID;
+  kv_result* r = const_cast<kv_result*>(cr);
+  try {
+    std::call_once(r->fail_once, [r]() {
+      // one pass over the statuses: records come rule-major, in resource order per part
+      std::unordered_map<uint64_t, uint32_t> compact;      // (path pnode, packed indices) -> path id
+      std::unordered_map<std::string, uint32_t> rendered;  // wide records: by rendered path
+      const PolicySet& ps = r->ps->ps;
+      for (uint32_t rl = 0; rl < r->n_rules; rl++) {
+        const uint8_t* row = r->status.data() + (size_t)rl * r->n_res;
+        for (const ResultPart& p : r->parts) {
+          uint64_t i = p.base[rl];
+          for (uint64_t q = p.lo; q < p.lo + p.n; q++) {
+            const uint8_t st = row[q];
+            if (st != ST_FAIL && st != ST_ERROR && st != ST_SKIP) continue;
+            uint32_t id = KV_PATH_NONE;
+            if (st == ST_FAIL) {
+              const ErrRec8 c = p.rec[i];
+              if ((c.w0 & ERR8_WIDE) && !p.recw.empty()) {
+                const std::string path = render_path(ps, r->batch_of(p), p.recw[i]);
+                auto it = rendered.find(path);
+                if (it == rendered.end()) {
+                  it = rendered.emplace(path, (uint32_t)r->f_paths.size()).first;
+                  r->f_paths.push_back(path);
+                }
+                id = it->second;
+              } else {
+                const ErrRec e = kv_result::decode(c);
+                const uint64_t key = (uint64_t)path_pnode(ps, e) << 32 | c.w1;
+                auto it = compact.find(key);
+                if (it == compact.end()) {
+                  const std::string path = render_path(ps, r->batch_of(p), e);
+                  auto jt = rendered.find(path);
+                  if (jt == rendered.end()) {
+                    jt = rendered.emplace(path, (uint32_t)r->f_paths.size()).first;
+                    r->f_paths.push_back(path);
+                  }
+                  it = compact.emplace(key, jt->second).first;
+                }
+                id = it->second;
+              }
+            }
+            r->f_rule.push_back(rl);
+            r->f_res.push_back(q);
+            r->f_path.push_back(id);
+            i++;
+          }
+        }
+      }
+    });
+  } catch (const std::exception&) {
+    return KV_E_NOMEM;
+  }
+  *n = r->f_rule.size();
+  if (rule) *rule = r->f_rule.data();
+  if (res) *res = r->f_res.data();
+  if (path_id) *path_id = r->f_path.data();
+  return 0;
+}
+
+const char* kv_path_string(const kv_result* r, uint32_t path_id) {
+  if (!r || path_id >= r->f_paths.size()) return nullptr;
+  return r->f_paths[path_id].c_str();
+}
+
 int kv_session_create(const kv_policyset* ps, const kv_batch* b, const char* ctx_json, int device, uint32_t mode,
                       kv_session** out, kv_error** err) {
   if (!ps || !b || !out) return fail(err, KV_E_INVALID, "null argument");
   if (b->owner != ps) return fail(err, KV_E_INVALID, "batch was ingested for a different policy set");
   try {
-    *out = new kv_session(const_cast<kv_policyset*>(ps), const_cast<kv_batch*>(b), ctx_json, device, mode);
+    *out = new kv_session(const_cast<kv_policyset*>(ps), const_cast<kv_batch*>(b), ctx_json, {device}, mode);
     return 0;
   } catch (const HipError& e) {
     return fail(err, KV_E_DEVICE, e.what());
@@ -887,13 +1289,52 @@ int kv_session_create(const kv_policyset* ps, const kv_batch* b, const char* ctx
   }
 }
 
+int kv_session_create_devices(const kv_policyset* ps, const kv_batch* b, const char* ctx_json, uint32_t device_mask,
+                              uint32_t mode, kv_session** out, kv_error** err) {
+  if (!ps || !b || !out) return fail(err, KV_E_INVALID, "null argument");
+  if (b->owner != ps) return fail(err, KV_E_INVALID, "batch was ingested for a different policy set");
+  try {
+    const std::vector<int> devs = mask_devices(device_mask);
+    if (devs.empty()) return fail(err, KV_E_INVALID, "empty device mask");
+    *out = new kv_session(const_cast<kv_policyset*>(ps), const_cast<kv_batch*>(b), ctx_json, devs, mode);
+    return 0;
+  } catch (const HipError& e) {
+    return fail(err, KV_E_DEVICE, e.what());
+  } catch (const std::exception& e) {
+    return fail(err, KV_E_PARSE, e.what());
+  }
+}
+
+int kv_session_parts(const kv_session* s, uint32_t* n_parts) {
+  if (!s || !n_parts) return KV_E_INVALID;
+  *n_parts = (uint32_t)s->set.parts.size();
+  return 0;
+}
+
+int kv_session_fetch(kv_session* s, kv_result** out, kv_error** err) {
+  if (!s || !out) return fail(err, KV_E_INVALID, "null argument");
+  try {
+    auto* r = new kv_result();
+    try {
+      s->set.fetch(r, 0.0);
+    } catch (...) {
+      delete r;
+      throw;
+    }
+    *out = r;
+    return 0;
+  } catch (const std::exception& e) {
+    return fail(err, KV_E_DEVICE, e.what());
+  }
+}
+
 int kv_session_run(kv_session* s, int iters, double* event_ms, kv_error** err) {
   if (!s || iters < 0) return fail(err, KV_E_INVALID, "bad argument");
   try {
-    double t = s->run(iters);
+    double t = s->set.run(iters);
     if (event_ms) *event_ms = t;
     return 0;
-  } catch (const HipError& e) {
+  } catch (const std::exception& e) {
     return fail(err, KV_E_DEVICE, e.what());
   }
 }
@@ -901,22 +1342,21 @@ int kv_session_run(kv_session* s, int iters, double* event_ms, kv_error** err) {
 int kv_session_counts(kv_session* s, int64_t* counts) {
   if (!s || !counts) return KV_E_INVALID;
   try {
-    std::vector<unsigned long long> c(s->nrules * KV_HIST);
-    if (s->nrules) HIPCHK(hipMemcpy(c.data(), s->cn.p, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < c.size(); i++) counts[i] = (int64_t)c[i];
+    s->set.reduce();
+    std::copy(s->set.counts_.begin(), s->set.counts_.end(), counts);
     return 0;
-  } catch (const HipError&) {
+  } catch (const std::exception&) {
     return KV_E_DEVICE;
   }
 }
 
 int kv_session_scope_counts(kv_session* s, int64_t* counts) {
-  if (!s || !counts || !(s->mode & KV_MODE_SCOPES)) return KV_E_INVALID;
+  if (!s || !counts || !(s->set.mode & KV_MODE_SCOPES)) return KV_E_INVALID;
   try {
-    std::vector<int64_t> c = s->scope_counts();
-    std::copy(c.begin(), c.end(), counts);
+    s->set.reduce();
+    std::copy(s->set.scope_counts_.begin(), s->set.scope_counts_.end(), counts);
     return 0;
-  } catch (const HipError&) {
+  } catch (const std::exception&) {
     return KV_E_DEVICE;
   }
 }

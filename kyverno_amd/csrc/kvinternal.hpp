@@ -189,6 +189,12 @@ std::vector<uint32_t> fold_filters(const PolicySet& ps, const char* ctx_json);
 void key_table(const PolicySet& ps, const Batch& b, std::vector<uint32_t>* off, std::vector<uint32_t>* len,
                std::string* ks);
 
+// Resource shards of a batch (kvshard.cpp): resources [lo, hi), lo a multiple of
+// KV_LANES; rows rebased, values renumbered onto those the shard references.
+void make_shard(const Batch& b, uint64_t lo, uint64_t hi, Batch* out);
+// G contiguous ranges [k*N/G, (k+1)*N/G) of N resources, cut at 64-resource boundaries
+std::vector<std::pair<uint64_t, uint64_t>> shard_ranges(uint64_t n, uint32_t g);
+
 // Go-semantics helpers shared by compiler and ingest
 bool wildcard_match_host(std::string_view pattern, std::string_view name);
 bool valid_label_key(const std::string& k);

@@ -352,6 +352,120 @@ hipError_t launch_mtab(const DevPS* P, const DevBatch* B, uint32_t words, uint32
 }  // namespace kv
 
 // ---------------------------------------------------------------------------
+// Error-record compaction (fetch time, outside the timed passes): the rule
+// kernels write an 8 B record per FAIL / ERROR / SKIP pair at its dense
+// [rule][res] slot; these kernels gather them, rule-major and in resource order,
+// into a compact array, so only the records cross PCIe. Tiles of KV_WG
+// resources: count -> per-rule exclusive scan over tiles -> rule bases -> scatter.
+namespace kv {
+
+__device__ __forceinline__ bool has_record(uint8_t s) { return s == ST_FAIL || s == ST_ERROR || s == ST_SKIP; }
+
+__global__ __launch_bounds__(KV_WG) void kv_rec_count_kernel(const uint8_t* __restrict__ status, uint32_t n_res,
+                                                              uint32_t tiles, uint32_t* __restrict__ counts) {
+  __shared__ uint32_t s_w[KV_WG / 64];
+  const uint32_t rule = blockIdx.y, r = blockIdx.x * KV_WG + threadIdx.x;
+  const bool f = r < n_res && has_record(status[(size_t)rule * n_res + r]);
+  const uint64_t m = __ballot(f);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < KV_WG / 64; w++) t += s_w[w];
+    counts[(size_t)rule * tiles + blockIdx.x] = t;
+  }
+}
+
+// in place exclusive scan of counts[rule][0..tiles); totals[rule] = the rule's records
+__global__ __launch_bounds__(KV_WG) void kv_rec_scan_kernel(uint32_t* __restrict__ counts, uint32_t tiles,
+                                                             unsigned long long* __restrict__ totals) {
+  __shared__ uint32_t s_v[KV_WG];
+  uint32_t* c = counts + (size_t)blockIdx.x * tiles;
+  uint32_t carry = 0;
+  for (uint32_t b = 0; b < tiles; b += KV_WG) {
+    const uint32_t i = b + threadIdx.x;
+    const uint32_t v = i < tiles ? c[i] : 0u;
+    s_v[threadIdx.x] = v;
+    __syncthreads();
+    for (uint32_t o = 1; o < KV_WG; o <<= 1) {  // Hillis-Steele inclusive scan
+      const uint32_t x = threadIdx.x >= o ? s_v[threadIdx.x - o] : 0u;
+      __syncthreads();
+      s_v[threadIdx.x] += x;
+      __syncthreads();
+    }
+    if (i < tiles) c[i] = carry + s_v[threadIdx.x] - v;
+    carry += s_v[KV_WG - 1];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) totals[blockIdx.x] = carry;
+}
+
+// base[rule] = records of rules < rule; base[n_rules] = all records (one workgroup)
+__global__ __launch_bounds__(KV_WG) void kv_rec_base_kernel(const unsigned long long* __restrict__ totals,
+                                                             uint32_t n_rules, unsigned long long* __restrict__ base) {
+  __shared__ unsigned long long s_v[KV_WG];
+  unsigned long long carry = 0;
+  for (uint32_t b = 0; b < n_rules; b += KV_WG) {
+    const uint32_t i = b + threadIdx.x;
+    const unsigned long long v = i < n_rules ? totals[i] : 0ull;
+    s_v[threadIdx.x] = v;
+    __syncthreads();
+    for (uint32_t o = 1; o < KV_WG; o <<= 1) {
+      const unsigned long long x = threadIdx.x >= o ? s_v[threadIdx.x - o] : 0ull;
+      __syncthreads();
+      s_v[threadIdx.x] += x;
+      __syncthreads();
+    }
+    if (i < n_rules) base[i] = carry + s_v[threadIdx.x] - v;
+    carry += s_v[KV_WG - 1];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) base[n_rules] = carry;
+}
+
+__global__ __launch_bounds__(KV_WG) void kv_rec_scatter_kernel(const uint8_t* __restrict__ status,
+                                                                const ErrRec8* __restrict__ err8,
+                                                                const ErrRec* __restrict__ errw, uint32_t n_res,
+                                                                uint32_t tiles, const uint32_t* __restrict__ offs,
+                                                                const unsigned long long* __restrict__ base,
+                                                                ErrRec8* __restrict__ out8, ErrRec* __restrict__ outw,
+                                                                uint32_t* __restrict__ wide) {
+  __shared__ uint32_t s_w[KV_WG / 64];
+  const uint32_t rule = blockIdx.y, r = blockIdx.x * KV_WG + threadIdx.x, lane = threadIdx.x & 63;
+  const size_t o = (size_t)rule * n_res + r;
+  const bool f = r < n_res && has_record(status[o]);
+  const uint64_t m = __ballot(f);
+  if (lane == 0) s_w[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+  __syncthreads();
+  if (!f) return;
+  uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+  for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) rank += s_w[w];
+  const unsigned long long idx = base[rule] + offs[(size_t)rule * tiles + blockIdx.x] + rank;
+  const ErrRec8 e = err8[o];
+  out8[idx] = e;
+  if (outw) outw[idx] = errw[o];
+  if (e.w0 & ERR8_WIDE) atomicOr(wide, 1u);
+}
+
+hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const ErrRec* errw, uint32_t n_res,
+                              uint32_t n_rules, uint32_t* offs, unsigned long long* totals, unsigned long long* base,
+                              ErrRec8* out8, ErrRec* outw, uint32_t* wide, int phase, hipStream_t stream) {
+  if (n_res == 0 || n_rules == 0) return hipSuccess;
+  const uint32_t tiles = (n_res + KV_WG - 1) / KV_WG;
+  if (phase == 0) {  // offsets and bases
+    hipLaunchKernelGGL(kv_rec_count_kernel, dim3(tiles, n_rules), dim3(KV_WG), 0, stream, status, n_res, tiles, offs);
+    hipLaunchKernelGGL(kv_rec_scan_kernel, dim3(n_rules), dim3(KV_WG), 0, stream, offs, tiles, totals);
+    hipLaunchKernelGGL(kv_rec_base_kernel, dim3(1), dim3(KV_WG), 0, stream, totals, n_rules, base);
+  } else {
+    hipLaunchKernelGGL(kv_rec_scatter_kernel, dim3(tiles, n_rules), dim3(KV_WG), 0, stream, status, err8, errw, n_res,
+                       tiles, offs, base, out8, outw, wide);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace kv
+
+// ---------------------------------------------------------------------------
 // Per-scope PolicyReport counts: counts[scope][rule][KV_HIST] from status[rule][res]
 // and the namespace index of every resource (scope = namespace, "" = cluster
 // scope), the summaries of pkg/kyverno/apply/report.go:76-179 and

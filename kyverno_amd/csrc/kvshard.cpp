@@ -1,0 +1,76 @@
+// Resource shards of an ingested batch for multi-device evaluation
+// (kv_validate_devices / kv_session_create_devices): resources
+// [lo, hi) with lo a multiple of KV_LANES, so the wave-group layout, lanes and
+// every kernel stay unchanged on the shard. The shard's node rows are rebased
+// to start at 0 and its scalar cells are renumbered onto the values the shard
+// references (kept in global order, so the value-predicate table of each device
+// covers only its own values, still grouped by position class). The string heap,
+// label / annotation lists, namespace tables and key ids stay global.
+#include <algorithm>
+#include <stdexcept>
+
+#include "kvinternal.hpp"
+
+namespace kvh {
+
+using namespace kv;
+
+void make_shard(const Batch& b, uint64_t lo, uint64_t hi, Batch* out) {
+  if (lo % KV_LANES != 0 || lo > hi || hi > b.res.size())
+    throw std::runtime_error("shard: range must start at a multiple of 64 resources");
+  Batch& s = *out;
+  s = Batch();
+  const uint64_t row_lo = lo < b.res.size() ? b.res[lo].root : b.n_rows;
+  const uint64_t row_hi = hi < b.res.size() ? b.res[hi].root : b.n_rows;
+  s.n_rows = row_hi - row_lo;
+  // values referenced by the shard, renumbered in global order
+  std::vector<uint32_t> vmap(b.vals.size(), 0xFFFFFFFFu);
+  const Node* src = b.nodes.data() + row_lo * KV_LANES;
+  const size_t ncell = (size_t)s.n_rows * KV_LANES;
+  auto scalar = [](uint32_t t) { return t == NT_BOOL || t == NT_INT || t == NT_FLOAT || t == NT_STR; };
+  for (size_t i = 0; i < ncell; i++)
+    if (scalar(node_type(src[i].kt))) vmap[src[i].a] = 0;
+  for (size_t v = 0; v < vmap.size(); v++)
+    if (vmap[v] == 0) {
+      vmap[v] = (uint32_t)s.vals.size();
+      s.vals.push_back(b.vals[v]);
+    }
+  s.nodes.resize(ncell);
+  for (size_t i = 0; i < ncell; i++) {
+    Node n = src[i];
+    const uint32_t t = node_type(n.kt);
+    if (t == NT_MAP || t == NT_ARR) n.a -= (uint32_t)row_lo;
+    else if (scalar(t)) n.a = vmap[n.a];
+    if (n.kt | n.a | n.b | n.c) s.cells_used++;
+    s.nodes[i] = n;
+  }
+  s.res.assign(b.res.begin() + lo, b.res.begin() + hi);
+  for (Res& r : s.res) r.root -= (uint32_t)row_lo;
+  s.kvs = b.kvs;
+  s.strs = b.strs;
+  s.dyn_keys = b.dyn_keys;
+  s.namespaces = b.namespaces;
+  s.nsms = b.nsms;
+  s.lsets = b.lsets;
+  s.asets = b.asets;
+  s.ns_labels = b.ns_labels;
+  s.ns_bits = b.ns_bits;
+  s.ns_words = b.ns_words;
+  s.bytes_referenced = s.cells_used * sizeof(Node) + s.vals.size() * sizeof(Val) + s.res.size() * sizeof(Res) +
+                       s.kvs.size() * sizeof(KV) + s.strs.size() + s.nsms.size() * sizeof(StrRef) +
+                       (s.lsets.size() + s.asets.size()) * sizeof(KVSet);
+}
+
+std::vector<std::pair<uint64_t, uint64_t>> shard_ranges(uint64_t n, uint32_t g) {
+  // contiguous ranges [k*N/G, (k+1)*N/G), cut at wave-group (64 resource) boundaries
+  std::vector<std::pair<uint64_t, uint64_t>> out;
+  const uint64_t groups = (n + KV_LANES - 1) / KV_LANES;
+  for (uint32_t k = 0; k < g; k++) {
+    const uint64_t a = std::min<uint64_t>(n, groups * k / g * KV_LANES);
+    const uint64_t e = std::min<uint64_t>(n, groups * (k + 1) / g * KV_LANES);
+    out.push_back({a, e});
+  }
+  return out;
+}
+
+}  // namespace kvh

@@ -59,7 +59,9 @@ def build(policies, workdir: str, env: dict | None = None, opt: str = "-O1", ext
     genv.update(KVGPU_JIT_DUMP=src, KVGPU_JIT_SKIP_COMPILE="1")
     _with_env(genv, lambda: batch.PolicySet(policies, specialize=True))
     data = open(src, "rb").read()
-    tag = hashlib.sha1(data + json.dumps(env or {}, sort_keys=True).encode() + opt.encode() + " ".join(extra).encode()).hexdigest()[:12]
+    host = hashlib.sha1(open(HOSTLIB, "rb").read()).hexdigest()  # the driver / host objects it links
+    tag = hashlib.sha1(data + json.dumps(env or {}, sort_keys=True).encode() + opt.encode() +
+                       " ".join(extra).encode() + host.encode()).hexdigest()[:12]
     exe = os.path.join(workdir, f"kvemu_{tag}")
     if not os.path.exists(exe):
         obj = os.path.join(workdir, f"gen_{tag}.o")

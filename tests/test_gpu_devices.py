@@ -1,0 +1,98 @@
+"""Multi-device evaluation behind the C ABI (kv_validate_devices / kv_session_create_devices,
+SURVEY.md §8b "Threading", §8e): contiguous resource shards, one host thread + HIP stream per
+part, policy set replicated, counts summed over the parts with RCCL inside libkvgpu.
+
+One GPU box: the shard path runs as logical shards on device 0 (KVGPU_SHARDS_PER_DEVICE, counts
+summed on the host), and the RCCL reduction runs through a one-rank communicator
+(KVGPU_RCCL_ALWAYS). Both must reproduce the single-device result exactly.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _env(**kw):
+    class E:
+        def __enter__(self):
+            self.old = {k: os.environ.get(k) for k in kw}
+            os.environ.update({k: str(v) for k, v in kw.items()})
+
+        def __exit__(self, *a):
+            for k, v in self.old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+    return E()
+
+
+@pytest.fixture(scope="module")
+def c5():
+    from kyverno_amd import batch, workloads
+
+    ps = batch.PolicySet(workloads.c5_policies(), specialize=True)
+    data = batch.synth(workloads.SEED + 31, 20_000, 1)
+    b = batch.Batch(ps, data)
+    return ps, b, data
+
+
+@pytest.mark.parametrize("shards", [2, 4, 8])
+def test_logical_shards_match_single_device(c5, shards):
+    from kyverno_amd import batch
+
+    ps, b, data = c5
+    mode = batch.MODE_STATUS | batch.MODE_ERRORS | batch.MODE_SCOPES
+    one = batch.validate(ps, b, mode=mode)
+    with _env(KVGPU_SHARDS_PER_DEVICE=shards):
+        many = batch.validate(ps, b, mode=mode, device_mask=1)
+    assert np.array_equal(one.status, many.status)
+    assert np.array_equal(one.counts, many.counts)
+    assert np.array_equal(one.scope_counts, many.scope_counts)
+    fails = np.argwhere(one.status == 1)
+    for a, c in fails[np.random.default_rng(shards).choice(len(fails), 300, replace=False)]:
+        assert one.path(int(a), int(c)) == many.path(int(a), int(c))
+    r1, q1, p1, s1 = one.failures()
+    r2, q2, p2, s2 = many.failures()
+    assert np.array_equal(r1, r2) and np.array_equal(q1, q2)
+    assert [s1[i] if i != 0xFFFFFFFF else None for i in p1[:5000]] == \
+           [s2[i] if i != 0xFFFFFFFF else None for i in p2[:5000]]
+
+
+def test_rccl_count_reduction(c5):
+    from kyverno_amd import batch
+
+    ps, b, _ = c5
+    mode = batch.MODE_COUNTS | batch.MODE_SCOPES
+    ref = batch.validate(ps, b, mode=mode)
+    with _env(KVGPU_RCCL_ALWAYS=1):
+        s = batch.Session(ps, b, mode=mode, device_mask=1)
+        s.run(3)
+        assert np.array_equal(s.counts(), ref.counts)
+        assert np.array_equal(s.scope_counts(len(b.namespaces)), ref.scope_counts)
+
+
+def test_session_fetch_and_bulk_failures(c5):
+    """kv_session_fetch returns the last pass like kv_validate; kv_result_failures lists every
+    FAIL / ERROR / SKIP pair with deduplicated failing-path ids matching kv_result_path."""
+    from kyverno_amd import batch
+
+    ps, b, _ = c5
+    mode = batch.MODE_STATUS | batch.MODE_ERRORS
+    ref = batch.validate(ps, b, mode=mode)
+    with _env(KVGPU_SHARDS_PER_DEVICE=3):
+        s = batch.Session(ps, b, mode=mode, device_mask=1)
+        assert s.n_parts == 3
+        s.run(2)
+        r = s.fetch()
+    assert np.array_equal(r.status, ref.status)
+    rule, res, pid, paths = r.failures()
+    st = ref.status
+    assert len(rule) == int(((st == 1) | (st == 3) | (st == 4)).sum())
+    assert np.array_equal(st[rule, res] != 1, pid == 0xFFFFFFFF)
+    idx = np.random.default_rng(5).choice(np.nonzero(pid != 0xFFFFFFFF)[0], 400, replace=False)
+    for i in idx:
+        assert paths[pid[i]] == ref.path(int(rule[i]), int(res[i]))
+    assert len(paths) < 1000  # paths are shared by pairs, not rendered per pair

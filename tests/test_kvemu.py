@@ -77,3 +77,30 @@ def test_generated_kernels_match_table(orc):
         assert np.array_equal(st, ost), (c["src"], st[:, 0].tolist(), ost[:, 0].tolist())
         want = 5 if c["errors_expected"] else 0
         assert (st[first[i]:first[i + 1], 0] == want).all(), c["src"]
+
+
+@pytest.mark.parametrize("shards", [2, 4, 8])
+def test_sharded_evaluation_matches_unsharded(orc, shards):
+    """The multi-device path's resource shards (kvshard.cpp: contiguous 64-aligned ranges, rows
+    rebased, values renumbered) through the generated kernels give the unsharded statuses and error
+    records, and per-rule counts summed over the shards equal the unsharded counts (what the RCCL
+    all-reduce of kv_validate_devices adds up)."""
+    from kyverno_amd import workloads
+
+    pols = workloads.c5_policies()
+    ress = _synth(workloads.SEED + 21, 1000, 1)
+    data = b"\n".join(json.dumps(r).encode() for r in ress)
+    exe = kvemu.build(pols, os.path.join(WORK, "c5"))
+    st1, rec1 = kvemu.run(exe, data, os.path.join(WORK, "c5"))
+    stg, recg = kvemu.run(exe, data, os.path.join(WORK, "c5"), env={"KVEMU_SHARDS": shards})
+    assert np.array_equal(st1, stg)
+    fail = (st1 == 1) | (st1 == 3) | (st1 == 4)
+    assert np.array_equal(rec1[fail], recg[fail])
+    from kyverno_amd import batch
+
+    bounds = np.linspace(0, len(ress) // 64, shards + 1).astype(int) * 64
+    bounds[-1] = len(ress)
+    summed = sum(np.stack([(stg[:, a:b] == s).sum(axis=1) for s in range(7)], axis=1)
+                 for a, b in zip(bounds[:-1], bounds[1:]))
+    assert np.array_equal(summed, np.stack([(st1 == s).sum(axis=1) for s in range(7)], axis=1))
+    assert np.array_equal(st1, oracle_status(orc, pols, ress))

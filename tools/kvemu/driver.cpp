@@ -90,8 +90,23 @@ int main(int argc, char** argv) {
     std::string ctx = strcmp(argv[3], "-") ? slurp(argv[3]) : std::string();
     PolicySet ps;
     compile_policies(pol.data(), pol.size(), &ps);
+    Batch whole;
+    ingest_resources(ps, res.data(), res.size(), nullptr, &whole);
+    // KVEMU_SHARDS=G: evaluate G contiguous shards (kvshard.cpp, as kv_validate_devices does)
+    // one after the other and assemble the statuses in resource order
+    const uint32_t G = getenv("KVEMU_SHARDS") ? (uint32_t)std::max(1, atoi(getenv("KVEMU_SHARDS"))) : 1u;
+    const auto ranges = shard_ranges(whole.res.size(), G);
+    const uint64_t n_total = whole.res.size();
+    std::vector<uint8_t> status_all(ps.rules.size() * n_total, 0xEE);
+    std::vector<ErrRec> err_all;
+    bool wide_any = false;
+    const bool want_err_all = !getenv("KVEMU_NO_ERR");
+    if (want_err_all) err_all.assign(ps.rules.size() * n_total, ErrRec{});
+    for (uint32_t sh = 0; sh < G; sh++) {
     Batch b;
-    ingest_resources(ps, res.data(), res.size(), nullptr, &b);
+    if (G == 1) b = std::move(whole);
+    else make_shard(whole, ranges[sh].first, ranges[sh].second, &b);
+    const uint64_t lo = ranges[sh].first;
     JitImage img;
     const char* ch = getenv("KVGPU_JIT_CHUNK");
     jit_generate(ps, ch ? (uint32_t)atoi(ch) : 8u, &img);
@@ -215,6 +230,17 @@ int main(int argc, char** argv) {
       e.idx[2] = c.w1 >> 22;
       errw[o] = e;
     }
+    wide_any |= wide;
+    for (uint64_t rl = 0; rl < nr; rl++) {
+      memcpy(status_all.data() + rl * n_total + lo, status.data() + rl * nres, nres);
+      if (want_err_all)
+        for (uint64_t q = 0; q < nres; q++) err_all[rl * n_total + lo + q] = errw[rl * nres + q];
+    }
+    }  // shards
+    const uint64_t nr = ps.rules.size(), nres = n_total;
+    const bool wide = wide_any;
+    const std::vector<uint8_t>& status = status_all;
+    const std::vector<ErrRec>& errw = err_all;
     const std::string out = argv[4];
     FILE* fs = fopen((out + ".status").c_str(), "wb");
     FILE* fe = fopen((out + ".err").c_str(), "wb");
