@@ -107,15 +107,17 @@ class Evaluation:
 
 
 def evaluate(policies: list[dict], resources: list[dict], device: int = 0, messages: bool = True,
-             namespace_labels: dict | None = None, specialize: bool = False) -> Evaluation:
+             namespace_labels: dict | None = None, specialize: bool = False, gpus: int = 1) -> Evaluation:
     """All (rule, resource) pairs on the GPU (``kv_compile`` → ``kv_ingest`` → ``kv_validate``).
     ``specialize`` selects the per-policy-set specialized kernels (worth their hiprtc compile on
-    large batches) over the bytecode interpreter; both write the same statuses and error records."""
+    large batches) over the bytecode interpreter; both write the same statuses and error records.
+    ``gpus`` > 1 shards the resources over devices [device, device + gpus) (kv_validate_devices)."""
     from . import batch
 
     ps = batch.PolicySet(policies, specialize=specialize)
     b = batch.Batch(ps, resources, namespace_labels)
-    r = batch.validate(ps, b, device=device)
+    mask = ((1 << gpus) - 1) << device if gpus > 1 else None
+    r = batch.validate(ps, b, device=device, device_mask=mask)
     ev = Evaluation(policies, resources, ps.rules, r.status)
     if messages:
         for ri, res in zip(*np.nonzero(r.status == FAIL)):
@@ -306,17 +308,17 @@ def policy_has_validate(policy: dict) -> bool:
 
 
 def apply(policy_paths: list[str], resource_paths: list[str], policy_report: bool = False, device: int = 0,
-          out=sys.stdout, evaluation_fn=None) -> tuple[ResultCounts, list]:
+          out=sys.stdout, evaluation_fn=None, gpus: int = 1) -> tuple[ResultCounts, list]:
     """applyCommandHelper (apply_command.go:147-310) for resource files. Returns counts and the
     policyreport infos. ``evaluation_fn(policies, resources) -> Evaluation`` replaces the device
     evaluation (tests of the host logic)."""
     policies = load_policies(policy_paths)
     resources = load_resources(resource_paths)
-    return apply_docs(policies, resources, policy_report, device, out, evaluation_fn)
+    return apply_docs(policies, resources, policy_report, device, out, evaluation_fn, gpus)
 
 
 def apply_docs(policies: list[dict], resources: list[dict], policy_report: bool = False, device: int = 0,
-               out=sys.stdout, evaluation_fn=None) -> tuple[ResultCounts, list]:
+               out=sys.stdout, evaluation_fn=None, gpus: int = 1) -> tuple[ResultCounts, list]:
     mutated = autogen.mutate_policies(policies)
     if len(mutated) > 0 and len(resources) > 0:
         msg_p = "1 policy" if len(mutated) <= 1 else f"{len(policies)} policies"
@@ -328,7 +330,7 @@ def apply_docs(policies: list[dict], resources: list[dict], policy_report: bool 
     active = [p for p in mutated if not has_unset_variables(p)]
     infos = []
     if active and resources:
-        ev = (evaluation_fn or (lambda p, r: evaluate(p, r, device=device)))(active, resources)
+        ev = (evaluation_fn or (lambda p, r: evaluate(p, r, device=device, gpus=gpus)))(active, resources)
         for pi, pol in enumerate(active):
             if not policy_has_validate(pol):
                 continue
@@ -430,14 +432,15 @@ def main(argv: list[str] | None = None) -> int:
     a.add_argument("policies", nargs="+")
     a.add_argument("-r", "--resource", action="append", default=[], help="Path to resource files")
     a.add_argument("--policy-report", action="store_true", help="Generates policy report when passed")
-    a.add_argument("--device", type=int, default=0, help="HIP device")
+    a.add_argument("--device", type=int, default=0, help="HIP device (first device with --gpus)")
+    a.add_argument("--gpus", type=int, default=1, help="shard the resources over this many devices")
     t = sub.add_parser("test", help="run tests from a directory holding test.yaml")
     t.add_argument("dir")
     t.add_argument("--device", type=int, default=0)
     args = ap.parse_args(argv)
     if args.cmd == "apply":
         try:
-            rc, _ = apply(args.policies, args.resource, args.policy_report, args.device)
+            rc, _ = apply(args.policies, args.resource, args.policy_report, args.device, gpus=args.gpus)
         except msgvars.MessageVariableError as e:
             # the Go CLI dies in buildErrorMessage (msgRaw.(string), validation.go:519-524): a
             # panic, exit status 2

@@ -113,3 +113,41 @@ def test_scenario_gpu(case):
     for (_, _, m), e in zip(rs, case["expected"]):
         if e["message"]:
             assert m == e["message"]
+
+
+# ------------------------------------------------------------------ per-call engine.Validate mirror (GPU)
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ENGINE, ids=lambda c: c["name"])
+def test_engine_validate_mirror(case):
+    """kyverno_amd.engine.validate(PolicyContext) -> EngineResponse against validation_test.go's
+    messages and IsSuccessful (pkg/engine/validation.go:26, response.go:115-122)."""
+    from kyverno_amd import engine
+
+    resp = engine.validate(engine.PolicyContext(policy=case["policy"], new_resource=json.loads(case["resource"])))
+    rules = resp.policy_response.rules
+    if case["messages"] is not None:
+        assert [r.message for r in rules] == case["messages"], case["src"]
+    assert resp.is_successful() == case["successful"], case["src"]
+    if rules:
+        assert resp.policy_response.policy_name == case["policy"]["metadata"]["name"]
+        assert resp.policy_response.rules_applied_count == sum(r.status in ("pass", "fail") for r in rules)
+    else:  # buildResponse leaves an empty response untouched (validation.go:53-56)
+        assert resp.policy_response.policy_name == ""
+
+
+@pytest.mark.gpu
+def test_engine_validate_batch_matches_per_call():
+    """validate_batch ([policy][resource] in one kv_validate) equals per-call validate on the
+    scenario fixtures, rule names / statuses / messages in order."""
+    from kyverno_amd import engine
+
+    pols = [c["policy"] for c in SCEN]
+    ress = [c["resource"] for c in SCEN]
+    grid = engine.validate_batch(pols, ress)
+    for i, c in enumerate(SCEN):
+        one = engine.validate(engine.PolicyContext(policy=c["policy"], new_resource=c["resource"]))
+        got = grid[i][i].policy_response.rules
+        assert [(r.name, r.status, r.message) for r in got] == \
+               [(r.name, r.status, r.message) for r in one.policy_response.rules]
+        assert [(r.name, r.status) for r in got] == [(e["name"], e["status"]) for e in c["expected"]]
