@@ -148,6 +148,7 @@ def main():
     if args.n_res is None:
         args.n_res = {"c2": 1_000_000, "c3": 10_000_000 // 8, "c4": 1_000_000, "c5": 50_000_000 // 8}[args.config]
     t0 = time.time()
+    os.environ.setdefault("KVGPU_PROGRESS", "1")  # hiprtc progress lines on stderr during long compiles
     ps = batch.PolicySet(pols, specialize=args.engine == "specialized")
     jit = ps.jit_info
     if jit["kernels"]:

@@ -12,7 +12,13 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <dlfcn.h>
+#include <sched.h>
+#include <spawn.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
+
+#include <cerrno>
 #include <unistd.h>
 
 #include <algorithm>
@@ -26,8 +32,11 @@
 #include <sstream>
 #include <stdexcept>
 #include <thread>
+#include <unordered_map>
 
 #include "kvjit.hpp"
+
+extern char** environ;
 
 namespace kvh {
 
@@ -1279,7 +1288,7 @@ std::string rule_signature(const PolicySet& ps, uint32_t ri) {
 void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   auto t0 = std::chrono::steady_clock::now();
   Gen g(ps);
-  g.o << kPrelude << "\nusing namespace kv;\n\n";
+  const std::string prelude = std::string(kPrelude) + "\nusing namespace kv;\n\n";
   // KVGPU_JIT_FUSE=0: one device function per rule (no cross-rule sharing), for A/B runs
   const char* fz = getenv("KVGPU_JIT_FUSE");
   const bool fused = !(fz && fz[0] == '0');
@@ -1350,13 +1359,59 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
     out->memo_words = (uint32_t)((g.mpreds.size() + 31) / 32);
     out->ptab_row = g.kPtabRow;
   }
-  out->common = g.o.str();
+  // Each kernel program = prelude + the helper functions it reaches + the kernel:
+  // helpers (g_glob_/g_atom_/g_pred_/m_pred_/g_blk_/g_match_/g_rule_) are split at
+  // their definitions and selected by a transitive scan of the identifiers they
+  // use, in generation order (which is dependency order).
+  const std::string helpers = g.o.str();
+  std::vector<std::pair<std::string, std::string>> defs;  // (name, text)
+  {
+    const std::string mark = "__device__ __forceinline__ ";
+    size_t at = helpers.find(mark);
+    while (at != std::string::npos) {
+      size_t next = helpers.find("\n" + mark, at + 1);
+      const size_t end = next == std::string::npos ? helpers.size() : next + 1;
+      const std::string text = helpers.substr(at, end - at);
+      const size_t nb = text.find(' ', mark.size() + 1) + 1;  // after the return type
+      const size_t ne = text.find('(', nb);
+      defs.push_back({text.substr(nb, ne - nb), text});
+      at = next == std::string::npos ? std::string::npos : next + 1;
+    }
+  }
+  std::unordered_map<std::string, size_t> def_index;
+  for (size_t i = 0; i < defs.size(); i++) def_index[defs[i].first] = i;
+  auto refs = [&](const std::string& text, std::vector<size_t>* out_ids) {
+    static const char* prefixes[] = {"g_glob_", "g_atom_", "g_pred_", "m_pred_", "g_blk_", "g_match_", "g_rule_"};
+    for (const char* pf : prefixes) {
+      const size_t pl = strlen(pf);
+      for (size_t q = text.find(pf); q != std::string::npos; q = text.find(pf, q + pl)) {
+        size_t e = q + pl;
+        while (e < text.size() && isdigit((unsigned char)text[e])) e++;
+        auto it = def_index.find(text.substr(q, e - q));
+        if (it != def_index.end()) out_ids->push_back(it->second);
+      }
+    }
+  };
+  out->common = prelude;
   out->kernel_name.clear();
   out->kernel_src.clear();
-  out->source = out->common;
+  out->source = prelude + helpers;
   for (auto& k : g.kernels) {
+    std::vector<char> used(defs.size(), 0);
+    std::vector<size_t> stack;
+    refs(k.second, &stack);
+    while (!stack.empty()) {
+      const size_t d = stack.back();
+      stack.pop_back();
+      if (used[d]) continue;
+      used[d] = 1;
+      refs(defs[d].second, &stack);
+    }
+    std::string prog;
+    for (size_t d = 0; d < defs.size(); d++)
+      if (used[d]) prog += defs[d].second;
     out->kernel_name.push_back(k.first);
-    out->kernel_src.push_back(k.second);
+    out->kernel_src.push_back(prog + k.second);
     out->source += k.second;
   }
   out->gen_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1424,6 +1479,98 @@ std::vector<char> compile_one(const std::string& src, const std::string& name) {
   hiprtcGetCode(prog, code.data());
   hiprtcDestroyProgram(&prog);
   return code;
+}
+
+// kvjitc next to libkvgpu.so (KVGPU_JITC overrides): compiles one program per process
+std::string jitc_path() {
+  if (const char* e = getenv("KVGPU_JITC")) return e;
+  Dl_info info{};
+  if (!dladdr((void*)&jitc_path, &info) || !info.dli_fname) return "";
+  std::string p = info.dli_fname;
+  const size_t slash = p.rfind('/');
+  p = (slash == std::string::npos ? std::string(".") : p.substr(0, slash)) + "/kvjitc";
+  return access(p.c_str(), X_OK) == 0 ? p : "";
+}
+
+// cores this process may use: affinity, capped by a cgroup v2 CPU quota
+unsigned host_threads() {
+  unsigned n = std::thread::hardware_concurrency();
+  cpu_set_t cs;
+  if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = (unsigned)CPU_COUNT(&cs);
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    unsigned long long per = 0;
+    if (fscanf(f, "%31s %llu", q, &per) == 2 && strcmp(q, "max") != 0 && per)
+      n = std::min<unsigned>(n, (unsigned)std::max(1ull, strtoull(q, nullptr, 10) / per));
+    fclose(f);
+  }
+  return std::max(1u, n);
+}
+
+// compile programs `todo` of img in child processes (kvjitc), `T` at a time
+void compile_in_children(JitImage* img, const std::vector<size_t>& todo, const std::string& jitc, unsigned T) {
+  const char* td = getenv("TMPDIR");
+  std::string tmpl = std::string(td && *td ? td : "/tmp") + "/kvjit.XXXXXX";
+  std::vector<char> tbuf(tmpl.begin(), tmpl.end());
+  tbuf.push_back('\0');
+  if (!mkdtemp(tbuf.data())) throw std::runtime_error("kvjit: mkdtemp failed");
+  const std::string dir(tbuf.data());
+  std::atomic<size_t> next{0}, done{0};
+  std::vector<std::string> errs(T);
+  // KVGPU_PROGRESS=1: a line on stderr at most every 15 s (long compiles stay visibly alive)
+  const bool progress = getenv("KVGPU_PROGRESS") && getenv("KVGPU_PROGRESS")[0] == '1';
+  const auto t0 = std::chrono::steady_clock::now();
+  std::atomic<int64_t> last_ms{0};
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < T; t++)
+    th.emplace_back([&, t]() {
+      for (size_t j; (j = next++) < todo.size();) {
+        const size_t i = todo[j];
+        const std::string src = dir + "/" + std::to_string(i) + ".hip", out = dir + "/" + std::to_string(i) + ".co";
+        {
+          FILE* f = fopen(src.c_str(), "wb");
+          const std::string prog = img->common + img->kernel_src[i];
+          if (!f || fwrite(prog.data(), 1, prog.size(), f) != prog.size()) {
+            errs[t] = "kvjit: cannot write " + src;
+            if (f) fclose(f);
+            return;
+          }
+          fclose(f);
+        }
+        std::vector<std::string> av = {jitc, src, out, img->kernel_name[i]};
+        std::vector<char*> argv;
+        for (auto& a : av) argv.push_back(&a[0]);
+        argv.push_back(nullptr);
+        pid_t pid = 0;
+        if (posix_spawn(&pid, jitc.c_str(), nullptr, nullptr, argv.data(), environ) != 0) {
+          errs[t] = "kvjit: cannot start " + jitc;
+          return;
+        }
+        int status = 0;
+        while (waitpid(pid, &status, 0) < 0 && errno == EINTR) {
+        }
+        std::vector<char> code;
+        if (!WIFEXITED(status) || WEXITSTATUS(status) != 0 || !read_file(out, &code)) {
+          errs[t] = "kvjit: compiling " + img->kernel_name[i] + " failed (kvjitc status " + std::to_string(status) + ")";
+          return;
+        }
+        img->codes[i] = std::move(code);
+        unlink(src.c_str());
+        unlink(out.c_str());
+        const size_t d = ++done;
+        if (progress) {
+          const int64_t now =
+              (int64_t)std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+          int64_t prev = last_ms.load();
+          if (now - prev >= 15000 && last_ms.compare_exchange_strong(prev, now))
+            fprintf(stderr, "[kvgpu] hiprtc: %zu/%zu kernel programs compiled (%.0f s)\n", d, todo.size(), now / 1e3);
+        }
+      }
+    });
+  for (auto& x : th) x.join();
+  rmdir(dir.c_str());
+  for (auto& e : errs)
+    if (!e.empty()) throw std::runtime_error(e);
 }
 
 }  // namespace
@@ -1526,34 +1673,31 @@ void jit_compile(JitImage* img) {
   (void)hiprtcVersion(&hv, &hv);
   opt_key += "hiprtc " + std::to_string(hv) + "\n";
   const uint64_t hcommon = fnv1a64(img->common, fnv1a64(opt_key));
-  unsigned T = std::thread::hardware_concurrency();
+  // cache lookups; the misses compile in child processes (hiprtc serialises the
+  // compilations of one process), or in this process when kvjitc is unavailable
+  // (KVGPU_JIT_PROCS=0 forces that)
+  std::vector<std::string> paths(K);
+  std::vector<size_t> todo;
+  uint32_t hits = 0;
+  for (size_t i = 0; i < K; i++) {
+    char key[40];
+    snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a64(img->kernel_src[i], hcommon));
+    paths[i] = dir.empty() ? "" : dir + "/" + img->kernel_name[i] + "-" + key + ".co";
+    if (!paths[i].empty() && read_file(paths[i], &img->codes[i])) hits++;
+    else todo.push_back(i);
+  }
+  unsigned T = std::min(16u, host_threads());
   if (const char* e = getenv("KVGPU_JIT_THREADS")) T = (unsigned)std::max(1, atoi(e));
-  T = std::max(1u, std::min<unsigned>(T, (unsigned)K));
-  std::atomic<size_t> next{0};
-  std::atomic<uint32_t> hits{0};
-  std::vector<std::string> errs(T);
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < T; t++)
-    th.emplace_back([&, t]() {
-      try {
-        for (size_t i; (i = next++) < K;) {
-          char key[40];
-          snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a64(img->kernel_src[i], hcommon));
-          const std::string path = dir.empty() ? "" : dir + "/" + img->kernel_name[i] + "-" + key + ".co";
-          if (!path.empty() && read_file(path, &img->codes[i])) {
-            hits++;
-            continue;
-          }
-          img->codes[i] = compile_one(img->common + img->kernel_src[i], img->kernel_name[i]);
-          if (!path.empty()) write_file_atomic(dir, path, img->codes[i]);
-        }
-      } catch (const std::exception& e) {
-        errs[t] = e.what();
-      }
-    });
-  for (auto& x : th) x.join();
-  for (auto& e : errs)
-    if (!e.empty()) throw std::runtime_error(e);
+  T = std::max(1u, std::min<unsigned>(T, (unsigned)todo.size()));
+  const std::string jitc = jitc_path();
+  const bool procs = !(getenv("KVGPU_JIT_PROCS") && getenv("KVGPU_JIT_PROCS")[0] == '0');
+  if (!todo.empty() && procs && !jitc.empty() && todo.size() > 1) {
+    compile_in_children(img, todo, jitc, T);
+  } else {
+    for (size_t i : todo) img->codes[i] = compile_one(img->common + img->kernel_src[i], img->kernel_name[i]);
+  }
+  if (!dir.empty())
+    for (size_t i : todo) write_file_atomic(dir, paths[i], img->codes[i]);
   img->cache_hits = hits;
   img->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
