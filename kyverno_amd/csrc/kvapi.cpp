@@ -620,6 +620,10 @@ struct DevSession {
       er8.alloc(nrules * nres * sizeof(ErrRec8), device);
       O.err8 = (ErrRec8*)er8.p;
       O.err = nullptr;  // full records: allocated by fetch() for the re-run pass, if some record is wide
+      if (getenv("KVGPU_JIT_STORE") && std::string(getenv("KVGPU_JIT_STORE")) == "lane") {
+        er.alloc(nrules * nres * sizeof(ErrRec), device);  // the variant writes them in every pass
+        O.err = (ErrRec*)er.p;
+      }
       O.full |= 2;
     }
     cn.alloc(std::max<uint64_t>(nrules, 1) * KV_HIST * sizeof(unsigned long long), device);

@@ -550,6 +550,15 @@ __device__ __forceinline__ void store_err(const DevOut& O, size_t o, uint32_t ki
     return;
   }
   const uint32_t fits = (i0 < 4096u) & (i1 < 1024u) & (i2 < 1024u) & (i3 == 0u) & (key == ABSENT) & (pn < (1u << 25));
+#ifdef KV_STORE_LANE_BRANCH
+  // round-1 variant kept for the 8-wave A/B (KVGPU_JIT_STORE=lane): the full record of a
+  // record that does not fit is written in the same pass, under a per-lane branch
+  if (!fits) {
+    uint4* x = (uint4*)(O.err + o);
+    x[0] = make_uint4(kind | (flags << 16), pn, key, res);
+    x[1] = make_uint4(i0, i1, i2, i3);
+  }
+#endif
   uint2 w;
   w.x = kind | (flags << 4) | ((fits ^ 1u) << 6) | (pn << 7);
   w.y = i0 | (i1 << 12) | (i2 << 22);

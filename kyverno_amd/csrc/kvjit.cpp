@@ -1288,7 +1288,10 @@ std::string rule_signature(const PolicySet& ps, uint32_t ri) {
 void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   auto t0 = std::chrono::steady_clock::now();
   Gen g(ps);
-  const std::string prelude = std::string(kPrelude) + "\nusing namespace kv;\n\n";
+  // KVGPU_JIT_STORE=lane: the per-lane-branch record store variant (8-wave A/B of DESIGN.md)
+  const bool lane_store = getenv("KVGPU_JIT_STORE") && std::string(getenv("KVGPU_JIT_STORE")) == "lane";
+  const std::string prelude =
+      std::string(lane_store ? "#define KV_STORE_LANE_BRANCH 1\n" : "") + kPrelude + "\nusing namespace kv;\n\n";
   // KVGPU_JIT_FUSE=0: one device function per rule (no cross-rule sharing), for A/B runs
   const char* fz = getenv("KVGPU_JIT_FUSE");
   const bool fused = !(fz && fz[0] == '0');
