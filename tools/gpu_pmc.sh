@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC counter passes (one rocprofv3 --pmc run per counter group), kernel-trace/stats only.
 set -o pipefail
-R="${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p "$R/gpurun_out/pmc"
+R="${GRAFT_REPO_ROOT:-/root/repo}"; O="$R/gpurun_out/${OUT:-pmc}"; mkdir -p "$O"
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 cd /tmp
 ARGS="--no-cpu-baseline --steps 2 --warmup 0 --n-res ${NRES:-1000000} ${EXTRA}"
@@ -10,11 +10,11 @@ for grp in "FETCH_SIZE" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" \
            "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace --stats -d "$R/gpurun_out/pmc" -o pass$i --output-format csv -- \
-      python -u "$R/bench.py" $ARGS > "$R/gpurun_out/pmc/pass$i.json" 2> "$R/gpurun_out/pmc/pass$i.err" || { echo "pass $i failed"; exit 1; }
+  timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace --stats -d "$O" -o pass$i --output-format csv -- \
+      python -u "$R/bench.py" $ARGS > "$O/pass$i.json" 2> "$O/pass$i.err" || { echo "pass $i failed"; exit 1; }
 done
 cd "$R"
-for f in $(find gpurun_out/pmc -name "*counter_collection.csv"); do echo "== $f"; python - "$f" <<'PY'
+for f in $(find "$O" -name "*counter_collection.csv"); do echo "== $f"; python - "$f" <<'PY'
 import csv, sys, collections
 rows = list(csv.DictReader(open(sys.argv[1])))
 agg = collections.defaultdict(float)  # (kernel, dispatch, counter) -> value summed over dimensions
