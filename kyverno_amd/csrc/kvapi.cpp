@@ -683,9 +683,19 @@ struct DevSession {
                                    nullptr));
     }
     DevOut Ov = O;
-    void* args[] = {(void*)&P, (void*)&bview, (void*)&N, (void*)&V, (void*)&S, (void*)&Ov};
-    for (hipFunction_t f : dps->fns)
-      HIPCHK(hipModuleLaunchKernel(f, blocks, 1, 1, KV_WG, 1, 1, 0, stream, args, nullptr));
+    uint32_t r0 = 0;
+    void* args[] = {(void*)&P, (void*)&bview, (void*)&N, (void*)&V, (void*)&S, (void*)&Ov, (void*)&r0};
+    // KVGPU_SLICES=k: resource slices outer, rule kernels inner (a slice's rows stay
+    // cache-resident across the kernels), for A/B runs
+    const char* sz = getenv("KVGPU_SLICES");
+    const uint32_t slices = std::max<uint32_t>(1u, std::min<uint32_t>(blocks, sz ? (uint32_t)atoi(sz) : 1u));
+    for (uint32_t k = 0; k < slices; k++) {
+      const uint32_t b0 = (uint32_t)((uint64_t)blocks * k / slices), b1 = (uint32_t)((uint64_t)blocks * (k + 1) / slices);
+      if (b1 == b0) continue;
+      r0 = b0 * KV_WG;
+      for (hipFunction_t f : dps->fns)
+        HIPCHK(hipModuleLaunchKernel(f, b1 - b0, 1, 1, KV_WG, 1, 1, 0, stream, args, nullptr));
+    }
   }
   std::vector<int64_t> read_counts() {
     HIPCHK(hipSetDevice(device));
@@ -960,8 +970,7 @@ int kv_compile(const char* policies_json, size_t len, uint32_t flags, kv_policys
       compile_policies(policies_json, len, &s->ps);
       if (flags & KV_COMPILE_SPECIALIZE) {
         s->jit = std::make_unique<JitImage>();
-        const char* ch = getenv("KVGPU_JIT_CHUNK");  // rules per fused chunk (experiments)
-        const uint32_t chunk = ch ? (uint32_t)atoi(ch) : 8u;
+        const uint32_t chunk = jit_chunk_rules();
         jit_generate(s->ps, chunk, s->jit.get());
         if (const char* dump = getenv("KVGPU_JIT_DUMP")) {
           if (FILE* f = fopen(dump, "w")) {

@@ -20,6 +20,25 @@
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Wave-uniform read of the read-only policy tables through the scalar data cache
+// (s_load into SGPRs, batched, no vector-memory round trip per criterion). The
+// device pointers in DevPS are generic; the cast names the constant address
+// space. A divergent address still compiles (to a vector load).
+#ifndef KV_SCONST
+#define KV_SCONST __attribute__((address_space(4)))
+#endif
+template <class T>
+__device__ __forceinline__ T sld(const T* p) {
+  static_assert(sizeof(T) % 4 == 0, "sld: whole words");
+  const KV_SCONST uint32_t* q = (const KV_SCONST uint32_t*)p;
+  uint32_t w[sizeof(T) / 4];
+#pragma unroll
+  for (uint32_t i = 0; i < sizeof(T) / 4; i++) w[i] = q[i];
+  T r;
+  __builtin_memcpy(&r, w, sizeof(T));
+  return r;
+}
+
 // node index of this lane's cell in a row (wave-group layout, kv_layout.h)
 __device__ __forceinline__ uint32_t ni(uint32_t row) { return row * KV_LANES + (threadIdx.x & (KV_LANES - 1)); }
 
@@ -65,7 +84,7 @@ __device__ __forceinline__ bool seg_at(const GWord* __restrict__ wd, uint32_t le
   for (uint32_t i = 0; i < nw; i++) {
     uint32_t hi = base[a + i + 1];
     uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, sh);
-    const GWord g = wd[i];
+    const GWord g = sld(wd + i);
     if ((v ^ g.w) & g.mask) return false;
     lo = hi;
   }
@@ -74,30 +93,30 @@ __device__ __forceinline__ bool seg_at(const GWord* __restrict__ wd, uint32_t le
 
 // compiled glob over a 4-byte aligned value string (see kv_layout.h GlobFlags)
 KV_FN bool glob_fast(const DevPS& P, const Atom& A, const uint8_t* s, uint32_t sl) {
-  const uint32_t fl = uni(A.gflags);
+  const uint32_t fl = sld(&A.gflags);
   if (fl & G_ALL) return true;
   if (fl & G_EMPTY) return sl == 0;
-  if (sl < uni(A.gmin)) return false;
+  if (sl < sld(&A.gmin)) return false;
   const uint32_t* base = (const uint32_t*)s;
-  const GSeg* segs = P.gsegs + uni(A.gfirst);
-  const uint32_t n = uni(A.gcount);
+  const GSeg* segs = P.gsegs + sld(&A.gfirst);
+  const uint32_t n = sld(&A.gcount);
   uint32_t pos = 0, end = sl, i0 = 0, i1 = n;
   if (!(fl & G_LEAD)) {
-    const GSeg s0 = segs[0];
+    const GSeg s0 = sld(segs);
     if (n == 1 && !(fl & G_TRAIL)) return sl == s0.len && seg_at(P.gwords + s0.wfirst, s0.len, base, 0);
     if (!seg_at(P.gwords + s0.wfirst, s0.len, base, 0)) return false;
     pos = s0.len;
     i0 = 1;
   }
   if (!(fl & G_TRAIL)) {
-    const GSeg st = segs[n - 1];
+    const GSeg st = sld(segs + n - 1);
     if (end < pos + st.len) return false;
     if (!seg_at(P.gwords + st.wfirst, st.len, base, end - st.len)) return false;
     end -= st.len;
     i1 = n - 1;
   }
   for (uint32_t i = i0; i < i1; i++) {
-    const GSeg sg = segs[i];
+    const GSeg sg = sld(segs + i);
     bool found = false;
     for (uint32_t k = pos; k + sg.len <= end; k++) {
       if (seg_at(P.gwords + sg.wfirst, sg.len, base, k)) { pos = k + sg.len; found = true; break; }
@@ -108,7 +127,7 @@ KV_FN bool glob_fast(const DevPS& P, const Atom& A, const uint8_t* s, uint32_t s
 }
 
 __device__ __forceinline__ bool glob_atom(const DevPS& P, const Atom& A, const uint8_t* s, uint32_t sl, bool ascii) {
-  if (ascii || !(uni(A.gflags) & G_HASQ)) return glob_fast(P, A, s, sl);
+  if (ascii || !(sld(&A.gflags) & G_HASQ)) return glob_fast(P, A, s, sl);
   return kv_glob(P.pstr + A.s_off, A.s_len & 0x7FFFFFFFu, s, sl);
 }
 
@@ -148,13 +167,13 @@ __device__ __forceinline__ bool cmp_ok(uint32_t op, int r) {
 // one atom of a string pattern against a scalar/absent node (type NT_NULL == Go nil)
 KV_FN bool atom_eval(const DevPS& P, const DevBatch& B, uint32_t ai, uint32_t type, const Node& n) {
   const Atom& A = P.atoms[ai];
-  const uint32_t kind = uni(A.kind);
+  const uint32_t kind = sld(&A.kind);
   if (kind == AT_FALSE) return false;
   if (type == NT_MAP || type == NT_ARR) return false;
   if (kind == AT_GLOB_E) {
     if (type == NT_NULL) return false;
     bool r = glob_atom(P, A, B.bstr + n.b, n.c & NC_LEN_MASK, n.c & NC_ASCII_E);
-    return uni(A.op) == CO_NE ? !r : r;
+    return sld(&A.op) == CO_NE ? !r : r;
   }
   if (type == NT_BOOL) return false;
   if (kind == AT_GLOB_N) {
@@ -172,18 +191,18 @@ KV_FN bool atom_eval(const DevPS& P, const DevBatch& B, uint32_t ai, uint32_t ty
     if (!(v.flags & VF_Q_VALID)) return false;
     r = q_cmp(v.flags, v.q_exp, v.q_hi, v.q_lo, A.q_flags, A.q_exp, A.q_hi, A.q_lo);
   }
-  return cmp_ok(uni(A.op), r);
+  return cmp_ok(sld(&A.op), r);
 }
 
 // ValidateValueWithPattern(value, pattern) for a scalar-pattern leaf; n = the
 // value node (ignored when type == NT_NULL, which also stands for absent)
 KV_FN bool pred_eval(const DevPS& P, const DevBatch& B, uint32_t pi, uint32_t type, const Node& n) {
   const Pred& pr = P.preds[pi];
-  const uint32_t kind = uni(pr.kind);
+  const uint32_t kind = sld(&pr.kind);
   switch (kind) {
-    case PK_BOOL: return type == NT_BOOL && ((n.c & NC_BOOLV) ? 1u : 0u) == uni(pr.flags);
+    case PK_BOOL: return type == NT_BOOL && ((n.c & NC_BOOLV) ? 1u : 0u) == sld(&pr.flags);
     case PK_FLOAT: {
-      if (type == NT_INT) return uni(pr.flags) && B.vals[n.a].i == pr.fi;
+      if (type == NT_INT) return sld(&pr.flags) && B.vals[n.a].i == pr.fi;
       if (type == NT_FLOAT) return B.vals[n.a].f == pr.f;
       if (type == NT_STR) {
         const Val& v = B.vals[n.a];
@@ -197,17 +216,17 @@ KV_FN bool pred_eval(const DevPS& P, const DevBatch& B, uint32_t pi, uint32_t ty
       return (n.c & NC_NILLIKE) != 0;
     case PK_MAPTYPE: return type == NT_MAP;
     case PK_STRING: {
-      const uint32_t af = uni(pr.first), an = uni(pr.count);
+      const uint32_t af = sld(&pr.first), an = sld(&pr.count);
       for (uint32_t a = af; a < af + an; a++) {
         const Alt& al = P.alts[a];
-        const uint32_t cf = uni(al.first), cn = uni(al.count);
+        const uint32_t cf = sld(&al.first), cn = sld(&al.count);
         bool all = true;
         for (uint32_t c = cf; c < cf + cn && all; c++) {
           const Conj& cj = P.conjs[c];
-          const uint32_t ck = uni(cj.kind);
-          bool r = atom_eval(P, B, uni(cj.a0), type, n);
-          if (ck == CJ_INRANGE) r = r && atom_eval(P, B, uni(cj.a1), type, n);
-          else if (ck == CJ_NOTINRANGE) r = r || atom_eval(P, B, uni(cj.a1), type, n);
+          const uint32_t ck = sld(&cj.kind);
+          bool r = atom_eval(P, B, sld(&cj.a0), type, n);
+          if (ck == CJ_INRANGE) r = r && atom_eval(P, B, sld(&cj.a1), type, n);
+          else if (ck == CJ_NOTINRANGE) r = r || atom_eval(P, B, sld(&cj.a1), type, n);
           all = r;
         }
         if (all) return true;
@@ -301,14 +320,14 @@ __device__ __forceinline__ bool keyglob_op(const DevPS& P, const DevBatch& B, co
 // ------------------------------------------------------------------ match/exclude
 // LabelSelectorAsSelector(ReplaceInSelector(selector, labels)).Matches(labels)
 // (pkg/engine/utils.go:99-107, pkg/engine/wildcards/wildcards.go:13-63) on one
-// label list; `si` must be uniform across the wave (selector fields via uni()).
+// label list; `si` must be uniform across the wave (selector fields read with sld()).
 KV_FN bool selector_match(const DevPS& P, const DevBatch& B, const KV* __restrict__ labels, uint32_t nl,
                                uint32_t si) {
   const Selector& S = P.sels[si];
-  const uint32_t fl = uni(S.flags);
+  const uint32_t fl = sld(&S.flags);
   if (fl & SF_STATIC_INVALID) return false;
   if (fl & SF_EVERYTHING) return true;
-  const uint32_t mf = uni(S.ml_first), mc = uni(S.ml_count);
+  const uint32_t mf = sld(&S.ml_first), mc = sld(&S.ml_count);
   auto resolve = [&](const SelLabel& E, const uint8_t** ok, uint32_t* okl, const uint8_t** ov, uint32_t* ovl,
                      bool* val) {
     if (!(E.flags & SL_WILD)) {
@@ -356,7 +375,7 @@ KV_FN bool selector_match(const DevPS& P, const DevBatch& B, const KV* __restric
     }
     if (!found) return false;
   }
-  const uint32_t ef = uni(S.me_first), ec = uni(S.me_count);
+  const uint32_t ef = sld(&S.me_first), ec = sld(&S.me_count);
   for (uint32_t j = ef; j < ef + ec; j++) {
     const SelExpr& E = P.selexprs[j];
     bool has = false, in = false;
@@ -369,7 +388,7 @@ KV_FN bool selector_match(const DevPS& P, const DevBatch& B, const KV* __restric
         break;
       }
     }
-    const uint32_t op = uni(E.op);
+    const uint32_t op = sld(&E.op);
     if ((op == 0 && !in) || (op == 1 && in) || (op == 2 && !has) || (op == 3 && has)) return false;
   }
   return true;
@@ -417,8 +436,8 @@ KV_FN void mtab_word(const DevPS& P, const DevBatch& B, uint32_t y, uint32_t e, 
     const StrRef s = B.nsms[e];
     for (uint32_t f = 0; f < P.n_filters; f++) {  // filters whose nss_bit falls in this word
       const MFilter& F = P.filters[f];
-      if (!(uni(F.flags) & MF_NSS) || (uni(F.nss_bit) >> 5) != y) continue;
-      if (namespaces_match(P, B.bstr + s.off, s.len, uni(F.nss_first), uni(F.nss_count))) w |= 1u << (F.nss_bit & 31u);
+      if (!(sld(&F.flags) & MF_NSS) || (sld(&F.nss_bit) >> 5) != y) continue;
+      if (namespaces_match(P, B.bstr + s.off, s.len, sld(&F.nss_first), sld(&F.nss_count))) w |= 1u << (F.nss_bit & 31u);
     }
     ns[(size_t)y * B.n_nsm + e] = w;
     return;
@@ -429,8 +448,8 @@ KV_FN void mtab_word(const DevPS& P, const DevBatch& B, uint32_t y, uint32_t e, 
     const KVSet a = B.asets[e];
     for (uint32_t f = 0; f < P.n_filters; f++) {
       const MFilter& F = P.filters[f];
-      if (!(uni(F.flags) & MF_ANN) || (uni(F.ann_bit) >> 5) != y) continue;
-      if (annotations_match(P, B, B.kvs + a.first, a.count, uni(F.ann_first), uni(F.ann_count)))
+      if (!(sld(&F.flags) & MF_ANN) || (sld(&F.ann_bit) >> 5) != y) continue;
+      if (annotations_match(P, B, B.kvs + a.first, a.count, sld(&F.ann_first), sld(&F.ann_count)))
         w |= 1u << (F.ann_bit & 31u);
     }
     an[(size_t)y * B.n_asets + e] = w;
@@ -451,13 +470,13 @@ KV_FN void mtab_word(const DevPS& P, const DevBatch& B, uint32_t y, uint32_t e, 
 KV_FN uint32_t block_errs_masked(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t rkind,
                                       uint32_t rflags, uint32_t f, uint32_t mask) {
   const MFilter& F = P.filters[f];
-  const uint32_t fl = uni(P.fflags[f]) & mask;
+  const uint32_t fl = sld(P.fflags + f) & mask;
   uint32_t errs = 0;
   if (fl & MF_KINDS) {
     bool ok = false;
-    const uint32_t kf = uni(F.kinds_first), kc = uni(F.kinds_count);
+    const uint32_t kf = sld(&F.kinds_first), kc = sld(&F.kinds_count);
     for (uint32_t k = kf; k < kf + kc && !ok; k++) {
-      const KindSpec ks = P.kinds[k];
+      const KindSpec ks = sld(P.kinds + k);
       switch (ks.form) {
         case 3: ok = true; break;
         case 0: ok = rkind == ks.kind; break;
@@ -475,9 +494,9 @@ KV_FN uint32_t block_errs_masked(const DevPS& P, const DevBatch& B, const Res* _
       any = kv_glob(P.pstr + P.strrefs[k].off, P.strrefs[k].len, B.bstr + R->name_off, R->name_len);
     errs += any ? 0 : 1;
   }
-  if (fl & MF_NSS) errs += mt_bit(P.mt_ns, uni(F.nss_bit), B.n_nsm, R->nsm) ? 0 : 1;
-  if (fl & MF_ANN) errs += mt_bit(P.mt_ann, uni(F.ann_bit), B.n_asets, R->aset) ? 0 : 1;
-  if (fl & MF_SEL) errs += mt_bit(P.mt_sel, uni(F.sel), B.n_lsets, R->lset) ? 0 : 1;
+  if (fl & MF_NSS) errs += mt_bit(P.mt_ns, sld(&F.nss_bit), B.n_nsm, R->nsm) ? 0 : 1;
+  if (fl & MF_ANN) errs += mt_bit(P.mt_ann, sld(&F.ann_bit), B.n_asets, R->aset) ? 0 : 1;
+  if (fl & MF_SEL) errs += mt_bit(P.mt_sel, sld(&F.sel), B.n_lsets, R->lset) ? 0 : 1;
   if ((fl & MF_NSSEL) && !(rflags & (RF_KIND_NAMESPACE | RF_KIND_EMPTY))) {
     const uint32_t bit = F.nssel_bit;
     errs += (B.ns_bits[R->ns_index * B.ns_words + bit / 32] >> (bit % 32)) & 1 ? 0 : 1;
@@ -493,30 +512,30 @@ __device__ __forceinline__ uint32_t block_errs(const DevPS& P, const DevBatch& B
 
 KV_FN bool rule_matches(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t rkind,
                              uint32_t rflags, const RuleRec& rr) {
-  const uint32_t mm = uni(rr.m_mode), mf = uni(rr.m_first), mc = uni(rr.m_count);
+  const uint32_t mm = sld(&rr.m_mode), mf = sld(&rr.m_first), mc = sld(&rr.m_count);
   bool ok;
   if (mm == 1) {
     ok = false;
-    for (uint32_t f = mf; f < mf + mc && !ok; f++) ok = !(P.fflags[f] & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, f) == 0;
+    for (uint32_t f = mf; f < mf + mc && !ok; f++) ok = !(sld(P.fflags + f) & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, f) == 0;
   } else if (mm == 2) {
     ok = true;
-    for (uint32_t f = mf; f < mf + mc && ok; f++) ok = !(P.fflags[f] & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, f) == 0;
+    for (uint32_t f = mf; f < mf + mc && ok; f++) ok = !(sld(P.fflags + f) & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, f) == 0;
   } else {
-    ok = !(P.fflags[mf] & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, mf) == 0;
+    ok = !(sld(P.fflags + mf) & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, mf) == 0;
   }
   if (!ok) return false;
-  const uint32_t xm = uni(rr.x_mode), xf = uni(rr.x_first), xc = uni(rr.x_count);
+  const uint32_t xm = sld(&rr.x_mode), xf = sld(&rr.x_first), xc = sld(&rr.x_count);
   if (xm == 1) {
     for (uint32_t f = xf; f < xf + xc; f++)
-      if (!(P.fflags[f] & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, f) == 0) return false;
+      if (!(sld(P.fflags + f) & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, f) == 0) return false;
     return true;
   }
   if (xm == 2) {
     for (uint32_t f = xf; f < xf + xc; f++)
-      if ((P.fflags[f] & MF_EMPTY) || block_errs(P, B, R, rkind, rflags, f) != 0) return true;
+      if ((sld(P.fflags + f) & MF_EMPTY) || block_errs(P, B, R, rkind, rflags, f) != 0) return true;
     return false;
   }
-  if (!(P.fflags[xf] & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, xf) == 0) return false;
+  if (!(sld(P.fflags + xf) & MF_EMPTY) && block_errs(P, B, R, rkind, rflags, xf) == 0) return false;
   return true;
 }
 

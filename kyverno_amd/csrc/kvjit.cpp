@@ -82,6 +82,11 @@ struct Gen {
   // kvj_ptab stages each value's bytes in LDS before its row of predicates;
   // KVGPU_PTAB_LDS=0 reads them from global memory per glob, for A/B runs
   bool ptab_lds = !(getenv("KVGPU_PTAB_LDS") && getenv("KVGPU_PTAB_LDS")[0] == '0');
+  // hoisted lookups are branch-free (a failed guard reads cell 0 and discards it)
+  // and are all placed at the top of their chunk / fused-loop body, so the loads
+  // of one tree level issue together instead of one dependent wait per lookup;
+  // KVGPU_JIT_HOIST=lazy places each just before its first use, for A/B runs
+  bool early_hoist = !(getenv("KVGPU_JIT_HOIST") && std::string(getenv("KVGPU_JIT_HOIST")) == "lazy");
   explicit Gen(const PolicySet& p) : ps(p) {}
 
   // call of leaf predicate `pi` on node `n` of type `t`
@@ -441,7 +446,7 @@ struct Gen {
     for (uint32_t a : ps.filter_name_atoms.at(f)) glob_once(a);  // before this function's text
     o << "__device__ __forceinline__ bool g_blk_" << f
       << "(const DevPS& P, const DevBatch& B, const Res* __restrict__ R, uint32_t rkind, uint32_t rflags) {\n"
-      << "  if (uni(P.fflags[" << f << "]) & (MF_EMPTY | MF_UI_FAIL)) return false;\n";
+      << "  if (sld(P.fflags + " << f << "u) & (MF_EMPTY | MF_UI_FAIL)) return false;\n";
     if (F.flags & MF_KINDS) {
       bool any_star = false;
       std::ostringstream k;
@@ -654,12 +659,12 @@ struct Gen {
     const uint32_t nr = ch.rule_end - ch.rule_begin;
     o << "extern \"C\" __global__ __launch_bounds__(KV_WG) void " << ch.name
       << "(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp, const Node* __restrict__ N, "
-         "const Val* __restrict__ V, const uint8_t* __restrict__ S, DevOut O) {\n"
+         "const Val* __restrict__ V, const uint8_t* __restrict__ S, DevOut O, uint32_t r0) {\n"
       << "  __shared__ uint32_t s_hist[" << nr << "][KV_HIST];\n"
       << "  const DevPS& P = *Pp;\n  const DevBatch& B = *Bp;\n"
       << "  for (uint32_t q = threadIdx.x; q < " << nr << "u * KV_HIST; q += KV_WG) (&s_hist[0][0])[q] = 0u;\n"
       << "  __syncthreads();\n"
-      << "  const uint32_t r = blockIdx.x * KV_WG + threadIdx.x;\n"
+      << "  const uint32_t r = r0 + blockIdx.x * KV_WG + threadIdx.x;\n"
       << "  const uint32_t n_res = B.n_res;\n"
       << "  const bool valid = r < n_res;\n"
       << "  const Res* __restrict__ R = B.res + (valid ? r : 0u);\n"
@@ -748,6 +753,14 @@ struct Gen {
       c << "  if (node_type(" << p.node << ".kt) == NT_MAP) for (uint32_t q_ = 0u; q_ < " << p.node << ".b; q_++) { "
         << "const uint32_t c_ = ni(" << p.node << ".a + q_); const Node t_ = N[c_]; if (node_key(t_.kt) == " << u32(a)
         << ") { " << h.idx << " = c_; " << h.node << " = t_; break; } }\n";
+    } else if (early_hoist) {
+      // the loaded node passes through v_perm (keep / zero) instead of a select,
+      // which the compiler would turn into a branch around a narrowed reload
+      c << "  { const bool ok_ = node_type(" << p.node << ".kt) == NT_MAP && " << u32(a) << " < " << p.node << ".b; "
+        << "const uint32_t c_ = ok_ ? ni(" << p.node << ".a + " << u32(a) << ") : 0u; const Node t_ = N[c_]; "
+        << "const bool hit_ = ok_ && node_type(t_.kt) != NT_ABSENT; const uint32_t m_ = hit_ ? 0x07060504u : 0x0c0c0c0cu; "
+        << h.idx << " = hit_ ? c_ : ABSENT; " << h.node << " = Node{__builtin_amdgcn_perm(t_.kt, 0u, m_), "
+        << "__builtin_amdgcn_perm(t_.a, 0u, m_), __builtin_amdgcn_perm(t_.b, 0u, m_), __builtin_amdgcn_perm(t_.c, 0u, m_)}; }\n";
     } else {
       c << "  if (node_type(" << p.node << ".kt) == NT_MAP && " << u32(a) << " < " << p.node << ".b) { "
         << "const uint32_t c_ = ni(" << p.node << ".a + " << u32(a) << "); const Node t_ = N[c_]; "
@@ -897,9 +910,17 @@ struct Gen {
             if (memo && pw && sl != pslot.end() && T) {
               const uint32_t word = sl->second / 32;
               const std::string wv = g.hv[d].node + "_w" + std::to_string(word);
-              if (T->words.insert(wv).second)
-                T->code.push_back("  const uint32_t " + wv + " = node_type(" + g.hv[d].node + ".kt) - 1u < 4u ? P.ptab[(size_t)" +
-                                  std::to_string(word) + "u * P.n_vals + " + g.hv[d].node + ".a] : 0u;\n");
+              const std::string hn = g.hv[d].node;
+              if (T->words.insert(wv).second) {
+                const std::string off = std::to_string(word) + "u * P.n_vals + ";
+                if (early_hoist)
+                  T->code.push_back("  const uint32_t " + wv + " = __builtin_amdgcn_perm(P.ptab[(size_t)" + off +
+                                    "(node_type(" + hn + ".kt) - 1u < 4u ? " + hn + ".a : 0u)], 0u, node_type(" + hn +
+                                    ".kt) - 1u < 4u ? 0x07060504u : 0x0c0c0c0cu);\n");
+                else
+                  T->code.push_back("  const uint32_t " + wv + " = node_type(" + hn + ".kt) - 1u < 4u ? P.ptab[(size_t)" +
+                                    off + hn + ".a] : 0u;\n");
+              }
               scalar = "(vt_ - 1u < 4u ? ((" + wv + " >> " + std::to_string(sl->second % 32) + "u) & 1u) != 0u : " +
                        "g_pred_" + std::to_string(in.a) + "(V, S, S + vn_.b, pstr, vt_, vn_))";
             }
@@ -1055,6 +1076,7 @@ struct Gen {
     };
     std::ostringstream body;  // everything after the per-rule declarations
     for (size_t k = 0; k <= K; k++) {
+      std::ostringstream seg;  // the stage-k segments of every rule
       for (RGen& g : gs) {
         if (k > g.loops.size()) continue;
         const uint32_t sb = k == 0 ? g.b : g.loops[k - 1].second + 1;
@@ -1067,14 +1089,16 @@ struct Gen {
         R.se = "R" + std::to_string(g.ri) + "_S" + std::to_string(k);
         std::ostringstream w;
         emit_region(g, R, w);
-        // hoisted lookups first used by this segment, then the resume dispatch
-        body << global.flush() << "  // rule " << g.ri << " stage " << k << "\n  switch (rs" << g.s << ") {\n";
-        if (k == 0) body << "    case " << u32(g.b) << ": goto R" << g.ri << "_L" << g.b << ";\n";
+        // hoisted lookups first used by this segment (lazy placement), then the resume dispatch
+        if (!early_hoist) seg << global.flush();
+        seg << "  // rule " << g.ri << " stage " << k << "\n  switch (rs" << g.s << ") {\n";
+        if (k == 0) seg << "    case " << u32(g.b) << ": goto R" << g.ri << "_L" << g.b << ";\n";
         for (uint32_t t : g.resume)
-          if (t >= sb && t < se) body << "    case " << u32(t) << ": goto R" << g.ri << "_L" << t << ";\n";
-        body << "    default: goto " << R.se << ";\n  }\n" << w.str() << R.se << ":;\n";
-        if (k == g.loops.size()) body << store(g.ri);  // the rule has finished for every lane
+          if (t >= sb && t < se) seg << "    case " << u32(t) << ": goto R" << g.ri << "_L" << t << ";\n";
+        seg << "    default: goto " << R.se << ";\n  }\n" << w.str() << R.se << ":;\n";
+        if (k == g.loops.size()) seg << store(g.ri);  // the rule has finished for every lane
       }
+      body << global.flush() << seg.str();
       if (k == K) break;
       // fused loops of stage k: group rules by the symbolic array cursor
       std::map<std::string, std::vector<RGen*>> groups;
@@ -1115,7 +1139,8 @@ struct Gen {
           std::ostringstream w;
           emit_region(g, R, w);
           const Inst& end = ps.prog[le];
-          bodies << T.flush() << "    if (rs" << g.s << " & ACT_) {\n      c" << (d + 1) << g.s << " = el" << tag << ";\n"
+          if (!early_hoist) bodies << T.flush();
+          bodies << "    if (rs" << g.s << " & ACT_) {\n      c" << (d + 1) << g.s << " = el" << tag << ";\n"
                  << w.str() << "R" << g.ri << "_L" << le << ":;\n"
                  << "      if (ek" << g.s << " & 15u) { if (ek" << g.s << " & " << u32(EF_COND << 4) << ") ek" << g.s
                  << " = 0u; else rs" << g.s << " = " << u32(end.c) << "; }\n    }\n";
@@ -1131,7 +1156,7 @@ struct Gen {
              << "    for (uint32_t fli" << tag << " = 0u; fli" << tag << " < fn" << tag << "; fli" << tag << "++) {\n"
              << "      const uint32_t el" << tag << " = ni(ff" << tag << " + fli" << tag << ");\n"
              << "      const Node eln" << tag << " = N[el" << tag << "];\n"
-             << bodies.str() << "    }\n";
+             << T.flush() << bodies.str() << "    }\n";
         for (RGen* gp : grp) body << "    rs" << gp->s << " &= ~ACT_;\n";
         body << "  }\n";
       }
@@ -1212,13 +1237,13 @@ struct Gen {
     const std::string lb = waves > 0 ? "KV_WG, " + std::to_string(waves) : "KV_WG";
     o << "extern \"C\" __global__ __launch_bounds__(" << lb << ") void " << name
       << "(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp, const Node* __restrict__ N, "
-         "const Val* __restrict__ V, const uint8_t* __restrict__ S, DevOut O) {\n"
+         "const Val* __restrict__ V, const uint8_t* __restrict__ S, DevOut O, uint32_t r0) {\n"
       << "  constexpr uint32_t FIN_ = " << u32(FIN) << ", ACT_ = " << u32(ACT) << ";\n"
       << "  __shared__ uint32_t s_hist[" << nr << "][KV_HIST];\n"
       << "  const DevPS& P = *Pp;\n  const DevBatch& B = *Bp;\n  const uint8_t* __restrict__ pstr = P.pstr;\n"
       << "  for (uint32_t q = threadIdx.x; q < " << nr << "u * KV_HIST; q += KV_WG) (&s_hist[0][0])[q] = 0u;\n"
       << "  __syncthreads();\n"
-      << "  const uint32_t r = blockIdx.x * KV_WG + threadIdx.x;\n"
+      << "  const uint32_t r = r0 + blockIdx.x * KV_WG + threadIdx.x;\n"
       << "  const uint32_t n_res = B.n_res;\n"
       << "  const bool valid = r < n_res;\n"
       << "  const Res* __restrict__ R = B.res + (valid ? r : 0u);\n"
@@ -1284,6 +1309,11 @@ std::string rule_signature(const PolicySet& ps, uint32_t ri) {
 }
 
 }  // namespace
+
+uint32_t jit_chunk_rules() {
+  const char* ch = getenv("KVGPU_JIT_CHUNK");
+  return ch && atoi(ch) > 0 ? (uint32_t)atoi(ch) : 4u;
+}
 
 void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   auto t0 = std::chrono::steady_clock::now();

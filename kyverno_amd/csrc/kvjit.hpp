@@ -45,6 +45,8 @@ struct JitImage {
 
 // Generate the specialized source for every rule of `ps` (chunks of at most
 // `chunk_rules` rules per kernel).
+// rules per fused chunk: KVGPU_JIT_CHUNK (experiments), default 4 (C2 sweep)
+uint32_t jit_chunk_rules();
 void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out);
 // Compile every kernel program with hiprtc for gfx950, on parallel host threads
 // (KVGPU_JIT_THREADS, default: hardware threads), through the code-object cache

@@ -40,7 +40,7 @@ extern "C" void kvemu_mtab(const DevPS* P, const DevBatch* B, uint32_t words, ui
                            uint32_t* an, uint32_t* sl);
 
 typedef void (*ptab_fn)(const DevPS*, const Val*, const uint8_t*, uint32_t, uint32_t*);
-typedef void (*chunk_fn)(const DevPS*, const DevBatch*, const Node*, const Val*, const uint8_t*, DevOut);
+typedef void (*chunk_fn)(const DevPS*, const DevBatch*, const Node*, const Val*, const uint8_t*, DevOut, uint32_t);
 
 static std::string slurp(const char* p) {
   std::ifstream f(p, std::ios::binary);
@@ -108,8 +108,7 @@ int main(int argc, char** argv) {
     else make_shard(whole, ranges[sh].first, ranges[sh].second, &b);
     const uint64_t lo = ranges[sh].first;
     JitImage img;
-    const char* ch = getenv("KVGPU_JIT_CHUNK");
-    jit_generate(ps, ch ? (uint32_t)atoi(ch) : 8u, &img);
+    jit_generate(ps, jit_chunk_rules(), &img);
     if (KVEMU_SRC_HASH && fnv1a(img.source) != (uint64_t)KVEMU_SRC_HASH)
       throw std::runtime_error("generated source differs from the one this binary was built from");
 
@@ -205,7 +204,7 @@ int main(int argc, char** argv) {
     }
     const uint32_t blocks = (uint32_t)((nres + KV_WG - 1) / KV_WG);
     auto pass = [&]() {
-      for (chunk_fn f : fns) grid(blocks, 1, [&]() { f(&P, &B, B.nodes, B.vals, B.bstr, O); });
+      for (chunk_fn f : fns) grid(blocks, 1, [&]() { f(&P, &B, B.nodes, B.vals, B.bstr, O, 0u); });
     };
     if (nres) pass();
     bool wide = false;

@@ -18,6 +18,7 @@
 #define __shared__ static thread_local
 #define __launch_bounds__(...)
 #define __restrict__ __restrict
+#define KV_SCONST
 
 struct kvemu_dim3 {
   uint32_t x, y, z;
@@ -56,5 +57,17 @@ static inline uint32_t kvemu_readfirstlane(uint32_t v) { return v; }
 static inline uint32_t kvemu_alignbyte(uint32_t hi, uint32_t lo, uint32_t sh) {
   return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (sh & 3)));
 }
+// v_perm_b32: byte i of the result = byte sel[i] of {s0 (bytes 4-7), s1 (bytes 0-3)}; 0x0c -> 0x00, >= 0x0d -> 0xff
+static inline uint32_t kvemu_perm(uint32_t s0, uint32_t s1, uint32_t sel) {
+  const uint64_t v = ((uint64_t)s0 << 32) | s1;
+  uint32_t r = 0;
+  for (int i = 0; i < 4; i++) {
+    const uint32_t b = (sel >> (8 * i)) & 0xFF;
+    const uint32_t x = b < 8 ? (uint32_t)(v >> (8 * b)) & 0xFF : b == 0x0c ? 0u : 0xFFu;
+    r |= x << (8 * i);
+  }
+  return r;
+}
+#define __builtin_amdgcn_perm(s0, s1, sel) kvemu_perm(s0, s1, sel)
 #define __builtin_amdgcn_readfirstlane(v) kvemu_readfirstlane(v)
 #define __builtin_amdgcn_alignbyte(hi, lo, sh) kvemu_alignbyte(hi, lo, sh)
