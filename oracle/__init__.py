@@ -59,6 +59,8 @@ class Oracle:
         L.orc_substitute.restype = ctypes.c_void_p
         L.orc_validate.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
         L.orc_substitute_message.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.orc_substitute_vars.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.orc_substitute_vars.restype = ctypes.c_void_p
         L.orc_substitute_message.restype = ctypes.c_void_p
         L.orc_validate.restype = ctypes.c_void_p
         L.orc_last_error.restype = ctypes.c_char_p
@@ -124,6 +126,12 @@ class Oracle:
 
     def substitute(self, pattern_json: str) -> dict:
         return json.loads(self._take(self.lib.orc_substitute(pattern_json.encode())))
+
+    def substitute_vars(self, pattern: dict | list, resource: dict) -> dict:
+        """SubstituteAll of a pattern document with request.object = resource:
+        {"doc": ...} | {"error": message} | {"scope": False} (outside the device scope)."""
+        return json.loads(self._take(self.lib.orc_substitute_vars(json.dumps(pattern).encode(),
+                                                                  json.dumps(resource).encode())))
 
     def substitute_message(self, msg: str, resource: dict | str):
         """buildErrorMessage's message substitution; None where the reference panics."""

@@ -158,6 +158,25 @@ char* orc_substitute(const char* pattern_json) {
   }
 }
 
+// SubstituteAll of a validate.pattern document with request.object = resource (references,
+// then variables): {"doc": ...} | {"error": ...} | {"scope": false} (outside the device scope)
+char* orc_substitute_vars(const char* pattern_json, const char* resource_json) {
+  try {
+    Value p = parse_json(pattern_json, NumMode::Float);
+    Value rv = parse_json(resource_json, NumMode::Unstructured);
+    std::string err;
+    if (!PatternVarsInScope(p)) return dup("{\"scope\":false}");
+    if (!SubstituteReferences(p, &err, !DocHasVariable(p))) return dup("{\"error\":" + jstr(err) + "}");
+    int r = SubstitutePatternVars(p, rv, &err);
+    if (r == 1) return dup("{\"error\":" + jstr(err) + "}");
+    if (r == 2) return dup("{\"scope\":false}");
+    return dup("{\"doc\":" + to_json(p) + "}");
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return nullptr;
+  }
+}
+
 // buildErrorMessage's SubstituteAll of a validate message against request.object = resource
 // (validation.go:518-524). Returns nullptr where the reference panics.
 char* orc_substitute_message(const char* msg, const char* resource_json) {

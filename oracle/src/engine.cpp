@@ -613,8 +613,12 @@ std::string route_reason(const Rule& rule) {
   if (rule.foreachP) return "foreach";
   if (rule.contextNonEmpty) return "context";
   if (rule.preconditionsP) return "preconditions";
-  if (rule.patternP) { if (DocHasVariable(rule.pattern)) return "variables"; return ""; }
-  if (rule.anyPatternP) { if (DocHasVariable(rule.anyPattern)) return "variables"; return ""; }
+  // variables: on the device when every one is request.object<path> or @ and none is in a key
+  if (rule.patternP) { if (DocHasVariable(rule.pattern) && !PatternVarsInScope(rule.pattern)) return "variables"; return ""; }
+  if (rule.anyPatternP) {
+    if (DocHasVariable(rule.anyPattern) && !PatternVarsInScope(rule.anyPattern)) return "variables";
+    return "";
+  }
   if (rule.denyP) return "deny";
   return "";
 }
@@ -627,18 +631,26 @@ RuleResult evaluate_rule(const Rule& rule, const Value& resource) {
   if (!rule.patternP && !rule.anyPatternP) { rr.status = NOMATCH; return rr; }  // validate() returns nil
   Value pattern, anyPattern;
   std::string err;
-  if (rule.patternP) {
-    pattern = rule.pattern;
-    if (!SubstituteReferences(pattern, &err)) {
+  // SubstituteAll (validation.go:549-571, vars.go:172-179): references, then variables
+  Value& doc = rule.patternP ? pattern : anyPattern;
+  doc = rule.patternP ? rule.pattern : rule.anyPattern;
+  const bool vars = DocHasVariable(doc);
+  if (!SubstituteReferences(doc, &err, !vars)) {
+    rr.status = ERROR;
+    rr.message = "variable substitution failed: " + err;
+    return rr;
+  }
+  if (vars) {
+    bool structural = false;
+    int r = SubstitutePatternVars(doc, resource, &err, &structural);
+    if (r == 1) {
       rr.status = ERROR;
       rr.message = "variable substitution failed: " + err;
       return rr;
     }
-  } else {
-    anyPattern = rule.anyPattern;
-    if (!SubstituteReferences(anyPattern, &err)) {
-      rr.status = ERROR;
-      rr.message = "variable substitution failed: " + err;
+    if (r == 2 || structural) {  // a value from the resource leaves the device scope (structural / nested variable)
+      rr.status = CPU;
+      rr.reason = "variables";
       return rr;
     }
   }

@@ -74,7 +74,14 @@ void ExpandInMetadata(Value& patternMap, const Value& resourceMap);
 
 // $() references: pkg/engine/variables/vars.go:253-309,450-554
 // Returns false with *err set on failure (message as the reference formats it).
-bool SubstituteReferences(Value& document, std::string* err);
+bool SubstituteReferences(Value& document, std::string* err, bool unescape = true);
+// validate.pattern variables (subst.cpp "pattern variables"): QueryObject returns 0 found
+// (*out, nullptr for null), 1 unknown key (*missing), 2 outside the device scope;
+// SubstitutePatternVars 0 ok, 1 error (*err = the reference's message), 2 outside scope;
+// *structural: some whole-string variable resolved to a map / array (a structural pattern)
+int QueryObject(const std::string& q, const Value& resource, const Value** out, std::string* missing);
+bool PatternVarsInScope(const Value& doc);
+int SubstitutePatternVars(Value& doc, const Value& resource, std::string* err, bool* structural = nullptr);
 bool SubstituteMessage(const std::string& msg, const Value& resource, std::string* out);
 // True if the string contains an unescaped {{...}} (RegexVariables, vars.go:20)
 bool HasVariable(const std::string& s);

@@ -320,11 +320,11 @@ bool DocHasVariable(const Value& v) {
   }
 }
 
-bool SubstituteReferences(Value& document, std::string* err) {
+bool SubstituteReferences(Value& document, std::string* err, bool unescape) {
   Value original = document;  // references resolve against the unmodified document
   Ctx cx{&original};
   if (!traverse(cx, document, "", err)) return false;
-  unescape_vars(document);
+  if (unescape) unescape_vars(document);  // (documents with variables: per string, after substitution)
   return true;
 }
 
@@ -541,6 +541,267 @@ bool SubstituteMessage(const std::string& msg, const Value& resource, std::strin
   for (const auto& e : find_escaped_vars(value)) value = replace_n(value, e, e.substr(1), -1);
   *out = value;
   return true;
+}
+
+
+// ---------------------------------------------------------------- pattern variables
+// substituteVars over a validate.pattern / anyPattern document (vars.go:319-398, traversal
+// jsonutils/traverse.go:58-130: the action runs on an element first, then the traversal
+// descends into what it returned; per map entry the key, then the value; canonical key
+// order) with the CLI / admission JSON context {"request":{"object": resource}} (numbers
+// read back as float64). Device scope: variables `request.object<path>`
+// (fields, "quoted" fields, [index]) and `@`; anything else is outside it.
+namespace {
+
+// regexVariableInit = ^\{\{[^{}]*\}\}
+bool var_initial(const std::string& v) {
+  if (v.compare(0, 2, "{{") != 0) return false;
+  size_t k = 2;
+  while (k < v.size() && v[k] != '{' && v[k] != '}') k++;
+  return v.compare(k, 2, "}}") == 0;
+}
+
+std::string trim_space(const std::string& s) {
+  size_t b = s.find_first_not_of(" \t\n\r\v\f"), e = s.find_last_not_of(" \t\n\r\v\f");
+  return b == std::string::npos ? "" : s.substr(b, e - b + 1);
+}
+
+// getJMESPath (vars.go:416-422): tokens [3:] of the traversal path joined with '.', then
+// regexPathDigit `\.?([\d])\.?` -> "[$1]." and '.' trimmed. false where the reference's
+// slice expression panics (fewer than 3 tokens).
+bool jmes_path_of(const std::string& raw, std::string* out) {
+  std::vector<std::string> tok;
+  size_t i = 0;
+  while (true) {
+    size_t j = raw.find('/', i);
+    tok.push_back(raw.substr(i, j == std::string::npos ? std::string::npos : j - i));
+    if (j == std::string::npos) break;
+    i = j + 1;
+  }
+  if (tok.size() < 3) return false;
+  std::string path;
+  for (size_t k = 3; k < tok.size(); k++) path += (k > 3 ? "." : "") + tok[k];
+  std::string b;
+  for (size_t k = 0; k < path.size();) {
+    size_t d = k;
+    if (path[d] == '.' && d + 1 < path.size() && isdigit((unsigned char)path[d + 1])) d++;
+    if (isdigit((unsigned char)path[d])) {
+      size_t e = d + 1;
+      if (e < path.size() && path[e] == '.') e++;
+      b += "[";
+      b += path[d];
+      b += "].";
+      k = e;
+      continue;
+    }
+    b += path[k++];
+  }
+  size_t s0 = b.find_first_not_of('.'), s1 = b.find_last_not_of('.');
+  *out = s0 == std::string::npos ? "" : b.substr(s0, s1 - s0 + 1);
+  return true;
+}
+
+// the query of one variable (after brace removal and trimming); false: outside the scope
+bool var_query(const std::string& var, const std::string& path, std::string* q) {
+  if (var == "@") {
+    std::string p;
+    if (!jmes_path_of(path, &p)) return false;
+    *q = (!p.empty() && p[0] == '[') ? "request.object" + p : "request.object." + p;
+    return true;
+  }
+  *q = var;
+  return true;
+}
+
+// a resource value as the JSON context returns it (numbers float64)
+void to_context(Value& v) {
+  if (v.t == T::Int) {
+    v = Value::mk_float((double)v.i);
+  } else if (v.t == T::Map) {
+    for (auto& e : v.m) to_context(*e.val);
+  } else if (v.t == T::Arr) {
+    for (auto* x : v.a) to_context(*x);
+  }
+}
+Value as_context(const Value* v) {
+  if (!v) return Value();
+  Value c = *v;
+  to_context(c);
+  return c;
+}
+
+// substituteVariablesIfAny on one string: 0 ok (*out = the new element), 1 error, 2 outside scope
+int subst_var_string(const std::string& s, const std::string& path, const Value& resource, Value* out,
+                     std::string* err, bool* structural) {
+  std::string value = s;
+  auto vars = find_vars(value);
+  while (!vars.empty()) {
+    std::string original = value;
+    for (std::string v : vars) {
+      const bool initial = var_initial(v);
+      const std::string old = v;
+      if (!initial) v = v.substr(1);
+      const std::string var = trim_space(replace_n(replace_n(v, "{{", "", -1), "}}", "", -1));
+      std::string q;
+      if (!var_query(var, path, &q)) return 2;
+      const Value* got = nullptr;
+      std::string missing;
+      int r = QueryObject(q, resource, &got, &missing);
+      if (r == 2) return 2;
+      if (r == 1) {
+        *err = "Unknown key \"" + missing + "\" in path";
+        return 1;
+      }
+      if (original == v) {
+        if (got && (got->t == T::Map || got->t == T::Arr)) *structural = true;
+        *out = as_context(got);
+        return 0;
+      }
+      const std::string prefix = initial ? "" : old.substr(0, 1);
+      const Value cv = as_context(got);
+      const std::string sub = got && got->t == T::Str ? got->s : json_marshal(got ? &cv : nullptr);
+      value = replace_n(original, prefix + v, prefix + sub, 1);
+    }
+    vars = find_vars(value);
+  }
+  for (const auto& e : find_escaped_vars(value)) value = replace_n(value, e, e.substr(1), -1);
+  *out = Value::mk_str(value);
+  return 0;
+}
+
+int traverse_vars(Value& v, const std::string& path, const Value& resource, std::string* err, bool* structural) {
+  if (v.t == T::Str) {
+    Value nv;
+    int r = subst_var_string(v.s, path, resource, &nv, err, structural);
+    if (r) return r;
+    v = nv;
+    if (v.t != T::Map && v.t != T::Arr) return 0;
+    // the traversal descends into what the action returned (traverse.go:63-76)
+  }
+  if (v.t == T::Map) {
+    std::vector<std::string> keys;
+    for (const auto* e : sorted_entries(v)) keys.push_back(e->key);
+    for (const auto& k : keys) {
+      if (HasVariable(k)) return 2;  // variables in keys: outside scope
+      std::string nk = k;
+      for (const auto& e : find_escaped_vars(k)) nk = replace_n(nk, e, e.substr(1), -1);
+      Value* child = v.get_mut(k);
+      int r = traverse_vars(*child, path + "/" + k, resource, err, structural);
+      if (r) return r;
+      if (nk != k) {
+        Value copy = *child;
+        std::string order;
+        for (auto& e : v.m)
+          if (e.key == k) order = e.order;
+        v.erase(k);
+        v.set(nk, copy, order);
+      }
+    }
+    return 0;
+  }
+  if (v.t == T::Arr) {
+    for (size_t k = 0; k < v.a.size(); k++) {
+      int r = traverse_vars(*v.a[k], path + "/" + std::to_string(k), resource, err, structural);
+      if (r) return r;
+    }
+  }
+  return 0;
+}
+
+bool vars_in_scope(const Value& v, const std::string& path) {
+  if (v.t == T::Str) {
+    for (std::string x : find_vars(v.s)) {
+      if (!var_initial(x)) x = x.substr(1);
+      const std::string var = trim_space(replace_n(replace_n(x, "{{", "", -1), "}}", "", -1));
+      std::string q;
+      if (!var_query(var, path, &q) || QueryObject(q, Value::mk_map(), nullptr, nullptr) == 2) return false;
+    }
+    return true;
+  }
+  if (v.t == T::Map) {
+    for (const auto& e : v.m)
+      if (HasVariable(e.key) || !vars_in_scope(*e.val, path + "/" + e.key)) return false;
+    return true;
+  }
+  if (v.t == T::Arr)
+    for (size_t k = 0; k < v.a.size(); k++)
+      if (!vars_in_scope(*v.a[k], path + "/" + std::to_string(k))) return false;
+  return true;
+}
+
+}  // namespace
+
+int QueryObject(const std::string& q, const Value& resource, const Value** out, std::string* missing) {
+  // grammar check first (out == nullptr: check only)
+  const std::string root = "request.object";
+  if (q.compare(0, root.size(), root) != 0) return 2;
+  const Value* cur = &resource;
+  bool lost = false;  // a missing key was met (the search stops there with NotFoundError)
+  std::string miss;
+  size_t i = root.size();
+  while (i < q.size()) {
+    if (q[i] == '[') {
+      size_t e = q.find(']', i);
+      if (e == std::string::npos || e == i + 1) return 2;
+      std::string num = q.substr(i + 1, e - i - 1);
+      for (size_t k = 0; k < num.size(); k++)
+        if (!(isdigit((unsigned char)num[k]) || (k == 0 && num[k] == '-' && num.size() > 1))) return 2;
+      long idx = atol(num.c_str());
+      if (!lost) {
+        if (cur && cur->t == T::Arr) {
+          long n = (long)cur->a.size();
+          if (idx < 0) idx += n;
+          cur = (idx >= 0 && idx < n) ? cur->a[idx] : nullptr;
+        } else {
+          cur = nullptr;
+        }
+      }
+      i = e + 1;
+      continue;
+    }
+    if (q[i] != '.') return 2;
+    i++;
+    std::string key;
+    if (i < q.size() && q[i] == '"') {
+      i++;
+      while (i < q.size() && q[i] != '"') {
+        if (q[i] == '\\' && i + 1 < q.size()) i++;
+        key += q[i++];
+      }
+      if (i >= q.size()) return 2;
+      i++;
+    } else {
+      size_t s = i;
+      while (i < q.size() && (isalnum((unsigned char)q[i]) || q[i] == '_')) i++;
+      if (i == s || isdigit((unsigned char)q[s])) return 2;
+      key = q.substr(s, i - s);
+    }
+    if (!lost) {
+      if (cur && cur->t == T::Map) {
+        const Value* nx = cur->get(key);
+        if (!nx) { lost = true; miss = key; }
+        cur = nx;
+      } else {
+        cur = nullptr;
+      }
+    }
+  }
+  if (!out) return 0;
+  if (lost) {
+    if (missing) *missing = miss;
+    return 1;
+  }
+  *out = cur;
+  return 0;
+}
+
+bool PatternVarsInScope(const Value& doc) { return vars_in_scope(doc, ""); }
+
+int SubstitutePatternVars(Value& doc, const Value& resource, std::string* err, bool* structural) {
+  bool st = false;
+  int r = traverse_vars(doc, "", resource, err, &st);
+  if (structural) *structural = st;
+  return r;
 }
 
 }  // namespace orc
