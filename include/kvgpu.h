@@ -134,6 +134,13 @@ int kv_result_error(const kv_result* r, uint32_t rule, uint64_t res, uint32_t* k
  * for other statuses or constant (compile-time) statuses, KV_E_PARSE for bad JSON. */
 int kv_result_error_message(const kv_result* r, uint32_t rule, uint64_t res, const char* resource_json, size_t len,
                             char* buf, size_t cap);
+
+/* Pattern variables: when rule `rule` is ERROR on `res` because
+ * substituting the `{{request.object...}}` variables of its pattern failed, writes the
+ * RuleResponse message "variable substitution failed: <error>" (pkg/engine/validation.go:
+ * 181-189, the reference's processValidationRule -> substitutePatterns) and returns its
+ * length; 0 when the pair's status has another cause. */
+int kv_result_subst_error(const kv_result* r, uint32_t rule, uint64_t res, char* buf, size_t cap);
 double kv_result_kernel_ms(const kv_result* r);
 
 /* Bulk export of the failing pairs (KV_MODE_ERRORS): every FAIL / ERROR / SKIP pair,

@@ -166,6 +166,19 @@ class Result:
             return None
         return buf.value.decode("utf-8")
 
+    def subst_error(self, rule: int, res: int) -> str | None:
+        """The RuleResponse message of an ERROR pair caused by the pattern's variables failing to
+        substitute ("variable substitution failed: ...", ``kv_result_subst_error``), else None."""
+        cap = 1 << 12
+        while True:
+            buf = ctypes.create_string_buffer(cap)
+            n = lib().kv_result_subst_error(self._h, rule, res, buf, cap)
+            if n <= 0:
+                return None
+            if n < cap:
+                return buf.raw[:n].decode("utf-8", "replace")
+            cap = n + 1
+
     def error_message(self, rule: int, res: int, resource) -> str | None:
         """err.Error() of the pattern error behind a FAIL / ERROR / SKIP pair (``kv_result_error_message``):
         the SKIP message, and the operand of the ERROR message. ``resource`` is the ingested document

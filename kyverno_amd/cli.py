@@ -99,6 +99,7 @@ class Evaluation:
     status: np.ndarray      # u8 [n_rules][n_res]
     paths: dict = field(default_factory=dict)   # (rule, res) -> failing path (FAIL pairs)
     errors: dict = field(default_factory=dict)  # (rule, res) -> err.Error() of ERROR / SKIP pairs
+    subst: dict = field(default_factory=dict)   # (rule, res) -> message of a pattern-variable substitution ERROR
     anypattern: dict = field(default_factory=dict)  # (rule, res) -> [(status, path)] per pattern
     warnings: list = field(default_factory=list)    # host-side limits met while rendering messages
 
@@ -123,13 +124,25 @@ def evaluate(policies: list[dict], resources: list[dict], device: int = 0, messa
         for ri, res in zip(*np.nonzero(r.status == FAIL)):
             if not ps.rules[ri].any_pattern:
                 ev.paths[(int(ri), int(res))] = r.path(int(ri), int(res))
-        for ri, res in zip(*np.nonzero((r.status == ERROR) | (r.status == SKIP))):
-            if not ps.rules[ri].any_pattern:
-                m = r.error_message(int(ri), int(res), resources[int(res)])
-                if m is not None:
-                    ev.errors[(int(ri), int(res))] = m
+        collect_errors(ev, ps, r, resources)
         _evaluate_anypatterns(ev, device, specialize, namespace_labels)
     return ev
+
+
+def collect_errors(ev: Evaluation, ps, r, resources: list) -> None:
+    """Messages of the ERROR / SKIP pairs: pattern-variable substitution errors (whole message),
+    else the pattern error's err.Error() (pattern rules; anyPattern rules render per pattern)."""
+    for ri, res in zip(*np.nonzero((r.status == ERROR) | (r.status == SKIP))):
+        key = (int(ri), int(res))
+        if r.status[ri, res] == ERROR:
+            m = r.subst_error(*key)
+            if m is not None:
+                ev.subst[key] = m
+                continue
+        if not ps.rules[ri].any_pattern:
+            m = r.error_message(int(ri), int(res), resources[int(res)])
+            if m is not None:
+                ev.errors[key] = m
 
 
 def _evaluate_anypatterns(ev: Evaluation, device: int, specialize: bool = False,
@@ -199,6 +212,8 @@ def rule_message(ev: Evaluation, rule, res: int) -> str:
     pkg/engine/validation.go:421-547): pass / fail from the status and failing path, skip / error
     from the device's error record rendered by ``kv_result_error_message``."""
     st = int(ev.status[rule.index, res])
+    if st == ERROR and (rule.index, res) in ev.subst:  # ruleError("variable substitution failed", err)
+        return ev.subst[(rule.index, res)]
     if rule.any_pattern:
         outs = ev.anypattern.get((rule.index, res), [])
         if st == PASS:

@@ -152,6 +152,28 @@ std::string go_format_g(double v) {
   return out;
 }
 
+// encoding/json's float64 encoding (floatEncoder): strconv 'f' -1, or 'e' -1 when
+// |v| < 1e-6 || |v| >= 1e21 (v != 0), with "e-0d" shortened to "e-d"
+std::string go_json_float(double v) {
+  const double a = std::fabs(v);
+  if (a != 0 && (a < 1e-6 || a >= 1e21)) {
+    char buf[64];
+    auto r = std::to_chars(buf, buf + sizeof buf, v, std::chars_format::scientific);
+    std::string s(buf, r.ptr);  // shortest d[.ddd]e±XX
+    const size_t e = s.find('e');
+    std::string ex = s.substr(e + 1);
+    const char sign = ex[0];
+    std::string digs = ex.substr(1);
+    while (digs.size() > 2 && digs[0] == '0') digs.erase(0, 1);
+    if (digs.size() < 2) digs = "0" + digs;
+    if (sign == '-' && digs.size() == 2 && digs[0] == '0') digs.erase(0, 1);
+    return s.substr(0, e) + "e" + sign + digs;
+  }
+  char buf[400];
+  auto r = std::to_chars(buf, buf + sizeof buf, v, std::chars_format::fixed);
+  return std::string(buf, r.ptr);
+}
+
 std::string go_format_f6(double v) {
   if (std::isnan(v)) return "NaN";
   if (std::isinf(v)) return v > 0 ? "+Inf" : "-Inf";

@@ -119,6 +119,8 @@ enum ResFlags : uint32_t {
   RF_BAD_META = 1u << 2,        // some metadata/labels/annotations shape would make ExpandInMetadata panic
   RF_MAGIC = 1u << 3,           // a string/key contains "conditional anchor mismatch" / "global anchor mismatch"
   RF_NAME_ASCII = 1u << 4,      // metadata.name is ASCII (word globs exact for '?')
+  RF_BAD_LABELS = 1u << 5,      // ... through a labels map (a non-map metadata, or non-string label values)
+  RF_BAD_ANN = 1u << 6,         // ... through an annotations map
 };
 
 struct KV {
@@ -176,6 +178,8 @@ enum Op : uint32_t {
   OP_ALT_BEGIN,   // anyPattern alternative start: reset error / anchors
   OP_ALT_END,     // anyPattern alternative end: PASS lanes finish
   OP_DONE,        // program end
+  OP_VLEAF,       // d, dynamic leaf, node: OP_LEAF with the per-resource predicate of a pattern
+                  // string holding variables (DevBatch::dleaf -> DevBatch::dps, kvvars.cpp)
 };
 
 // Key-lookup ops (KEY, KEYV, AREG, NEG): `a` is the slot index of the key in
@@ -283,8 +287,14 @@ struct RuleRec {
   uint32_t m_mode, m_first, m_count;  // match: 0 legacy, 1 any, 2 all; filters
   uint32_t x_mode, x_first, x_count;  // exclude
   uint32_t n_alts;          // 0: pattern; >0: anyPattern alternatives
-  uint32_t pad;
+  uint32_t dyn;             // pattern variables: 1 + dynamic-rule index (DevBatch::dyn_st), 0 none
 };
-enum RuleFlags : uint32_t { RR_META_EXPAND = 1 };
+// RR_META_LABELS / RR_META_ANN: the pattern's ExpandInMetadata sites read labels / annotations
+// (wildcards.go:69-139 panics on a resource whose map of that tag is not a string map)
+enum RuleFlags : uint32_t { RR_META_EXPAND = 1, RR_META_LABELS = 2, RR_META_ANN = 4 };
+// resource flags that make rule flags `rf` panic in ExpandInMetadata (routed: ST_CPU)
+KV_HD constexpr uint32_t meta_bad_flags(uint32_t rf) {
+  return ((rf & RR_META_LABELS) ? (uint32_t)RF_BAD_LABELS : 0u) | ((rf & RR_META_ANN) ? (uint32_t)RF_BAD_ANN : 0u);
+}
 
 }  // namespace kv

@@ -97,6 +97,9 @@ struct DevPolicySet {
 
 struct DevBatchRes {
   DevBuf nodes, vals, res, kvs, bstr, nsbits, koff, klen, kstr, nsms, lsets, asets, view_dev;
+  // pattern variables (kvvars.cpp): the batch predicate table (a DevPS with its pred tables),
+  // outcome ids per [dynamic leaf][res], statuses per [dynamic rule][res]
+  DevBuf dpreds, dalts, dconjs, datoms, dgsegs, dgwords, dpstr, dps, dleaf, dynst;
   DevBatch view{};
 };
 
@@ -114,6 +117,12 @@ struct kv_batch {
   const kv_policyset* owner = nullptr;
   std::mutex mu;
   std::map<int, std::unique_ptr<DevBatchRes>> dev;
+  std::once_flag dyn_once;
+  DynHost dyn;  // pattern-variable tables (build_dyn), on first use
+  const DynHost& dyn_host(const PolicySet& ps) {
+    std::call_once(dyn_once, [&]() { build_dyn(ps, b, &dyn); });
+    return dyn;
+  }
 };
 
 namespace {
@@ -368,6 +377,30 @@ DevBatchRes& dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
   v.n_asets = (uint32_t)b.asets.size();
   v.ns_words = b.ns_words;
   v.n_res = (uint32_t)b.res.size();
+  {  // pattern variables: every pointer valid (16-byte buffers when the policy set has none)
+    const DynHost& h = bt->dyn_host(ps);
+    d->dpreds.upload(h.tbl.preds, device);
+    d->dalts.upload(h.tbl.alts, device);
+    d->dconjs.upload(h.tbl.conjs, device);
+    d->datoms.upload(h.tbl.atoms, device);
+    d->dgsegs.upload(h.tbl.gsegs, device);
+    d->dgwords.upload(h.tbl.gwords, device);
+    d->dpstr.upload_raw(h.tbl.strs.data(), h.tbl.strs.size(), device);
+    DevPS dv{};
+    dv.preds = (const Pred*)d->dpreds.p;
+    dv.alts = (const Alt*)d->dalts.p;
+    dv.conjs = (const Conj*)d->dconjs.p;
+    dv.atoms = (const Atom*)d->datoms.p;
+    dv.gsegs = (const GSeg*)d->dgsegs.p;
+    dv.gwords = (const GWord*)d->dgwords.p;
+    dv.pstr = (const uint8_t*)d->dpstr.p;
+    d->dps.upload_raw(&dv, sizeof(DevPS), device);
+    d->dleaf.upload(h.dleaf, device);
+    d->dynst.upload(h.dyn_st, device);
+    v.dps = (const DevPS*)d->dps.p;
+    v.dleaf = (const uint32_t*)d->dleaf.p;
+    v.dyn_st = (const uint8_t*)d->dynst.p;
+  }
   d->view_dev.upload_raw(&d->view, sizeof(DevBatch), device);
   auto& ref = *d;
   bt->dev[device] = std::move(d);
@@ -494,10 +527,12 @@ int64_t res_at(const JDoc& d, const std::vector<PathSeg>& segs) {
 // (pkg/engine/validate/validate.go:62-172, pkg/engine/anchor/anchor.go:61-261;
 // condition / global anchor handlers wrap what propagates through them,
 // anchor.go:72-95 with common/anchorKey.go:21-40)
-std::string error_message(const PolicySet& ps, const Batch& b, const ErrRec& e, const JDoc& doc) {
+std::string error_message(const PolicySet& ps, const Batch& b, const ErrRec& e, const JDoc& doc,
+                          const std::string* dyn_pat_v = nullptr) {
   const uint32_t kind = err_kind(e);
   if (e.pnode >= ps.pnodes.size()) return "";
-  const PNodeInfo& P = ps.pnodes[e.pnode];
+  PNodeInfo P = ps.pnodes[e.pnode];
+  if (P.dleaf >= 0 && dyn_pat_v) P.pat_v = *dyn_pat_v;  // the resource's substituted pattern value
   const std::vector<PathSeg> segs = path_segs(ps, b, e, e.pnode);
   const std::string path = join_path(segs);
   std::string m;
@@ -1206,11 +1241,44 @@ int kv_result_error_message(const kv_result* r, uint32_t rule, uint64_t res, con
     ErrRec e;
     const Batch* bt = nullptr;
     if (!r->err(rule, res, &e, &bt)) return KV_E_INVALID;
-    m = error_message(r->ps->ps, *bt, e, doc);
+    std::string pv;
+    const std::string* dyn_pv = nullptr;
+    if (e.pnode < r->ps->ps.pnodes.size() && r->ps->ps.pnodes[e.pnode].dleaf >= 0) {
+      const ResultPart* p = r->part_of(res);
+      kv_batch* kb = p->shard ? p->shard.get() : const_cast<kv_batch*>(r->b);
+      const DynHost& h = kb->dyn_host(r->ps->ps);
+      const uint64_t nl = kb->b.res.size(), local = res - p->lo;
+      const uint32_t o = h.dleaf[(size_t)r->ps->ps.pnodes[e.pnode].dleaf * nl + local];
+      pv = pattern_go_v(outcome_value(kb->b.vout_tab[o]));
+      dyn_pv = &pv;
+    }
+    m = error_message(r->ps->ps, *bt, e, doc, dyn_pv);
   } catch (const std::exception&) {
     return KV_E_PARSE;
   }
   if (m.empty()) return KV_E_INVALID;  // a compile-time constant status: no pattern error record
+  if (buf && cap) {
+    size_t n = std::min(cap - 1, m.size());
+    memcpy(buf, m.data(), n);
+    buf[n] = 0;
+  }
+  return (int)m.size();
+}
+
+int kv_result_subst_error(const kv_result* r, uint32_t rule, uint64_t res, char* buf, size_t cap) {
+  if (!r) return KV_E_INVALID;
+  if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
+  const RuleRec& rr = r->ps->ps.rules[rule];
+  if (!rr.dyn || r->status[(size_t)rule * r->n_res + res] != ST_ERROR) return 0;
+  const ResultPart* p = r->part_of(res);
+  if (!p) return 0;
+  kv_batch* kb = p->shard ? p->shard.get() : const_cast<kv_batch*>(r->b);
+  const DynHost& h = kb->dyn_host(r->ps->ps);
+  const uint64_t nl = kb->b.res.size(), local = res - p->lo;
+  const size_t q = (size_t)(rr.dyn - 1) * nl + local;
+  if (h.dyn_st[q] != ST_ERROR) return 0;
+  // ruleError(rule, Validation, "variable substitution failed", err) (validation.go:186-188)
+  const std::string m = "variable substitution failed: " + kb->b.vout_tab[h.dyn_msg[q]].substr(1);
   if (buf && cap) {
     size_t n = std::min(cap - 1, m.size());
     memcpy(buf, m.data(), n);

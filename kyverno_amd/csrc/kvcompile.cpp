@@ -833,7 +833,7 @@ struct Compiler {
           bool wild = false;
           for (auto& k : lm.mk) wild |= has_wild(k);
           if (wild && array_ctx > 0) { cpu_reason = "wildcard metadata keys under an array"; return; }
-          rule_flags |= RR_META_EXPAND;
+          rule_flags |= RR_META_EXPAND | (tag[0] == 'l' ? RR_META_LABELS : RR_META_ANN);
         }
         if (rule_flags & RR_META_EXPAND) emit(OP_METACHK, d, 0, 0, 0, cs);
       }
@@ -863,7 +863,7 @@ struct Compiler {
         return;
       }
       if (p0.t != J_ARR) {  // scalar: every element
-        emit(OP_LEAF, d, 0, pred(p0), pn, cs);
+        leaf(p0, d, pn, cs);
         return;
       }
       // nested arrays: positional
@@ -878,6 +878,19 @@ struct Compiler {
         uint32_t e = emit(OP_POS_END, d, 0, 0, 0, cs);
         end_scope(s, e);
       }
+      return;
+    }
+    leaf(P, d, pn, cs);
+  }
+
+  // scalar pattern leaf: a compiled predicate, or (a string holding variables) a dynamic
+  // leaf whose predicate is the resource's substituted value (kvvars.cpp)
+  void leaf(const PV& P, uint32_t d, uint32_t pn, uint32_t cs) {
+    if (P.t == J_STR && P.vstr >= 0) {
+      const uint32_t dl = (uint32_t)ps.dleaf_vstr.size();
+      ps.dleaf_vstr.push_back((uint32_t)P.vstr);
+      ps.pnodes[pn].dleaf = (int32_t)dl;
+      emit(OP_VLEAF, d, 0, dl, pn, cs);
       return;
     }
     emit(OP_LEAF, d, 0, pred(P), pn, cs);
@@ -1047,6 +1060,74 @@ struct Compiler {
 
 // ---------------------------------------------------------------- policies
 namespace {
+
+// Pattern strings holding variables, in the reference's traversal order (jsonutils/traverse.go:
+// per map entry the key then the value, keys in canonical byte order; arrays in order), with
+// their traversal paths: marks each with its VarStr and unescapes `\{{..}}` in every other
+// string and key (substituteVariablesIfAny unescapes each leaf / key it visits, vars.go:393-395).
+static void collect_var_strings(PolicySet& ps, PV& v, const std::string& path, uint32_t rule, bool label_value,
+                                std::map<std::pair<std::string, std::string>, uint32_t>& keys) {
+  if (v.t == J_STR) {
+    if (!var_string(v.s)) {
+      v.s = unescape_var_string(v.s);
+      return;
+    }
+    VarStr vs;
+    vs.rule = rule;
+    vs.text = v.s;
+    vs.path = path;
+    vs.want_string = label_value;
+    auto k = std::make_pair(v.s, path);
+    auto it = keys.find(k);
+    if (it == keys.end()) {
+      it = keys.emplace(k, (uint32_t)ps.vkeys.size()).first;
+      ps.vkeys.push_back(k);
+    }
+    vs.key = it->second;
+    v.vstr = (int32_t)ps.vstrs.size();
+    ps.vstrs.push_back(vs);
+    return;
+  }
+  if (v.t == J_MAP) {
+    std::vector<size_t> idx(v.mk.size());
+    for (size_t i = 0; i < idx.size(); i++) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return v.mk[a] < v.mk[b]; });
+    for (size_t i : idx) {
+      const std::string k = v.mk[i];
+      const std::string ak = remove_anchor(k, nullptr);
+      // values of metadata.labels / annotations maps (ExpandInMetadata reads them as strings)
+      const bool lbl = (ak == "labels" || ak == "annotations") && path.size() >= 9 &&
+                       remove_anchor(path.substr(path.rfind('/') + 1), nullptr) == "metadata";
+      collect_var_strings(ps, v.mv[i], path + "/" + k, rule, false, keys);
+      if (lbl && v.mv[i].t == J_MAP)
+        for (auto& x : v.mv[i].mv)
+          if (x.t == J_STR && x.vstr >= 0) ps.vstrs[x.vstr].want_string = true;
+      const std::string nk = unescape_var_string(k);
+      if (nk != k) {
+        v.mk[i] = nk;
+        if (v.mo[i] == k) v.mo[i] = nk;
+      }
+    }
+    return;
+  }
+  if (v.t == J_ARR)
+    for (size_t i = 0; i < v.a.size(); i++)
+      collect_var_strings(ps, v.a[i], path + "/" + std::to_string(i), rule, false, keys);
+}
+
+// every variable of the document is request.object<path> or @ (kvvars.cpp), none in a key
+static bool pattern_vars_in_scope(const PV& v, const std::string& path) {
+  if (v.t == J_STR) return !var_string(v.s) || var_string_in_scope(v.s, path);
+  if (v.t == J_MAP) {
+    for (size_t i = 0; i < v.mk.size(); i++)
+      if (var_string(v.mk[i]) || !pattern_vars_in_scope(v.mv[i], path + "/" + v.mk[i])) return false;
+    return true;
+  }
+  if (v.t == J_ARR)
+    for (size_t i = 0; i < v.a.size(); i++)
+      if (!pattern_vars_in_scope(v.a[i], path + "/" + std::to_string(i))) return false;
+  return true;
+}
 
 std::string jstr(const JDoc& d, int64_t n) {
   if (n < 0 || d.at((uint32_t)n).t != J_STR) return "";
@@ -1344,6 +1425,7 @@ void compile_policies(const char* json, size_t len, PolicySet* ps) {
   }
   ps->intern("");  // id 0: empty string
   Compiler C(*ps);
+  std::map<std::pair<std::string, std::string>, uint32_t> var_keys;  // distinct (text, path) of VarStrs
   // keys always needed by match/ingest
   for (const char* k : {"metadata", "labels", "annotations", "name", "namespace", "kind", "apiVersion", "Namespace"})
     ps->intern(k);
@@ -1395,7 +1477,8 @@ void compile_policies(const char* json, size_t len, PolicySet* ps) {
           else { rr.route = 2; rh.route_reason = "no pattern"; }  // validate() returns nil
         } else {
           PV doc = to_pv(d, patP ? (uint32_t)pat : (uint32_t)ap);
-          if (doc_has_variable(doc)) {
+          const bool vars = doc_has_variable(doc);
+          if (vars && !pattern_vars_in_scope(doc, "")) {
             rr.route = 1;
             rh.route_reason = "variables";
           } else if (doc_has_magic(doc) || has_magic(rh.name)) {
@@ -1409,7 +1492,14 @@ void compile_policies(const char* json, size_t len, PolicySet* ps) {
               rr.const_status = ST_ERROR;
               rh.const_message = "variable substitution failed: " + err;
             } else {
-              unescape_vars(doc);
+              const size_t vs0 = ps->vstrs.size();
+              if (vars) {  // variables: resolved per resource (kvvars.cpp); other strings unescaped here
+                collect_var_strings(*ps, doc, "", (uint32_t)ps->rules.size(), false, var_keys);
+                ps->dyn_rules.push_back({(uint32_t)vs0, (uint32_t)(ps->vstrs.size() - vs0)});
+                rr.dyn = (uint32_t)ps->dyn_rules.size();
+              } else {
+                unescape_vars(doc);
+              }
               std::vector<PV> pats;
               bool ok = true;
               if (patP) {
@@ -1461,6 +1551,13 @@ void compile_policies(const char* json, size_t len, PolicySet* ps) {
     if (it == tn.slot.end()) throw std::runtime_error("compiler: key missing from projection trie: " + std::get<2>(f));
     in.a = it->second;
   }
+}
+
+std::string pattern_go_v(const PV& p) { return go_v(p); }
+
+uint32_t compile_leaf_pred(PolicySet& tbl, const PV& value) {
+  Compiler C(tbl);
+  return C.pred(value);
 }
 
 }  // namespace kvh

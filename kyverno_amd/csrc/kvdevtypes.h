@@ -78,6 +78,12 @@ struct DevBatch {
   uint32_t n_nsm, n_lsets, n_asets;
   uint32_t ns_words;
   uint32_t n_res;
+  // pattern variables (kvvars.cpp build_dyn): predicate table of the batch's distinct
+  // substituted leaves, outcome (= predicate) id per [dynamic leaf][res], and the status
+  // substitution decides per [dynamic rule][res] (0: evaluate, ST_ERROR, ST_CPU)
+  const DevPS* dps;
+  const uint32_t* dleaf;
+  const uint8_t* dyn_st;
 };
 
 struct DevOut {

@@ -302,21 +302,25 @@ struct Ingest {
   }
 
   // ExpandInMetadata panics on non-map metadata / labels, non-string label values
-  bool bad_meta(const JDoc& d) {
+  // (wildcards.go:69-139, per tag the pattern reads): RF_BAD_LABELS / RF_BAD_ANN. Any
+  // `metadata` key at any depth counts (the pattern's expansion sites may be nested).
+  uint32_t bad_meta(const JDoc& d) {
+    uint32_t f = 0;
     for (const JNode& m : d.nodes) {
       if (m.t != J_MAP) continue;
       for (uint32_t c = m.first; c < m.first + m.count; c++) {
         const JNode& ch = d.at(c);
         if (d.key(ch) != "metadata" || ch.t == J_NULL) continue;
-        if (ch.t != J_MAP) return true;
+        if (ch.t != J_MAP) return RF_BAD_LABELS | RF_BAD_ANN;
         for (uint32_t g = ch.first; g < ch.first + ch.count; g++) {
           const JNode& t = d.at(g);
           std::string_view k = d.key(t);
-          if ((k == "labels" || k == "annotations") && t.t != J_NULL && !is_str_map(d, t)) return true;
+          if ((k == "labels" || k == "annotations") && t.t != J_NULL && !is_str_map(d, t))
+            f |= k == "labels" ? RF_BAD_LABELS : RF_BAD_ANN;
         }
       }
     }
-    return false;
+    return f;
   }
 
   // Interned label / annotation list of a resource: identical lists (same pairs, same
@@ -417,11 +421,21 @@ struct Ingest {
       b.namespaces.push_back(nss);
     }
     r.ns_index = it->second;
-    if (bad_meta(d)) r.flags |= RF_BAD_META;
+    if (const uint32_t bm = bad_meta(d)) r.flags |= RF_BAD_META | bm;
     if (d.strs.find("conditional anchor mismatch") != std::string::npos ||
         d.strs.find("global anchor mismatch") != std::string::npos)
       r.flags |= RF_MAGIC;
     b.res.push_back(r);  // root row assigned by flush_group
+    // pattern variables: every distinct (string, path) resolved on this resource (kvvars.cpp)
+    for (const auto& vk : ps.vkeys) {
+      std::string o = resolve_var_string(vk.first, vk.second, d);
+      auto it = b.vout_id.find(o);
+      if (it == b.vout_id.end()) {
+        it = b.vout_id.emplace(o, (uint32_t)b.vout_tab.size()).first;
+        b.vout_tab.push_back(std::move(o));
+      }
+      b.vout.push_back(it->second);
+    }
   }
 
   void take(JDoc& d) {
@@ -615,6 +629,24 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
     }
     b.cells_used += q.cells_used;
   }
+  // pattern-variable outcomes: re-interned globally, rows concatenated in resource order
+  {
+    std::unordered_map<std::string, uint32_t> gid;
+    for (size_t k = 0; k < P; k++) {
+      Batch& q = parts[k];
+      std::vector<uint32_t> m(q.vout_tab.size());
+      for (size_t i = 0; i < q.vout_tab.size(); i++) {
+        auto it = gid.find(q.vout_tab[i]);
+        if (it == gid.end()) {
+          it = gid.emplace(q.vout_tab[i], (uint32_t)b.vout_tab.size()).first;
+          b.vout_tab.push_back(q.vout_tab[i]);
+        }
+        m[i] = it->second;
+      }
+      for (uint32_t x : q.vout) b.vout.push_back(m[x]);
+      std::vector<uint32_t>().swap(q.vout);
+    }
+  }
   if (H >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: string heap exceeds 4 GiB");
   if (R * KV_LANES >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: batch too large for 32-bit node indices");
   b.strs.assign(H, '\0');
@@ -759,6 +791,7 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
   // word-granular readers may touch up to 8 bytes past the last string
   b->strs.append(16, '\0');
   // interning keys are only needed while ingesting
+  std::unordered_map<std::string, uint32_t>().swap(b->vout_id);
   std::vector<std::string>().swap(b->nsm_keys);
   std::vector<std::string>().swap(b->lset_keys);
   std::vector<std::string>().swap(b->aset_keys);

@@ -21,6 +21,7 @@ struct PV {
   std::vector<std::string> mo;  // canonical order keys (== mk unless renamed)
   std::vector<PV> mv;           // map values
   std::vector<PV> a;            // array elements
+  int32_t vstr = -1;            // J_STR holding {{ }} variables: its VarStr (PolicySet::vstrs)
   int find(const std::string& k) const {
     for (size_t i = 0; i < mk.size(); i++)
       if (mk[i] == k) return (int)i;
@@ -41,6 +42,17 @@ struct PNodeInfo {
   std::string pat_t;     // Go %T of the pattern value ("map[string]interface {}", "[]interface {}", ...)
   std::string pat_v;     // Go %v of the compared scalar (the value, or element 0 of a scalar list)
   uint32_t pat_len = 0;  // pattern array length (validate.go:172)
+  int32_t dleaf = -1;    // a dynamic leaf (pattern variables) compares here: pat_v is per resource
+};
+
+// A pattern string holding {{ }} variables (kvvars.cpp): `text` after $() references, `path`
+// its traversal path in the pattern document (getJMESPath of {{@}}), `key` the distinct
+// (text, path) resolved once per resource at ingest.
+struct VarStr {
+  uint32_t rule = 0;
+  std::string text, path;
+  uint32_t key = 0;
+  bool want_string = false;  // under metadata.labels / annotations (ExpandInMetadata needs a string)
 };
 
 // Projection trie over resource key paths referenced by any compiled pattern
@@ -153,6 +165,13 @@ struct PolicySet {
   std::vector<std::tuple<uint32_t, uint32_t, std::string>> slot_fix;  // (pc, trie node, key)
   uint32_t max_depth = 0, max_loops = 0;
   std::string flags_info;
+  // pattern variables (kvvars.cpp): strings in traversal order per rule, distinct
+  // (text, path) keys, dynamic leaves (OP_VLEAF a) -> VarStr, and per dynamic rule
+  // (RuleRec::dyn - 1) its VarStr range
+  std::vector<VarStr> vstrs;
+  std::vector<std::pair<std::string, std::string>> vkeys;
+  std::vector<uint32_t> dleaf_vstr;
+  std::vector<std::pair<uint32_t, uint32_t>> dyn_rules;
 };
 
 // Compiles a JSON list of (already autogen-expanded) ClusterPolicy/Policy
@@ -178,7 +197,31 @@ struct Batch {
   std::vector<uint32_t> ns_bits;     // [n_ns][ceil(n_nssel/32)]
   uint32_t ns_words = 1;
   uint64_t bytes_referenced = 0;     // algorithmic bytes of the projected store
+  // pattern variables: outcome id per (resource, PolicySet::vkeys entry), resource-major,
+  // and the distinct outcomes (kvvars.cpp resolve_var_string encoding)
+  std::vector<uint32_t> vout;
+  std::vector<std::string> vout_tab;
+  std::unordered_map<std::string, uint32_t> vout_id;  // (ingest only)
 };
+
+// Per-batch tables of the pattern variables (kvvars.cpp build_dyn): the predicate of every
+// distinct outcome (pred id == outcome id), the outcome of each dynamic leaf
+// [dleaf][res], and the status substitution decides per [dyn rule][res] (0 / ST_ERROR /
+// ST_CPU) with the ERROR's outcome id (its message) in dyn_msg.
+struct DynHost {
+  PolicySet tbl;
+  std::vector<uint32_t> dleaf;
+  std::vector<uint8_t> dyn_st;
+  std::vector<uint32_t> dyn_msg;
+};
+void build_dyn(const PolicySet& ps, const Batch& b, DynHost* out);
+bool var_string(const std::string& s);
+bool var_string_in_scope(const std::string& s, const std::string& path);
+std::string unescape_var_string(const std::string& s);
+std::string resolve_var_string(const std::string& tmpl, const std::string& path, const JDoc& d);
+PV outcome_value(const std::string& o);
+uint32_t compile_leaf_pred(PolicySet& tbl, const PV& value);  // kvcompile.cpp
+std::string pattern_go_v(const PV& p);                         // Go %v of a scalar pattern value
 
 void ingest_resources(const PolicySet& ps, const char* json, size_t len, const char* ns_labels_json, Batch* b);
 

@@ -528,7 +528,8 @@ struct Gen {
     }
     o << "__device__ __forceinline__ uint32_t g_rule_" << ri
       << "(const DevPS& P, const DevBatch& B, const Node* __restrict__ N, const Val* __restrict__ V, "
-         "const uint8_t* __restrict__ S, uint32_t root, EState& e) {\n";
+         "const uint8_t* __restrict__ S, uint32_t root, uint32_t r, EState& e) {\n"
+      << "  const uint32_t n_res = B.n_res; (void)n_res; (void)r;\n";
     o << "  uint32_t c0 = root";
     for (uint32_t d = 1; d < maxd; d++) o << ", c" << d << " = ABSENT";
     o << ";\n  uint32_t lf0 = 0u, lf1 = 0u, lf2 = 0u, lf3 = 0u, ll0 = 0u, ll1 = 0u, ll2 = 0u, ll3 = 0u;\n"
@@ -597,6 +598,15 @@ struct Gen {
             << "    if (vt_ == NT_ARR) { ok_ = true; for (uint32_t k_ = 0; k_ < vn_.b && ok_; k_++) { const Node en_ = N[ni(vn_.a + k_)]; "
             << "ok_ = " << pred_call(in.a, "node_type(en_.kt)", "en_") << "; } }\n"
             << "    else ok_ = " << pred_call(in.a, "vt_", "vn_") << ";\n"
+            << "    if (!ok_) " << raise("E_VALUE", in.b, cd, in.c) << " }\n";
+          break;
+        case OP_VLEAF:
+          o << "  { Node vn_{0u, 0u, 0u, 0u}; if (" << cd << " != ABSENT) vn_ = N[" << cd << "];\n"
+            << "    const uint32_t dp_ = B.dleaf[(size_t)" << u32(in.a) << " * n_res + r];\n"
+            << "    const uint32_t vt_ = node_type(vn_.kt); bool ok_;\n"
+            << "    if (vt_ == NT_ARR) { ok_ = true; for (uint32_t k_ = 0; k_ < vn_.b && ok_; k_++) "
+               "ok_ = pred_node(*B.dps, B, N, dp_, ni(vn_.a + k_)); }\n"
+            << "    else ok_ = pred_eval(*B.dps, B, dp_, vt_, vn_);\n"
             << "    if (!ok_) " << raise("E_VALUE", in.b, cd, in.c) << " }\n";
           break;
         case OP_RAISE:
@@ -682,8 +692,10 @@ struct Gen {
         case 3: o << "      st = " << u32(rr.const_status) << ";\n"; break;
         default:
           o << "      if (rflags & RF_MAGIC) st = ST_CPU;\n";
-          if (rr.flags & RR_META_EXPAND) o << "      else if (rflags & RF_BAD_META) st = ST_CPU;\n";
-          o << "      else st = g_rule_" << ri << "(P, B, N, V, S, root, e);\n";
+          if (rr.flags & RR_META_EXPAND) o << "      else if (rflags & " << u32(meta_bad_flags(rr.flags)) << ") st = ST_CPU;\n";
+          if (rr.dyn) o << "      else if (B.dyn_st[(size_t)" << (rr.dyn - 1) << "u * n_res + r]) st = B.dyn_st[(size_t)"
+                        << (rr.dyn - 1) << "u * n_res + r];\n";
+          o << "      else st = g_rule_" << ri << "(P, B, N, V, S, root, r, e);\n";
           break;
       }
       o << "    }\n"
@@ -935,6 +947,16 @@ struct Gen {
             << "    if (!ok_) " << raise("E_VALUE", in.b, in.c) << " }\n";
           break;
         }
+        case OP_VLEAF:  // pattern variables: the resource's substituted value (kvvars.cpp)
+          if (known(d)) w << "  { const Node vn_ = " << NODE(d) << ";\n";
+          else w << "  { Node vn_{0u, 0u, 0u, 0u}; if (" << cd << " != ABSENT) vn_ = N[" << cd << "];\n";
+          w << "    const uint32_t dp_ = B.dleaf[(size_t)" << u32(in.a) << " * n_res + r];\n"
+            << "    const uint32_t vt_ = node_type(vn_.kt); bool ok_;\n"
+            << "    if (vt_ == NT_ARR) { ok_ = true; for (uint32_t k_ = 0; k_ < vn_.b && ok_; k_++) "
+               "ok_ = pred_node(*B.dps, B, N, dp_, ni(vn_.a + k_)); }\n"
+            << "    else ok_ = pred_eval(*B.dps, B, dp_, vt_, vn_);\n"
+            << "    if (!ok_) " << raise("E_VALUE", in.b, in.c) << " }\n";
+          break;
         case OP_RAISE:
           w << "  " << raise(u32(in.b), in.a, in.c) << "\n";
           break;
@@ -1203,7 +1225,11 @@ struct Gen {
         case 3: k << "    rs" << s << " = FIN_ | " << u32(rr.const_status) << ";\n"; break;
         default:
           k << "    if (rflags & RF_MAGIC) rs" << s << " = FIN_ | ST_CPU;\n";
-          if (rr.flags & RR_META_EXPAND) k << "    else if (rflags & RF_BAD_META) rs" << s << " = FIN_ | ST_CPU;\n";
+          if (rr.flags & RR_META_EXPAND)
+            k << "    else if (rflags & " << u32(meta_bad_flags(rr.flags)) << ") rs" << s << " = FIN_ | ST_CPU;\n";
+          if (rr.dyn)
+            k << "    else if (B.dyn_st[(size_t)" << (rr.dyn - 1) << "u * n_res + r]) rs" << s << " = FIN_ | B.dyn_st[(size_t)"
+              << (rr.dyn - 1) << "u * n_res + r];\n";
           k << "    else rs" << s << " = " << u32(rr.prog) << ";\n";
           break;
       }

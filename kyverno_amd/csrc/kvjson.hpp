@@ -58,6 +58,7 @@ bool go_parse_int(std::string_view s, int64_t* out);
 bool go_parse_float(std::string_view s, double* out);
 std::string go_format_E(double v);
 std::string go_format_f6(double v);
+std::string go_json_float(double v);  // encoding/json float64
 std::string go_format_g(double v);  // fmt %v of a float64
 bool utf8_ascii(std::string_view s);
 

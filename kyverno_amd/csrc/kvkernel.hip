@@ -82,7 +82,8 @@ extern "C" __global__ __launch_bounds__(KV_WG) __attribute__((amdgpu_waves_per_e
         else if (route == 2) st = ST_NOMATCH;
         else if (route == 3) st = (uint8_t)uni(rr.const_status);
         else if (rflags & RF_MAGIC) st = ST_CPU;
-        else if ((uni(rr.flags) & RR_META_EXPAND) && (rflags & RF_BAD_META)) st = ST_CPU;
+        else if (rflags & meta_bad_flags(uni(rr.flags))) st = ST_CPU;
+        else if (uni(rr.dyn) && B.dyn_st[(size_t)(uni(rr.dyn) - 1u) * n_res + r]) st = B.dyn_st[(size_t)(uni(rr.dyn) - 1u) * n_res + r];
         else run = true;
       }
       uint32_t ekind = 0, eflags = 0, epn = 0, ekey = ABSENT, eres = ABSENT;
@@ -191,6 +192,23 @@ extern "C" __global__ __launch_bounds__(KV_WG) __attribute__((amdgpu_waves_per_e
                   for (uint32_t k = 0; k < vn.b && ok; k++) ok = pred_node(P, B, N, ia, ni(vn.a + k));
                 } else {
                   ok = pred_eval(P, B, ia, vt, vn);
+                }
+                if (!ok) raise(E_VALUE, ib, v, ic);
+              }
+              break;
+            case OP_VLEAF:  // the resource's substituted pattern value (kvvars.cpp): batch predicate table
+              if (A) {
+                const uint32_t v = s_cur[d][lane];
+                const uint32_t dp = B.dleaf[(size_t)ia * n_res + r];
+                Node vn{NT_NULL, 0, 0, 0};
+                if (v != ABSENT) vn = N[v];
+                const uint32_t vt = node_type(vn.kt);
+                bool ok;
+                if (vt == NT_ARR) {
+                  ok = true;
+                  for (uint32_t k = 0; k < vn.b && ok; k++) ok = pred_node(*B.dps, B, N, dp, ni(vn.a + k));
+                } else {
+                  ok = pred_eval(*B.dps, B, dp, vt, vn);
                 }
                 if (!ok) raise(E_VALUE, ib, v, ic);
               }

@@ -56,6 +56,11 @@ void make_shard(const Batch& b, uint64_t lo, uint64_t hi, Batch* out) {
   s.ns_labels = b.ns_labels;
   s.ns_bits = b.ns_bits;
   s.ns_words = b.ns_words;
+  if (!b.vout.empty()) {  // pattern-variable outcomes of the shard's resources (ids stay global)
+    const size_t K = b.vout.size() / b.res.size();
+    s.vout.assign(b.vout.begin() + lo * K, b.vout.begin() + hi * K);
+    s.vout_tab = b.vout_tab;
+  }
   s.bytes_referenced = s.cells_used * sizeof(Node) + s.vals.size() * sizeof(Val) + s.res.size() * sizeof(Res) +
                        s.kvs.size() * sizeof(KV) + s.strs.size() + s.nsms.size() * sizeof(StrRef) +
                        (s.lsets.size() + s.asets.size()) * sizeof(KVSet);

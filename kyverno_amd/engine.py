@@ -112,11 +112,7 @@ def validate_batch(policies: list[dict], resources: list[dict], admission_info: 
     for ri, res in zip(*(r.status == cli.FAIL).nonzero()):
         if not ps.rules[ri].any_pattern:
             ev.paths[(int(ri), int(res))] = r.path(int(ri), int(res))
-    for ri, res in zip(*((r.status == cli.ERROR) | (r.status == cli.SKIP)).nonzero()):
-        if not ps.rules[ri].any_pattern:
-            m = r.error_message(int(ri), int(res), resources[int(res)])
-            if m is not None:
-                ev.errors[(int(ri), int(res))] = m
+    cli.collect_errors(ev, ps, r, resources)
     cli._evaluate_anypatterns(ev, device, specialize, namespace_labels)
     return [[_response(ev, pi, res) for res in range(len(resources))] for pi in range(len(policies))]
 

@@ -640,7 +640,10 @@ int subst_var_string(const std::string& s, const std::string& path, const Value&
     for (std::string v : vars) {
       const bool initial = var_initial(v);
       const std::string old = v;
-      if (!initial) v = v.substr(1);
+      if (!initial) {
+        if ((unsigned char)old[0] >= 0x80) return 2;  // a rune split by v[1:]: "failed to resolve" (outside scope)
+        v = v.substr(1);
+      }
       const std::string var = trim_space(replace_n(replace_n(v, "{{", "", -1), "}}", "", -1));
       std::string q;
       if (!var_query(var, path, &q)) return 2;
@@ -711,7 +714,10 @@ int traverse_vars(Value& v, const std::string& path, const Value& resource, std:
 bool vars_in_scope(const Value& v, const std::string& path) {
   if (v.t == T::Str) {
     for (std::string x : find_vars(v.s)) {
-      if (!var_initial(x)) x = x.substr(1);
+      if (!var_initial(x)) {
+        if ((unsigned char)x[0] >= 0x80) return false;
+        x = x.substr(1);
+      }
       const std::string var = trim_space(replace_n(replace_n(x, "{{", "", -1), "}}", "", -1));
       std::string q;
       if (!var_query(var, path, &q) || QueryObject(q, Value::mk_map(), nullptr, nullptr) == 2) return false;

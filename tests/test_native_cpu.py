@@ -35,6 +35,10 @@ def test_compile_routes():
         {"name": "gpu", "match": {"resources": {"kinds": ["Pod"]}}, "validate": {"pattern": {"a": "b"}}},
         {"name": "vars", "match": {"resources": {"kinds": ["Pod"]}},
          "validate": {"pattern": {"a": "{{request.object.metadata.name}}"}}},
+        {"name": "uservars", "match": {"resources": {"kinds": ["Pod"]}},
+         "validate": {"pattern": {"a": "{{request.userInfo.username}}"}}},
+        {"name": "keyvars", "match": {"resources": {"kinds": ["Pod"]}},
+         "validate": {"pattern": {"{{request.object.kind}}": "x"}}},
         {"name": "deny", "match": {"resources": {"kinds": ["Pod"]}}, "validate": {"deny": {}}},
         {"name": "ctx", "context": [{"name": "x"}], "match": {"resources": {"kinds": ["Pod"]}},
          "validate": {"pattern": {"a": "b"}}},
@@ -45,7 +49,11 @@ def test_compile_routes():
     ps = batch.PolicySet([pol])
     routes = {r.name: (r.route, r.route_reason) for r in ps.rules}
     assert routes["gpu"][0] == batch.ROUTE_GPU
-    assert routes["vars"] == (batch.ROUTE_CPU, "variables")
+    # request.object / @ variables are evaluated on the device (kvvars.cpp); other variables and
+    # variables in keys stay with the reference engine
+    assert routes["vars"] == (batch.ROUTE_GPU, "")
+    assert routes["uservars"] == (batch.ROUTE_CPU, "variables")
+    assert routes["keyvars"] == (batch.ROUTE_CPU, "variables")
     assert routes["deny"] == (batch.ROUTE_CPU, "deny")
     assert routes["ctx"] == (batch.ROUTE_CPU, "context")
     assert routes["mutate"][0] == batch.ROUTE_NORESPONSE

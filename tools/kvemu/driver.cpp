@@ -162,6 +162,20 @@ int main(int argc, char** argv) {
     B.n_asets = (uint32_t)b.asets.size();
     B.ns_words = b.ns_words;
     B.n_res = (uint32_t)b.res.size();
+    // pattern variables (as dev_batch in kvapi.cpp)
+    DynHost dyn;
+    build_dyn(ps, b, &dyn);
+    DevPS PD{};
+    PD.preds = dyn.tbl.preds.data();
+    PD.alts = dyn.tbl.alts.data();
+    PD.conjs = dyn.tbl.conjs.data();
+    PD.atoms = dyn.tbl.atoms.data();
+    PD.gsegs = dyn.tbl.gsegs.data();
+    PD.gwords = dyn.tbl.gwords.data();
+    PD.pstr = (const uint8_t*)dyn.tbl.strs.data();
+    B.dps = &PD;
+    B.dleaf = dyn.dleaf.data();
+    B.dyn_st = dyn.dyn_st.data();
     // match tables (as kv_session: one allocation, three [word][entity] tables)
     P.mt_ns_words = (ps.n_nss_bits + 31) / 32;
     P.mt_ann_words = (ps.n_ann_bits + 31) / 32;
