@@ -60,6 +60,8 @@ class Oracle:
         L.orc_validate.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
         L.orc_substitute_message.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
         L.orc_substitute_vars.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.orc_enumerate.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
+        L.orc_enumerate.restype = ctypes.c_void_p
         L.orc_substitute_vars.restype = ctypes.c_void_p
         L.orc_substitute_message.restype = ctypes.c_void_p
         L.orc_validate.restype = ctypes.c_void_p
@@ -132,6 +134,14 @@ class Oracle:
         {"doc": ...} | {"error": message} | {"scope": False} (outside the device scope)."""
         return json.loads(self._take(self.lib.orc_substitute_vars(json.dumps(pattern).encode(),
                                                                   json.dumps(resource).encode())))
+
+    def enumerate(self, policy: dict, resource: dict, ctx: dict | None = None, cap: int = 4096) -> list:
+        """Enumerate mode: per rule, every (status, failing path) the reference can produce over the
+        Go map iteration orders of validateMap / expandWildcards, with the number of evaluations and
+        whether `cap` cut the search short."""
+        out = self._take(self.lib.orc_enumerate(json.dumps(policy).encode(), json.dumps(resource).encode(),
+                                                json.dumps(ctx or {}).encode(), cap))
+        return json.loads(out)["rules"]
 
     def substitute_message(self, msg: str, resource: dict | str):
         """buildErrorMessage's message substitution; None where the reference panics."""

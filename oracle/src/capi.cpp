@@ -209,6 +209,19 @@ char* orc_validate(const char* policy_json, const char* resource_json, const cha
   }
 }
 
+// Enumerate mode: {"rules": [{"name", "outcomes": [[status, path]...], "runs", "truncated"}]}
+char* orc_enumerate(const char* policy_json, const char* resource_json, const char* ctx_json, int cap) {
+  try {
+    Value pv = parse_json(policy_json, NumMode::Float);
+    Value rv = parse_json(resource_json, NumMode::Unstructured);
+    Value cv = parse_json(ctx_json && *ctx_json ? ctx_json : "{}", NumMode::Float);
+    return dup(EnumerateToJSON(pv, rv, cv, cap));
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return nullptr;
+  }
+}
+
 // Batch: policies_json = JSON list of policies; resources = JSON list of
 // resources. Writes status[n_res * n_rules_total] (rule-major:
 // status[rule * n_res + res]) and returns elapsed evaluation seconds

@@ -738,6 +738,63 @@ std::string ValidateToJSON(const Value& policy, const Value& resource, const Val
   return out;
 }
 
+// Enumerate mode: every outcome (status, failing path) the reference can produce for each
+// rule of `policy` on `resource` over the Go map iteration orders (matcher.hpp Chooser):
+// depth-first over choice sequences, at most `cap` evaluations per rule.
+std::string EnumerateToJSON(const Value& policy, const Value& resource, const Value& ctx, int cap) {
+  Policy pol = parse_policy(policy);
+  EngineCtx cx = parse_ctx(ctx);
+  Resource r = make_resource(resource);
+  std::vector<std::pair<std::string, std::string>> ns;
+  auto it = cx.nsLabels.find(r.ns);
+  if (it != cx.nsLabels.end()) ns = it->second;
+  std::string out = "{\"rules\":[";
+  for (size_t k = 0; k < pol.rules.size(); k++) {
+    const Rule& rule = pol.rules[k];
+    if (k) out += ",";
+    out += "{\"name\":" + js(rule.name);
+    if (!rule.hasValidate || !MatchesResourceDescription(r, rule, cx.ai, cx.excludeGroupRole, ns)) {
+      out += ",\"outcomes\":[[\"nomatch\",\"\"]],\"runs\":1,\"truncated\":false}";
+      continue;
+    }
+    std::set<std::pair<int, std::string>> seen;
+    std::vector<std::vector<int>> stack{{}};
+    int runs = 0;
+    while (!stack.empty() && runs < cap) {
+      Chooser ch;
+      ch.prefix = stack.back();
+      stack.pop_back();
+      g_choose = &ch;
+      RuleResult rr;
+      try {
+        rr = evaluate_rule(rule, resource);
+      } catch (...) {
+        g_choose = nullptr;
+        throw;
+      }
+      g_choose = nullptr;
+      runs++;
+      seen.insert({rr.status, rr.status == FAIL ? rr.path : std::string()});
+      for (size_t d = ch.prefix.size(); d < ch.taken.size(); d++)
+        for (int c = 1; c < ch.arity[d]; c++) {
+          std::vector<int> p(ch.taken.begin(), ch.taken.begin() + d);
+          p.push_back(c);
+          stack.push_back(std::move(p));
+        }
+    }
+    out += ",\"outcomes\":[";
+    bool first = true;
+    for (const auto& o : seen) {
+      if (!first) out += ",";
+      first = false;
+      out += "[" + js(status_name(o.first)) + "," + js(o.second) + "]";
+    }
+    out += "],\"runs\":" + std::to_string(runs) + ",\"truncated\":" + (stack.empty() ? "false" : "true") + "}";
+  }
+  out += "]}";
+  return out;
+}
+
 double BatchValidate(const char* policies_json, const char* resources_json, const char* ctx_json, int nthreads,
                      unsigned char* status_out, long long* n_rules_out, long long* n_res_out) {
   Value pl = parse_json(policies_json, NumMode::Float);

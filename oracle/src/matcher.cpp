@@ -24,6 +24,8 @@
 
 namespace orc {
 
+thread_local Chooser* g_choose = nullptr;
+
 // ---------------------------------------------------------------- anchors
 bool IsConditionAnchor(const std::string& s) {
   if (s.size() < 2) return false;
@@ -402,8 +404,15 @@ static void expandWildcardsInTag(const std::string& tag, Value& patternMetadata,
       std::string prefix;
       std::string af = RemoveAnchor(k, &prefix);
       std::string matchK = af;
-      for (const auto& r : rdata) {
-        if (wildcard_match(af, r.first)) { matchK = r.first; break; }
+      if (g_choose) {  // enumerate mode: the first match in any map order
+        std::vector<std::string> hits;
+        for (const auto& r : rdata)
+          if (wildcard_match(af, r.first)) hits.push_back(r.first);
+        if (!hits.empty()) matchK = hits[g_choose->choose((int)hits.size())];
+      } else {
+        for (const auto& r : rdata) {
+          if (wildcard_match(af, r.first)) { matchK = r.first; break; }
+        }
       }
       if (!prefix.empty()) matchK = prefix + matchK + ")";
       results.set(matchK, Value::mk_str(kv.second), k);
@@ -560,6 +569,25 @@ static PathErr validateMap(const Value& resMap, Value& patternMap, const std::st
   });
   // Entries may not be reallocated during handling: handlers only mutate
   // nested maps (ExpandInMetadata replaces the metadata child's children).
+  if (g_choose) {  // enumerate mode: any order within each Go map iteration
+    auto run = [&](std::vector<Value::Entry*> left) -> PathErr {
+      while (!left.empty()) {
+        const int c = g_choose->choose((int)left.size());
+        Value::Entry* e = left[c];
+        left.erase(left.begin() + c);
+        PathErr r = handle(e->key, *e->val, path, resMap, ac);
+        if (r.err.set) return r;
+      }
+      return ok();
+    };
+    std::vector<Value::Entry*> fr, bk;
+    for (auto* e : resources) (front(e) ? fr : bk).push_back(e);
+    PathErr r = run(anchors);
+    if (r.err.set) return r;
+    r = run(fr);
+    if (r.err.set) return r;
+    return run(bk);
+  }
   for (auto* e : anchors) {
     PathErr r = handle(e->key, *e->val, path, resMap, ac);
     if (r.err.set) return r;

@@ -2,6 +2,7 @@
 #pragma once
 #include <map>
 #include <string>
+#include <vector>
 
 #include "ovalue.hpp"
 
@@ -86,5 +87,26 @@ bool SubstituteMessage(const std::string& msg, const Value& resource, std::strin
 // True if the string contains an unescaped {{...}} (RegexVariables, vars.go:20)
 bool HasVariable(const std::string& s);
 bool DocHasVariable(const Value& v);
+
+// Enumerate mode: where the reference iterates a Go map (random order)
+// — the anchors and the non-anchor keys of validateMap (validate.go:110-135, with
+// getSortedNestedAnchorResource's front / back lists, validate/utils.go:37-51) and the
+// resource label keys of expandWildcards (wildcards.go:38-49) — the oracle asks g_choose
+// (thread-local, null = canonical order) which element comes next; the enumerator replays
+// every sequence of choices to collect the set of outcomes.
+struct Chooser {
+  std::vector<int> prefix;   // choices to replay
+  std::vector<int> taken;    // choices made this run
+  std::vector<int> arity;    // number of options at each choice
+  int choose(int n) {
+    if (n <= 1) return 0;
+    const size_t k = taken.size();
+    const int c = k < prefix.size() ? prefix[k] : 0;
+    taken.push_back(c);
+    arity.push_back(n);
+    return c;
+  }
+};
+extern thread_local Chooser* g_choose;
 
 }  // namespace orc
