@@ -133,7 +133,10 @@ class Batch:
 
 
 class Result:
-    def __init__(self, h, policyset: PolicySet, batch: Batch):
+    """kv_result: statuses [rule][res] (a copy, or with copy=False a read-only view of the library's
+    page-locked buffer, valid while this object lives), per-rule counts, failing paths / messages."""
+
+    def __init__(self, h, policyset: PolicySet, batch: Batch, copy: bool = True):
         self._h = h
         self.policyset = policyset
         self.batch = batch
@@ -144,7 +147,11 @@ class Result:
         self.n_rules, self.n_res = nr.value, nn.value
         if p.value:
             buf = (ctypes.c_uint8 * (self.n_rules * self.n_res)).from_address(p.value)
-            self.status = np.frombuffer(buf, dtype=np.uint8).reshape(self.n_rules, self.n_res).copy()
+            self.status = np.frombuffer(buf, dtype=np.uint8).reshape(self.n_rules, self.n_res)
+            if copy:
+                self.status = self.status.copy()
+            else:
+                self.status.flags.writeable = False
         else:
             self.status = None
         c = ctypes.c_void_p()
@@ -236,9 +243,10 @@ class Result:
 
 def validate(policyset: PolicySet, batch: Batch, admission: dict | None = None,
              exclude_group_role: list | None = None, device: int = 0,
-             mode: int = MODE_STATUS | MODE_ERRORS, device_mask: int | None = None) -> Result:
+             mode: int = MODE_STATUS | MODE_ERRORS, device_mask: int | None = None, copy: bool = True) -> Result:
     """kv_validate on `device`, or kv_validate_devices over the devices of `device_mask`
-    (contiguous resource shards, counts all-reduced over RCCL inside the library)."""
+    (contiguous resource shards, counts all-reduced over RCCL inside the library). copy=False: the
+    status matrix is a view of the result's buffer (no host copy)."""
     ctx = {}
     if admission:
         ctx["admission"] = admission
@@ -252,7 +260,7 @@ def validate(policyset: PolicySet, batch: Batch, admission: dict | None = None,
         rc = lib().kv_validate_devices(policyset._h, batch._h, _dumps(ctx), device_mask, mode, ctypes.byref(h),
                                        ctypes.byref(err))
     check(rc, err)
-    return Result(h, policyset, batch)
+    return Result(h, policyset, batch, copy=copy)
 
 
 def bench(policyset: PolicySet, batch: Batch, device: int = 0, mode: int = MODE_COUNTS, warmup: int = 2,

@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -62,7 +63,70 @@ struct DevBuf {
     dev = device;
     n = bytes;
     HIPCHK(hipMalloc(&p, std::max<size_t>(bytes, 16)));
-    if (bytes) HIPCHK(hipMemcpy(p, src, bytes, hipMemcpyHostToDevice));
+    if (bytes) upload_h2d(p, src, bytes);
+  }
+  // Host-to-device copy of a (pageable) host range. Large ranges go through a pinned staging
+  // ring: host threads copy chunk i into a page-locked buffer while the DMA engine moves chunk
+  // i-1 (KVGPU_UPLOAD=pageable: one hipMemcpy, for A/B runs).
+  static void upload_h2d(void* dst, const void* src, size_t bytes) {
+    static const std::string how = getenv("KVGPU_UPLOAD") ? getenv("KVGPU_UPLOAD") : "staged";
+    static const size_t kChunk = (size_t)(getenv("KVGPU_UPLOAD_CHUNK_MB") ? atoi(getenv("KVGPU_UPLOAD_CHUNK_MB")) : 32) << 20;
+    constexpr size_t kMin = 16u << 20;
+    constexpr int kRing = 4;
+    if (how == "pageable" || bytes < kMin) {
+      HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+      return;
+    }
+    if (how == "register") {  // A/B: page-lock the source range for the copy
+      const uintptr_t a = (uintptr_t)src & ~(uintptr_t)4095, e = ((uintptr_t)src + bytes + 4095) & ~(uintptr_t)4095;
+      if (hipHostRegister((void*)a, e - a, hipHostRegisterDefault) == hipSuccess) {
+        HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+        (void)hipHostUnregister((void*)a);
+        return;
+      }
+      (void)hipGetLastError();
+    }
+    static std::mutex mu;  // one staged upload at a time per process (the ring is shared)
+    static char* ring[kRing] = {};
+    std::lock_guard<std::mutex> g(mu);
+    if (!ring[0]) {
+      for (int i = 0; i < kRing; i++) {
+        if (hipHostMalloc((void**)&ring[i], kChunk, hipHostMallocPortable) != hipSuccess) {
+          (void)hipGetLastError();
+          for (int j = 0; j < i; j++) (void)hipHostFree(ring[j]);
+          ring[0] = nullptr;
+          HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+          return;
+        }
+      }
+    }
+    hipStream_t st;
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    hipEvent_t ev[kRing];
+    for (int i = 0; i < kRing; i++) HIPCHK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+    bool used[kRing] = {};
+    static const unsigned T = std::max(1u, std::min(getenv("KVGPU_UPLOAD_THREADS") ? (unsigned)atoi(getenv("KVGPU_UPLOAD_THREADS")) : 16u,
+                                                    std::thread::hardware_concurrency()));
+    size_t k = 0;
+    for (size_t off = 0; off < bytes; off += kChunk, k++) {
+      const int i = (int)(k % kRing);
+      const size_t len = std::min(kChunk, bytes - off);
+      if (used[i]) HIPCHK(hipEventSynchronize(ev[i]));  // the DMA out of this buffer is done
+      const char* s = (const char*)src + off;
+      std::vector<std::thread> th;
+      const size_t part = (len + T - 1) / T;
+      for (unsigned t = 0; t < T; t++) {
+        const size_t a = std::min(len, t * part), e = std::min(len, a + part);
+        if (a < e) th.emplace_back([=]() { memcpy(ring[i] + a, s + a, e - a); });
+      }
+      for (auto& x : th) x.join();
+      HIPCHK(hipMemcpyAsync((char*)dst + off, ring[i], len, hipMemcpyHostToDevice, st));
+      HIPCHK(hipEventRecord(ev[i], st));
+      used[i] = true;
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    for (int i = 0; i < kRing; i++) (void)hipEventDestroy(ev[i]);
+    (void)hipStreamDestroy(st);
   }
   void alloc(size_t bytes, int device) {
     dev = device;
@@ -127,38 +191,82 @@ struct kv_batch {
 
 namespace {
 
-// Host array without value-initialisation; page-locked (hipHostMalloc) unless
+// Page-locked host blocks are expensive to create (pinning), so released result
+// buffers are kept for the next result of the process (up to 8 GiB): a host that
+// validates batch after batch pays the pinning once.
+struct PinnedPool {
+  std::mutex mu;
+  std::multimap<size_t, void*> free;  // capacity -> block
+  size_t held = 0;
+  static PinnedPool& get() {
+    static PinnedPool* p = new PinnedPool();  // never destroyed: blocks may outlive static teardown
+    return *p;
+  }
+  void* take(size_t bytes, size_t* cap) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      auto it = free.lower_bound(bytes);
+      if (it != free.end() && it->first <= 2 * bytes + (1u << 20)) {
+        void* p = it->second;
+        *cap = it->first;
+        held -= it->first;
+        free.erase(it);
+        return p;
+      }
+    }
+    // headroom (+1/8, 16 MiB granules) so the next batch's slightly larger result fits the block
+    const size_t want = bytes < (16u << 20) ? bytes : ((bytes + bytes / 8 + (16u << 20) - 1) & ~(size_t)((16u << 20) - 1));
+    void* p = nullptr;
+    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    *cap = want;
+    return p;
+  }
+  void give(void* p, size_t cap) {
+    std::lock_guard<std::mutex> g(mu);
+    if (held + cap > (8ull << 30)) {
+      (void)hipHostFree(p);
+      return;
+    }
+    free.emplace(cap, p);
+    held += cap;
+  }
+};
+
+// Host array without value-initialisation; page-locked (pooled hipHostMalloc) unless
 // KVGPU_PINNED=0, so device-to-host copies of results are direct DMA.
 template <class T>
 struct HostArray {
   T* p = nullptr;
-  size_t n = 0;
+  size_t n = 0, cap = 0;
   bool pinned = false;
   HostArray() = default;
   HostArray(const HostArray&) = delete;
   HostArray& operator=(const HostArray&) = delete;
-  HostArray(HostArray&& o) noexcept : p(o.p), n(o.n), pinned(o.pinned) { o.p = nullptr; o.n = 0; }
+  HostArray(HostArray&& o) noexcept : p(o.p), n(o.n), cap(o.cap), pinned(o.pinned) { o.p = nullptr; o.n = 0; }
   ~HostArray() { release(); }
   void alloc(size_t count) {
     release();
     n = count;
     if (!count) return;
     static const bool use_pinned = !(getenv("KVGPU_PINNED") && getenv("KVGPU_PINNED")[0] == '0');
-    if (use_pinned && hipHostMalloc((void**)&p, count * sizeof(T), hipHostMallocDefault) == hipSuccess) {
+    if (use_pinned && (p = (T*)PinnedPool::get().take(count * sizeof(T), &cap)) != nullptr) {
       pinned = true;
       return;
     }
-    (void)hipGetLastError();
     p = (T*)malloc(count * sizeof(T));
     if (!p) throw std::bad_alloc();
   }
   void release() {
     if (p) {
-      if (pinned) (void)hipHostFree(p);
+      if (pinned) PinnedPool::get().give(p, cap);
       else free(p);
     }
     p = nullptr;
     n = 0;
+    cap = 0;
     pinned = false;
   }
   T* data() const { return p; }
@@ -610,8 +718,12 @@ struct DevSession {
   DevSession(kv_policyset* p, kv_batch* b, const char* ctx_json, int dev, uint32_t m)
       : ps(p), bt(b), device(dev), mode(m) {
     HIPCHK(hipSetDevice(device));
+    const auto tc0 = std::chrono::steady_clock::now();
     DevPolicySet& dp = dev_ps(ps, device);
     DevBatchRes& db = dev_batch(bt, ps->ps, device);
+    if (getenv("KVGPU_VERBOSE"))
+      fprintf(stderr, "[kvgpu] session: policy set + batch upload %.1f ms\n",
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc0).count());
     bview = (const DevBatch*)db.view_dev.p;
     bhost = &db.view;
     dps = &dp;
@@ -748,9 +860,18 @@ struct DevSession {
   // the compacted error records of this shard
   void fetch(kv_result* out, ResultPart* part, uint64_t lo, uint64_t n_total) {
     HIPCHK(hipSetDevice(device));
+    const bool verbose = getenv("KVGPU_VERBOSE") != nullptr;
+    const auto tf0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+      if (!verbose) return;
+      HIPCHK(hipStreamSynchronize(stream));
+      fprintf(stderr, "[kvgpu] fetch: %s at %.1f ms\n", what,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count());
+    };
     if (O.status && (mode & (KV_MODE_STATUS | KV_MODE_ERRORS)) && nres && nrules)
       HIPCHK(hipMemcpy2DAsync(out->status.data() + lo, n_total, st.p, nres, nres, nrules, hipMemcpyDeviceToHost,
                               stream));
+    lap("status D2H");
     if (O.err8 && nres && nrules) {
       const uint32_t tiles = (uint32_t)((nres + KV_WG - 1) / KV_WG);
       part->tiles = tiles;
@@ -770,6 +891,7 @@ struct DevSession {
       HIPCHK(hipMemcpyAsync(part->offs.data(), r_offs.p, part->offs.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
                             stream));
       HIPCHK(hipStreamSynchronize(stream));
+      lap("record counts");
       const uint64_t total = part->base[nrules];
       if (r_out8.n < total * sizeof(ErrRec8)) r_out8.alloc(std::max<uint64_t>(total, 1) * sizeof(ErrRec8), device);
       HIPCHK(hipMemsetAsync(r_wide.p, 0, sizeof(uint32_t), stream));
@@ -782,6 +904,7 @@ struct DevSession {
       uint32_t wide = 0;
       HIPCHK(hipMemcpyAsync(&wide, r_wide.p, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
       HIPCHK(hipStreamSynchronize(stream));
+      lap("records scatter + D2H");
       if (wide) {  // re-run the pass once writing full records (same statuses), compact those too
         if (!er.p) er.alloc(nrules * nres * sizeof(ErrRec), device);
         O.err = (ErrRec*)er.p;
@@ -979,12 +1102,21 @@ std::vector<int> mask_devices(uint32_t mask) {
 void run(kv_policyset* ps, kv_batch* bt, const char* ctx_json, const std::vector<int>& devices, uint32_t mode,
          kv_result* out, int warmup, int iters, double* ms) {
   if (devices.empty()) throw std::runtime_error("empty device mask");
+  const auto t0 = std::chrono::steady_clock::now();
   SessionSet s(ps, bt, ctx_json, devices, mode);
+  const auto t1 = std::chrono::steady_clock::now();
   if (warmup > 0) s.run(warmup);
   int n = std::max(iters, 1);
   double t = s.run(n) / n;
+  const auto t2 = std::chrono::steady_clock::now();
   if (ms) *ms = t;
   if (out) s.fetch(out, t);
+  if (getenv("KVGPU_VERBOSE")) {  // host-boundary breakdown
+    const auto t3 = std::chrono::steady_clock::now();
+    auto d = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    fprintf(stderr, "[kvgpu] kv_validate: setup+upload %.1f ms, passes %.1f ms, fetch %.1f ms\n", d(t0, t1), d(t1, t2),
+            d(t2, t3));
+  }
 }
 
 }  // namespace
