@@ -435,6 +435,23 @@ struct Gen {
                            "  ((uint16_t*)PT)[((size_t)(blockIdx.y >> 1) * NV + v) * 2u + (blockIdx.y & 1u)] = (uint16_t)w;\n}\n\n");
   }
 
+  // dynamic leaves (pattern variables, kvvars.cpp): the generic predicate evaluator on the
+  // batch table, out of line (one copy per program; inlined per leaf it multiplies the
+  // kernel's code and its compile time)
+  bool dleaf_done = false;
+  void dleaf_fn() {
+    if (dleaf_done) return;
+    dleaf_done = true;
+    o << "__device__ __forceinline__ bool g_dleaf_0(const DevBatch& B, const Node* __restrict__ N, uint32_t dp, "
+         "const Node& vn) { return kv_dleaf_impl(B, N, dp, vn); }\n"
+      << "__device__ __noinline__ bool kv_dleaf_impl(const DevBatch& B, const Node* __restrict__ N, uint32_t dp, Node vn) {\n"
+      << "  const uint32_t vt = node_type(vn.kt);\n"
+      << "  if (vt == NT_ARR) {\n"
+      << "    for (uint32_t k = 0; k < vn.b; k++) if (!pred_node(*B.dps, B, N, dp, ni(vn.a + k))) return false;\n"
+      << "    return true;\n  }\n"
+      << "  return pred_eval(*B.dps, B, dp, vt, vn);\n}\n";
+  }
+
   // ---------------------------------------------------------------- match / exclude
   // blk_ok(f) == !(MF_EMPTY) && doesResourceMatchConditionBlock(f) has no errors
   // (pkg/engine/utils.go:265-336); MF_EMPTY / MF_UI_FAIL are folded per launch
@@ -601,13 +618,10 @@ struct Gen {
             << "    if (!ok_) " << raise("E_VALUE", in.b, cd, in.c) << " }\n";
           break;
         case OP_VLEAF:
+          dleaf_fn();
           o << "  { Node vn_{0u, 0u, 0u, 0u}; if (" << cd << " != ABSENT) vn_ = N[" << cd << "];\n"
-            << "    const uint32_t dp_ = B.dleaf[(size_t)" << u32(in.a) << " * n_res + r];\n"
-            << "    const uint32_t vt_ = node_type(vn_.kt); bool ok_;\n"
-            << "    if (vt_ == NT_ARR) { ok_ = true; for (uint32_t k_ = 0; k_ < vn_.b && ok_; k_++) "
-               "ok_ = pred_node(*B.dps, B, N, dp_, ni(vn_.a + k_)); }\n"
-            << "    else ok_ = pred_eval(*B.dps, B, dp_, vt_, vn_);\n"
-            << "    if (!ok_) " << raise("E_VALUE", in.b, cd, in.c) << " }\n";
+            << "    if (!g_dleaf_0(B, N, B.dleaf[(size_t)" << u32(in.a) << " * n_res + r], vn_)) "
+            << raise("E_VALUE", in.b, cd, in.c) << " }\n";
           break;
         case OP_RAISE:
           o << "  " << raise(u32(in.b), in.a, cd, in.c) << "\n";
@@ -950,12 +964,9 @@ struct Gen {
         case OP_VLEAF:  // pattern variables: the resource's substituted value (kvvars.cpp)
           if (known(d)) w << "  { const Node vn_ = " << NODE(d) << ";\n";
           else w << "  { Node vn_{0u, 0u, 0u, 0u}; if (" << cd << " != ABSENT) vn_ = N[" << cd << "];\n";
-          w << "    const uint32_t dp_ = B.dleaf[(size_t)" << u32(in.a) << " * n_res + r];\n"
-            << "    const uint32_t vt_ = node_type(vn_.kt); bool ok_;\n"
-            << "    if (vt_ == NT_ARR) { ok_ = true; for (uint32_t k_ = 0; k_ < vn_.b && ok_; k_++) "
-               "ok_ = pred_node(*B.dps, B, N, dp_, ni(vn_.a + k_)); }\n"
-            << "    else ok_ = pred_eval(*B.dps, B, dp_, vt_, vn_);\n"
-            << "    if (!ok_) " << raise("E_VALUE", in.b, in.c) << " }\n";
+          dleaf_fn();
+          w << "    if (!g_dleaf_0(B, N, B.dleaf[(size_t)" << u32(in.a) << " * n_res + r], vn_)) "
+            << raise("E_VALUE", in.b, in.c) << " }\n";
           break;
         case OP_RAISE:
           w << "  " << raise(u32(in.b), in.a, in.c) << "\n";
@@ -1347,7 +1358,8 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   // KVGPU_JIT_STORE=lane: the per-lane-branch record store variant (8-wave A/B of DESIGN.md)
   const bool lane_store = getenv("KVGPU_JIT_STORE") && std::string(getenv("KVGPU_JIT_STORE")) == "lane";
   const std::string prelude =
-      std::string(lane_store ? "#define KV_STORE_LANE_BRANCH 1\n" : "") + kPrelude + "\nusing namespace kv;\n\n";
+      std::string(lane_store ? "#define KV_STORE_LANE_BRANCH 1\n" : "") + kPrelude + "\nusing namespace kv;\n\n" +
+      "__device__ __noinline__ bool kv_dleaf_impl(const DevBatch& B, const Node* __restrict__ N, uint32_t dp, Node vn);\n\n";
   // KVGPU_JIT_FUSE=0: one device function per rule (no cross-rule sharing), for A/B runs
   const char* fz = getenv("KVGPU_JIT_FUSE");
   const bool fused = !(fz && fz[0] == '0');
@@ -1440,7 +1452,8 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   std::unordered_map<std::string, size_t> def_index;
   for (size_t i = 0; i < defs.size(); i++) def_index[defs[i].first] = i;
   auto refs = [&](const std::string& text, std::vector<size_t>* out_ids) {
-    static const char* prefixes[] = {"g_glob_", "g_atom_", "g_pred_", "m_pred_", "g_blk_", "g_match_", "g_rule_"};
+    static const char* prefixes[] = {"g_glob_", "g_atom_", "g_pred_", "m_pred_", "g_blk_", "g_match_", "g_rule_",
+                                     "g_dleaf_"};
     for (const char* pf : prefixes) {
       const size_t pl = strlen(pf);
       for (size_t q = text.find(pf); q != std::string::npos; q = text.find(pf, q + pl)) {
