@@ -21,7 +21,9 @@ def per_pass(csv_path, counter):
     agg = collections.defaultdict(float)
     for r in csv.DictReader(open(csv_path)):
         k = r.get("Kernel_Name", "")
-        if r["Counter_Name"] == counter and k.startswith(("kv_", "kvj_")):
+        # the pass's kernels; the record-compaction kernels (kv::kv_rec_*) run once per fetch,
+        # outside the timed passes (the e2e leg of the same command)
+        if r["Counter_Name"] == counter and k.startswith(("kv_", "kvj_", "kv::")) and "kv_rec_" not in k:
             agg[(k, r["Dispatch_Id"])] += float(r["Counter_Value"])
     per_k = collections.defaultdict(list)
     for (k, _), v in agg.items():
@@ -53,6 +55,14 @@ def main():
         if "WRITE_SIZE" in heads:
             write = per_pass(f, "WRITE_SIZE")
     bench = json.loads(open(os.path.join(dst, "bench.json")).read().strip().splitlines()[-1])
+    run_id = name
+    try:  # the gpurun call that produced these files: its verdict file's time
+        import datetime
+
+        t = os.path.getmtime(os.path.join(src, ".last_call.json"))
+        run_id = f"{name} @ {datetime.datetime.utcfromtimestamp(t).strftime('%Y-%m-%dT%H:%M:%SZ')}"
+    except OSError:
+        pass
     if fetch is not None and write is not None:
         traffic = 2 * fetch * 1024 + write * 1024
         out = {"workload": bench["config"]["workload"], "resources_per_gpu": bench["config"]["resources_per_gpu"],
@@ -60,7 +70,8 @@ def main():
                "engine": bench["config"]["engine"],
                "fetch_size_kb": fetch, "write_size_kb": write, "bytes_per_pass": traffic,
                "algorithmic_bytes_per_pass": bench["roofline"]["bytes_per_launch"],
-               "source": f"profiles/{name}/pass*_counter_collection.csv (2 x FETCH_SIZE + WRITE_SIZE, KB->B)"}
+               "source": f"profiles/{name}/pass*_counter_collection.csv (2 x FETCH_SIZE + WRITE_SIZE, KB->B)",
+               "run_id": run_id}
         json.dump(out, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
         print(json.dumps(out, indent=1))
 
