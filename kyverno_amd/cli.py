@@ -17,8 +17,8 @@ Mirrors the reference CLI for validate rules:
 Evaluation runs on the GPU through the C ABI (``kyverno_amd.batch``): one
 ``kv_validate`` over the whole (rule × resource) cross product instead of the
 reference's per-pair ``engine.Validate`` loop (apply_command.go:270-310). Rules
-the device does not evaluate (JMESPath variables, context, preconditions, deny,
-foreach — ``KV_ROUTE_CPU``) are reported as routed to the reference engine and
+the device does not evaluate (variables other than ``request.object`` paths,
+context, preconditions, deny, foreach — ``KV_ROUTE_CPU``) are reported as routed to the reference engine and
 not counted; a Go host runs them through ``engine.Validate``.
 
     python -m kyverno_amd apply policy.yaml -r pods.yaml [--policy-report] [--device N]

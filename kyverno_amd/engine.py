@@ -10,8 +10,8 @@ error (``addRuleResponse``, validation.go:111-123). A response without rule resp
 ``EngineResponse`` (``buildResponse`` returns early, validation.go:53-56). Policies are taken as
 given: the CLI's defaults + autogen (``kyverno_amd.autogen``) happen before, as in the reference.
 
-Rules the device does not evaluate (context, preconditions, deny, foreach, ``{{}}`` variables in
-the pattern: ``KV_ROUTE_CPU``) come back with status ``"cpu"``: the Go host runs
+Rules the device does not evaluate (context, preconditions, deny, foreach, pattern variables other
+than ``request.object`` paths: ``KV_ROUTE_CPU``) come back with status ``"cpu"``: the Go host runs
 ``processValidationRule`` for them. They are not counted.
 """
 from __future__ import annotations
