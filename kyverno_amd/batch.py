@@ -339,6 +339,9 @@ def synth(seed: int, n: int, kind_mix: int = 0, first: int = 0) -> bytes:
     rc = lib().kv_synth_range(seed, first, n, kind_mix, ctypes.byref(p), ctypes.byref(ln))
     if rc != 0:
         raise _native.KvError(rc, "kv_synth failed")
-    data = ctypes.string_at(p.value, ln.value)
+    # ctypes.string_at takes a C int size: copy buffers over 2 GiB in pieces
+    step = 1 << 30
+    data = b"".join(ctypes.string_at(p.value + o, min(step, ln.value - o)) for o in range(0, ln.value, step)) \
+        if ln.value > step else ctypes.string_at(p.value, ln.value)
     lib().kv_free_buffer(p)
     return data

@@ -1400,10 +1400,11 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
     }
     out->n_chunks = (uint32_t)chs.size();
     if (out->plan.empty()) {
-      // KVGPU_JIT_GROUP: fused chunks run back to back inside one kernel (default 5);
+      // KVGPU_JIT_GROUP: fused chunks run back to back inside one kernel (default 25: C2 1.56 ms
+      // vs 1.58 at 5, C3 22.6 ms vs 27.3, C4 1.73 vs 1.90; compile 11-13 s);
       // KVGPU_JIT_WAVES: launch bound in waves per SIMD (default 8, 0: none)
       const char* gz = getenv("KVGPU_JIT_GROUP");
-      const uint32_t group = gz ? (uint32_t)std::max(1, atoi(gz)) : 5u;
+      const uint32_t group = gz ? (uint32_t)std::max(1, atoi(gz)) : 25u;
       const char* wz = getenv("KVGPU_JIT_WAVES");
       const int waves = wz ? atoi(wz) : 8;
       for (uint32_t b = 0; b < chs.size(); b += group)
@@ -1715,12 +1716,17 @@ bool jit_plan_spills(JitImage* img) {
       continue;
     }
     changed = true;
-    if (kp.count > 1) {  // split the group: fewer rules' state per kernel
+    // A kernel that spills under the wave bound is recompiled without the bound (it takes the
+    // registers it needs, at lower occupancy). Splitting the group instead (KVGPU_JIT_SPILL=split)
+    // multiplies the kernels, each re-walking the resources: C4 1.73 ms (16 kernels) against
+    // 1.34 ms (2 unbounded kernels), C2 1.56 against 1.52 ms.
+    static const bool split = getenv("KVGPU_JIT_SPILL") && std::string(getenv("KVGPU_JIT_SPILL")) == "split";
+    if (split && kp.count > 1) {
       const uint32_t h = kp.count / 2;
       next.push_back({kp.first, h, kp.waves});
       next.push_back({kp.first + h, kp.count - h, kp.waves});
-    } else {  // one fused chunk that still spills under the bound: let it take the registers it needs
-      next.push_back({kp.first, 1, 0});
+    } else {
+      next.push_back({kp.first, kp.count, 0});
     }
   }
   if (changed) img->plan = next;
