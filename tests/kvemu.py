@@ -31,8 +31,13 @@ def fnv1a(b: bytes) -> int:
 
 
 def build_host() -> None:
-    subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "kyverno_amd", "csrc")], check=True)
-    subprocess.run(["make", "-s", "-j8", "-C", EMU], check=True, stderr=subprocess.DEVNULL)
+    import fcntl
+
+    os.makedirs(os.path.join(ROOT, "build"), exist_ok=True)
+    with open(os.path.join(ROOT, "build", ".kvemu.lock"), "w") as lk:  # one make at a time (pytest -n)
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "kyverno_amd", "csrc")], check=True)
+        subprocess.run(["make", "-s", "-j8", "-C", EMU], check=True, stderr=subprocess.DEVNULL)
 
 
 def _with_env(env: dict, fn):
