@@ -75,6 +75,60 @@ def cpu_baseline(policies, pairs: float, threads: int, kind_mix: int = 0, label:
                       f"{secs:.2f} s"}
 
 
+def pmc_traffic(args) -> dict | None:
+    """HBM bytes per pass of this workload from rocprofv3 PMC counters, measured by this command:
+    two child runs of this script (2 passes + the first), one counter each (FETCH_SIZE, WRITE_SIZE;
+    one rocprofv3 --pmc run per counter group, kernel-trace/stats only). Per MI355X_MICROARCH.md
+    (HBM section): the counters are KB, and on gfx950 FETCH_SIZE counts half the bytes of coalesced
+    reads, so it is doubled. Sum over the pass's kernels (the record-compaction kernels kv_rec_*
+    run at fetch, outside the pass)."""
+    import csv
+    import collections
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+
+    rp = shutil.which("rocprofv3")
+    if not rp:
+        return None
+    out = tempfile.mkdtemp(prefix="kvpmc.", dir=os.environ.get("TMPDIR", "/tmp"))
+    passes = 3  # the child's first pass + --warmup 0 + --steps 2
+    child = [sys.executable, "-u", os.path.abspath(__file__), "--config", args.config, "--n-res", str(args.n_res),
+             "--mode", args.mode, "--engine", args.engine, "--steps", "2", "--warmup", "0", "--no-cpu-baseline",
+             "--no-e2e", "--no-traffic"]
+    vals = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        cmd = [rp, "--pmc", ctr, "--kernel-trace", "--stats", "-d", out, "-o", ctr, "--output-format", "csv", "--"] + child
+        p = subprocess.Popen(cmd, cwd=out, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, start_new_session=True)
+        try:
+            _, err = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            log(f"pmc {ctr}: timed out")
+            return None
+        if p.returncode != 0:
+            log(f"pmc {ctr}: rocprofv3 exit {p.returncode}: {err.decode(errors='replace')[-400:]}")
+            return None
+        agg = collections.defaultdict(float)
+        for f in sorted(set(__import__("glob").glob(os.path.join(out, "**", f"{ctr}*counter_collection.csv"),
+                                                    recursive=True))):
+            for r in csv.DictReader(open(f)):
+                k = r.get("Kernel_Name", "")
+                if r["Counter_Name"] == ctr and k.startswith(("kv_", "kvj_", "kv::")) and "kv_rec_" not in k:
+                    agg[k] += float(r["Counter_Value"])
+        if not agg:
+            return None
+        vals[ctr] = {k: v * 1024 / passes for k, v in agg.items()}
+    shutil.rmtree(out, ignore_errors=True)
+    fetch = 2 * sum(vals["FETCH_SIZE"].values())
+    write = sum(vals["WRITE_SIZE"].values())
+    return {"bytes_per_pass": fetch + write, "read_bytes": fetch, "write_bytes": write,
+            "per_kernel_read": {k: 2 * v for k, v in sorted(vals["FETCH_SIZE"].items())},
+            "run_id": f"in-run PMC, pid {os.getpid()}, {time.strftime('%Y-%m-%dT%H:%M:%SZ', time.gmtime())}"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -99,8 +153,8 @@ def main():
                     help="torch.distributed backend for N>1 (default: nccl = RCCL when GPUs are visible); "
                          "gloo lets several ranks share one GPU for a rehearsal")
     ap.add_argument("--rule-filter", default="", help="diagnostics: regex over C2 rule names")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_v10", "traffic.json"),
-                    help="PMC-derived HBM bytes per pass of this same command (tools/collect_profile.py)")
+    ap.add_argument("--no-traffic", action="store_true",
+                    help="skip the PMC traffic measurement (two rocprofv3 --pmc child runs of this workload)")
     ap.add_argument("--engine", choices=["vm", "specialized"], default="specialized",
                     help="bytecode interpreter kernel, or per-policy-set specialized kernels (hiprtc)")
     args = ap.parse_args()
@@ -212,16 +266,7 @@ def main():
                  "scopes": 2 * n_pairs_rank + 4 * b.n_res}[args.mode]
     b_alg = b.store_bytes + prog_bytes + out_bytes
     achieved = b_alg / (kernel_ms / 1e3) / 1e9
-    traffic, traffic_src = None, None
-    try:  # HBM bytes per pass from an OFFLINE rocprofv3 PMC run of this workload (rocprofv3 cannot run
-        # inside this process): reported only when that run's workload matches, labelled with its run id
-        tj = json.load(open(args.traffic_json))
-        if (tj["workload"], tj["resources_per_gpu"], tj["rules"], tj["output"], tj["engine"]) == \
-                (workload, b.n_res, ps.n_rules, args.mode, args.engine):
-            traffic = tj["bytes_per_pass"]
-            traffic_src = f"offline PMC, {os.path.relpath(args.traffic_json, ROOT)} (run {tj.get('run_id', '?')})"
-    except (OSError, ValueError, KeyError):
-        pass
+    traffic, traffic_src = None, None  # filled below by the in-run PMC measurement (rank 0, N=1)
     out = {
         "metric": "resource×rule validate evals/sec (node)",
         "value": value,
@@ -253,7 +298,7 @@ def main():
     if rank == 0 and world == 1 and args.mode == "full" and not args.no_e2e:
         # PCIe-inclusive rate of the host boundary: kv_validate on a freshly ingested
         # batch = H2D upload of the projected store + one pass + D2H of statuses and error records
-        del sess
+        sess = None
         # steady state of a host that validates batch after batch: one untimed kv_validate on another
         # batch first (the library keeps its pinned staging / result buffers), then the timed one on a
         # freshly ingested batch
@@ -274,6 +319,20 @@ def main():
         # nproc and the CPU model are recorded beside it)
         threads = host_cpu()["available"]
         out["cpu_baseline"] = cpu_baseline(pols, args.cpu_pairs, threads, kind_mix, args.config.upper())
+    if rank == 0 and world == 1 and not args.no_traffic:
+        # measured HBM bytes of the same workload (child rocprofv3 --pmc runs), after this
+        # process's device buffers are freed
+        sess = None
+        import gc
+
+        gc.collect()
+        t = pmc_traffic(args)
+        if t is not None:
+            out["roofline"]["traffic"] = t["bytes_per_pass"]
+            out["roofline"]["traffic_source"] = t["run_id"] + " (2 x FETCH_SIZE + WRITE_SIZE, rocprofv3 --pmc)"
+            out["roofline"]["traffic_over_alg"] = t["bytes_per_pass"] / b_alg
+            out["roofline"]["traffic_detail"] = {"read": t["read_bytes"], "write": t["write_bytes"],
+                                                 "per_kernel_read": t["per_kernel_read"]}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -38,6 +38,8 @@ struct HipError : std::runtime_error {
     if (e_ != hipSuccess) throw HipError(std::string(#x) + ": " + hipGetErrorString(e_));      \
   } while (0)
 
+bool pinned_src(const void* src, size_t bytes);  // page-locked store array (PinnedStore)
+
 struct DevBuf {
   void* p = nullptr;
   size_t n = 0;
@@ -55,8 +57,8 @@ struct DevBuf {
       }
     }
   }
-  template <class T>
-  void upload(const std::vector<T>& v, int device) {
+  template <class T, class A>
+  void upload(const std::vector<T, A>& v, int device) {
     upload_raw(v.data(), v.size() * sizeof(T), device);
   }
   void upload_raw(const void* src, size_t bytes, int device) {
@@ -73,7 +75,7 @@ struct DevBuf {
     static const size_t kChunk = (size_t)(getenv("KVGPU_UPLOAD_CHUNK_MB") ? atoi(getenv("KVGPU_UPLOAD_CHUNK_MB")) : 32) << 20;
     constexpr size_t kMin = 16u << 20;
     constexpr int kRing = 4;
-    if (how == "pageable" || bytes < kMin) {
+    if (how == "pageable" || bytes < kMin || pinned_src(src, bytes)) {
       HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
       return;
     }
@@ -234,6 +236,68 @@ struct PinnedPool {
     held += cap;
   }
 };
+
+// Page-locked store arrays of ingested batches (kvinternal.hpp HostMem): blocks from the
+// pool, registered by address so the upload can tell a page-locked source (direct DMA)
+// from a pageable one (staging ring), and so a block returns to the pool when freed.
+struct PinnedStore {
+  std::mutex mu;
+  std::map<uintptr_t, size_t> live;  // block -> capacity
+  static PinnedStore& get() {
+    static PinnedStore* p = new PinnedStore();
+    return *p;
+  }
+  static bool enabled() {
+    static const bool on = []() {
+      if (getenv("KVGPU_PINNED") && getenv("KVGPU_PINNED")[0] == '0') return false;
+      int n = 0;  // no device (host-only use of the library): plain memory
+      if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        return false;
+      }
+      return true;
+    }();
+    return on;
+  }
+  static void* take(size_t bytes) {
+    if (!enabled()) return nullptr;
+    size_t cap = 0;
+    void* p = PinnedPool::get().take(bytes, &cap);
+    if (!p) return nullptr;
+    std::lock_guard<std::mutex> g(get().mu);
+    get().live[(uintptr_t)p] = cap;
+    return p;
+  }
+  static bool give(void* p) {
+    size_t cap = 0;
+    {
+      std::lock_guard<std::mutex> g(get().mu);
+      auto it = get().live.find((uintptr_t)p);
+      if (it == get().live.end()) return false;
+      cap = it->second;
+      get().live.erase(it);
+    }
+    PinnedPool::get().give(p, cap);
+    return true;
+  }
+  // [src, src + bytes) inside one live page-locked block
+  static bool contains(const void* src, size_t bytes) {
+    std::lock_guard<std::mutex> g(get().mu);
+    auto& m = get().live;
+    auto it = m.upper_bound((uintptr_t)src);
+    if (it == m.begin()) return false;
+    --it;
+    return (uintptr_t)src + bytes <= it->first + it->second;
+  }
+};
+struct InstallHostMem {
+  InstallHostMem() {
+    g_hostmem.take = &PinnedStore::take;
+    g_hostmem.give = &PinnedStore::give;
+  }
+} install_host_mem_;
+
+bool pinned_src(const void* src, size_t bytes) { return PinnedStore::contains(src, bytes); }
 
 // Host array without value-initialisation; page-locked (pooled hipHostMalloc) unless
 // KVGPU_PINNED=0, so device-to-host copies of results are direct DMA.

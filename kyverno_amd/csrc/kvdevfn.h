@@ -75,6 +75,23 @@ KV_GLOB_FN bool kv_glob(const uint8_t* p, uint32_t pl, const uint8_t* s, uint32_
   return pi == pl && si == sl;
 }
 
+// 64-bit mask of the byte positions p < 64 of the 16 words `w` whose byte may equal
+// the byte replicated in c4 (SWAR zero-byte test of w ^ c4: every equal byte is
+// flagged; a byte c4 ^ 1 right after an equal one can be flagged too, so callers
+// verify each candidate). Straight-line: no per-lane loop.
+__device__ __forceinline__ uint64_t kv_bmask(const uint32_t* w, uint32_t c4) {
+  uint32_t lo = 0u, hi = 0u;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; i++) {
+    const uint32_t x = w[i] ^ c4, y = w[i + 8] ^ c4;
+    // bits 7, 15, 23, 31 of m -> bits 28..31 of m * 0x00204081 (no carries between them)
+    const uint32_t mx = (x - 0x01010101u) & ~x & 0x80808080u, my = (y - 0x01010101u) & ~y & 0x80808080u;
+    lo |= ((mx * 0x00204081u) >> 28) << (4u * i);
+    hi |= ((my * 0x00204081u) >> 28) << (4u * i);
+  }
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // segment (uniform words) == value bytes [k, k+len) ; value base 4-byte aligned
 __device__ __forceinline__ bool seg_at(const GWord* __restrict__ wd, uint32_t len, const uint32_t* __restrict__ base,
                                        uint32_t k) {

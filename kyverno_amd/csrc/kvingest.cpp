@@ -23,6 +23,8 @@
 
 namespace kvh {
 
+HostMem g_hostmem;
+
 using namespace kv;
 
 namespace {
@@ -553,7 +555,7 @@ std::vector<KeyCount> val_order_cursors(const std::vector<KeyCount>& hists) {
   return cur;
 }
 
-KeyCount val_hist(const std::vector<Val>& vals) {
+KeyCount val_hist(const StoreVec<Val>& vals) {
   KeyCount h;
   for (const Val& v : vals) h[val_order_key(v)]++;
   return h;
@@ -563,7 +565,7 @@ KeyCount val_hist(const std::vector<Val>& vals) {
 void order_vals(Batch& b) {
   std::vector<KeyCount> cur = val_order_cursors({val_hist(b.vals)});
   std::vector<uint32_t> perm(b.vals.size());
-  std::vector<Val> out(b.vals.size());
+  StoreVec<Val> out(b.vals.size(), Val{}, b.vals.get_allocator());
   for (size_t i = 0; i < b.vals.size(); i++) {
     perm[i] = cur[0][val_order_key(b.vals[i])]++;
     out[perm[i]] = b.vals[i];
@@ -649,6 +651,7 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
   }
   if (H >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: string heap exceeds 4 GiB");
   if (R * KV_LANES >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: batch too large for 32-bit node indices");
+  b.pin_store();
   b.strs.assign(H, '\0');
   b.vals.resize(V);
   b.kvs.resize(K);

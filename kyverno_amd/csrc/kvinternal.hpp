@@ -1,7 +1,10 @@
 // Host-side internal structures of libkvgpu (compiled policy set, ingested batch).
 #pragma once
 #include <cstdint>
+#include <cstdlib>
+#include <new>
 #include <string>
+#include <type_traits>
 #include <tuple>
 #include <unordered_map>
 #include <vector>
@@ -178,13 +181,64 @@ struct PolicySet {
 // objects. Throws std::runtime_error on malformed input.
 void compile_policies(const char* json, size_t len, PolicySet* ps);
 
+// Host memory of the large store arrays of an ingested batch. libkvgpu (kvapi.cpp)
+// installs a pooled page-locked allocator, so the store's H2D upload is one direct
+// DMA instead of a copy through a staging ring; without it (host-only builds) plain
+// malloc. `take` returns nullptr to fall back; `give` returns false for a block it
+// does not own.
+struct HostMem {
+  void* (*take)(size_t bytes) = nullptr;
+  bool (*give)(void* p) = nullptr;
+};
+extern HostMem g_hostmem;  // kvingest.cpp
+
+// Allocator of the store arrays: `pinned` (the merged batch and its shards) takes
+// blocks of >= 16 MiB from g_hostmem; the ingest's per-thread parts stay pageable.
+template <class T>
+struct StoreAlloc {
+  using value_type = T;
+  using propagate_on_container_swap = std::true_type;
+  using propagate_on_container_move_assignment = std::true_type;
+  using propagate_on_container_copy_assignment = std::true_type;
+  using is_always_equal = std::false_type;
+  bool pinned = false;
+  StoreAlloc() = default;
+  explicit StoreAlloc(bool p) : pinned(p) {}
+  template <class U>
+  StoreAlloc(const StoreAlloc<U>& o) : pinned(o.pinned) {}
+  T* allocate(size_t n) {
+    const size_t bytes = n * sizeof(T);
+    if (pinned && g_hostmem.take && bytes >= (16u << 20))
+      if (void* p = g_hostmem.take(bytes)) return (T*)p;
+    void* p = malloc(bytes ? bytes : 1);
+    if (!p) throw std::bad_alloc();
+    return (T*)p;
+  }
+  void deallocate(T* p, size_t) {
+    if (pinned && g_hostmem.give && g_hostmem.give(p)) return;
+    free(p);
+  }
+  template <class U>
+  bool operator==(const StoreAlloc<U>& o) const { return pinned == o.pinned; }
+  template <class U>
+  bool operator!=(const StoreAlloc<U>& o) const { return pinned != o.pinned; }
+};
+template <class T>
+using StoreVec = std::vector<T, StoreAlloc<T>>;
+
 // Ingested batch (host mirror of the HBM store)
 struct Batch {
-  std::vector<kv::Node> nodes;       // [n_rows][KV_LANES] (wave-group layout, kvingest.cpp)
+  StoreVec<kv::Node> nodes;          // [n_rows][KV_LANES] (wave-group layout, kvingest.cpp)
   uint64_t n_rows = 0;
   uint64_t cells_used = 0;           // populated cells (incl. absent-slot markers)
-  std::vector<kv::Val> vals;
-  std::vector<kv::Res> res;
+  StoreVec<kv::Val> vals;
+  StoreVec<kv::Res> res;
+  // the store arrays in page-locked memory when g_hostmem provides it (merged batch, shards)
+  void pin_store() {
+    nodes = StoreVec<kv::Node>(StoreAlloc<kv::Node>(true));
+    vals = StoreVec<kv::Val>(StoreAlloc<kv::Val>(true));
+    res = StoreVec<kv::Res>(StoreAlloc<kv::Res>(true));
+  }
   std::vector<kv::KV> kvs;
   std::string strs;                  // string heap
   std::vector<std::string> dyn_keys; // key ids >= ps.keys.size()

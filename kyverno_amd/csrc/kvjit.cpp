@@ -82,6 +82,9 @@ struct Gen {
   // kvj_ptab stages each value's bytes in LDS before its row of predicates;
   // KVGPU_PTAB_LDS=0 reads them from global memory per glob, for A/B runs
   bool ptab_lds = !(getenv("KVGPU_PTAB_LDS") && getenv("KVGPU_PTAB_LDS")[0] == '0');
+  // kvj_ptab evaluates globs on a register copy of the value with shared byte masks
+  // (qglob_fn); KVGPU_PTAB=words keeps the per-glob word loops (A/B runs)
+  bool ptab_regs = !(getenv("KVGPU_PTAB") && std::string(getenv("KVGPU_PTAB")) == "words");
   // hoisted lookups are branch-free (a failed guard reads cell 0 and discards it)
   // and are all placed at the top of their chunk / fused-loop body, so the loads
   // of one tree level issue together instead of one dependent wait per lookup;
@@ -197,6 +200,182 @@ struct Gen {
         << "    if (!found) return false; }\n";
     }
     o << "  (void)pos; (void)end;\n  return true;\n}\n";
+  }
+
+  // ---------------------------------------------------------------- kvj_ptab globs (register path)
+  // In kvj_ptab a value's bytes (<= 64) sit in 16 registers `w` (plus an LDS copy
+  // `lw` for reads at a per-lane offset). A middle segment's candidates are the
+  // positions of one of its literal bytes, taken from a 64-bit byte mask `bm[slot]`
+  // that the row computes once per distinct byte (kv_bmask: straight-line SWAR over
+  // the 16 words) and that every glob of the row sharing that byte reuses; the
+  // leftmost verified candidate at or after `pos` wins (the same leftmost-occurrence
+  // search as glob_fn, without the per-lane word loop that made the kernel
+  // scalar-issue bound: 2.1e8 SALU against 6.0e7 VALU instructions per pass on C2).
+  std::map<uint32_t, uint32_t> bslot;  // byte -> slot of bm[]
+  std::map<uint32_t, std::set<uint32_t>> glob_bytes;  // atom -> bytes its middle segments search
+  std::set<uint32_t> qglobs_done, qatoms_done, qpreds_done;
+  static constexpr uint32_t kMaxBSlots = 48;
+
+  // first literal byte of segment `sg` and its offset in the segment (-1: all '?')
+  std::pair<int32_t, uint32_t> seg_key(const GSeg& sg) const {
+    for (uint32_t q = 0; q < sg.len; q++) {
+      const GWord& gw = ps.gwords[sg.wfirst + q / 4];
+      if ((gw.mask >> (8 * (q % 4))) & 0xFFu) return {(int32_t)q, (gw.w >> (8 * (q % 4))) & 0xFFu};
+    }
+    return {-1, 0u};
+  }
+
+  void qglob_fn(uint32_t ai) {
+    if (!qglobs_done.insert(ai).second) return;
+    const Atom& A = ps.atoms[ai];
+    std::ostringstream& q = o;
+    // branch-free: every step folds into `ok` (indices clamped so a failed step reads in
+    // bounds); only a segment whose leftmost candidate fails verification loops over the rest
+    q << "__device__ __forceinline__ bool q_glob_" << ai
+      << "(const uint32_t* w, const uint32_t* lw, const uint64_t* bm, uint32_t sl, bool ascii, "
+         "const uint8_t* __restrict__ pstr) {\n";
+    const uint32_t fl = A.gflags;
+    if (fl & G_ALL) { q << "  return true;\n}\n"; return; }
+    if (fl & G_EMPTY) { q << "  return sl == 0u;\n}\n"; return; }
+    if (fl & G_HASQ)
+      q << "  if (!ascii) return kv_glob(pstr + " << u32(A.s_off) << ", " << u32(A.s_len & 0x7FFFFFFFu)
+        << ", (const uint8_t*)lw, sl);\n";
+    const uint32_t n = A.gcount;
+    const GSeg* segs = ps.gsegs.data() + A.gfirst;
+    uint32_t i0 = 0, i1 = n;
+    q << "  const uint32_t* base = lw;\n  bool ok = sl >= " << u32(A.gmin) << ";\n  uint32_t pos = 0u, end = sl;\n";
+    auto prefix_expr = [&](const GSeg& sg) {  // aligned compare at 0 from the registers
+      std::ostringstream e;
+      e << "((0u";
+      for (uint32_t i = 0; i < (sg.len + 3) / 4; i++) {
+        const GWord& g = ps.gwords[sg.wfirst + i];
+        if (g.mask) e << " | ((w[" << i << "] ^ " << hex32(g.w) << ") & " << hex32(g.mask) << ")";
+      }
+      e << ") == 0u)";
+      return e.str();
+    };
+    if (!(fl & G_LEAD)) {
+      const GSeg& s0 = segs[0];
+      if (n == 1 && !(fl & G_TRAIL)) {
+        q << "  return (sl == " << u32(s0.len) << ") & " << prefix_expr(s0) << ";\n}\n";
+        return;
+      }
+      q << "  ok &= " << prefix_expr(s0) << ";\n  pos = " << u32(s0.len) << ";\n";
+      i0 = 1;
+    }
+    if (!(fl & G_TRAIL)) {
+      const GSeg& st = segs[n - 1];
+      q << "  { const bool fit_ = ok & (end >= pos + " << u32(st.len) << ");\n"
+        << "    const uint32_t ks_ = fit_ ? end - " << u32(st.len) << " : 0u;\n"
+        << "    ok = fit_ & " << seg_expr(st, "ks_", false) << ";\n"
+        << "    end = ks_; }\n";
+      i1 = n - 1;
+    }
+    for (uint32_t i = i0; i < i1; i++) {
+      const GSeg& sg = segs[i];
+      const auto [j, cb] = seg_key(sg);
+      if (j < 0) {  // all-'?' segment: its leftmost occurrence is pos itself
+        q << "  ok &= end >= pos + " << u32(sg.len) << ";\n  pos += " << u32(sg.len) << ";\n";
+        continue;
+      }
+      auto it = bslot.find(cb);
+      if (it == bslot.end() && bslot.size() < kMaxBSlots) it = bslot.emplace(cb, (uint32_t)bslot.size()).first;
+      const std::string mask = it != bslot.end() ? "bm[" + u32(it->second) + "]" : "kv_bmask(w, " + hex32(cb * 0x01010101u) + ")";
+      if (it != bslot.end()) glob_bytes[ai].insert(cb);
+      // candidates p in [plo, phi] (phi <= 63: end <= sl <= 64 and j < len)
+      q << "  { ok &= end >= pos + " << u32(sg.len) << ";\n"
+        << "    const uint32_t plo = ok ? pos + " << u32(j) << " : 0u, phi = ok ? end - " << u32(sg.len) << " + " << u32(j)
+        << " : 0u;\n"
+        << "    uint64_t cm = ok ? " << mask << " & (~0ull << plo) & (~0ull >> (63u - phi)) : 0ull;\n"
+        << "    uint32_t kf = cm ? (uint32_t)__builtin_ctzll(cm) - " << u32(j) << " : 0u;\n"
+        << "    bool found = (cm != 0ull) & " << seg_expr(sg, "kf", false) << ";\n"
+        << "    cm &= cm - 1ull;\n"
+        << "    if (!found && cm) {\n"
+        << "      while (cm) {\n"
+        << "        const uint32_t k = (uint32_t)__builtin_ctzll(cm) - " << u32(j) << "; cm &= cm - 1ull;\n"
+        << "        if (" << seg_expr(sg, "k", false) << ") { kf = k; found = true; break; }\n"
+        << "      }\n"
+        << "    }\n"
+        << "    ok &= found;\n"
+        << "    pos = kf + " << u32(sg.len) << "; }\n";
+    }
+    q << "  (void)pos; (void)end; (void)base;\n  return ok;\n}\n";
+  }
+
+  void qatom_fn(uint32_t ai) {
+    if (!qatoms_done.insert(ai).second) return;
+    const Atom& A = ps.atoms[ai];
+    atom_fn(ai);
+    if (A.kind == AT_GLOB_E || A.kind == AT_GLOB_N) qglob_fn(ai);
+    o << "__device__ __forceinline__ bool q_atom_" << ai
+      << "(const Val* __restrict__ V, const uint8_t* __restrict__ S, const uint32_t* w, const uint32_t* lw, "
+         "const uint64_t* bm, const uint8_t* __restrict__ pstr, uint32_t type, const Node& n) {\n";
+    switch (A.kind) {
+      case AT_GLOB_E:
+        o << "  const bool r = q_glob_" << ai << "(w, lw, bm, n.c & NC_LEN_MASK, (n.c & NC_ASCII_E) != 0u, pstr);\n"
+          << "  return (type != NT_MAP) & (type != NT_ARR) & (type != NT_NULL) & " << (A.op == CO_NE ? "!r" : "r") << ";\n";
+        break;
+      case AT_GLOB_N:
+        o << "  if (type != NT_FLOAT && type != NT_MAP && type != NT_ARR && type != NT_BOOL && type != NT_NULL)\n"
+          << "    return q_glob_" << ai << "(w, lw, bm, n.c & NC_LEN_MASK, (n.c & NC_ASCII_E) != 0u, pstr);\n"
+          << "  return g_atom_" << ai << "(V, S, (const uint8_t*)lw, pstr, type, n);\n";
+        break;
+      default:
+        o << "  return g_atom_" << ai << "(V, S, (const uint8_t*)lw, pstr, type, n);\n";
+        break;
+    }
+    o << "}\n";
+  }
+
+  // the row's predicates on the register copy; non-string predicates are the g_pred ones
+  void qpred_fn(uint32_t pi) {
+    if (!qpreds_done.insert(pi).second) return;
+    const Pred& pr = ps.preds[pi];
+    if (pr.kind == PK_STRING)
+      for (uint32_t a = pr.first; a < pr.first + pr.count; a++) {
+        const Alt& al = ps.alts[a];
+        for (uint32_t c = al.first; c < al.first + al.count; c++) {
+          qatom_fn(ps.conjs[c].a0);
+          if (ps.conjs[c].kind != CJ_ATOM) qatom_fn(ps.conjs[c].a1);
+        }
+      }
+    o << "__device__ __forceinline__ bool q_pred_" << pi
+      << "(const Val* __restrict__ V, const uint8_t* __restrict__ S, const uint32_t* w, const uint32_t* lw, "
+         "const uint64_t* bm, const uint8_t* __restrict__ pstr, uint32_t type, const Node& n) {\n";
+    if (pr.kind != PK_STRING) {
+      o << "  return g_pred_" << pi << "(V, S, (const uint8_t*)lw, pstr, type, n);\n}\n";
+      return;
+    }
+    // every alternative and conjunct evaluated (straight-line atoms), combined without branches
+    o << "  return false";
+    for (uint32_t a = pr.first; a < pr.first + pr.count; a++) {
+      const Alt& al = ps.alts[a];
+      o << "\n    | (true";
+      for (uint32_t c = al.first; c < al.first + al.count; c++) {
+        const Conj& cj = ps.conjs[c];
+        auto call = [&](uint32_t at) { return "q_atom_" + std::to_string(at) + "(V, S, w, lw, bm, pstr, type, n)"; };
+        if (cj.kind == CJ_INRANGE) o << " & (" << call(cj.a0) << " & " << call(cj.a1) << ")";
+        else if (cj.kind == CJ_NOTINRANGE) o << " & (" << call(cj.a0) << " | " << call(cj.a1) << ")";
+        else o << " & " << call(cj.a0);
+      }
+      o << ")";
+    }
+    o << ";\n}\n";
+  }
+
+  // bytes whose masks the q_pred of `pi` reads
+  void pred_bytes(uint32_t pi, std::set<uint32_t>* out) {
+    const Pred& pr = ps.preds[pi];
+    if (pr.kind != PK_STRING) return;
+    for (uint32_t a = pr.first; a < pr.first + pr.count; a++) {
+      const Alt& al = ps.alts[a];
+      for (uint32_t c = al.first; c < al.first + al.count; c++) {
+        for (uint32_t at : {ps.conjs[c].a0, ps.conjs[c].kind != CJ_ATOM ? ps.conjs[c].a1 : ps.conjs[c].a0}) {
+          auto it = glob_bytes.find(at);
+          if (it != glob_bytes.end()) out->insert(it->second.begin(), it->second.end());
+        }
+      }
+    }
   }
 
   // ---------------------------------------------------------------- atoms / predicates
@@ -379,6 +558,94 @@ struct Gen {
   };
 
   void ptab_kernel() {
+    // register-path predicates (helpers: emitted before the kernel text)
+    if (ptab_regs)
+      for (uint32_t k = 0; k < mpreds.size(); k++) qpred_fn(mpreds[k]);
+    if (!ptab_regs) {  // KVGPU_PTAB=words: the per-glob word loops of round 1 (A/B runs)
+      ptab_kernel_words();
+      return;
+    }
+    KernelText kt(*this, "kvj_ptab");
+    o << "extern \"C\" __global__ __launch_bounds__(KV_WG) void kvj_ptab(const DevPS* __restrict__ Pp, "
+         "const Val* __restrict__ V, const uint8_t* __restrict__ S, uint32_t NV, uint32_t* __restrict__ PT) {\n"
+      << "  const uint32_t v = blockIdx.x * KV_WG + threadIdx.x;\n"
+      << "  if (v >= NV) return;\n"
+      << "  // Vals are numbered grouped by class (kvingest.cpp val_order_key): most waves\n"
+      << "  // are uniform in vc, and a wave no predicate of its row applies to stops here\n"
+      << "  const uint32_t vc = V[v].cls;\n"
+      << "  uint32_t rm = 0u;\n"
+      << "  switch (blockIdx.y) {\n";
+    auto pm = [&](uint32_t k) { auto it = pmask.find(mpreds[k]); return it == pmask.end() ? 0xFFFFFFFFu : it->second; };
+    for (uint32_t k0 = 0; k0 < mpreds.size(); k0 += kPtabRow) {
+      const uint32_t k1 = (uint32_t)std::min<size_t>(k0 + kPtabRow, mpreds.size());
+      uint32_t wm = 0;
+      for (uint32_t q = k0; q < k1; q++) wm |= pm(q);
+      o << "    case " << (k0 / kPtabRow) << "u: rm = " << u32(wm) << "; break;\n";
+    }
+    o << "    default: break;\n  }\n"
+      << "  uint32_t w = 0u;\n"
+      << "  if (" << (getenv("KVGPU_PTAB_EARLY") && getenv("KVGPU_PTAB_EARLY")[0] == '0' ? "true" : "vc & rm") << ") {\n"
+      << "  const uint8_t* __restrict__ pstr = Pp->pstr;\n"
+      << "  const Val& val = V[v];\n"
+      << "  const uint32_t type = val.type;\n"
+      << "  Node n{type, v, val.e_off, val.e_len};\n"
+      << "  if (val.flags & VF_ASCII_E) n.c |= NC_ASCII_E;\n"
+      << "  if (val.flags & VF_BOOLV) n.c |= NC_BOOLV;\n"
+      << "  if (val.flags & VF_NILLIKE) n.c |= NC_NILLIKE;\n"
+      << "  const uint8_t* __restrict__ E = S + val.e_off;\n"
+      // values of <= 64 bytes: 16 words in registers (loads clamped to the word after the
+      // string, which the word-wise readers already touch) and an LDS copy of 17 words
+      // (odd stride: no bank conflicts) for the reads at a per-lane offset
+      << "  __shared__ uint32_t lds_e[KV_WG * 17];\n"
+      << "  uint32_t* lw = lds_e + threadIdx.x * 17u;\n"
+      << "  const bool fast = val.e_len <= 64u;\n"
+      << "  uint32_t sw[16];\n"
+      << "  if (fast) {\n"
+      << "    const uint32_t* __restrict__ src = (const uint32_t*)E;\n"
+      << "    const uint32_t lastw = (val.e_len + 3u) >> 2;\n"
+      << "#pragma unroll\n"
+      << "    for (uint32_t i = 0; i < 16u; i++) sw[i] = src[i < lastw ? i : lastw];\n"
+      << "#pragma unroll\n"
+      << "    for (uint32_t i = 0; i < 16u; i++) lw[i] = sw[i];\n"
+      << "    lw[16] = src[lastw];\n"
+      << "  }\n"
+      << "  switch (blockIdx.y) {\n";
+    for (uint32_t k0 = 0; k0 < mpreds.size(); k0 += kPtabRow) {
+      const uint32_t k1 = (uint32_t)std::min<size_t>(k0 + kPtabRow, mpreds.size());
+      std::set<uint32_t> bytes;
+      for (uint32_t k = k0; k < k1; k++) pred_bytes(mpreds[k], &bytes);
+      o << "    case " << (k0 / kPtabRow) << "u:\n      if (fast) {\n";
+      if (!bytes.empty()) {
+        o << "        uint64_t bm[" << kMaxBSlots << "];\n";
+        for (uint32_t c : bytes)
+          o << "        bm[" << bslot.at(c) << "] = kv_bmask(sw, " << hex32(c * 0x01010101u) << ");\n";
+      } else {
+        o << "        const uint64_t* bm = nullptr;\n";
+      }
+      // predicates of one position class share one test (uniform in most waves)
+      for (uint32_t k = k0; k < k1;) {
+        uint32_t ke = k;
+        while (ke < k1 && pm(ke) == pm(k)) ke++;
+        o << "        if (vc & " << u32(pm(k)) << ") {\n";
+        for (uint32_t q = k; q < ke; q++)
+          o << "          w |= q_pred_" << mpreds[q] << "(V, S, sw, lw, bm, pstr, type, n) ? " << u32(1u << (q % kPtabRow))
+            << " : 0u;\n";
+        o << "        }\n";
+        k = ke;
+      }
+      o << "      } else {\n";
+      for (uint32_t k = k0; k < k1; k++)
+        o << "        if ((vc & " << u32(pm(k)) << ") && g_pred_" << mpreds[k] << "(V, S, E, pstr, type, n)) w |= "
+          << u32(1u << (k % kPtabRow)) << ";\n";
+      o << "      }\n      break;\n";
+    }
+    o << "    default: break;\n  }\n  }\n"
+      << (kPtabRow == 32 ? "  PT[(size_t)blockIdx.y * NV + v] = w;\n}\n\n"
+                         : "  // row y = bits [16 (y % 2), +16) of table word y / 2 (little-endian u16 halves)\n"
+                           "  ((uint16_t*)PT)[((size_t)(blockIdx.y >> 1) * NV + v) * 2u + (blockIdx.y & 1u)] = (uint16_t)w;\n}\n\n");
+  }
+
+  void ptab_kernel_words() {
     KernelText kt(*this, "kvj_ptab");
     o << "extern \"C\" __global__ __launch_bounds__(KV_WG) void kvj_ptab(const DevPS* __restrict__ Pp, "
          "const Val* __restrict__ V, const uint8_t* __restrict__ S, uint32_t NV, uint32_t* __restrict__ PT) {\n"
@@ -1454,7 +1721,7 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   for (size_t i = 0; i < defs.size(); i++) def_index[defs[i].first] = i;
   auto refs = [&](const std::string& text, std::vector<size_t>* out_ids) {
     static const char* prefixes[] = {"g_glob_", "g_atom_", "g_pred_", "m_pred_", "g_blk_", "g_match_", "g_rule_",
-                                     "g_dleaf_"};
+                                     "g_dleaf_", "q_glob_", "q_atom_", "q_pred_"};
     for (const char* pf : prefixes) {
       const size_t pl = strlen(pf);
       for (size_t q = text.find(pf); q != std::string::npos; q = text.find(pf, q + pl)) {

@@ -20,6 +20,7 @@ void make_shard(const Batch& b, uint64_t lo, uint64_t hi, Batch* out) {
     throw std::runtime_error("shard: range must start at a multiple of 64 resources");
   Batch& s = *out;
   s = Batch();
+  s.pin_store();
   const uint64_t row_lo = lo < b.res.size() ? b.res[lo].root : b.n_rows;
   const uint64_t row_hi = hi < b.res.size() ? b.res[hi].root : b.n_rows;
   s.n_rows = row_hi - row_lo;
@@ -30,6 +31,9 @@ void make_shard(const Batch& b, uint64_t lo, uint64_t hi, Batch* out) {
   auto scalar = [](uint32_t t) { return t == NT_BOOL || t == NT_INT || t == NT_FLOAT || t == NT_STR; };
   for (size_t i = 0; i < ncell; i++)
     if (scalar(node_type(src[i].kt))) vmap[src[i].a] = 0;
+  size_t nv = 0;
+  for (uint32_t m : vmap) nv += m == 0;
+  s.vals.reserve(nv);
   for (size_t v = 0; v < vmap.size(); v++)
     if (vmap[v] == 0) {
       vmap[v] = (uint32_t)s.vals.size();
