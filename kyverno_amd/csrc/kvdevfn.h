@@ -39,6 +39,18 @@ __device__ __forceinline__ T sld(const T* p) {
   return r;
 }
 
+// Load through a global-address-space pointer: the tables reached through DevPS /
+// DevBatch members are generic pointers, which the compiler lowers to flat loads
+// (waiting on both the vector-memory and the LDS/scalar counters).
+template <class T>
+__device__ __forceinline__ T kv_gld(const T* p, size_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return ((const __attribute__((address_space(1))) T*)p)[i];
+#else
+  return p[i];
+#endif
+}
+
 // node index of this lane's cell in a row (wave-group layout, kv_layout.h)
 __device__ __forceinline__ uint32_t ni(uint32_t row) { return row * KV_LANES + (threadIdx.x & (KV_LANES - 1)); }
 

@@ -477,7 +477,7 @@ struct Gen {
       o << "__device__ __forceinline__ bool m_pred_" << pi
         << "(const DevPS& P, const Val* __restrict__ V, const uint8_t* __restrict__ S, const uint8_t* __restrict__ pstr, "
            "uint32_t type, const Node& n) {\n"
-        << "  if (type - 1u < 4u) return (P.ptab[(size_t)" << (slot / 32) << "u * P.n_vals + n.a] >> " << (slot % 32)
+        << "  if (type - 1u < 4u) return (kv_gld(P.ptab, (size_t)" << (slot / 32) << "u * P.n_vals + n.a) >> " << (slot % 32)
         << "u) & 1u;\n"
         << "  return g_pred_" << pi << "(V, S, S + n.b, pstr, type, n);\n}\n";
     }
@@ -1207,12 +1207,12 @@ struct Gen {
               if (T->words.insert(wv).second) {
                 const std::string off = std::to_string(word) + "u * P.n_vals + ";
                 if (early_hoist)
-                  T->code.push_back("  const uint32_t " + wv + " = __builtin_amdgcn_perm(P.ptab[(size_t)" + off +
-                                    "(node_type(" + hn + ".kt) - 1u < 4u ? " + hn + ".a : 0u)], 0u, node_type(" + hn +
+                  T->code.push_back("  const uint32_t " + wv + " = __builtin_amdgcn_perm(kv_gld(P.ptab, (size_t)" + off +
+                                    "(node_type(" + hn + ".kt) - 1u < 4u ? " + hn + ".a : 0u)), 0u, node_type(" + hn +
                                     ".kt) - 1u < 4u ? 0x07060504u : 0x0c0c0c0cu);\n");
                 else
-                  T->code.push_back("  const uint32_t " + wv + " = node_type(" + hn + ".kt) - 1u < 4u ? P.ptab[(size_t)" +
-                                    off + hn + ".a] : 0u;\n");
+                  T->code.push_back("  const uint32_t " + wv + " = node_type(" + hn + ".kt) - 1u < 4u ? kv_gld(P.ptab, (size_t)" +
+                                    off + hn + ".a) : 0u;\n");
               }
               scalar = "(vt_ - 1u < 4u ? ((" + wv + " >> " + std::to_string(sl->second % 32) + "u) & 1u) != 0u : " +
                        "g_pred_" + std::to_string(in.a) + "(V, S, S + vn_.b, pstr, vt_, vn_))";
