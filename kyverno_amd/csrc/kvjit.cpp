@@ -557,34 +557,35 @@ struct Gen {
     }
   };
 
+  // predicates per kvj_ptab thread: all of them (one grid row) on the register path
+  uint32_t ptab_row_out() const { return ptab_regs ? std::max<uint32_t>(1u, (uint32_t)mpreds.size()) : kPtabRow; }
+
   void ptab_kernel() {
-    // register-path predicates (helpers: emitted before the kernel text)
-    if (ptab_regs)
-      for (uint32_t k = 0; k < mpreds.size(); k++) qpred_fn(mpreds[k]);
-    if (!ptab_regs) {  // KVGPU_PTAB=words: the per-glob word loops of round 1 (A/B runs)
+    if (!ptab_regs) {  // KVGPU_PTAB=words: 16-predicate grid rows with per-glob word loops (round 1; A/B runs)
       ptab_kernel_words();
       return;
     }
+    // register-path predicates (helpers: emitted before the kernel text)
+    for (uint32_t k = 0; k < mpreds.size(); k++) qpred_fn(mpreds[k]);
     KernelText kt(*this, "kvj_ptab");
+    const uint32_t nw = (uint32_t)((mpreds.size() + 31) / 32);
+    auto pm = [&](uint32_t k) { auto it = pmask.find(mpreds[k]); return it == pmask.end() ? 0xFFFFFFFFu : it->second; };
+    // predicates grouped by position class: a value runs the groups its class bits select
+    // (Vals are numbered by class, kvingest.cpp val_order_key, so the tests are uniform in
+    // most waves); one thread per value writes every word of its table column
+    std::map<uint32_t, std::vector<uint32_t>> groups;  // class mask -> memo slots
+    uint32_t all = 0;
+    for (uint32_t k = 0; k < mpreds.size(); k++) {
+      groups[pm(k)].push_back(k);
+      all |= pm(k);
+    }
     o << "extern \"C\" __global__ __launch_bounds__(KV_WG) void kvj_ptab(const DevPS* __restrict__ Pp, "
          "const Val* __restrict__ V, const uint8_t* __restrict__ S, uint32_t NV, uint32_t* __restrict__ PT) {\n"
       << "  const uint32_t v = blockIdx.x * KV_WG + threadIdx.x;\n"
       << "  if (v >= NV) return;\n"
-      << "  // Vals are numbered grouped by class (kvingest.cpp val_order_key): most waves\n"
-      << "  // are uniform in vc, and a wave no predicate of its row applies to stops here\n"
       << "  const uint32_t vc = V[v].cls;\n"
-      << "  uint32_t rm = 0u;\n"
-      << "  switch (blockIdx.y) {\n";
-    auto pm = [&](uint32_t k) { auto it = pmask.find(mpreds[k]); return it == pmask.end() ? 0xFFFFFFFFu : it->second; };
-    for (uint32_t k0 = 0; k0 < mpreds.size(); k0 += kPtabRow) {
-      const uint32_t k1 = (uint32_t)std::min<size_t>(k0 + kPtabRow, mpreds.size());
-      uint32_t wm = 0;
-      for (uint32_t q = k0; q < k1; q++) wm |= pm(q);
-      o << "    case " << (k0 / kPtabRow) << "u: rm = " << u32(wm) << "; break;\n";
-    }
-    o << "    default: break;\n  }\n"
-      << "  uint32_t w = 0u;\n"
-      << "  if (" << (getenv("KVGPU_PTAB_EARLY") && getenv("KVGPU_PTAB_EARLY")[0] == '0' ? "true" : "vc & rm") << ") {\n"
+      << "  uint32_t w[" << nw << "] = {};\n"
+      << "  if (vc & " << u32(all) << ") {\n"
       << "  const uint8_t* __restrict__ pstr = Pp->pstr;\n"
       << "  const Val& val = V[v];\n"
       << "  const uint32_t type = val.type;\n"
@@ -598,51 +599,41 @@ struct Gen {
       // (odd stride: no bank conflicts) for the reads at a per-lane offset
       << "  __shared__ uint32_t lds_e[KV_WG * 17];\n"
       << "  uint32_t* lw = lds_e + threadIdx.x * 17u;\n"
-      << "  const bool fast = val.e_len <= 64u;\n"
-      << "  uint32_t sw[16];\n"
-      << "  if (fast) {\n"
+      << "  if (val.e_len <= 64u) {\n"
+      << "    uint32_t sw[16];\n"
       << "    const uint32_t* __restrict__ src = (const uint32_t*)E;\n"
       << "    const uint32_t lastw = (val.e_len + 3u) >> 2;\n"
       << "#pragma unroll\n"
       << "    for (uint32_t i = 0; i < 16u; i++) sw[i] = src[i < lastw ? i : lastw];\n"
       << "#pragma unroll\n"
       << "    for (uint32_t i = 0; i < 16u; i++) lw[i] = sw[i];\n"
-      << "    lw[16] = src[lastw];\n"
-      << "  }\n"
-      << "  switch (blockIdx.y) {\n";
-    for (uint32_t k0 = 0; k0 < mpreds.size(); k0 += kPtabRow) {
-      const uint32_t k1 = (uint32_t)std::min<size_t>(k0 + kPtabRow, mpreds.size());
+      << "    lw[16] = src[lastw];\n";
+    for (auto& [m, ks] : groups) {
       std::set<uint32_t> bytes;
-      for (uint32_t k = k0; k < k1; k++) pred_bytes(mpreds[k], &bytes);
-      o << "    case " << (k0 / kPtabRow) << "u:\n      if (fast) {\n";
+      for (uint32_t k : ks) pred_bytes(mpreds[k], &bytes);
+      o << "    if (vc & " << u32(m) << ") {\n";
       if (!bytes.empty()) {
-        o << "        uint64_t bm[" << kMaxBSlots << "];\n";
-        for (uint32_t c : bytes)
-          o << "        bm[" << bslot.at(c) << "] = kv_bmask(sw, " << hex32(c * 0x01010101u) << ");\n";
+        o << "      uint64_t bm[" << kMaxBSlots << "];\n";
+        for (uint32_t c : bytes) o << "      bm[" << bslot.at(c) << "] = kv_bmask(sw, " << hex32(c * 0x01010101u) << ");\n";
       } else {
-        o << "        const uint64_t* bm = nullptr;\n";
+        o << "      const uint64_t* bm = nullptr;\n";
       }
-      // predicates of one position class share one test (uniform in most waves)
-      for (uint32_t k = k0; k < k1;) {
-        uint32_t ke = k;
-        while (ke < k1 && pm(ke) == pm(k)) ke++;
-        o << "        if (vc & " << u32(pm(k)) << ") {\n";
-        for (uint32_t q = k; q < ke; q++)
-          o << "          w |= q_pred_" << mpreds[q] << "(V, S, sw, lw, bm, pstr, type, n) ? " << u32(1u << (q % kPtabRow))
-            << " : 0u;\n";
-        o << "        }\n";
-        k = ke;
-      }
-      o << "      } else {\n";
-      for (uint32_t k = k0; k < k1; k++)
-        o << "        if ((vc & " << u32(pm(k)) << ") && g_pred_" << mpreds[k] << "(V, S, E, pstr, type, n)) w |= "
-          << u32(1u << (k % kPtabRow)) << ";\n";
-      o << "      }\n      break;\n";
+      for (uint32_t k : ks)
+        o << "      w[" << k / 32 << "] |= q_pred_" << mpreds[k] << "(V, S, sw, lw, bm, pstr, type, n) ? " << u32(1u << (k % 32))
+          << " : 0u;\n";
+      o << "    }\n";
     }
-    o << "    default: break;\n  }\n  }\n"
-      << (kPtabRow == 32 ? "  PT[(size_t)blockIdx.y * NV + v] = w;\n}\n\n"
-                         : "  // row y = bits [16 (y % 2), +16) of table word y / 2 (little-endian u16 halves)\n"
-                           "  ((uint16_t*)PT)[((size_t)(blockIdx.y >> 1) * NV + v) * 2u + (blockIdx.y & 1u)] = (uint16_t)w;\n}\n\n");
+    o << "  } else {\n";
+    for (auto& [m, ks] : groups) {
+      o << "    if (vc & " << u32(m) << ") {\n";
+      for (uint32_t k : ks)
+        o << "      if (g_pred_" << mpreds[k] << "(V, S, E, pstr, type, n)) w[" << k / 32 << "] |= " << u32(1u << (k % 32))
+          << ";\n";
+      o << "    }\n";
+    }
+    o << "  }\n  }\n";
+    for (uint32_t i = 0; i < nw; i++) o << "  PT[(size_t)" << i << "u * NV + v] = w[" << i << "];\n";
+    o << "}\n\n";
   }
 
   void ptab_kernel_words() {
@@ -1696,7 +1687,7 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
     g.ptab_kernel();
     out->memo_preds = g.mpreds;
     out->memo_words = (uint32_t)((g.mpreds.size() + 31) / 32);
-    out->ptab_row = g.kPtabRow;
+    out->ptab_row = g.ptab_row_out();
   }
   // Each kernel program = prelude + the helper functions it reaches + the kernel:
   // helpers (g_glob_/g_atom_/g_pred_/m_pred_/g_blk_/g_match_/g_rule_) are split at
