@@ -479,6 +479,7 @@ struct Gen {
            "uint32_t type, const Node& n) {\n"
         << "  if (type - 1u < 4u) return (kv_gld(P.ptab, (size_t)" << (slot / 32) << "u * P.n_vals + n.a) >> " << (slot % 32)
         << "u) & 1u;\n"
+        << "  __builtin_assume(type - 1u >= 4u);  // null / map / array: the string and number code is dead here\n"
         << "  return g_pred_" << pi << "(V, S, S + n.b, pstr, type, n);\n}\n";
     }
   }
@@ -1206,7 +1207,8 @@ struct Gen {
                                     off + hn + ".a) : 0u;\n");
               }
               scalar = "(vt_ - 1u < 4u ? ((" + wv + " >> " + std::to_string(sl->second % 32) + "u) & 1u) != 0u : " +
-                       "g_pred_" + std::to_string(in.a) + "(V, S, S + vn_.b, pstr, vt_, vn_))";
+                       "([&]() -> bool { __builtin_assume(vt_ - 1u >= 4u); return g_pred_" + std::to_string(in.a) +
+                       "(V, S, S + vn_.b, pstr, vt_, vn_); })())";
             }
           } else {
             w << "  { Node vn_{0u, 0u, 0u, 0u}; if (" << cd << " != ABSENT) vn_ = N[" << cd << "];\n";
