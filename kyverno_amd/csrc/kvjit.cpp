@@ -1652,11 +1652,32 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
     for (uint32_t ri = 0; ri < n; ri++)
       order.push_back({ps.rules[ri].route == 0 ? "0" + rule_signature(ps, ri) : "1", ri});
     std::stable_sort(order.begin(), order.end());
+    // chunks of chunk_rules rules; a run of rules with one signature (the same array walk and
+    // the same leaves: one set of hoisted loads, a few registers of state per rule) may grow
+    // to KVGPU_JIT_SIGCHUNK rules, so its array is walked fewer times
+    const char* sz = getenv("KVGPU_JIT_SIGCHUNK");
+    const uint32_t sigmax = std::max<uint32_t>(chunk_rules, sz ? (uint32_t)std::max(1, atoi(sz)) : chunk_rules);
     std::vector<JitChunk> chs;
-    for (uint32_t b = 0; b < n; b += chunk_rules) {
-      JitChunk ch;
-      for (uint32_t q = b; q < std::min(n, b + chunk_rules); q++) ch.rules.push_back(order[q].second);
-      chs.push_back(ch);
+    {
+      JitChunk cur;
+      std::string cur_sig;
+      bool uniform = true;
+      for (uint32_t q = 0; q < n; q++) {
+        const std::string& sig = order[q].first;
+        if (!cur.rules.empty()) {
+          const bool same = uniform && sig == cur_sig;
+          if (cur.rules.size() >= sigmax || (cur.rules.size() >= chunk_rules && !same)) {
+            chs.push_back(cur);
+            cur = JitChunk();
+            uniform = true;
+          } else if (sig != cur_sig) {
+            uniform = false;
+          }
+        }
+        if (cur.rules.empty()) cur_sig = sig;
+        cur.rules.push_back(order[q].second);
+      }
+      if (!cur.rules.empty()) chs.push_back(cur);
     }
     out->n_chunks = (uint32_t)chs.size();
     if (out->plan.empty()) {
