@@ -104,6 +104,36 @@ __device__ __forceinline__ uint64_t kv_bmask(const uint32_t* w, uint32_t c4) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// byte-position masks of values of <= 128 bytes (32 words): positions 0-63 in lo, 64-127 in hi
+struct KvM2 {
+  uint64_t lo, hi;
+};
+__device__ __forceinline__ KvM2 kv_bmask2(const uint32_t* w, uint32_t c4) { return {kv_bmask(w, c4), kv_bmask(w + 16, c4)}; }
+
+// candidate-mask helpers of the kvj_ptab register globs, on both mask types: the bits of m
+// in [plo, phi] (none when !ok; plo <= phi < mask width when ok), non-empty test, lowest
+// set position, lowest bit cleared
+__device__ __forceinline__ uint64_t kv_mrange(uint64_t m, uint32_t plo, uint32_t phi, bool ok) {
+  return ok ? m & (~0ull << plo) & (~0ull >> (63u - phi)) : 0ull;
+}
+__device__ __forceinline__ bool kv_mnz(uint64_t m) { return m != 0ull; }
+__device__ __forceinline__ uint32_t kv_mctz(uint64_t m) { return (uint32_t)__builtin_ctzll(m); }
+__device__ __forceinline__ uint64_t kv_mpop(uint64_t m) { return m & (m - 1ull); }
+__device__ __forceinline__ KvM2 kv_mrange(KvM2 m, uint32_t plo, uint32_t phi, bool ok) {
+  if (!ok) return {0ull, 0ull};
+  const uint64_t lo_lo = plo < 64u ? ~0ull << plo : 0ull, lo_hi = phi < 64u ? ~0ull >> (63u - phi) : ~0ull;
+  const uint64_t hi_lo = plo <= 64u ? ~0ull : ~0ull << (plo - 64u), hi_hi = phi >= 64u ? ~0ull >> (127u - phi) : 0ull;
+  return {m.lo & lo_lo & lo_hi, m.hi & hi_lo & hi_hi};
+}
+__device__ __forceinline__ bool kv_mnz(KvM2 m) { return (m.lo | m.hi) != 0ull; }
+__device__ __forceinline__ uint32_t kv_mctz(KvM2 m) {
+  return m.lo ? (uint32_t)__builtin_ctzll(m.lo) : 64u + (uint32_t)__builtin_ctzll(m.hi);
+}
+__device__ __forceinline__ KvM2 kv_mpop(KvM2 m) {
+  if (m.lo) return {m.lo & (m.lo - 1ull), m.hi};
+  return {0ull, m.hi & (m.hi - 1ull)};
+}
+
 // segment (uniform words) == value bytes [k, k+len) ; value base 4-byte aligned
 __device__ __forceinline__ bool seg_at(const GWord* __restrict__ wd, uint32_t len, const uint32_t* __restrict__ base,
                                        uint32_t k) {

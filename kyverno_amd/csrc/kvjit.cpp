@@ -213,8 +213,18 @@ struct Gen {
   // scalar-issue bound: 2.1e8 SALU against 6.0e7 VALU instructions per pass on C2).
   std::map<uint32_t, uint32_t> bslot;  // byte -> slot of bm[]
   std::map<uint32_t, std::set<uint32_t>> glob_bytes;  // atom -> bytes its middle segments search
-  std::set<uint32_t> qglobs_done, qatoms_done, qpreds_done;
+  std::set<std::pair<char, uint32_t>> qglobs_done, qatoms_done, qpreds_done;
   static constexpr uint32_t kMaxBSlots = 48;
+  // register-path variants: values of <= 64 bytes (16 words, 64-bit masks, prefix q_) and
+  // of <= 128 bytes (32 words, two-word masks KvM2, prefix r_); the mask helpers
+  // (kv_mrange / kv_mctz / kv_mpop) are overloaded on the mask type
+  struct QV {
+    char pfx;
+    const char* mt;   // mask type
+    const char* bmk;  // mask builder
+    uint32_t words;
+  };
+  static constexpr QV kQ64{'q', "uint64_t", "kv_bmask", 16}, kQ128{'r', "KvM2", "kv_bmask2", 32};
 
   // first literal byte of segment `sg` and its offset in the segment (-1: all '?')
   std::pair<int32_t, uint32_t> seg_key(const GSeg& sg) const {
@@ -225,14 +235,19 @@ struct Gen {
     return {-1, 0u};
   }
 
-  void qglob_fn(uint32_t ai) {
-    if (!qglobs_done.insert(ai).second) return;
+  std::string qsig(const QV& v) const {
+    return std::string("(const Val* __restrict__ V, const uint8_t* __restrict__ S, const uint32_t* w, const uint32_t* lw, const ") +
+           v.mt + "* bm, const uint8_t* __restrict__ pstr, uint32_t type, const Node& n)";
+  }
+
+  void qglob_fn(uint32_t ai, const QV& v) {
+    if (!qglobs_done.insert({v.pfx, ai}).second) return;
     const Atom& A = ps.atoms[ai];
     std::ostringstream& q = o;
     // branch-free: every step folds into `ok` (indices clamped so a failed step reads in
     // bounds); only a segment whose leftmost candidate fails verification loops over the rest
-    q << "__device__ __forceinline__ bool q_glob_" << ai
-      << "(const uint32_t* w, const uint32_t* lw, const uint64_t* bm, uint32_t sl, bool ascii, "
+    q << "__device__ __forceinline__ bool " << v.pfx << "_glob_" << ai
+      << "(const uint32_t* w, const uint32_t* lw, const " << v.mt << "* bm, uint32_t sl, bool ascii, "
          "const uint8_t* __restrict__ pstr) {\n";
     const uint32_t fl = A.gflags;
     if (fl & G_ALL) { q << "  return true;\n}\n"; return; }
@@ -280,19 +295,20 @@ struct Gen {
       }
       auto it = bslot.find(cb);
       if (it == bslot.end() && bslot.size() < kMaxBSlots) it = bslot.emplace(cb, (uint32_t)bslot.size()).first;
-      const std::string mask = it != bslot.end() ? "bm[" + u32(it->second) + "]" : "kv_bmask(w, " + hex32(cb * 0x01010101u) + ")";
+      const std::string mask =
+          it != bslot.end() ? "bm[" + u32(it->second) + "]" : std::string(v.bmk) + "(w, " + hex32(cb * 0x01010101u) + ")";
       if (it != bslot.end()) glob_bytes[ai].insert(cb);
-      // candidates p in [plo, phi] (phi <= 63: end <= sl <= 64 and j < len)
+      // candidates p in [plo, phi] (phi < 4 * words: end <= sl and j < len)
       q << "  { ok &= end >= pos + " << u32(sg.len) << ";\n"
         << "    const uint32_t plo = ok ? pos + " << u32(j) << " : 0u, phi = ok ? end - " << u32(sg.len) << " + " << u32(j)
         << " : 0u;\n"
-        << "    uint64_t cm = ok ? " << mask << " & (~0ull << plo) & (~0ull >> (63u - phi)) : 0ull;\n"
-        << "    uint32_t kf = cm ? (uint32_t)__builtin_ctzll(cm) - " << u32(j) << " : 0u;\n"
-        << "    bool found = (cm != 0ull) & " << seg_expr(sg, "kf", false) << ";\n"
-        << "    cm &= cm - 1ull;\n"
-        << "    if (!found && cm) {\n"
-        << "      while (cm) {\n"
-        << "        const uint32_t k = (uint32_t)__builtin_ctzll(cm) - " << u32(j) << "; cm &= cm - 1ull;\n"
+        << "    " << v.mt << " cm = kv_mrange(" << mask << ", plo, phi, ok);\n"
+        << "    uint32_t kf = kv_mnz(cm) ? kv_mctz(cm) - " << u32(j) << " : 0u;\n"
+        << "    bool found = kv_mnz(cm) & " << seg_expr(sg, "kf", false) << ";\n"
+        << "    cm = kv_mpop(cm);\n"
+        << "    if (!found && kv_mnz(cm)) {\n"
+        << "      while (kv_mnz(cm)) {\n"
+        << "        const uint32_t k = kv_mctz(cm) - " << u32(j) << "; cm = kv_mpop(cm);\n"
         << "        if (" << seg_expr(sg, "k", false) << ") { kf = k; found = true; break; }\n"
         << "      }\n"
         << "    }\n"
@@ -302,22 +318,21 @@ struct Gen {
     q << "  (void)pos; (void)end; (void)base;\n  return ok;\n}\n";
   }
 
-  void qatom_fn(uint32_t ai) {
-    if (!qatoms_done.insert(ai).second) return;
+  void qatom_fn(uint32_t ai, const QV& v) {
+    if (!qatoms_done.insert({v.pfx, ai}).second) return;
     const Atom& A = ps.atoms[ai];
     atom_fn(ai);
-    if (A.kind == AT_GLOB_E || A.kind == AT_GLOB_N) qglob_fn(ai);
-    o << "__device__ __forceinline__ bool q_atom_" << ai
-      << "(const Val* __restrict__ V, const uint8_t* __restrict__ S, const uint32_t* w, const uint32_t* lw, "
-         "const uint64_t* bm, const uint8_t* __restrict__ pstr, uint32_t type, const Node& n) {\n";
+    if (A.kind == AT_GLOB_E || A.kind == AT_GLOB_N) qglob_fn(ai, v);
+    const std::string g = std::string(1, v.pfx) + "_glob_" + std::to_string(ai);
+    o << "__device__ __forceinline__ bool " << v.pfx << "_atom_" << ai << qsig(v) << " {\n";
     switch (A.kind) {
       case AT_GLOB_E:
-        o << "  const bool r = q_glob_" << ai << "(w, lw, bm, n.c & NC_LEN_MASK, (n.c & NC_ASCII_E) != 0u, pstr);\n"
+        o << "  const bool r = " << g << "(w, lw, bm, n.c & NC_LEN_MASK, (n.c & NC_ASCII_E) != 0u, pstr);\n"
           << "  return (type != NT_MAP) & (type != NT_ARR) & (type != NT_NULL) & " << (A.op == CO_NE ? "!r" : "r") << ";\n";
         break;
       case AT_GLOB_N:
         o << "  if (type != NT_FLOAT && type != NT_MAP && type != NT_ARR && type != NT_BOOL && type != NT_NULL)\n"
-          << "    return q_glob_" << ai << "(w, lw, bm, n.c & NC_LEN_MASK, (n.c & NC_ASCII_E) != 0u, pstr);\n"
+          << "    return " << g << "(w, lw, bm, n.c & NC_LEN_MASK, (n.c & NC_ASCII_E) != 0u, pstr);\n"
           << "  return g_atom_" << ai << "(V, S, (const uint8_t*)lw, pstr, type, n);\n";
         break;
       default:
@@ -328,20 +343,18 @@ struct Gen {
   }
 
   // the row's predicates on the register copy; non-string predicates are the g_pred ones
-  void qpred_fn(uint32_t pi) {
-    if (!qpreds_done.insert(pi).second) return;
+  void qpred_fn(uint32_t pi, const QV& v) {
+    if (!qpreds_done.insert({v.pfx, pi}).second) return;
     const Pred& pr = ps.preds[pi];
     if (pr.kind == PK_STRING)
       for (uint32_t a = pr.first; a < pr.first + pr.count; a++) {
         const Alt& al = ps.alts[a];
         for (uint32_t c = al.first; c < al.first + al.count; c++) {
-          qatom_fn(ps.conjs[c].a0);
-          if (ps.conjs[c].kind != CJ_ATOM) qatom_fn(ps.conjs[c].a1);
+          qatom_fn(ps.conjs[c].a0, v);
+          if (ps.conjs[c].kind != CJ_ATOM) qatom_fn(ps.conjs[c].a1, v);
         }
       }
-    o << "__device__ __forceinline__ bool q_pred_" << pi
-      << "(const Val* __restrict__ V, const uint8_t* __restrict__ S, const uint32_t* w, const uint32_t* lw, "
-         "const uint64_t* bm, const uint8_t* __restrict__ pstr, uint32_t type, const Node& n) {\n";
+    o << "__device__ __forceinline__ bool " << v.pfx << "_pred_" << pi << qsig(v) << " {\n";
     if (pr.kind != PK_STRING) {
       o << "  return g_pred_" << pi << "(V, S, (const uint8_t*)lw, pstr, type, n);\n}\n";
       return;
@@ -353,7 +366,9 @@ struct Gen {
       o << "\n    | (true";
       for (uint32_t c = al.first; c < al.first + al.count; c++) {
         const Conj& cj = ps.conjs[c];
-        auto call = [&](uint32_t at) { return "q_atom_" + std::to_string(at) + "(V, S, w, lw, bm, pstr, type, n)"; };
+        auto call = [&](uint32_t at) {
+          return std::string(1, v.pfx) + "_atom_" + std::to_string(at) + "(V, S, w, lw, bm, pstr, type, n)";
+        };
         if (cj.kind == CJ_INRANGE) o << " & (" << call(cj.a0) << " & " << call(cj.a1) << ")";
         else if (cj.kind == CJ_NOTINRANGE) o << " & (" << call(cj.a0) << " | " << call(cj.a1) << ")";
         else o << " & " << call(cj.a0);
@@ -363,7 +378,7 @@ struct Gen {
     o << ";\n}\n";
   }
 
-  // bytes whose masks the q_pred of `pi` reads
+  // bytes whose masks the q_pred / r_pred of `pi` reads
   void pred_bytes(uint32_t pi, std::set<uint32_t>* out) {
     const Pred& pr = ps.preds[pi];
     if (pr.kind != PK_STRING) return;
@@ -567,7 +582,8 @@ struct Gen {
       return;
     }
     // register-path predicates (helpers: emitted before the kernel text)
-    for (uint32_t k = 0; k < mpreds.size(); k++) qpred_fn(mpreds[k]);
+    for (uint32_t k = 0; k < mpreds.size(); k++) qpred_fn(mpreds[k], kQ64);
+    for (uint32_t k = 0; k < mpreds.size(); k++) qpred_fn(mpreds[k], kQ128);
     KernelText kt(*this, "kvj_ptab");
     const uint32_t nw = (uint32_t)((mpreds.size() + 31) / 32);
     auto pm = [&](uint32_t k) { auto it = pmask.find(mpreds[k]); return it == pmask.end() ? 0xFFFFFFFFu : it->second; };
@@ -595,34 +611,39 @@ struct Gen {
       << "  if (val.flags & VF_BOOLV) n.c |= NC_BOOLV;\n"
       << "  if (val.flags & VF_NILLIKE) n.c |= NC_NILLIKE;\n"
       << "  const uint8_t* __restrict__ E = S + val.e_off;\n"
-      // values of <= 64 bytes: 16 words in registers (loads clamped to the word after the
-      // string, which the word-wise readers already touch) and an LDS copy of 17 words
-      // (odd stride: no bank conflicts) for the reads at a per-lane offset
-      << "  __shared__ uint32_t lds_e[KV_WG * 17];\n"
-      << "  uint32_t* lw = lds_e + threadIdx.x * 17u;\n"
-      << "  if (val.e_len <= 64u) {\n"
-      << "    uint32_t sw[16];\n"
-      << "    const uint32_t* __restrict__ src = (const uint32_t*)E;\n"
-      << "    const uint32_t lastw = (val.e_len + 3u) >> 2;\n"
-      << "#pragma unroll\n"
-      << "    for (uint32_t i = 0; i < 16u; i++) sw[i] = src[i < lastw ? i : lastw];\n"
-      << "#pragma unroll\n"
-      << "    for (uint32_t i = 0; i < 16u; i++) lw[i] = sw[i];\n"
-      << "    lw[16] = src[lastw];\n";
-    for (auto& [m, ks] : groups) {
-      std::set<uint32_t> bytes;
-      for (uint32_t k : ks) pred_bytes(mpreds[k], &bytes);
-      o << "    if (vc & " << u32(m) << ") {\n";
-      if (!bytes.empty()) {
-        o << "      uint64_t bm[" << kMaxBSlots << "];\n";
-        for (uint32_t c : bytes) o << "      bm[" << bslot.at(c) << "] = kv_bmask(sw, " << hex32(c * 0x01010101u) << ");\n";
-      } else {
-        o << "      const uint64_t* bm = nullptr;\n";
+      // values of <= 64 (<= 128) bytes: 16 (32) words in registers (loads clamped to the
+      // word after the string, which the word-wise readers already touch) and an LDS copy of
+      // 33 words (odd stride: no bank conflicts) for the reads at a per-lane offset; values
+      // are numbered by length bucket within their class, so a wave runs one of the paths
+      << "  __shared__ uint32_t lds_e[KV_WG * 33];\n"
+      << "  uint32_t* lw = lds_e + threadIdx.x * 33u;\n";
+    for (const QV* qv : {&kQ64, &kQ128}) {
+      const uint32_t W = qv->words;
+      o << (W == 16 ? "  if (val.e_len <= 64u) {\n" : "  } else if (val.e_len <= 128u) {\n")
+        << "    uint32_t sw[" << W << "];\n"
+        << "    const uint32_t* __restrict__ src = (const uint32_t*)E;\n"
+        << "    const uint32_t lastw = (val.e_len + 3u) >> 2;\n"
+        << "#pragma unroll\n"
+        << "    for (uint32_t i = 0; i < " << W << "u; i++) sw[i] = src[i < lastw ? i : lastw];\n"
+        << "#pragma unroll\n"
+        << "    for (uint32_t i = 0; i < " << W << "u; i++) lw[i] = sw[i];\n"
+        << "    lw[" << W << "] = src[lastw];\n";
+      for (auto& [m, ks] : groups) {
+        std::set<uint32_t> bytes;
+        for (uint32_t k : ks) pred_bytes(mpreds[k], &bytes);
+        o << "    if (vc & " << u32(m) << ") {\n";
+        if (!bytes.empty()) {
+          o << "      " << qv->mt << " bm[" << kMaxBSlots << "];\n";
+          for (uint32_t c : bytes)
+            o << "      bm[" << bslot.at(c) << "] = " << qv->bmk << "(sw, " << hex32(c * 0x01010101u) << ");\n";
+        } else {
+          o << "      const " << qv->mt << "* bm = nullptr;\n";
+        }
+        for (uint32_t k : ks)
+          o << "      w[" << k / 32 << "] |= " << qv->pfx << "_pred_" << mpreds[k] << "(V, S, sw, lw, bm, pstr, type, n) ? "
+            << u32(1u << (k % 32)) << " : 0u;\n";
+        o << "    }\n";
       }
-      for (uint32_t k : ks)
-        o << "      w[" << k / 32 << "] |= q_pred_" << mpreds[k] << "(V, S, sw, lw, bm, pstr, type, n) ? " << u32(1u << (k % 32))
-          << " : 0u;\n";
-      o << "    }\n";
     }
     o << "  } else {\n";
     for (auto& [m, ks] : groups) {
@@ -1735,7 +1756,7 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   for (size_t i = 0; i < defs.size(); i++) def_index[defs[i].first] = i;
   auto refs = [&](const std::string& text, std::vector<size_t>* out_ids) {
     static const char* prefixes[] = {"g_glob_", "g_atom_", "g_pred_", "m_pred_", "g_blk_", "g_match_", "g_rule_",
-                                     "g_dleaf_", "q_glob_", "q_atom_", "q_pred_"};
+                                     "g_dleaf_", "q_glob_", "q_atom_", "q_pred_", "r_glob_", "r_atom_", "r_pred_"};
     for (const char* pf : prefixes) {
       const size_t pl = strlen(pf);
       for (size_t q = text.find(pf); q != std::string::npos; q = text.find(pf, q + pl)) {
