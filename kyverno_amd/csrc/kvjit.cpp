@@ -90,6 +90,9 @@ struct Gen {
   // of one tree level issue together instead of one dependent wait per lookup;
   // KVGPU_JIT_HOIST=lazy places each just before its first use, for A/B runs
   bool early_hoist = !(getenv("KVGPU_JIT_HOIST") && std::string(getenv("KVGPU_JIT_HOIST")) == "lazy");
+  // fused array loops software-pipelined (next element's lookups issued before this
+  // element's rules); KVGPU_JIT_PIPE=1 enables, for A/B runs
+  bool pipe_loops = getenv("KVGPU_JIT_PIPE") && getenv("KVGPU_JIT_PIPE")[0] == '1';
   explicit Gen(const PolicySet& p) : ps(p) {}
 
   // call of leaf predicate `pi` on node `n` of type `t`
@@ -1466,11 +1469,48 @@ struct Gen {
         body << "  { // fused loop " << tag << " over " << key << " (" << grp.size() << " rules)\n"
              << "    uint32_t fn" << tag << " = 0u, ff" << tag << " = 0u;\n    if ((0u";
         for (RGen* gp : grp) body << " | rs" << gp->s;
-        body << ") & ACT_) { const Node an_ = " << arr_node << "; ff" << tag << " = an_.a; fn" << tag << " = an_.b; }\n"
-             << "    for (uint32_t fli" << tag << " = 0u; fli" << tag << " < fn" << tag << "; fli" << tag << "++) {\n"
-             << "      const uint32_t el" << tag << " = ni(ff" << tag << " + fli" << tag << ");\n"
-             << "      const Node eln" << tag << " = N[el" << tag << "];\n"
-             << T.flush() << bodies.str() << "    }\n";
+        body << ") & ACT_) { const Node an_ = " << arr_node << "; ff" << tag << " = an_.a; fn" << tag << " = an_.b; }\n";
+        if (!pipe_loops || !early_hoist || T.code.empty()) {
+          body << "    for (uint32_t fli" << tag << " = 0u; fli" << tag << " < fn" << tag << "; fli" << tag << "++) {\n"
+               << "      const uint32_t el" << tag << " = ni(ff" << tag << " + fli" << tag << ");\n"
+               << "      const Node eln" << tag << " = N[el" << tag << "];\n"
+               << T.flush() << bodies.str() << "    }\n";
+        } else {
+          // software-pipelined: the element node and the hoisted lookups of element i + 1 are
+          // issued before the rules run on element i (a second copy of the hoist statements
+          // under renamed variables, rotated at the end of the iteration), so one element's
+          // dependent loads overlap the previous element's compares instead of stalling the wave
+          const std::string hs = T.flush();
+          auto rename = [&](std::string t) {
+            auto repl = [&](const std::string& a, const std::string& b) {
+              for (size_t q = t.find(a); q != std::string::npos; q = t.find(a, q + b.size())) t.replace(q, a.size(), b);
+            };
+            repl(T.prefix, T.prefix + "n");
+            repl("eln" + tag, "elnX" + tag);
+            repl("el" + tag, "elX" + tag);
+            return t;
+          };
+          auto unconst = [&](std::string t) {  // word loads become assignable (rotated)
+            const std::string a = "const uint32_t " + T.prefix;
+            for (size_t q = t.find(a); q != std::string::npos; q = t.find(a, q + 1)) t.erase(q, 6);
+            return t;
+          };
+          body << "    uint32_t el" << tag << " = ni(ff" << tag << ");\n"
+               << "    Node eln" << tag << " = N[el" << tag << "];\n"
+               << unconst(hs)
+               << "    for (uint32_t fli" << tag << " = 0u; fli" << tag << " < fn" << tag << "; fli" << tag << "++) {\n"
+               << "      const uint32_t elX" << tag << " = ni(ff" << tag << " + (fli" << tag << " + 1u < fn" << tag
+               << " ? fli" << tag << " + 1u : fli" << tag << "));\n"
+               << "      const Node elnX" << tag << " = N[elX" << tag << "];\n"
+               << rename(hs) << bodies.str();
+          body << "      el" << tag << " = elX" << tag << "; eln" << tag << " = elnX" << tag << ";\n";
+          for (auto& [ex, hv] : T.vars) {
+            const std::string nidx = rename(hv.idx), nnode = rename(hv.node);
+            body << "      " << hv.idx << " = " << nidx << "; " << hv.node << " = " << nnode << ";\n";
+          }
+          for (const std::string& wv : T.words) body << "      " << wv << " = " << rename(wv) << ";\n";
+          body << "    }\n";
+        }
         for (RGen* gp : grp) body << "    rs" << gp->s << " &= ~ACT_;\n";
         body << "  }\n";
       }
