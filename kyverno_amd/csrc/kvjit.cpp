@@ -1093,6 +1093,8 @@ struct Gen {
   };
 
   HoistTable* gT = nullptr;  // global (root-derived) hoist table of the current chunk
+  HoistTable* shared_global = nullptr;  // the group kernel's table (KVGPU_JIT_SHARED_HOIST=1)
+  bool share_hoist = getenv("KVGPU_JIT_SHARED_HOIST") && getenv("KVGPU_JIT_SHARED_HOIST")[0] == '1';
 
   void emit_region(RGen& g, const Region& R, std::ostringstream& w) {
     const std::string& s = g.s;
@@ -1358,8 +1360,11 @@ struct Gen {
   std::string fused_block(const JitChunk& ch, uint32_t hbase) {
     const uint32_t nr = (uint32_t)ch.rules.size();
     std::vector<RGen> gs;
-    HoistTable global;
-    global.prefix = "g";
+    HoistTable local;
+    local.prefix = "g";
+    // group kernels may share one root-derived table over all their chunks (kernel-level
+    // declarations, loaded once per lane instead of once per chunk)
+    HoistTable& global = shared_global ? *shared_global : local;
     gT = &global;
     size_t K = 0;
     for (uint32_t ri : ch.rules) {
@@ -1415,7 +1420,7 @@ struct Gen {
         seg << "    default: goto " << R.se << ";\n  }\n" << w.str() << R.se << ":;\n";
         if (k == g.loops.size()) seg << store(g.ri);  // the rule has finished for every lane
       }
-      body << global.flush() << seg.str();
+      body << (shared_global ? std::string() : global.flush()) << seg.str();
       if (k == K) break;
       // fused loops of stage k: group rules by the symbolic array cursor
       std::map<std::string, std::vector<RGen*>> groups;
@@ -1580,10 +1585,14 @@ struct Gen {
   void group_kernel(const std::string& name, const std::vector<const JitChunk*>& chs, int waves) {
     std::vector<std::string> blocks;
     std::vector<uint32_t> rules;
+    HoistTable shared;
+    shared.prefix = "g";
+    if (share_hoist && early_hoist) shared_global = &shared;
     for (const JitChunk* c : chs) {
       blocks.push_back(fused_block(*c, (uint32_t)rules.size()));
       rules.insert(rules.end(), c->rules.begin(), c->rules.end());
     }
+    shared_global = nullptr;
     const uint32_t nr = (uint32_t)rules.size();
     KernelText kt(*this, name);
     o << "__device__ const uint32_t " << name << "_rules[" << nr << "] = {";
@@ -1607,7 +1616,8 @@ struct Gen {
       << "  const Res* __restrict__ R = B.res + (valid ? r : 0u);\n"
       << "  uint32_t root = ABSENT, rkind = KEY_NONE, rflags = 0u;\n"
       << "  if (valid) { root = ni(R->root); rkind = R->kind; rflags = R->flags; }\n"
-      << "  Node rootn{0u, 0u, 0u, 0u};\n  if (valid) rootn = N[root];\n";
+      << "  Node rootn{0u, 0u, 0u, 0u};\n  if (valid) rootn = N[root];\n"
+      << shared.flush();
     for (const std::string& b : blocks) o << "  {\n" << b << "  }\n";
     o << "  __syncthreads();\n"
       << "  for (uint32_t q = threadIdx.x; q < " << nr << "u * KV_HIST; q += KV_WG) {\n"
