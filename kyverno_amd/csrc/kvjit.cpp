@@ -999,6 +999,12 @@ struct Gen {
         << "    store_result(O, " << ri << "u, n_res, r, valid, st, e, &s_hist[" << (ri - ch.rule_begin) << "][0]);\n"
         << "  }\n";
     }
+    // KVGPU_JIT_NOATOMIC=1: no per-workgroup count flush (wrong counts; timing A/B only)
+    static const bool no_flush = getenv("KVGPU_JIT_NOATOMIC") && getenv("KVGPU_JIT_NOATOMIC")[0] == '1';
+    if (no_flush) {
+      o << "}\n\n";
+      return;
+    }
     o << "  __syncthreads();\n"
       << "  for (uint32_t q = threadIdx.x; q < " << nr << "u * KV_HIST; q += KV_WG) {\n"
       << "    const uint32_t v = (&s_hist[0][0])[q];\n"
@@ -1619,6 +1625,12 @@ struct Gen {
       << "  Node rootn{0u, 0u, 0u, 0u};\n  if (valid) rootn = N[root];\n"
       << shared.flush();
     for (const std::string& b : blocks) o << "  {\n" << b << "  }\n";
+    // KVGPU_JIT_NOATOMIC=1: no per-workgroup count flush (wrong counts; timing A/B only)
+    static const bool no_flush = getenv("KVGPU_JIT_NOATOMIC") && getenv("KVGPU_JIT_NOATOMIC")[0] == '1';
+    if (no_flush) {
+      o << "}\n\n";
+      return;
+    }
     o << "  __syncthreads();\n"
       << "  for (uint32_t q = threadIdx.x; q < " << nr << "u * KV_HIST; q += KV_WG) {\n"
       << "    const uint32_t v = (&s_hist[0][0])[q];\n"
