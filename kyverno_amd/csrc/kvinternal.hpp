@@ -5,6 +5,7 @@
 #include <new>
 #include <string>
 #include <type_traits>
+#include <utility>
 #include <tuple>
 #include <unordered_map>
 #include <vector>
@@ -217,6 +218,16 @@ struct StoreAlloc {
   void deallocate(T* p, size_t) {
     if (pinned && g_hostmem.give && g_hostmem.give(p)) return;
     free(p);
+  }
+  // resize() leaves trivially constructible elements uninitialised (the merge and the
+  // shard builder write every element; zero-filling 1.5 GB of cells was a serial pass)
+  template <class U>
+  void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) {
+    ::new ((void*)p) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new ((void*)p) U(std::forward<A>(a)...);
   }
   template <class U>
   bool operator==(const StoreAlloc<U>& o) const { return pinned == o.pinned; }
