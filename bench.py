@@ -92,6 +92,11 @@ def pmc_traffic(args) -> dict | None:
     rp = shutil.which("rocprofv3")
     if not rp:
         return None
+    # not when this process already runs under a profiler (its preloaded library has initialised
+    # the GPU here; a nested rocprofv3 would exec from a GPU-initialised process)
+    if "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ):
+        log("pmc: running under a profiler, in-run traffic skipped")
+        return None
     out = tempfile.mkdtemp(prefix="kvpmc.", dir=os.environ.get("TMPDIR", "/tmp"))
     passes = 3  # the child's first pass + --warmup 0 + --steps 2
     child = [sys.executable, "-u", os.path.abspath(__file__), "--config", args.config, "--n-res", str(args.n_res),
@@ -99,7 +104,9 @@ def pmc_traffic(args) -> dict | None:
              "--no-e2e", "--no-traffic"]
     vals = {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-        cmd = [rp, "--pmc", ctr, "--kernel-trace", "--stats", "-d", out, "-o", ctr, "--output-format", "csv", "--"] + child
+        launcher = [sys.executable, rp] if open(rp, "rb").read(2) == b"#!" else [rp]
+        cmd = launcher + ["--pmc", ctr, "--kernel-trace", "--stats", "-d", out, "-o", ctr, "--output-format", "csv",
+                          "--"] + child
         p = subprocess.Popen(cmd, cwd=out, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, start_new_session=True)
         try:
             _, err = p.communicate(timeout=240)

@@ -15,7 +15,7 @@ for spec in "$@"; do
   i=$((i+1))
   envs=""; [ "$spec" != "-" ] && envs=$(echo "$spec" | tr ',' ' ')
   (cd /tmp && env $envs timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/ab/p$i" -o run --output-format csv -- \
-     python -u "$R/bench.py" --config ${CFG:-c2} --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ${BENCH_ARGS} \
+     python -u "$R/bench.py" --config ${CFG:-c2} --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --no-traffic ${BENCH_ARGS} \
      > "$R/gpurun_out/ab/r$i.json" 2> "$R/gpurun_out/ab/r$i.err") || { echo "bench $spec failed"; tail -5 gpurun_out/ab/r$i.err; exit 1; }
   python - "$spec" "gpurun_out/ab/r$i.json" gpurun_out/ab/p$i <<'PY'
 import csv, glob, json, sys

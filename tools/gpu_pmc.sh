@@ -4,7 +4,7 @@ set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"; O="$R/gpurun_out/${OUT:-pmc}"; mkdir -p "$O"
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 cd /tmp
-ARGS="--no-cpu-baseline --steps 2 --warmup 0 --n-res ${NRES:-1000000} ${EXTRA}"
+ARGS="--no-cpu-baseline --no-traffic --steps 2 --warmup 0 --n-res ${NRES:-1000000} ${EXTRA}"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" \
            "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \

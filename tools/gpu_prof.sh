@@ -9,7 +9,7 @@ cd "$R"
 timeout -k 10 400 python -u bench.py ${BENCH_ARGS} > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err && \
 cd /tmp && \
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- \
-   python -u "$R/bench.py" --no-cpu-baseline --steps 5 --warmup 1 ${PROF_ARGS} > "$R/gpurun_out/bench_prof.json" 2> "$R/gpurun_out/bench_prof.err"
+   python -u "$R/bench.py" --no-cpu-baseline --no-traffic --steps 5 --warmup 1 ${PROF_ARGS} > "$R/gpurun_out/bench_prof.json" 2> "$R/gpurun_out/bench_prof.err"
 rc=$?
 cd "$R"
 echo "rc=$rc"; cat gpurun_out/bench_full.json; tail -3 gpurun_out/bench_full.err; cat gpurun_out/bench_prof.json
