@@ -515,7 +515,20 @@ DevBatchRes& dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
   if (it != bt->dev.end()) return *it->second;
   auto d = std::make_unique<DevBatchRes>();
   const Batch& b = bt->b;
-  d->nodes.upload(b.nodes, device);
+  if (!b.rmask.empty() && b.rmask.size() == b.n_rows && b.nodes.size() == b.n_rows * KV_LANES) {
+    // packed rows (merged batches): upload the non-zero cells, masks and row offsets, then
+    // expand to the wave-group layout on the device
+    DevBuf pc, rm, ro;
+    pc.upload(b.pcells, device);
+    rm.upload(b.rmask, device);
+    ro.upload(b.roff, device);
+    d->nodes.alloc(b.nodes.size() * sizeof(Node), device);
+    HIPCHK(launch_expand_rows((const Node*)pc.p, (const uint64_t*)rm.p, (const uint32_t*)ro.p, b.n_rows,
+                              (Node*)d->nodes.p, nullptr));
+    HIPCHK(hipStreamSynchronize(nullptr));
+  } else {
+    d->nodes.upload(b.nodes, device);
+  }
   d->vals.upload(b.vals, device);
   d->res.upload(b.res, device);
   d->kvs.upload(b.kvs, device);

@@ -35,4 +35,9 @@ constexpr uint32_t KV_SCOPE_LDS = 2048;     // scopes held in LDS (2048 x 8 x 4 
 hipError_t launch_scope_counts(const uint8_t* status, const uint32_t* scope, uint32_t n_res, uint32_t n_rules,
                                uint32_t n_scopes, unsigned long long* out, hipStream_t stream);
 
+// nodes[row][lane] = the packed cell of (row, lane) when bit `lane` of rmask[row] is set
+// (rank among the row's set bits, from roff[row]), else the zero cell (row padding)
+hipError_t launch_expand_rows(const Node* pcells, const uint64_t* rmask, const uint32_t* roff, uint64_t n_rows,
+                              Node* nodes, hipStream_t stream);
+
 }  // namespace kv

@@ -656,7 +656,13 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
   }
   if (H >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: string heap exceeds 4 GiB");
   if (R * KV_LANES >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: batch too large for 32-bit node indices");
-  b.pin_store();
+  b.pin_store(true);
+  std::vector<uint64_t> pcb(P + 1, 0);  // packed-cell base of each part (its non-zero cells)
+  for (size_t k = 0; k < P; k++) pcb[k + 1] = pcb[k] + parts[k].cells_used;
+  b.pcells.resize(pcb[P]);
+  b.rmask.resize(R);
+  b.roff.resize(R);
+  std::vector<std::string> perr(P);
   b.strs.assign(H, '\0');
   b.vals.resize(V);
   b.kvs.resize(K);
@@ -699,6 +705,28 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
         else if (t == NT_BOOL || t == NT_INT || t == NT_FLOAT || t == NT_STR) { nd.a = perm[nd.a]; nd.b += h; }
         out[i] = nd;
       }
+      // packed transfer form of the part's rows (remapping keeps zero cells zero and
+      // non-zero cells non-zero, so the part's count from ingest sizes its range)
+      uint64_t pc = pcb[k];
+      for (uint64_t row = 0; row < q.n_rows; row++) {
+        const Node* cells = out + row * KV_LANES;
+        uint64_t m = 0;
+        b.roff[r0 + row] = (uint32_t)pc;
+        for (uint32_t l = 0; l < KV_LANES; l++)
+          if (cells[l].kt | cells[l].a | cells[l].b | cells[l].c) {
+            if (pc >= pcb[k + 1]) {
+              perr[k] = "ingest: packed cell count mismatch";
+              return;
+            }
+            m |= 1ull << l;
+            b.pcells[pc++] = cells[l];
+          }
+        b.rmask[r0 + row] = m;
+      }
+      if (pc != pcb[k + 1]) {
+        perr[k] = "ingest: packed cell count mismatch";
+        return;
+      }
       for (size_t i = 0; i < q.res.size(); i++) {
         Res r = q.res[i];
         r.root += r0;
@@ -712,6 +740,8 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
       Batch().nodes.swap(q.nodes);
     });
   for (auto& t : th) t.join();
+  for (auto& e : perr)
+    if (!e.empty()) throw std::runtime_error(e);
 }
 
 }  // namespace

@@ -244,11 +244,23 @@ struct Batch {
   uint64_t cells_used = 0;           // populated cells (incl. absent-slot markers)
   StoreVec<kv::Val> vals;
   StoreVec<kv::Res> res;
-  // the store arrays in page-locked memory when g_hostmem provides it (merged batch, shards)
-  void pin_store() {
-    nodes = StoreVec<kv::Node>(StoreAlloc<kv::Node>(true));
+  // Transfer form of `nodes` (merged batches): the non-zero cells of every row in row
+  // order, a 64-bit lane mask per row and the first packed cell of each row. kv_validate
+  // uploads these and expands the rows on the device (kv_expand_rows_kernel), so the row
+  // padding of the wave-group layout (40+ % of the cells at C2) does not cross PCIe.
+  StoreVec<kv::Node> pcells;
+  StoreVec<uint64_t> rmask;
+  StoreVec<uint32_t> roff;
+  // the arrays that cross PCIe in page-locked memory when g_hostmem provides it: the
+  // merged batch uploads the packed rows (its padded `nodes` stay pageable), a shard its
+  // padded rows
+  void pin_store(bool packed_rows) {
+    nodes = StoreVec<kv::Node>(StoreAlloc<kv::Node>(!packed_rows));
     vals = StoreVec<kv::Val>(StoreAlloc<kv::Val>(true));
     res = StoreVec<kv::Res>(StoreAlloc<kv::Res>(true));
+    pcells = StoreVec<kv::Node>(StoreAlloc<kv::Node>(true));
+    rmask = StoreVec<uint64_t>(StoreAlloc<uint64_t>(true));
+    roff = StoreVec<uint32_t>(StoreAlloc<uint32_t>(true));
   }
   std::vector<kv::KV> kvs;
   std::string strs;                  // string heap

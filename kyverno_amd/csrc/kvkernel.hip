@@ -548,4 +548,30 @@ hipError_t launch_scope_counts(const uint8_t* status, const uint32_t* scope, uin
   return hipGetLastError();
 }
 
+// One wave per row of the wave-group layout: lane l takes its packed cell (the number of
+// set mask bits below l is its rank in the row) or the zero cell. Reads the packed cells
+// and masks once, writes every cell once (coalesced 1 KB per row).
+__global__ __launch_bounds__(KV_WG) void kv_expand_rows_kernel(const Node* __restrict__ pcells,
+                                                               const uint64_t* __restrict__ rmask,
+                                                               const uint32_t* __restrict__ roff, uint64_t n_rows,
+                                                               Node* __restrict__ nodes) {
+  const uint64_t row = (uint64_t)blockIdx.x * (KV_WG / KV_LANES) + threadIdx.x / KV_LANES;
+  if (row >= n_rows) return;
+  const uint32_t lane = threadIdx.x & (KV_LANES - 1);
+  const uint64_t m = rmask[row];
+  Node v{0u, 0u, 0u, 0u};
+  if ((m >> lane) & 1ull) v = pcells[roff[row] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))];
+  nodes[row * KV_LANES + lane] = v;
+}
+
+hipError_t launch_expand_rows(const Node* pcells, const uint64_t* rmask, const uint32_t* roff, uint64_t n_rows,
+                              Node* nodes, hipStream_t stream) {
+  if (n_rows == 0) return hipSuccess;
+  const uint64_t blocks = (n_rows + KV_WG / KV_LANES - 1) / (KV_WG / KV_LANES);
+  if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kv_expand_rows_kernel, dim3((uint32_t)blocks), dim3(KV_WG), 0, stream, pcells, rmask, roff, n_rows,
+                     nodes);
+  return hipGetLastError();
+}
+
 }  // namespace kv

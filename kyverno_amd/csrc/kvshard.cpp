@@ -20,7 +20,7 @@ void make_shard(const Batch& b, uint64_t lo, uint64_t hi, Batch* out) {
     throw std::runtime_error("shard: range must start at a multiple of 64 resources");
   Batch& s = *out;
   s = Batch();
-  s.pin_store();
+  s.pin_store(false);
   const uint64_t row_lo = lo < b.res.size() ? b.res[lo].root : b.n_rows;
   const uint64_t row_hi = hi < b.res.size() ? b.res[hi].root : b.n_rows;
   s.n_rows = row_hi - row_lo;
