@@ -123,7 +123,10 @@ def pmc_traffic(args) -> dict | None:
                                                     recursive=True))):
             for r in csv.DictReader(open(f)):
                 k = r.get("Kernel_Name", "")
-                if r["Counter_Name"] == ctr and k.startswith(("kv_", "kvj_", "kv::")) and "kv_rec_" not in k:
+                # the pass's kernels: not the record compaction of a fetch (kv_rec_*) nor the
+                # row expansion of the batch upload (kv_expand_rows), which run once per batch
+                if r["Counter_Name"] == ctr and k.startswith(("kv_", "kvj_", "kv::")) and "kv_rec_" not in k \
+                        and "kv_expand_rows" not in k:
                     agg[k] += float(r["Counter_Value"])
         if not agg:
             return None

@@ -23,7 +23,8 @@ def per_pass(csv_path, counter):
         k = r.get("Kernel_Name", "")
         # the pass's kernels; the record-compaction kernels (kv::kv_rec_*) run once per fetch,
         # outside the timed passes (the e2e leg of the same command)
-        if r["Counter_Name"] == counter and k.startswith(("kv_", "kvj_", "kv::")) and "kv_rec_" not in k:
+        if r["Counter_Name"] == counter and k.startswith(("kv_", "kvj_", "kv::")) and "kv_rec_" not in k \
+                and "kv_expand_rows" not in k:
             agg[(k, r["Dispatch_Id"])] += float(r["Counter_Value"])
     per_k = collections.defaultdict(list)
     for (k, _), v in agg.items():

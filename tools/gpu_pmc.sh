@@ -20,7 +20,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 agg = collections.defaultdict(float)  # (kernel, dispatch, counter) -> value summed over dimensions
 for r in rows:
     k = r.get("Kernel_Name", "")
-    if k.startswith(("kv_", "kvj_")):
+    if k.startswith(("kv_", "kvj_")) and "kv_expand_rows" not in k:
         agg[(k, r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
 per = collections.defaultdict(list)
 for (k, d, c), v in agg.items():
