@@ -653,6 +653,9 @@ __device__ __forceinline__ void store_result2(const DevOut& O, uint32_t ri, uint
     if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP))
       store_err(O, o, e.kind, e.flags, e.pn, e.key, e.res, e.i0, e.i1, e.i2, e.i3);
   }
+#ifdef KV_NOHIST
+  return;  // timing A/B only (KVGPU_JIT_NOHIST=1): no per-rule histogram
+#endif
   const uint64_t m_pass = __ballot(valid && st == ST_PASS), m_fail = __ballot(valid && st == ST_FAIL);
   const uint64_t m_nm = __ballot(valid && st == ST_NOMATCH);
   const uint64_t m_rest = __ballot(valid && st != ST_PASS && st != ST_FAIL && st != ST_NOMATCH);

@@ -1701,7 +1701,9 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   // KVGPU_JIT_STORE=lane: the per-lane-branch record store variant (8-wave A/B of DESIGN.md)
   const bool lane_store = getenv("KVGPU_JIT_STORE") && std::string(getenv("KVGPU_JIT_STORE")) == "lane";
   const std::string prelude =
-      std::string(lane_store ? "#define KV_STORE_LANE_BRANCH 1\n" : "") + kPrelude + "\nusing namespace kv;\n\n" +
+      std::string(lane_store ? "#define KV_STORE_LANE_BRANCH 1\n" : "") +
+      std::string(getenv("KVGPU_JIT_NOHIST") && getenv("KVGPU_JIT_NOHIST")[0] == '1' ? "#define KV_NOHIST 1\n" : "") +
+      kPrelude + "\nusing namespace kv;\n\n" +
       "__device__ __noinline__ bool kv_dleaf_impl(const DevBatch& B, const Node* __restrict__ N, uint32_t dp, Node vn);\n\n";
   // KVGPU_JIT_FUSE=0: one device function per rule (no cross-rule sharing), for A/B runs
   const char* fz = getenv("KVGPU_JIT_FUSE");
