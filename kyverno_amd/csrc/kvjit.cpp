@@ -1003,6 +1003,7 @@ struct Gen {
     static const bool no_flush = getenv("KVGPU_JIT_NOATOMIC") && getenv("KVGPU_JIT_NOATOMIC")[0] == '1';
     if (no_flush) {
       o << "}\n\n";
+      hist_lds = false;
       return;
     }
     o << "  __syncthreads();\n"
@@ -1100,6 +1101,11 @@ struct Gen {
 
   HoistTable* gT = nullptr;  // global (root-derived) hoist table of the current chunk
   HoistTable* shared_global = nullptr;  // the group kernel's table (KVGPU_JIT_SHARED_HOIST=1)
+  // per-rule histogram of a group kernel from its statuses staged in LDS (one byte per rule and
+  // lane, counted once at the end: kv_count_status_lds) instead of ballots + LDS atomics per
+  // rule and wave; KVGPU_JIT_HIST=ballot keeps the ballots (A/B runs)
+  bool hist_lds = false;
+  bool hist_lds_on = !(getenv("KVGPU_JIT_HIST") && std::string(getenv("KVGPU_JIT_HIST")) == "ballot");
   bool share_hoist = getenv("KVGPU_JIT_SHARED_HOIST") && getenv("KVGPU_JIT_SHARED_HOIST")[0] == '1';
 
   void emit_region(RGen& g, const Region& R, std::ostringstream& w) {
@@ -1398,8 +1404,12 @@ struct Gen {
       } else {
         k << "  { EState e_{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u};\n";
       }
-      k << "    store_result2(O, " << ri << "u, n_res, r, valid, rs" << s << " & 0xFFu, e_, &s_hist[" << (hbase + q)
-        << "][0]); }\n";
+      if (hist_lds)
+        k << "    store_result_lds(O, " << ri << "u, n_res, r, valid, rs" << s << " & 0xFFu, e_, (uint8_t*)s_stw + "
+          << u32((hbase + q) * 256u) << "); }\n";
+      else
+        k << "    store_result2(O, " << ri << "u, n_res, r, valid, rs" << s << " & 0xFFu, e_, &s_hist[" << (hbase + q)
+          << "][0]); }\n";
       return k.str();
     };
     std::ostringstream body;  // everything after the per-rule declarations
@@ -1594,6 +1604,9 @@ struct Gen {
     HoistTable shared;
     shared.prefix = "g";
     if (share_hoist && early_hoist) shared_global = &shared;
+    uint32_t nr_all = 0;
+    for (const JitChunk* c : chs) nr_all += (uint32_t)c->rules.size();
+    hist_lds = hist_lds_on && nr_all * 256u <= 48u * 1024u;  // <= 48 KB of status bytes
     for (const JitChunk* c : chs) {
       blocks.push_back(fused_block(*c, (uint32_t)rules.size()));
       rules.insert(rules.end(), c->rules.begin(), c->rules.end());
@@ -1612,11 +1625,13 @@ struct Gen {
       << "(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp, const Node* __restrict__ N, "
          "const Val* __restrict__ V, const uint8_t* __restrict__ S, DevOut O, uint32_t r0) {\n"
       << "  constexpr uint32_t FIN_ = " << u32(FIN) << ", ACT_ = " << u32(ACT) << ";\n"
-      << "  __shared__ uint32_t s_hist[" << nr << "][KV_HIST];\n"
-      << "  const DevPS& P = *Pp;\n  const DevBatch& B = *Bp;\n  const uint8_t* __restrict__ pstr = P.pstr;\n"
-      << "  for (uint32_t q = threadIdx.x; q < " << nr << "u * KV_HIST; q += KV_WG) (&s_hist[0][0])[q] = 0u;\n"
-      << "  __syncthreads();\n"
-      << "  const uint32_t r = r0 + blockIdx.x * KV_WG + threadIdx.x;\n"
+      << (hist_lds ? "  __shared__ uint32_t s_stw[" + std::to_string(nr * 256u / 4) + "];\n"
+                   : "  __shared__ uint32_t s_hist[" + std::to_string(nr) + "][KV_HIST];\n")
+      << "  const DevPS& P = *Pp;\n  const DevBatch& B = *Bp;\n  const uint8_t* __restrict__ pstr = P.pstr;\n";
+    if (!hist_lds)
+      o << "  for (uint32_t q = threadIdx.x; q < " << nr << "u * KV_HIST; q += KV_WG) (&s_hist[0][0])[q] = 0u;\n"
+        << "  __syncthreads();\n";
+    o << "  const uint32_t r = r0 + blockIdx.x * KV_WG + threadIdx.x;\n"
       << "  const uint32_t n_res = B.n_res;\n"
       << "  const bool valid = r < n_res;\n"
       << "  const Res* __restrict__ R = B.res + (valid ? r : 0u);\n"
@@ -1629,6 +1644,15 @@ struct Gen {
     static const bool no_flush = getenv("KVGPU_JIT_NOATOMIC") && getenv("KVGPU_JIT_NOATOMIC")[0] == '1';
     if (no_flush) {
       o << "}\n\n";
+      hist_lds = false;
+      return;
+    }
+    if (hist_lds) {
+      // one thread per rule counts its 256 status bytes and adds the non-zero counts
+      o << "  __syncthreads();\n"
+        << "  if (threadIdx.x < " << nr << "u) kv_count_status_lds(s_stw + threadIdx.x * (KV_WG / 4u), O.counts + (size_t)"
+        << name << "_rules[threadIdx.x] * KV_HIST);\n}\n\n";
+      hist_lds = false;
       return;
     }
     o << "  __syncthreads();\n"

@@ -36,6 +36,7 @@ static inline uint4 make_uint4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
 static inline void __syncthreads() {}
 static inline uint64_t __ballot(bool p) { return p ? (1ull << (threadIdx.x & 63)) : 0ull; }
 static inline int __popcll(uint64_t v) { return __builtin_popcountll(v); }
+static inline int __popc(uint32_t v) { return __builtin_popcount(v); }
 static inline uint32_t __shfl_xor(uint32_t v, int, int) { return v; }
 static inline uint32_t atomicAdd(uint32_t* p, uint32_t v) {
   uint32_t o = *p;
