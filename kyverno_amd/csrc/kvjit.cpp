@@ -1072,7 +1072,10 @@ struct Gen {
     } else if (early_hoist) {
       // the loaded node passes through v_perm (keep / zero) instead of a select,
       // which the compiler would turn into a branch around a narrowed reload
-      c << "  { const bool ok_ = node_type(" << p.node << ".kt) == NT_MAP && " << u32(a) << " < " << p.node << ".b; "
+      // below the root, a chunk's lookups run only on lanes where one of its rules matched
+      // (`ca_`): other lanes read cell 0 (one shared cached line) instead of their rows
+      const std::string guard = root_guard && p.node == "rootn" ? "ca_ && " : "";
+      c << "  { const bool ok_ = " << guard << "node_type(" << p.node << ".kt) == NT_MAP && " << u32(a) << " < " << p.node << ".b; "
         << "const uint32_t c_ = ok_ ? ni(" << p.node << ".a + " << u32(a) << ") : 0u; const Node t_ = N[c_]; "
         << "const bool hit_ = ok_ && node_type(t_.kt) != NT_ABSENT; const uint32_t m_ = hit_ ? 0x07060504u : 0x0c0c0c0cu; "
         << h.idx << " = hit_ ? c_ : ABSENT; " << h.node << " = Node{__builtin_amdgcn_perm(t_.kt, 0u, m_), "
@@ -1101,6 +1104,9 @@ struct Gen {
 
   HoistTable* gT = nullptr;  // global (root-derived) hoist table of the current chunk
   HoistTable* shared_global = nullptr;  // the group kernel's table (KVGPU_JIT_SHARED_HOIST=1)
+  // root lookups of a chunk guarded by its activity `ca_` (KVGPU_JIT_GUARD=0 disables, A/B)
+  bool root_guard = false;
+  bool guard_on = !(getenv("KVGPU_JIT_GUARD") && getenv("KVGPU_JIT_GUARD")[0] == '0');
   // per-rule histogram of a group kernel from its statuses staged in LDS (one byte per rule and
   // lane, counted once at the end: kv_count_status_lds) instead of ballots + LDS atomics per
   // rule and wave; KVGPU_JIT_HIST=ballot keeps the ballots (A/B runs)
@@ -1378,6 +1384,7 @@ struct Gen {
     // declarations, loaded once per lane instead of once per chunk)
     HoistTable& global = shared_global ? *shared_global : local;
     gT = &global;
+    root_guard = guard_on && early_hoist && !shared_global;
     size_t K = 0;
     for (uint32_t ri : ch.rules) {
       if (ps.rules[ri].route != 0) continue;
@@ -1591,6 +1598,12 @@ struct Gen {
     // rules of other routes are final after match / route
     for (uint32_t ri : ch.rules)
       if (ps.rules[ri].route != 0) k << store(ri);
+    if (root_guard) {  // some rule of the chunk still runs on this lane (rs below FIN)
+      k << "  const bool ca_ = ((FIN_";
+      for (uint32_t ri : ch.rules) k << " & rs_" << ri;
+      k << ") & FIN_) != FIN_;\n";
+    }
+    root_guard = false;
     k << body.str();
     return k.str();
   }
