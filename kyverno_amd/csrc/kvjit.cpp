@@ -1104,9 +1104,10 @@ struct Gen {
 
   HoistTable* gT = nullptr;  // global (root-derived) hoist table of the current chunk
   HoistTable* shared_global = nullptr;  // the group kernel's table (KVGPU_JIT_SHARED_HOIST=1)
-  // root lookups of a chunk guarded by its activity `ca_` (KVGPU_JIT_GUARD=0 disables, A/B)
+  // root lookups of a chunk guarded by its activity `ca_` (KVGPU_JIT_GUARD=1, A/B: C2 +1 %,
+  // C3 +3.6 %, C4 +0.6 % — the kernels are not bound by those loads)
   bool root_guard = false;
-  bool guard_on = !(getenv("KVGPU_JIT_GUARD") && getenv("KVGPU_JIT_GUARD")[0] == '0');
+  bool guard_on = getenv("KVGPU_JIT_GUARD") && getenv("KVGPU_JIT_GUARD")[0] == '1';
   // per-rule histogram of a group kernel from its statuses staged in LDS (one byte per rule and
   // lane, counted once at the end: kv_count_status_lds) instead of ballots + LDS atomics per
   // rule and wave; KVGPU_JIT_HIST=ballot keeps the ballots (A/B runs)
