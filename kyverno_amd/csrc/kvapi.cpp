@@ -780,8 +780,9 @@ struct DevSession {
   int device = 0;
   uint32_t mode = 0;
   uint64_t nrules = 0, nres = 0;
-  DevBuf fflags, pview, st, er8, er, cn, scope, scn, ptab, mtab;
+  DevBuf fflags, pview, st, er8, er, cn, scope, scn, ptab, mtab, part;
   DevBuf r_offs, r_tot, r_base, r_out8, r_outw, r_wide;  // record compaction (fetch)
+  uint32_t part_blocks = 0;
   uint32_t mt_words = 0, mt_entities = 0;
   uint32_t *mt_ns = nullptr, *mt_ann = nullptr, *mt_sel = nullptr;
   uint32_t nscopes = 0, nvals = 0;
@@ -852,6 +853,17 @@ struct DevSession {
     }
     cn.alloc(std::max<uint64_t>(nrules, 1) * KV_HIST * sizeof(unsigned long long), device);
     O.counts = (unsigned long long*)cn.p;
+    O.part = nullptr;
+    O.part_pitch = 0;
+    // specialized kernels: per-workgroup partial histograms summed by one reduce kernel
+    // instead of per-workgroup atomics on the counts (KVGPU_JIT_PARTIAL=0: atomics)
+    static const bool use_part = !(getenv("KVGPU_JIT_PARTIAL") && getenv("KVGPU_JIT_PARTIAL")[0] == '0');
+    if (use_part && dp.specialized() && nres && nrules) {
+      part_blocks = (uint32_t)((nres + KV_WG - 1) / KV_WG);
+      part.alloc((size_t)part_blocks * nrules * KV_HIST * sizeof(uint32_t), device);
+      O.part = (uint32_t*)part.p;
+      O.part_pitch = (uint32_t)(nrules * KV_HIST);
+    }
     if (mode & KV_MODE_SCOPES) {
       // scope of every resource = its namespace index in the batch namespace table
       std::vector<uint32_t> sc(nres);
@@ -877,8 +889,14 @@ struct DevSession {
     for (int i = 0; i < iters; i++) {
       HIPCHK(hipMemsetAsync(cn.p, 0, cn.n, stream));
       HIPCHK(launch_mtab((const DevPS*)pview.p, bview, mt_words, mt_entities, mt_ns, mt_ann, mt_sel, stream));
-      if (dps->specialized()) launch_specialized();
-      else HIPCHK(launch_validate((const DevPS*)pview.p, bview, (uint32_t)nres, O, 0, (uint32_t)nrules, stream));
+      if (dps->specialized()) {
+        // partial rows of rules whose kernel keeps the atomic histogram stay zero
+        if (O.part) HIPCHK(hipMemsetAsync(part.p, 0, part.n, stream));
+        launch_specialized();
+        if (O.part) HIPCHK(launch_part_reduce(O.part, part_blocks, O.part_pitch, O.counts, stream));
+      } else {
+        HIPCHK(launch_validate((const DevPS*)pview.p, bview, (uint32_t)nres, O, 0, (uint32_t)nrules, stream));
+      }
       if (mode & KV_MODE_SCOPES) {
         HIPCHK(hipMemsetAsync(scn.p, 0, scn.n, stream));
         HIPCHK(launch_scope_counts(O.status, (const uint32_t*)scope.p, (uint32_t)nres, (uint32_t)nrules, nscopes,

@@ -687,6 +687,33 @@ __device__ __forceinline__ void kv_count_status_lds(const uint32_t* w, unsigned 
   }
 }
 
+// histogram of one rule's KV_WG status bytes written whole (8 u32, zeros included) to the
+// workgroup's partial row (kv_part_reduce_kernel sums the rows)
+__device__ __forceinline__ void kv_count_status_part(const uint32_t* w, uint32_t* out) {
+  uint32_t c[KV_HIST] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  uint32_t cx = 0u;
+#pragma unroll 8
+  for (uint32_t i = 0; i < KV_WG / 4u; i++) {
+    const uint32_t x = w[i];
+    c[ST_PASS] += kv_count_bytes(x, 0x00000000u);
+    c[ST_FAIL] += kv_count_bytes(x, 0x01010101u);
+    c[ST_NOMATCH] += kv_count_bytes(x, 0x05050505u);
+    cx += kv_count_bytes(x, 0xFFFFFFFFu);
+  }
+  if (c[ST_PASS] + c[ST_FAIL] + c[ST_NOMATCH] + cx < (uint32_t)KV_WG) {
+    for (uint32_t i = 0; i < KV_WG / 4u; i++) {
+      const uint32_t x = w[i];
+      c[ST_WARN] += kv_count_bytes(x, 0x02020202u);
+      c[ST_ERROR] += kv_count_bytes(x, 0x03030303u);
+      c[ST_SKIP] += kv_count_bytes(x, 0x04040404u);
+      c[ST_CPU] += kv_count_bytes(x, 0x06060606u);
+    }
+  }
+  uint4* o = (uint4*)out;
+  o[0] = make_uint4(c[0], c[1], c[2], c[3]);
+  o[1] = make_uint4(c[4], c[5], c[6], c[7]);
+}
+
 // status + error record (FAIL/ERROR/SKIP) + per-rule histogram with the
 // common statuses counted by one ballot each (fused specialized kernels)
 __device__ __forceinline__ void store_result2(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, bool valid,

@@ -1664,8 +1664,12 @@ struct Gen {
     if (hist_lds) {
       // one thread per rule counts its 256 status bytes and adds the non-zero counts
       o << "  __syncthreads();\n"
-        << "  if (threadIdx.x < " << nr << "u) kv_count_status_lds(s_stw + threadIdx.x * (KV_WG / 4u), O.counts + (size_t)"
-        << name << "_rules[threadIdx.x] * KV_HIST);\n}\n\n";
+        << "  if (threadIdx.x < " << nr << "u) {\n"
+        << "    const uint32_t* w_ = s_stw + threadIdx.x * (KV_WG / 4u);\n"
+        << "    if (O.part) kv_count_status_part(w_, O.part + (size_t)(r0 / KV_WG + blockIdx.x) * O.part_pitch + " << name
+        << "_rules[threadIdx.x] * KV_HIST);\n"
+        << "    else kv_count_status_lds(w_, O.counts + (size_t)" << name << "_rules[threadIdx.x] * KV_HIST);\n"
+        << "  }\n}\n\n";
       hist_lds = false;
       return;
     }
