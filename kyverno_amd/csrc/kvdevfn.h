@@ -487,40 +487,56 @@ __device__ __forceinline__ bool mt_bit(const uint32_t* __restrict__ t, uint32_t 
 // workgroup, so the 32 criteria of the word are uniform across the wave; x =
 // entity). Rows y enumerate the namespace words, then the annotation words, then
 // the selector words.
-KV_FN void mtab_word(const DevPS& P, const DevBatch& B, uint32_t y, uint32_t e, uint32_t* __restrict__ ns,
-                          uint32_t* __restrict__ an, uint32_t* __restrict__ sl) {
-  uint32_t w = 0;
+// Bit k of match-table row y for entity e (row y: namespace-glob words, then annotation
+// words, then selector words; e: a distinct namespace string / annotation list / label
+// list of the batch), and the entity count of row y's table.
+KV_FN uint32_t mtab_entities(const DevPS& P, const DevBatch& B, uint32_t y) {
+  if (y < P.mt_ns_words) return B.n_nsm;
+  if (y < P.mt_ns_words + P.mt_ann_words) return B.n_asets;
+  return B.n_lsets;
+}
+KV_FN bool mtab_bit(const DevPS& P, const DevBatch& B, uint32_t y, uint32_t e, uint32_t k) {
+  const uint32_t bit = y * 32u + k;
   if (y < P.mt_ns_words) {
-    if (e >= B.n_nsm) return;
     const StrRef s = B.nsms[e];
-    for (uint32_t f = 0; f < P.n_filters; f++) {  // filters whose nss_bit falls in this word
+    bool r = false;
+    for (uint32_t f = 0; f < P.n_filters; f++) {  // the filters whose nss_bit is this bit
       const MFilter& F = P.filters[f];
-      if (!(sld(&F.flags) & MF_NSS) || (sld(&F.nss_bit) >> 5) != y) continue;
-      if (namespaces_match(P, B.bstr + s.off, s.len, sld(&F.nss_first), sld(&F.nss_count))) w |= 1u << (F.nss_bit & 31u);
+      if (!(sld(&F.flags) & MF_NSS) || sld(&F.nss_bit) != bit) continue;
+      r = r || namespaces_match(P, B.bstr + s.off, s.len, sld(&F.nss_first), sld(&F.nss_count));
     }
-    ns[(size_t)y * B.n_nsm + e] = w;
-    return;
+    return r;
   }
   y -= P.mt_ns_words;
   if (y < P.mt_ann_words) {
-    if (e >= B.n_asets) return;
+    const uint32_t abit = y * 32u + k;
     const KVSet a = B.asets[e];
+    bool r = false;
     for (uint32_t f = 0; f < P.n_filters; f++) {
       const MFilter& F = P.filters[f];
-      if (!(sld(&F.flags) & MF_ANN) || (sld(&F.ann_bit) >> 5) != y) continue;
-      if (annotations_match(P, B, B.kvs + a.first, a.count, sld(&F.ann_first), sld(&F.ann_count)))
-        w |= 1u << (F.ann_bit & 31u);
+      if (!(sld(&F.flags) & MF_ANN) || sld(&F.ann_bit) != abit) continue;
+      r = r || annotations_match(P, B, B.kvs + a.first, a.count, sld(&F.ann_first), sld(&F.ann_count));
     }
-    an[(size_t)y * B.n_asets + e] = w;
-    return;
+    return r;
   }
   y -= P.mt_ann_words;
-  if (e >= B.n_lsets) return;
+  const uint32_t si = y * 32u + k;
+  if (si >= P.n_sels) return false;
   const KVSet l = B.lsets[e];
-  const uint32_t s1 = P.n_sels < (y + 1) * 32u ? P.n_sels : (y + 1) * 32u;
-  for (uint32_t si = y * 32u; si < s1; si++)
-    if (selector_match(P, B, B.kvs + l.first, l.count, si)) w |= 1u << (si & 31u);
-  sl[(size_t)y * B.n_lsets + e] = w;
+  return selector_match(P, B, B.kvs + l.first, l.count, si);
+}
+
+// Word y of the match tables for entity e, one bit after the other (host emulator; the
+// device kernel evaluates the 32 bits on 32 lanes, kv_mtab_kernel)
+KV_FN void mtab_word(const DevPS& P, const DevBatch& B, uint32_t y, uint32_t e, uint32_t* __restrict__ ns,
+                     uint32_t* __restrict__ an, uint32_t* __restrict__ sl) {
+  if (e >= mtab_entities(P, B, y)) return;
+  uint32_t w = 0;
+  for (uint32_t k = 0; k < 32u; k++)
+    if (mtab_bit(P, B, y, e, k)) w |= 1u << k;
+  if (y < P.mt_ns_words) ns[(size_t)y * B.n_nsm + e] = w;
+  else if (y < P.mt_ns_words + P.mt_ann_words) an[(size_t)(y - P.mt_ns_words) * B.n_asets + e] = w;
+  else sl[(size_t)(y - P.mt_ns_words - P.mt_ann_words) * B.n_lsets + e] = w;
 }
 
 // doesResourceMatchConditionBlock: number of failed criteria (0 == block matches)

@@ -353,17 +353,31 @@ hipError_t launch_validate(const DevPS* P, const DevBatch* B, uint32_t n_res, co
 // batch (DevPS::mt_*). grid.y = table word, grid.x = entities.
 namespace kv {
 
+// 32 lanes per (row y, entity): lane k evaluates bit k, a ballot assembles the words of
+// the wave's two entities (a batch has few distinct match inputs, so one thread per word
+// ran 32 criteria serially on a handful of waves: C4 108 us per pass)
 __global__ __launch_bounds__(KV_WG) void kv_mtab_kernel(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp,
                                                          uint32_t* __restrict__ ns, uint32_t* __restrict__ an,
                                                          uint32_t* __restrict__ sl) {
-  mtab_word(*Pp, *Bp, blockIdx.y, blockIdx.x * KV_WG + threadIdx.x, ns, an, sl);
+  const DevPS& P = *Pp;
+  const DevBatch& B = *Bp;
+  const uint32_t y = blockIdx.y, k = threadIdx.x & 31u;
+  const uint32_t e = blockIdx.x * (KV_WG / 32) + threadIdx.x / 32u;
+  const uint32_t ne = mtab_entities(P, B, y);
+  const bool v = e < ne && mtab_bit(P, B, y, e, k);
+  const uint64_t m = __ballot(v);
+  if (k != 0 || e >= ne) return;
+  const uint32_t w = (threadIdx.x & 32u) ? (uint32_t)(m >> 32) : (uint32_t)m;
+  if (y < P.mt_ns_words) ns[(size_t)y * B.n_nsm + e] = w;
+  else if (y < P.mt_ns_words + P.mt_ann_words) an[(size_t)(y - P.mt_ns_words) * B.n_asets + e] = w;
+  else sl[(size_t)(y - P.mt_ns_words - P.mt_ann_words) * B.n_lsets + e] = w;
 }
 
 hipError_t launch_mtab(const DevPS* P, const DevBatch* B, uint32_t words, uint32_t max_entities, uint32_t* ns,
                        uint32_t* an, uint32_t* sl, hipStream_t stream) {
   if (words == 0 || max_entities == 0) return hipSuccess;
-  hipLaunchKernelGGL(kv_mtab_kernel, dim3((max_entities + KV_WG - 1) / KV_WG, words), dim3(KV_WG), 0, stream, P, B, ns,
-                     an, sl);
+  hipLaunchKernelGGL(kv_mtab_kernel, dim3((max_entities + KV_WG / 32 - 1) / (KV_WG / 32), words), dim3(KV_WG), 0, stream,
+                     P, B, ns, an, sl);
   return hipGetLastError();
 }
 
