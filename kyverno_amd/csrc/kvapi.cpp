@@ -780,7 +780,7 @@ struct DevSession {
   int device = 0;
   uint32_t mode = 0;
   uint64_t nrules = 0, nres = 0;
-  DevBuf fflags, pview, st, er8, er, cn, scope, scn, ptab, mtab, part;
+  DevBuf fflags, pview, st, er8, er, cn, scope, scn, ptab, mtab, mtbf, part;
   DevBuf r_offs, r_tot, r_base, r_out8, r_outw, r_wide;  // record compaction (fetch)
   uint32_t part_blocks = 0;
   uint32_t mt_words = 0, mt_entities = 0;
@@ -828,6 +828,8 @@ struct DevSession {
       mt_sel = mt_ann + n_an;
       P.mt_ns = mt_ns;
       P.mt_ann = mt_ann;
+      mtbf.upload(mtab_bit_filters(pp), device);
+      P.mt_bitf = (const uint32_t*)mtbf.p;
       P.mt_sel = mt_sel;
       mt_words = P.mt_ns_words + P.mt_ann_words + P.mt_sel_words;
       mt_entities = (uint32_t)std::max({bb.nsms.size(), bb.asets.size(), bb.lsets.size()});
@@ -855,9 +857,10 @@ struct DevSession {
     O.counts = (unsigned long long*)cn.p;
     O.part = nullptr;
     O.part_pitch = 0;
-    // specialized kernels: per-workgroup partial histograms summed by one reduce kernel
-    // instead of per-workgroup atomics on the counts (KVGPU_JIT_PARTIAL=0: atomics)
-    static const bool use_part = !(getenv("KVGPU_JIT_PARTIAL") && getenv("KVGPU_JIT_PARTIAL")[0] == '0');
+    // KVGPU_JIT_PARTIAL=1: per-workgroup partial histograms summed by one reduce kernel
+    // instead of per-workgroup atomics on the counts (A/B: C2 rule kernel -13 us, reduce
+    // +92 us, so the atomics stay the default)
+    static const bool use_part = getenv("KVGPU_JIT_PARTIAL") && getenv("KVGPU_JIT_PARTIAL")[0] == '1';
     if (use_part && dp.specialized() && nres && nrules) {
       part_blocks = (uint32_t)((nres + KV_WG - 1) / KV_WG);
       part.alloc((size_t)part_blocks * nrules * KV_HIST * sizeof(uint32_t), device);

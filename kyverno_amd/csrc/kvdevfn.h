@@ -496,30 +496,18 @@ KV_FN uint32_t mtab_entities(const DevPS& P, const DevBatch& B, uint32_t y) {
   return B.n_lsets;
 }
 KV_FN bool mtab_bit(const DevPS& P, const DevBatch& B, uint32_t y, uint32_t e, uint32_t k) {
-  const uint32_t bit = y * 32u + k;
-  if (y < P.mt_ns_words) {
-    const StrRef s = B.nsms[e];
-    bool r = false;
-    for (uint32_t f = 0; f < P.n_filters; f++) {  // the filters whose nss_bit is this bit
-      const MFilter& F = P.filters[f];
-      if (!(sld(&F.flags) & MF_NSS) || sld(&F.nss_bit) != bit) continue;
-      r = r || namespaces_match(P, B.bstr + s.off, s.len, sld(&F.nss_first), sld(&F.nss_count));
+  if (y < P.mt_ns_words + P.mt_ann_words) {
+    const uint32_t f = P.mt_bitf[y * 32u + k];  // the filter owning this bit
+    if (f == KV_SENT) return false;
+    const MFilter& F = P.filters[f];
+    if (y < P.mt_ns_words) {
+      const StrRef s = B.nsms[e];
+      return namespaces_match(P, B.bstr + s.off, s.len, F.nss_first, F.nss_count);
     }
-    return r;
-  }
-  y -= P.mt_ns_words;
-  if (y < P.mt_ann_words) {
-    const uint32_t abit = y * 32u + k;
     const KVSet a = B.asets[e];
-    bool r = false;
-    for (uint32_t f = 0; f < P.n_filters; f++) {
-      const MFilter& F = P.filters[f];
-      if (!(sld(&F.flags) & MF_ANN) || sld(&F.ann_bit) != abit) continue;
-      r = r || annotations_match(P, B, B.kvs + a.first, a.count, sld(&F.ann_first), sld(&F.ann_count));
-    }
-    return r;
+    return annotations_match(P, B, B.kvs + a.first, a.count, F.ann_first, F.ann_count);
   }
-  y -= P.mt_ann_words;
+  y -= P.mt_ns_words + P.mt_ann_words;
   const uint32_t si = y * 32u + k;
   if (si >= P.n_sels) return false;
   const KVSet l = B.lsets[e];

@@ -60,6 +60,9 @@ struct DevPS {
   const uint32_t* mt_ns;
   const uint32_t* mt_ann;
   const uint32_t* mt_sel;
+  // filter of each namespace-glob bit (mt_ns_words * 32 entries), then of each annotation bit
+  // (mt_ann_words * 32); KV_SENT for unused bits (mtab_bit_filters, kvfold.cpp)
+  const uint32_t* mt_bitf;
 };
 
 struct DevBatch {

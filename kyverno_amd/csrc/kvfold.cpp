@@ -123,4 +123,15 @@ void key_table(const PolicySet& ps, const Batch& b, std::vector<uint32_t>* off, 
   ks->append(16, '\0');
 }
 
+std::vector<uint32_t> mtab_bit_filters(const PolicySet& ps) {
+  const uint32_t ns_w = (ps.n_nss_bits + 31) / 32, an_w = (ps.n_ann_bits + 31) / 32;
+  std::vector<uint32_t> out((size_t)(ns_w + an_w) * 32, 0xFFFFFFFFu);
+  for (uint32_t f = 0; f < ps.filters.size(); f++) {
+    const MFilter& F = ps.filters[f];
+    if (F.flags & MF_NSS) out[F.nss_bit] = f;
+    if (F.flags & MF_ANN) out[(size_t)ns_w * 32 + F.ann_bit] = f;
+  }
+  return out;
+}
+
 }  // namespace kvh

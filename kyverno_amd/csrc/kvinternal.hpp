@@ -306,6 +306,9 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
 // user-info criteria folded in (ctx_json: AdmissionInfo / ExcludeGroupRole, or
 // NULL), and the batch key string table (4-byte aligned entries).
 std::vector<uint32_t> fold_filters(const PolicySet& ps, const char* ctx_json);
+// DevPS::mt_bitf: the filter owning each namespace-glob bit, then each annotation bit
+// (rows padded to 32 bits, 0xFFFFFFFF where no filter)
+std::vector<uint32_t> mtab_bit_filters(const PolicySet& ps);
 void key_table(const PolicySet& ps, const Batch& b, std::vector<uint32_t>* off, std::vector<uint32_t>* len,
                std::string* ks);
 

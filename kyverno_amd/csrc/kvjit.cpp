@@ -1332,13 +1332,12 @@ struct Gen {
             w << "\n";
           }
           break;
-        case OP_DONE:
-          w << "  if (" << kindof << " == 0u) " << finish("ST_PASS") << "\n"
-            << "  if (" << kindof << " == E_CPU) " << finish("ST_CPU") << "\n"
-            << "  if (" << ek << " & " << u32((EF_COND | EF_GLOBAL) << 4) << ") " << finish("ST_SKIP") << "\n";
-          if (g.uses_anchor) w << "  if (areg" << s << " & ~apres" << s << ") " << finish("ST_ERROR") << "\n";
-          w << "  if (" << kindof << " == E_LEN) " << finish("ST_ERROR") << "\n"
-            << "  " << finish("ST_FAIL") << "\n";
+        case OP_DONE:  // the MatchPattern epilogue as one select chain (no per-lane branches)
+          if (R.kind != 0) throw std::runtime_error("kvjit: rule end inside a fused loop");
+          w << "  { const uint32_t k_ = " << kindof << ";\n    rs" << s << " = FIN_ | (k_ == 0u ? ST_PASS : k_ == E_CPU ? ST_CPU : ("
+            << ek << " & " << u32((EF_COND | EF_GLOBAL) << 4) << ") ? ST_SKIP : ";
+          if (g.uses_anchor) w << "(areg" << s << " & ~apres" << s << ") ? ST_ERROR : ";
+          w << "k_ == E_LEN ? ST_ERROR : ST_FAIL);\n    goto " << R.se << "; }\n";
           break;
         default:  // OP_NOP, OP_METACHK (handled per resource by RF_BAD_META)
           break;

@@ -204,6 +204,8 @@ int main(int argc, char** argv) {
     std::vector<uint32_t> mt(std::max<size_t>(n_ns + n_an + n_sl, 1), 0xA5A5A5A5u);
     P.mt_ns = mt.data();
     P.mt_ann = mt.data() + n_ns;
+    const std::vector<uint32_t> bitf = mtab_bit_filters(ps);
+    P.mt_bitf = bitf.data();
     P.mt_sel = mt.data() + n_ns + n_an;
     kvemu_mtab(&P, &B, P.mt_ns_words + P.mt_ann_words + P.mt_sel_words,
                std::max({B.n_nsm, B.n_asets, B.n_lsets}), mt.data(), mt.data() + n_ns, mt.data() + n_ns + n_an);
