@@ -246,3 +246,38 @@ def test_wide_error_records(orc, spec):
     assert r.path(0, 1) == "/spec/containers/1/ports/1500/containerPort/"
     assert r.path(1, 0) == "/metadata/labels/app-x/"
     assert r.path(2, 3) == "/spec/l/1/l/1/l/1/l/1/v/"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", [False, True], ids=["vm", "specialized"])
+def test_glob_stress_long_values(orc, spec):
+    """The glob stress at value lengths 0-200 (kvj_ptab's 64-byte and 128-byte register
+    paths and the word-loop fallback beyond) with non-ASCII values under `?` globs."""
+    import random
+
+    rnd = random.Random(11)
+    alpha = list("ab:/.-") + ["é", "日"]
+
+    def word(n):
+        s = ""
+        while len(s.encode()) < n:
+            s += rnd.choice(alpha)
+        return s
+
+    pats = set()
+    while len(pats) < 120:
+        parts = []
+        for _ in range(rnd.randrange(1, 6)):
+            r = rnd.random()
+            parts.append("*" if r < 0.35 else "?" if r < 0.45 else word(rnd.randrange(1, 5)))
+        p = "".join(parts)
+        if rnd.random() < 0.15:
+            p = "!" + p
+        pats.add(p)
+    vals = [word(rnd.choice([rnd.randrange(0, 30), rnd.randrange(50, 80), rnd.randrange(100, 140),
+                             rnd.randrange(120, 200)])) for _ in range(600)]
+    pols = [_policy({"key": p}, name=f"g{i}") for i, p in enumerate(sorted(pats))]
+    ress = [{"key": v} for v in vals]
+    mism, r, ost = compare(orc, pols, ress, specialize=spec)
+    assert not mism, "\n".join(mism)
+    assert (r.status == 0).sum() > 1000 and (r.status == 1).sum() > 1000

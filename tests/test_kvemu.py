@@ -104,3 +104,38 @@ def test_sharded_evaluation_matches_unsharded(orc, shards):
                  for a, b in zip(bounds[:-1], bounds[1:]))
     assert np.array_equal(summed, np.stack([(st1 == s).sum(axis=1) for s in range(7)], axis=1))
     assert np.array_equal(st1, oracle_status(orc, pols, ress))
+
+
+def test_register_path_globs_long_and_unicode(orc):
+    """kvj_ptab's register-path globs (values <= 64 and <= 128 bytes: byte masks, leftmost
+    verified candidate) and its word-loop fallback (longer values, non-ASCII under '?')
+    against the oracle's minio wildcard.Match restatement, on random values of 0-200
+    bytes built from the globs' literal bytes."""
+    import random
+
+    from kyverno_amd import workloads
+
+    rnd = random.Random(0x6B7A)
+    globs = list(workloads.IMAGE_GLOBS) + ["*a?b*", "??*:*", "*::*", "a*b*c*d", "*é*", "?é*", "*-?-*", "*.*.*.*",
+                                           "x*", "*y", "*@*@*", "*1?:??*"]
+    rules = [{"name": f"g{i:02d}", "match": {"resources": {"kinds": ["Pod"]}},
+              "validate": {"pattern": {"spec": {"containers": [{"image": g}]}}}} for i, g in enumerate(globs)]
+    pols = [{"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "globs"},
+             "spec": {"validationFailureAction": "audit", "rules": rules}}]
+    alpha = list("abcdxy:@/.-12v?*") + ["nginx", "redis", "latest", "sha256:", "docker.io/", "é", "日"]
+    ress = []
+    for i in range(600):
+        conts = []
+        for c in range(1 + rnd.randrange(3)):
+            n = rnd.choice([rnd.randrange(0, 20), rnd.randrange(20, 70), rnd.randrange(60, 140), rnd.randrange(120, 200)])
+            s = ""
+            while len(s.encode()) < n:
+                s += rnd.choice(alpha)
+            conts.append({"name": f"c{c}", "image": s})
+        ress.append({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": f"p{i}", "namespace": "default"},
+                     "spec": {"containers": conts}})
+    st, _ = _emulate(pols, ress, "globs_long")
+    ost = oracle_status(orc, pols, ress)
+    bad = np.argwhere(st != ost)
+    assert not len(bad), [(int(a), int(b), int(st[a, b]), int(ost[a, b])) for a, b in bad[:20]]
+    assert (st == 0).sum() > 0 and (st == 1).sum() > 0
