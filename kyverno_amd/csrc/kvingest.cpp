@@ -32,27 +32,93 @@ namespace {
 struct Ingest {
   const PolicySet& ps;
   Batch& b;
-  std::unordered_map<std::string, uint32_t> str_off;   // dedup of string heap
-  std::unordered_map<std::string, uint32_t> val_id;    // dedup of scalars
+  // Interning tables (open addressing, linear probing, keyed by a 64-bit hash of the bytes;
+  // a hit is confirmed against the bytes already stored in the heap / the value record, so
+  // no key string is built or kept per lookup)
+  struct Probe {
+    std::vector<uint64_t> h;   // 0 = empty slot
+    std::vector<uint32_t> id;
+    size_t n = 0;
+    void init(size_t cap) {
+      size_t c = 1024;
+      while (c < cap * 2) c <<= 1;
+      h.assign(c, 0);
+      id.assign(c, 0);
+      n = 0;
+    }
+    template <class Eq>
+    int64_t find(uint64_t hv, Eq eq) const {
+      const size_t m = h.size() - 1;
+      for (size_t i = hv & m;; i = (i + 1) & m) {
+        if (h[i] == 0) return -1;
+        if (h[i] == hv && eq(id[i])) return id[i];
+      }
+    }
+    void insert(uint64_t hv, uint32_t v) {
+      if ((n + 1) * 2 > h.size()) grow();
+      const size_t m = h.size() - 1;
+      size_t i = hv & m;
+      while (h[i] != 0) i = (i + 1) & m;
+      h[i] = hv;
+      id[i] = v;
+      n++;
+    }
+    void grow() {
+      std::vector<uint64_t> oh;
+      std::vector<uint32_t> oi;
+      oh.swap(h);
+      oi.swap(id);
+      h.assign(oh.size() * 2, 0);
+      id.assign(oh.size() * 2, 0);
+      n = 0;
+      for (size_t i = 0; i < oh.size(); i++)
+        if (oh[i]) insert(oh[i], oi[i]);
+    }
+  };
+  static uint64_t hash_bytes(const void* p, size_t len, uint64_t seed) {
+    const uint8_t* s = (const uint8_t*)p;  // FNV-1a 64 over 8-byte words, then a final mix
+    uint64_t h = 1469598103934665603ull ^ seed ^ (len * 0x9E3779B97F4A7C15ull);
+    size_t i = 0;
+    for (; i + 8 <= len; i += 8) {
+      uint64_t w;
+      memcpy(&w, s + i, 8);
+      h = (h ^ w) * 1099511628211ull;
+      h ^= h >> 29;
+    }
+    for (; i < len; i++) h = (h ^ s[i]) * 1099511628211ull;
+    h ^= h >> 32;
+    h *= 0xD6E8FEB86659FD93ull;
+    h ^= h >> 32;
+    return h ? h : 1;
+  }
+  Probe str_off;  // string heap offsets (id = offset; length checked against the stored bytes)
+  Probe val_id;   // scalars (id = value index; type and bytes checked against the Val)
   std::unordered_map<std::string, uint32_t> dyn_key;   // batch-local key ids
   std::unordered_map<std::string, uint32_t> ns_index;
   uint32_t nstatic;
   std::vector<std::vector<uint32_t>> slot_ids;  // per trie node: key ids of its slots
 
   Ingest(const PolicySet& p, Batch& bb) : ps(p), b(bb), nstatic((uint32_t)p.keys.size()), slot_ids(p.trie.nodes.size()) {
+    str_off.init(1 << 14);
+    val_id.init(1 << 14);
     // offset 0 holds "0": convertNumberToString(nil) for the device glob (kvkernel.hip atom_eval)
     str("0");
   }
 
+  std::vector<std::pair<uint32_t, uint32_t>> str_ents;  // (offset, length) per interned string
+
   uint32_t str(std::string_view s) {
-    std::string k(s);
-    auto it = str_off.find(k);
-    if (it != str_off.end()) return it->second;
+    const uint64_t hv = hash_bytes(s.data(), s.size(), 0x5354u);
+    const int64_t e = str_off.find(hv, [&](uint32_t x) {
+      return str_ents[x].second == s.size() && memcmp(b.strs.data() + str_ents[x].first, s.data(), s.size()) == 0;
+    });
+    if (e >= 0) return str_ents[(size_t)e].first;
     // 4-byte aligned: the device glob compares whole words (kvkernel.hip seg_at)
     while (b.strs.size() & 3) b.strs.push_back('\0');
     uint32_t off = (uint32_t)b.strs.size();
     b.strs.append(s.data(), s.size());
-    str_off.emplace(std::move(k), off);
+    str_off.insert(hv, (uint32_t)str_ents.size());
+    str_ents.push_back({off, (uint32_t)s.size()});
     return off;
   }
 
@@ -70,15 +136,25 @@ struct Ingest {
   }
 
   uint32_t val(const JDoc& d, const JNode& n) {
-    std::string k;
+    uint64_t hv;
+    std::string_view sv;
     switch (n.t) {
-      case J_BOOL: k = n.b ? "b1" : "b0"; break;
-      case J_INT: k = "i" + std::to_string(n.i); break;
-      case J_FLOAT: { k = "f"; k.append((const char*)&n.f, 8); break; }
-      default: k = "s"; k += d.sval(n); break;
+      case J_BOOL: hv = hash_bytes(n.b ? "1" : "0", 1, 'b'); break;
+      case J_INT: hv = hash_bytes(&n.i, 8, 'i'); break;
+      case J_FLOAT: hv = hash_bytes(&n.f, 8, 'f'); break;
+      default: sv = d.sval(n); hv = hash_bytes(sv.data(), sv.size(), 's'); break;
     }
-    auto it = val_id.find(k);
-    if (it != val_id.end()) return it->second;
+    const int64_t hit = val_id.find(hv, [&](uint32_t x) {
+      const Val& v = b.vals[x];
+      switch (n.t) {
+        case J_BOOL: return v.type == NT_BOOL && ((v.flags & VF_BOOLV) != 0) == n.b;
+        case J_INT: return v.type == NT_INT && v.i == n.i;
+        case J_FLOAT: return v.type == NT_FLOAT && memcmp(&v.f, &n.f, 8) == 0;
+        default:
+          return v.type == NT_STR && v.e_len == sv.size() && memcmp(b.strs.data() + v.e_off, sv.data(), sv.size()) == 0;
+      }
+    });
+    if (hit >= 0) return (uint32_t)hit;
     Val v{};
     std::string e, num;
     bool nvalid = true;
@@ -134,7 +210,7 @@ struct Ingest {
     }
     uint32_t id = (uint32_t)b.vals.size();
     b.vals.push_back(v);
-    val_id.emplace(std::move(k), id);
+    val_id.insert(hv, id);
     return id;
   }
 
@@ -154,6 +230,20 @@ struct Ingest {
     std::vector<Shape> kids;   // map block (slot-addressed: one per slot key; keep-all: max count)
     std::vector<Shape> elems;  // array block (max length)
   };
+
+  // slot of key k in a slot-addressed trie node (binary search of its byte-sorted keys,
+  // no string built per lookup), -1 when the key is not projected
+  static int32_t slot_of(const Trie::N& tn, std::string_view k) {
+    size_t lo = 0, hi = tn.slot_keys.size();
+    while (lo < hi) {
+      const size_t mid = (lo + hi) / 2;
+      const int c = std::string_view(tn.slot_keys[mid]).compare(k);
+      if (c == 0) return (int32_t)mid;
+      if (c < 0) lo = mid + 1;
+      else hi = mid;
+    }
+    return -1;
+  }
 
   void sorted_children(const JDoc& d, const JNode& n, std::vector<uint32_t>* out) {
     out->clear();
@@ -181,8 +271,8 @@ struct Ingest {
         for (size_t i = 0; i < ch.size(); i++) unite(s.kids[i], d, ch[i]);
       } else {
         for (uint32_t c = n.first; c < n.first + n.count; c++) {
-          auto it = tn.slot.find(std::string(d.key(d.at(c))));
-          if (it != tn.slot.end()) unite(s.kids[it->second], d, c);
+          const int32_t si = slot_of(tn, d.key(d.at(c)));
+          if (si >= 0) unite(s.kids[si], d, c);
         }
       }
     } else if (n.t == J_ARR) {
@@ -255,8 +345,8 @@ struct Ingest {
           for (uint32_t i = (uint32_t)ids.size(); i < K; i++) ids.push_back(key_of(tn.slot_keys[i]));
           for (uint32_t i = 0; i < K; i++) cell(s.map_row + i, lane) = Node{(ids[i] & KEY_NONE28) << 4 | NT_ABSENT, 0, 0, 0};
           for (uint32_t c = n.first; c < n.first + n.count; c++) {
-            auto it = tn.slot.find(std::string(d.key(d.at(c))));
-            if (it != tn.slot.end()) put(s.kids[it->second], d, c, lane, ids[it->second], s.kids[it->second].t);
+            const int32_t si = slot_of(tn, d.key(d.at(c)));
+            if (si >= 0) put(s.kids[si], d, c, lane, ids[si], s.kids[si].t);
           }
         }
         break;
