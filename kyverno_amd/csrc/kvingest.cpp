@@ -364,6 +364,7 @@ struct Ingest {
 
   std::vector<JDoc> group;
   uint32_t group_n = 0;
+  size_t expected_res = 0;  // resources this Ingest will take (0: unknown)
 
   void flush_group() {
     if (group_n == 0) return;
@@ -376,7 +377,14 @@ struct Ingest {
     base_row = b.n_rows;
     b.n_rows += rows;
     if (b.n_rows * KV_LANES >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: batch too large for 32-bit node indices");
-    b.nodes.resize((size_t)b.n_rows * KV_LANES, Node{NT_NULL, 0, 0, 0});
+    // capacity for the rest of the part from the rows per group so far (+1/8), instead of
+    // the vector's doubling (each doubling copies every cell written so far)
+    const size_t want = (size_t)b.n_rows * KV_LANES;
+    if (want > b.nodes.capacity() && expected_res > b.res.size()) {
+      const double per_res = (double)b.n_rows / (double)b.res.size();
+      b.nodes.reserve(std::max(want, (size_t)(per_res * (double)expected_res * 1.125) * KV_LANES));
+    }
+    b.nodes.resize(want, Node{NT_NULL, 0, 0, 0});
     for (uint32_t l = 0; l < group_n; l++) {
       put(root, group[l], group[l].root, l, KEY_NONE, 0);
       b.res[b.res.size() - group_n + l].root = (uint32_t)base_row;
@@ -861,6 +869,7 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
           Ingest in(ps, parts[k]);
           JDoc doc;
           const size_t e = std::min(nres, (k + 1) * per);
+          in.expected_res = e > k * per ? e - k * per : 0;
           for (size_t i = k * per; i < e; i++) {
             const size_t end = i + 1 < nres ? starts[i + 1] : len;
             doc.nodes.clear();
