@@ -1644,7 +1644,16 @@ struct Gen {
     if (!hist_lds)
       o << "  for (uint32_t q = threadIdx.x; q < " << nr << "u * KV_HIST; q += KV_WG) (&s_hist[0][0])[q] = 0u;\n"
         << "  __syncthreads();\n";
-    o << "  const uint32_t r = r0 + blockIdx.x * KV_WG + threadIdx.x;\n"
+    // KVGPU_JIT_XCD=1: workgroup b runs tile (b % 8) * n/8 + b / 8, so each XCD (blocks b,
+    // b+8, ... share one) walks a contiguous resource range and its L2 sees the values those
+    // resources share (the value table and ptab lines are numbered by first occurrence)
+    static const bool xcd_map = getenv("KVGPU_JIT_XCD") && getenv("KVGPU_JIT_XCD")[0] == '1';
+    if (xcd_map)
+      o << "  const uint32_t nb_ = gridDim.x, x_ = blockIdx.x & 7u, per_ = nb_ >> 3, rem_ = nb_ & 7u;\n"
+        << "  const uint32_t bx_ = x_ * per_ + (x_ < rem_ ? x_ : rem_) + (blockIdx.x >> 3);\n";
+    else
+      o << "  const uint32_t bx_ = blockIdx.x;\n";
+    o << "  const uint32_t r = r0 + bx_ * KV_WG + threadIdx.x;\n"
       << "  const uint32_t n_res = B.n_res;\n"
       << "  const bool valid = r < n_res;\n"
       << "  const Res* __restrict__ R = B.res + (valid ? r : 0u);\n"
@@ -1665,7 +1674,7 @@ struct Gen {
       o << "  __syncthreads();\n"
         << "  if (threadIdx.x < " << nr << "u) {\n"
         << "    const uint32_t* w_ = s_stw + threadIdx.x * (KV_WG / 4u);\n"
-        << "    if (O.part) kv_count_status_part(w_, O.part + (size_t)(r0 / KV_WG + blockIdx.x) * O.part_pitch + " << name
+        << "    if (O.part) kv_count_status_part(w_, O.part + (size_t)(r0 / KV_WG + bx_) * O.part_pitch + " << name
         << "_rules[threadIdx.x] * KV_HIST);\n"
         << "    else kv_count_status_lds(w_, O.counts + (size_t)" << name << "_rules[threadIdx.x] * KV_HIST);\n"
         << "  }\n}\n\n";

@@ -34,7 +34,7 @@ using namespace kvh;
 struct kvemu_dim3 {
   uint32_t x, y, z;
 };
-thread_local kvemu_dim3 threadIdx, blockIdx;
+thread_local kvemu_dim3 threadIdx, blockIdx, gridDim;
 
 extern "C" void kvemu_mtab(const DevPS* P, const DevBatch* B, uint32_t words, uint32_t max_entities, uint32_t* ns,
                            uint32_t* an, uint32_t* sl);
@@ -71,6 +71,7 @@ static void grid(uint32_t bx, uint32_t by, F f) {
     th.emplace_back([&]() {
       for (uint64_t i; (i = next++) < total;) {
         blockIdx = {(uint32_t)(i % bx), (uint32_t)(i / bx), 0};
+        gridDim = {bx, by, 1};
         for (uint32_t x = 0; x < (uint32_t)KV_WG; x++) {
           threadIdx = {x, 0, 0};
           f();

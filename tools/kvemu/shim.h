@@ -23,7 +23,7 @@
 struct kvemu_dim3 {
   uint32_t x, y, z;
 };
-extern thread_local kvemu_dim3 threadIdx, blockIdx;
+extern thread_local kvemu_dim3 threadIdx, blockIdx, gridDim;
 
 struct uint2 {
   uint32_t x, y;
