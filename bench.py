@@ -84,6 +84,7 @@ def pmc_traffic(args) -> dict | None:
     run at fetch, outside the pass)."""
     import csv
     import collections
+    import glob
     import shutil
     import signal
     import subprocess
@@ -119,8 +120,7 @@ def pmc_traffic(args) -> dict | None:
             log(f"pmc {ctr}: rocprofv3 exit {p.returncode}: {err.decode(errors='replace')[-400:]}")
             return None
         agg = collections.defaultdict(float)
-        for f in sorted(set(__import__("glob").glob(os.path.join(out, "**", f"{ctr}*counter_collection.csv"),
-                                                    recursive=True))):
+        for f in sorted(set(glob.glob(os.path.join(out, "**", f"{ctr}*counter_collection.csv"), recursive=True))):
             for r in csv.DictReader(open(f)):
                 k = r.get("Kernel_Name", "")
                 # the pass's kernels: not the record compaction of a fetch (kv_rec_*) nor the
