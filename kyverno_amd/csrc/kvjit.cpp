@@ -1644,10 +1644,11 @@ struct Gen {
     if (!hist_lds)
       o << "  for (uint32_t q = threadIdx.x; q < " << nr << "u * KV_HIST; q += KV_WG) (&s_hist[0][0])[q] = 0u;\n"
         << "  __syncthreads();\n";
-    // KVGPU_JIT_XCD=1: workgroup b runs tile (b % 8) * n/8 + b / 8, so each XCD (blocks b,
-    // b+8, ... share one) walks a contiguous resource range and its L2 sees the values those
-    // resources share (the value table and ptab lines are numbered by first occurrence)
-    static const bool xcd_map = getenv("KVGPU_JIT_XCD") && getenv("KVGPU_JIT_XCD")[0] == '1';
+    // Workgroup b runs tile (b % 8) * n/8 + b / 8, so each XCD (blocks b, b+8, ... share one)
+    // walks a contiguous resource range and its L2 sees the values those resources share
+    // (the value table and ptab lines are numbered by first occurrence): C2 -0.6 %, C3 -1 %
+    // per pass, traffic -1 %; KVGPU_JIT_XCD=0 keeps block b on tile b (A/B runs)
+    static const bool xcd_map = !(getenv("KVGPU_JIT_XCD") && getenv("KVGPU_JIT_XCD")[0] == '0');
     if (xcd_map)
       o << "  const uint32_t nb_ = gridDim.x, x_ = blockIdx.x & 7u, per_ = nb_ >> 3, rem_ = nb_ & 7u;\n"
         << "  const uint32_t bx_ = x_ * per_ + (x_ < rem_ ? x_ : rem_) + (blockIdx.x >> 3);\n";
