@@ -79,8 +79,8 @@ struct Gen {
   // with the cursor (issued with the other lookups of the region instead of one
   // dependent load per rule); KVGPU_JIT_PW=0 disables, for A/B runs
   bool pw = true;
-  // kvj_ptab stages each value's bytes in LDS before its row of predicates;
-  // KVGPU_PTAB_LDS=0 reads them from global memory per glob, for A/B runs
+  // the round-1 kvj_ptab (KVGPU_PTAB=words) stages each value's bytes in LDS before its
+  // row of predicates; KVGPU_PTAB_LDS=0 reads them from global memory per glob (A/B runs)
   bool ptab_lds = !(getenv("KVGPU_PTAB_LDS") && getenv("KVGPU_PTAB_LDS")[0] == '0');
   // kvj_ptab evaluates globs on a register copy of the value with shared byte masks
   // (qglob_fn); KVGPU_PTAB=words keeps the per-glob word loops (A/B runs)
@@ -91,7 +91,7 @@ struct Gen {
   // KVGPU_JIT_HOIST=lazy places each just before its first use, for A/B runs
   bool early_hoist = !(getenv("KVGPU_JIT_HOIST") && std::string(getenv("KVGPU_JIT_HOIST")) == "lazy");
   // fused array loops software-pipelined (next element's lookups issued before this
-  // element's rules); KVGPU_JIT_PIPE=1 enables, for A/B runs
+  // element's rules); KVGPU_JIT_PIPE=1 enables, for A/B runs (C2: rule kernel +30 %)
   bool pipe_loops = getenv("KVGPU_JIT_PIPE") && getenv("KVGPU_JIT_PIPE")[0] == '1';
   explicit Gen(const PolicySet& p) : ps(p) {}
 
