@@ -104,11 +104,41 @@ __device__ __forceinline__ uint64_t kv_bmask(const uint32_t* w, uint32_t c4) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// kv_bmask over the first nw words only (nw wave-uniform, a multiple of 4): the mask bits
+// of later words are never read (candidates lie below the value length)
+__device__ __forceinline__ uint32_t kv_bmask_q(const uint32_t* w, uint32_t c4, uint32_t q) {
+  uint32_t r = 0u;  // words 4q .. 4q+3 -> mask bits 16q' .. (nibbles at 4 * (i % 8))
+#pragma unroll
+  for (uint32_t i = 0; i < 4; i++) {
+    const uint32_t x = w[4 * q + i] ^ c4;
+    const uint32_t m = (x - 0x01010101u) & ~x & 0x80808080u;
+    r |= ((m * 0x00204081u) >> 28) << (4u * ((4 * q + i) & 7u));
+  }
+  return r;
+}
+__device__ __forceinline__ uint64_t kv_bmask_n(const uint32_t* w, uint32_t c4, uint32_t nw) {
+  uint32_t lo = kv_bmask_q(w, c4, 0), hi = 0u;
+  if (nw > 4u) lo |= kv_bmask_q(w, c4, 1);
+  if (nw > 8u) hi = kv_bmask_q(w, c4, 2);
+  if (nw > 12u) hi |= kv_bmask_q(w, c4, 3);
+  return ((uint64_t)hi << 32) | lo;
+}
+// the smallest multiple of 4 words (<= W) covering the value of every active lane
+__device__ __forceinline__ uint32_t kv_wave_words(uint32_t lastw, uint32_t W) {
+  uint32_t n = W;
+  while (n > 4u && __ballot(lastw > n - 4u) == 0ull) n -= 4u;
+  return n;
+}
+
 // byte-position masks of values of <= 128 bytes (32 words): positions 0-63 in lo, 64-127 in hi
 struct KvM2 {
   uint64_t lo, hi;
 };
 __device__ __forceinline__ KvM2 kv_bmask2(const uint32_t* w, uint32_t c4) { return {kv_bmask(w, c4), kv_bmask(w + 16, c4)}; }
+__device__ __forceinline__ uint64_t kv_bmask_n(const uint32_t* w, uint32_t c4, uint32_t nw);
+__device__ __forceinline__ KvM2 kv_bmask2_n(const uint32_t* w, uint32_t c4, uint32_t nw) {
+  return {kv_bmask_n(w, c4, nw < 16u ? nw : 16u), nw > 16u ? kv_bmask_n(w + 16, c4, nw - 16u) : 0ull};
+}
 
 // candidate-mask helpers of the kvj_ptab register globs, on both mask types: the bits of m
 // in [plo, phi] (none when !ok; plo <= phi < mask width when ok), non-empty test, lowest

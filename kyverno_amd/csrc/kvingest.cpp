@@ -629,11 +629,12 @@ bool scan_values(const char* p, size_t n, unsigned T, std::vector<size_t>* start
 // divergence. Buckets are ordered by key and stable inside (ingest order).
 // KVGPU_VAL_ORDER=0 keeps ingest order (A/B runs)
 const bool g_val_order = [] { const char* e = getenv("KVGPU_VAL_ORDER"); return !(e && e[0] == '0'); }();
-// class, type, then length bucket of the e-form bytes (<= 64, <= 128, longer): kvj_ptab keeps
-// values of <= 64 bytes in registers, so a wave of one bucket runs one path
+// class, type, then length bucket of the e-form bytes (16-byte steps up to 64, <= 128,
+// longer): kvj_ptab keeps values of <= 64 / <= 128 bytes in registers, so a wave of one
+// bucket runs one path, and its byte masks cover only the words its bucket occupies
 inline uint64_t val_order_key(const Val& v) {
-  return g_val_order ? ((uint64_t)v.cls << 16 | (uint64_t)v.type << 8 | (v.e_len <= 64u ? 0u : v.e_len <= 128u ? 1u : 2u))
-                     : 0u;
+  const uint32_t lb = v.e_len <= 64u ? (v.e_len + 15u) / 16u : v.e_len <= 128u ? 5u : 6u;
+  return g_val_order ? ((uint64_t)v.cls << 16 | (uint64_t)v.type << 8 | lb) : 0u;
 }
 
 using KeyCount = std::unordered_map<uint64_t, uint32_t>;

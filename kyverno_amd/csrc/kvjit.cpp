@@ -85,6 +85,7 @@ struct Gen {
   // kvj_ptab evaluates globs on a register copy of the value with shared byte masks
   // (qglob_fn); KVGPU_PTAB=words keeps the per-glob word loops (A/B runs)
   bool ptab_regs = !(getenv("KVGPU_PTAB") && std::string(getenv("KVGPU_PTAB")) == "words");
+  bool ptab_trim = !(getenv("KVGPU_PTAB_TRIM") && getenv("KVGPU_PTAB_TRIM")[0] == '0');
   // hoisted lookups are branch-free (a failed guard reads cell 0 and discards it)
   // and are all placed at the top of their chunk / fused-loop body, so the loads
   // of one tree level issue together instead of one dependent wait per lookup;
@@ -630,7 +631,10 @@ struct Gen {
         << "    for (uint32_t i = 0; i < " << W << "u; i++) sw[i] = src[i < lastw ? i : lastw];\n"
         << "#pragma unroll\n"
         << "    for (uint32_t i = 0; i < " << W << "u; i++) lw[i] = sw[i];\n"
-        << "    lw[" << W << "] = src[lastw];\n";
+        << "    lw[" << W << "] = src[lastw];\n"
+        // byte masks only over the words the wave's values occupy (KVGPU_PTAB_TRIM=0: all)
+        << "    const uint32_t nwu_ = " << (ptab_trim ? "kv_wave_words(lastw, " + std::to_string(W) + "u)" : std::to_string(W) + "u")
+        << ";\n";
       for (auto& [m, ks] : groups) {
         std::set<uint32_t> bytes;
         for (uint32_t k : ks) pred_bytes(mpreds[k], &bytes);
@@ -638,7 +642,7 @@ struct Gen {
         if (!bytes.empty()) {
           o << "      " << qv->mt << " bm[" << kMaxBSlots << "];\n";
           for (uint32_t c : bytes)
-            o << "      bm[" << bslot.at(c) << "] = " << qv->bmk << "(sw, " << hex32(c * 0x01010101u) << ");\n";
+            o << "      bm[" << bslot.at(c) << "] = " << qv->bmk << "_n(sw, " << hex32(c * 0x01010101u) << ", nwu_);\n";
         } else {
           o << "      const " << qv->mt << "* bm = nullptr;\n";
         }
