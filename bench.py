@@ -167,10 +167,18 @@ def main():
                     help="skip the PMC traffic measurement (two rocprofv3 --pmc child runs of this workload)")
     ap.add_argument("--engine", choices=["vm", "specialized"], default="specialized",
                     help="bytecode interpreter kernel, or per-policy-set specialized kernels (hiprtc)")
+    ap.add_argument("--parts-per-gpu", type=int, default=1,
+                    help="in-process multi-device path only: run each device's share as this many logical "
+                         "parts on device 0 (KVGPU_SHARDS_PER_DEVICE; rehearses --gpus N on one GPU)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", str(args.gpus if args.gpus == 1 else 1)))
+    # --gpus N without a launcher (no WORLD_SIZE): one process drives the N devices through the
+    # library's own multi-device session (kv_session_create_devices: one host thread + stream per
+    # device, per-rule counts all-reduced over RCCL inside libkvgpu). Under torch.distributed.run
+    # (WORLD_SIZE set) every rank is one process on one GPU and evaluates its own shard.
+    inproc = "WORLD_SIZE" not in os.environ and args.gpus > 1
+    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
@@ -197,8 +205,8 @@ def main():
         workload = "C2: synthetic Pods x 100 validate.pattern rules (image globs, ?*, quantities, |-lists)"
     elif args.config == "c3":
         pols = workloads.c3_policies(1000)
-        kind_mix = 1
-        workload = "C3: Pods/Deployments/Services 60/25/15 x 1000 policies with match/exclude"
+        kind_mix = workloads.C3_KIND_MIX  # 1 000 namespaces
+        workload = "C3: Pods/Deployments/Services 60/25/15 over 1000 namespaces x 1000 policies with match/exclude"
     elif args.config == "c4":
         pols = workloads.c4_policies()
         kind_mix = 0
@@ -218,8 +226,10 @@ def main():
     if jit["kernels"]:
         log(f"[rank {rank}] specialized kernels: {jit['kernels']} ({jit['code_bytes'] / 1e3:.0f} KB code), "
             f"hiprtc {jit['compile_ms'] / 1e3:.1f}s")
-    # rank r evaluates the contiguous shard [r * N, (r + 1) * N) of one synthetic stream
-    data = batch.synth(workloads.SEED, args.n_res, kind_mix, first=rank * args.n_res)
+    # rank r evaluates the contiguous shard [r * N, (r + 1) * N) of one synthetic stream; the
+    # in-process path ingests [0, G * N) and the library cuts the same G shards of it
+    n_devs = args.gpus if inproc else 1
+    data = batch.synth(workloads.SEED, args.n_res * n_devs, kind_mix, first=rank * args.n_res)
     ndjson_bytes = len(data)
     t1 = time.time()
     b = batch.Batch(ps, data)
@@ -231,7 +241,19 @@ def main():
             "scopes": batch.MODE_COUNTS | batch.MODE_SCOPES}[args.mode]
 
     # device-resident session: inputs uploaded and output buffers allocated once (untimed)
-    sess = batch.Session(ps, b, device=local, mode=mode)
+    if inproc:
+        mask = (1 << args.gpus) - 1
+        if args.parts_per_gpu > 1:  # rehearsal: the G parts as logical shards of device 0
+            if args.parts_per_gpu != args.gpus:
+                raise SystemExit("--parts-per-gpu must equal --gpus (all parts on device 0)")
+            os.environ["KVGPU_SHARDS_PER_DEVICE"] = str(args.parts_per_gpu)
+            mask = 1
+        sess = batch.Session(ps, b, mode=mode, device_mask=mask)
+        if sess.n_parts != args.gpus:
+            raise SystemExit(f"multi-device session has {sess.n_parts} parts, expected {args.gpus}")
+        log(f"in-process multi-device session: {sess.n_parts} parts (device mask {mask:#x})")
+    else:
+        sess = batch.Session(ps, b, device=local, mode=mode)
     sess.run(1)
     counts = sess.counts()
     n_fail = int(counts[:, 1].sum() + counts[:, 3].sum() + counts[:, 4].sum())
@@ -265,23 +287,26 @@ def main():
         scopes = {"reports": len(summ), "fail": sum(v["fail"] for v in summ.values()),
                   "pass": sum(v["pass"] for v in summ.values())}
 
-    n_pairs_rank = b.n_res * ps.n_rules
-    value = world * n_pairs_rank * args.steps / t_max
+    n_gpus = n_devs * world
+    rehearsal = inproc and args.parts_per_gpu > 1  # G logical parts on one physical device
+    n_pairs_rank = b.n_res * ps.n_rules // n_devs  # per GPU
+    value = n_gpus * n_pairs_rank * args.steps / t_max
     # algorithmic bytes per launch: projected store read once + program tables + outputs
     prog_bytes = 0  # program/predicate tables are KB-scale (<0.01%)
     # full: 1 B status + 8 B compact error record per FAIL/ERROR/SKIP pair (kvdevtypes.h ErrRec8;
     # the rare records that do not fit also write 32 B, not counted); scopes: status written and read back
     # by the scope-count kernel (2 B per pair) + the 4 B scope index of every resource
-    out_bytes = {"full": n_pairs_rank + 8 * n_fail, "counts": 0,
-                 "scopes": 2 * n_pairs_rank + 4 * b.n_res}[args.mode]
-    b_alg = b.store_bytes + prog_bytes + out_bytes
+    out_bytes = {"full": n_pairs_rank + 8 * n_fail // n_devs, "counts": 0,
+                 "scopes": 2 * n_pairs_rank + 4 * b.n_res // n_devs}[args.mode]
+    b_alg = b.store_bytes // n_devs + prog_bytes + out_bytes  # per GPU (the slowest part's event time below)
     achieved = b_alg / (kernel_ms / 1e3) / 1e9
     traffic, traffic_src = None, None  # filled below by the in-run PMC measurement (rank 0, N=1)
     out = {
         "metric": "resource×rule validate evals/sec (node)",
         "value": value,
         "unit": "evals/s",
-        "n_gpus": world,
+        "n_gpus": 1 if rehearsal else n_gpus,
+        "parts": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": t_max / args.steps * 1e3,
@@ -290,8 +315,12 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": f"synthetic (kv_synth_range, seed 0x6B79766E, rank shard [r*N, (r+1)*N), N={args.n_res})",
-        "config": {"workload": workload, "resources_per_gpu": b.n_res, "rules": ps.n_rules,
-                   "pairs_per_gpu": n_pairs_rank, "output": args.mode, "parallelism": f"resource-shard x{world}",
+        "config": {"workload": workload, "resources_per_gpu": b.n_res // n_devs, "rules": ps.n_rules,
+                   "pairs_per_gpu": n_pairs_rank, "output": args.mode,
+                   "parallelism": (f"resource-shard x{n_gpus} (one process, kv_session_create_devices, "
+                                   f"RCCL count all-reduce in libkvgpu"
+                                   + (f", {args.parts_per_gpu} logical parts on device 0)" if args.parts_per_gpu > 1
+                                      else ")")) if inproc else f"resource-shard x{world}",
                    "engine": args.engine},
         "kernel_ms_per_step": kernel_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -305,7 +334,7 @@ def main():
     out["ingest"] = {"seconds": t2 - t1, "resources_per_s": b.n_res / (t2 - t1),
                      "MB_per_s": ndjson_bytes / (t2 - t1) / 1e6,
                      "threads": int(os.environ.get("KVGPU_INGEST_THREADS", min(16, os.cpu_count() or 1)))}
-    if rank == 0 and world == 1 and args.mode == "full" and not args.no_e2e:
+    if rank == 0 and n_gpus == 1 and args.mode == "full" and not args.no_e2e:
         # PCIe-inclusive rate of the host boundary: kv_validate on a freshly ingested
         # batch = H2D upload of the projected store + one pass + D2H of statuses and error records
         sess = None
@@ -324,12 +353,12 @@ def main():
                                   "includes": "H2D store upload + 1 pass + D2H status/error records "
                                               "(steady state: after one untimed kv_validate of another batch)"}
         del r2, b2
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
         # every core this process may run on (the GPU box grants a share of the machine's cores;
         # nproc and the CPU model are recorded beside it)
         threads = host_cpu()["available"]
         out["cpu_baseline"] = cpu_baseline(pols, args.cpu_pairs, threads, kind_mix, args.config.upper())
-    if rank == 0 and world == 1 and not args.no_traffic:
+    if rank == 0 and n_gpus == 1 and not args.no_traffic:
         # measured HBM bytes of the same workload (child rocprofv3 --pmc runs), after this
         # process's device buffers are freed
         sess = None

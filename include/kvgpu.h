@@ -179,7 +179,8 @@ int kv_session_scope_counts(kv_session* s, int64_t* counts /* [n_scopes][n_rules
 void kv_free_session(kv_session* s);
 
 /* Synthetic resource generator for the benchmark configs:
- * kind_mix 0 = Pods; 1 = Pods/Deployments/Services 60/25/15. Returns NDJSON
+ * kind_mix 0 = Pods; 1 = Pods/Deployments/Services 60/25/15 (64 namespaces each);
+ * 2 = the mixed kinds over 1 000 namespaces (C3). Returns NDJSON
  * (free with kv_free_buffer). */
 int kv_synth(uint64_t seed, uint64_t n, uint32_t kind_mix, char** json_out, size_t* len);
 /* resources [first, first + n) of the same stream (a rank's contiguous shard) */

@@ -132,11 +132,30 @@ class Batch:
             self._h = None
 
 
+class _ResultHandle:
+    """Owner of one kv_result handle: freed when the Result and every copy=False status view of
+    its buffer are gone (the view's ctypes buffer holds a reference to this object)."""
+
+    def __init__(self, h):
+        self.h = h
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            try:
+                lib().kv_free_result(h)
+            except Exception:
+                pass
+            self.h = None
+
+
 class Result:
     """kv_result: statuses [rule][res] (a copy, or with copy=False a read-only view of the library's
-    page-locked buffer, valid while this object lives), per-rule counts, failing paths / messages."""
+    page-locked buffer; the view keeps the result's buffers alive), per-rule counts, failing
+    paths / messages."""
 
     def __init__(self, h, policyset: PolicySet, batch: Batch, copy: bool = True):
+        self._owner = _ResultHandle(h)
         self._h = h
         self.policyset = policyset
         self.batch = batch
@@ -147,6 +166,7 @@ class Result:
         self.n_rules, self.n_res = nr.value, nn.value
         if p.value:
             buf = (ctypes.c_uint8 * (self.n_rules * self.n_res)).from_address(p.value)
+            buf._kv_owner = self._owner  # the view outlives this Result only together with the handle
             self.status = np.frombuffer(buf, dtype=np.uint8).reshape(self.n_rules, self.n_res)
             if copy:
                 self.status = self.status.copy()
@@ -231,14 +251,6 @@ class Result:
             return None
         return k.value, f.value
 
-    def __del__(self):
-        h = getattr(self, "_h", None)
-        if h is not None and h.value:
-            try:
-                lib().kv_free_result(h)
-            except Exception:
-                pass
-            self._h = None
 
 
 def validate(policyset: PolicySet, batch: Batch, admission: dict | None = None,

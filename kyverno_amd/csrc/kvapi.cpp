@@ -69,24 +69,14 @@ struct DevBuf {
   }
   // Host-to-device copy of a (pageable) host range. Large ranges go through a pinned staging
   // ring: host threads copy chunk i into a page-locked buffer while the DMA engine moves chunk
-  // i-1 (KVGPU_UPLOAD=pageable: one hipMemcpy, for A/B runs).
+  // i-1 (32 MB chunks, 4 buffers, up to 16 copy threads).
   static void upload_h2d(void* dst, const void* src, size_t bytes) {
-    static const std::string how = getenv("KVGPU_UPLOAD") ? getenv("KVGPU_UPLOAD") : "staged";
-    static const size_t kChunk = (size_t)(getenv("KVGPU_UPLOAD_CHUNK_MB") ? atoi(getenv("KVGPU_UPLOAD_CHUNK_MB")) : 32) << 20;
+    constexpr size_t kChunk = 32u << 20;
     constexpr size_t kMin = 16u << 20;
     constexpr int kRing = 4;
-    if (how == "pageable" || bytes < kMin || pinned_src(src, bytes)) {
+    if (bytes < kMin || pinned_src(src, bytes)) {
       HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
       return;
-    }
-    if (how == "register") {  // A/B: page-lock the source range for the copy
-      const uintptr_t a = (uintptr_t)src & ~(uintptr_t)4095, e = ((uintptr_t)src + bytes + 4095) & ~(uintptr_t)4095;
-      if (hipHostRegister((void*)a, e - a, hipHostRegisterDefault) == hipSuccess) {
-        HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
-        (void)hipHostUnregister((void*)a);
-        return;
-      }
-      (void)hipGetLastError();
     }
     static std::mutex mu;  // one staged upload at a time per process (the ring is shared)
     static char* ring[kRing] = {};
@@ -107,8 +97,7 @@ struct DevBuf {
     hipEvent_t ev[kRing];
     for (int i = 0; i < kRing; i++) HIPCHK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
     bool used[kRing] = {};
-    static const unsigned T = std::max(1u, std::min(getenv("KVGPU_UPLOAD_THREADS") ? (unsigned)atoi(getenv("KVGPU_UPLOAD_THREADS")) : 16u,
-                                                    std::thread::hardware_concurrency()));
+    static const unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     size_t k = 0;
     for (size_t off = 0; off < bytes; off += kChunk, k++) {
       const int i = (int)(k % kRing);
@@ -494,8 +483,8 @@ DevPolicySet& dev_ps(kv_policyset* s, int device) {
         int regs = 0, local = 0;
         (void)hipFuncGetAttribute(&regs, HIP_FUNC_ATTRIBUTE_NUM_REGS, f);
         (void)hipFuncGetAttribute(&local, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, f);
-        fprintf(stderr, "[kvgpu] %s: %zu rules, %d VGPRs, %d B scratch/lane\n", ch.name.c_str(),
-                ch.rules.empty() ? (size_t)(ch.rule_end - ch.rule_begin) : ch.rules.size(), regs, local);
+        fprintf(stderr, "[kvgpu] %s: %zu rules, %d VGPRs, %d B scratch/lane\n", ch.name.c_str(), ch.rules.size(), regs,
+                local);
       }
     }
     if (J.memo_words) {
@@ -780,9 +769,8 @@ struct DevSession {
   int device = 0;
   uint32_t mode = 0;
   uint64_t nrules = 0, nres = 0;
-  DevBuf fflags, pview, st, er8, er, cn, scope, scn, ptab, mtab, mtbf, part;
+  DevBuf fflags, pview, st, er8, er, cn, scope, scn, ptab, mtab, mtbf;
   DevBuf r_offs, r_tot, r_base, r_out8, r_outw, r_wide;  // record compaction (fetch)
-  uint32_t part_blocks = 0;
   uint32_t mt_words = 0, mt_entities = 0;
   uint32_t *mt_ns = nullptr, *mt_ann = nullptr, *mt_sel = nullptr;
   uint32_t nscopes = 0, nvals = 0;
@@ -847,26 +835,10 @@ struct DevSession {
       er8.alloc(nrules * nres * sizeof(ErrRec8), device);
       O.err8 = (ErrRec8*)er8.p;
       O.err = nullptr;  // full records: allocated by fetch() for the re-run pass, if some record is wide
-      if (getenv("KVGPU_JIT_STORE") && std::string(getenv("KVGPU_JIT_STORE")) == "lane") {
-        er.alloc(nrules * nres * sizeof(ErrRec), device);  // the variant writes them in every pass
-        O.err = (ErrRec*)er.p;
-      }
       O.full |= 2;
     }
     cn.alloc(std::max<uint64_t>(nrules, 1) * KV_HIST * sizeof(unsigned long long), device);
     O.counts = (unsigned long long*)cn.p;
-    O.part = nullptr;
-    O.part_pitch = 0;
-    // KVGPU_JIT_PARTIAL=1: per-workgroup partial histograms summed by one reduce kernel
-    // instead of per-workgroup atomics on the counts (A/B: C2 rule kernel -13 us, reduce
-    // +92 us, so the atomics stay the default)
-    static const bool use_part = getenv("KVGPU_JIT_PARTIAL") && getenv("KVGPU_JIT_PARTIAL")[0] == '1';
-    if (use_part && dp.specialized() && nres && nrules) {
-      part_blocks = (uint32_t)((nres + KV_WG - 1) / KV_WG);
-      part.alloc((size_t)part_blocks * nrules * KV_HIST * sizeof(uint32_t), device);
-      O.part = (uint32_t*)part.p;
-      O.part_pitch = (uint32_t)(nrules * KV_HIST);
-    }
     if (mode & KV_MODE_SCOPES) {
       // scope of every resource = its namespace index in the batch namespace table
       std::vector<uint32_t> sc(nres);
@@ -893,10 +865,7 @@ struct DevSession {
       HIPCHK(hipMemsetAsync(cn.p, 0, cn.n, stream));
       HIPCHK(launch_mtab((const DevPS*)pview.p, bview, mt_words, mt_entities, mt_ns, mt_ann, mt_sel, stream));
       if (dps->specialized()) {
-        // partial rows of rules whose kernel keeps the atomic histogram stay zero
-        if (O.part) HIPCHK(hipMemsetAsync(part.p, 0, part.n, stream));
         launch_specialized();
-        if (O.part) HIPCHK(launch_part_reduce(O.part, part_blocks, O.part_pitch, O.counts, stream));
       } else {
         HIPCHK(launch_validate((const DevPS*)pview.p, bview, (uint32_t)nres, O, 0, (uint32_t)nrules, stream));
       }
@@ -930,17 +899,7 @@ struct DevSession {
     DevOut Ov = O;
     uint32_t r0 = 0;
     void* args[] = {(void*)&P, (void*)&bview, (void*)&N, (void*)&V, (void*)&S, (void*)&Ov, (void*)&r0};
-    // KVGPU_SLICES=k: resource slices outer, rule kernels inner (a slice's rows stay
-    // cache-resident across the kernels), for A/B runs
-    const char* sz = getenv("KVGPU_SLICES");
-    const uint32_t slices = std::max<uint32_t>(1u, std::min<uint32_t>(blocks, sz ? (uint32_t)atoi(sz) : 1u));
-    for (uint32_t k = 0; k < slices; k++) {
-      const uint32_t b0 = (uint32_t)((uint64_t)blocks * k / slices), b1 = (uint32_t)((uint64_t)blocks * (k + 1) / slices);
-      if (b1 == b0) continue;
-      r0 = b0 * KV_WG;
-      for (hipFunction_t f : dps->fns)
-        HIPCHK(hipModuleLaunchKernel(f, b1 - b0, 1, 1, KV_WG, 1, 1, 0, stream, args, nullptr));
-    }
+    for (hipFunction_t f : dps->fns) HIPCHK(hipModuleLaunchKernel(f, blocks, 1, 1, KV_WG, 1, 1, 0, stream, args, nullptr));
   }
   std::vector<int64_t> read_counts() {
     HIPCHK(hipSetDevice(device));
@@ -1133,14 +1092,19 @@ struct SessionSet {
     const bool scopes = (mode & KV_MODE_SCOPES) != 0;
     if (!comms.empty()) {
       if (ncclGroupStart() != ncclSuccess) throw HipError("ncclGroupStart failed");
-      for (size_t k = 0; k < parts.size(); k++) {
+      ncclResult_t enq = ncclSuccess;  // first failed enqueue; the group is still closed below
+      for (size_t k = 0; k < parts.size() && enq == ncclSuccess; k++) {
         DevSession& d = *parts[k];
         HIPCHK(hipSetDevice(d.device));
-        ncclAllReduce(d.cn.p, d.cn.p, nrules * KV_HIST, ncclUint64, ncclSum, comms[k], d.stream);
-        if (scopes)
-          ncclAllReduce(d.scn.p, d.scn.p, (size_t)d.nscopes * nrules * KV_HIST, ncclUint64, ncclSum, comms[k], d.stream);
+        enq = ncclAllReduce(d.cn.p, d.cn.p, nrules * KV_HIST, ncclUint64, ncclSum, comms[k], d.stream);
+        if (scopes && enq == ncclSuccess)
+          enq = ncclAllReduce(d.scn.p, d.scn.p, (size_t)d.nscopes * nrules * KV_HIST, ncclUint64, ncclSum, comms[k],
+                              d.stream);
       }
-      if (ncclGroupEnd() != ncclSuccess) throw HipError("RCCL all-reduce failed");
+      const ncclResult_t end = ncclGroupEnd();
+      if (enq != ncclSuccess)
+        throw HipError(std::string("ncclAllReduce failed: ") + ncclGetErrorString(enq));
+      if (end != ncclSuccess) throw HipError(std::string("RCCL all-reduce failed: ") + ncclGetErrorString(end));
       for (auto& d : parts) {
         HIPCHK(hipSetDevice(d->device));
         HIPCHK(hipStreamSynchronize(d->stream));
@@ -1498,23 +1462,28 @@ int kv_result_error_message(const kv_result* r, uint32_t rule, uint64_t res, con
 int kv_result_subst_error(const kv_result* r, uint32_t rule, uint64_t res, char* buf, size_t cap) {
   if (!r) return KV_E_INVALID;
   if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
-  const RuleRec& rr = r->ps->ps.rules[rule];
-  if (!rr.dyn || r->status[(size_t)rule * r->n_res + res] != ST_ERROR) return 0;
-  const ResultPart* p = r->part_of(res);
-  if (!p) return 0;
-  kv_batch* kb = p->shard ? p->shard.get() : const_cast<kv_batch*>(r->b);
-  const DynHost& h = kb->dyn_host(r->ps->ps);
-  const uint64_t nl = kb->b.res.size(), local = res - p->lo;
-  const size_t q = (size_t)(rr.dyn - 1) * nl + local;
-  if (h.dyn_st[q] != ST_ERROR) return 0;
-  // ruleError(rule, Validation, "variable substitution failed", err) (validation.go:186-188)
-  const std::string m = "variable substitution failed: " + kb->b.vout_tab[h.dyn_msg[q]].substr(1);
-  if (buf && cap) {
-    size_t n = std::min(cap - 1, m.size());
-    memcpy(buf, m.data(), n);
-    buf[n] = 0;
+  if (r->status.empty()) return KV_E_INVALID;  // counts-only result: no statuses were fetched
+  try {
+    const RuleRec& rr = r->ps->ps.rules[rule];
+    if (!rr.dyn || r->status[(size_t)rule * r->n_res + res] != ST_ERROR) return 0;
+    const ResultPart* p = r->part_of(res);
+    if (!p) return 0;
+    kv_batch* kb = p->shard ? p->shard.get() : const_cast<kv_batch*>(r->b);
+    const DynHost& h = kb->dyn_host(r->ps->ps);
+    const uint64_t nl = kb->b.res.size(), local = res - p->lo;
+    const size_t q = (size_t)(rr.dyn - 1) * nl + local;
+    if (h.dyn_st[q] != ST_ERROR) return 0;
+    // ruleError(rule, Validation, "variable substitution failed", err) (validation.go:186-188)
+    const std::string m = "variable substitution failed: " + kb->b.vout_tab[h.dyn_msg[q]].substr(1);
+    if (buf && cap) {
+      size_t n = std::min(cap - 1, m.size());
+      memcpy(buf, m.data(), n);
+      buf[n] = 0;
+    }
+    return (int)m.size();
+  } catch (const std::exception&) {
+    return KV_E_INVALID;
   }
-  return (int)m.size();
 }
 
 double kv_result_kernel_ms(const kv_result* r) { return r ? r->kernel_ms : -1.0; }

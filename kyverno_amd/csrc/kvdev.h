@@ -40,8 +40,4 @@ hipError_t launch_scope_counts(const uint8_t* status, const uint32_t* scope, uin
 hipError_t launch_expand_rows(const Node* pcells, const uint64_t* rmask, const uint32_t* roff, uint64_t n_rows,
                               Node* nodes, hipStream_t stream);
 
-// counts[c] += sum over rows b < n_blocks of part[b * pitch + c], c < pitch (u32 partials)
-hipError_t launch_part_reduce(const uint32_t* part, uint32_t n_blocks, uint32_t pitch, unsigned long long* counts,
-                              hipStream_t stream);
-
 }  // namespace kv

@@ -662,15 +662,6 @@ __device__ __forceinline__ void store_err(const DevOut& O, size_t o, uint32_t ki
     return;
   }
   const uint32_t fits = (i0 < 4096u) & (i1 < 1024u) & (i2 < 1024u) & (i3 == 0u) & (key == ABSENT) & (pn < (1u << 25));
-#ifdef KV_STORE_LANE_BRANCH
-  // round-1 variant kept for the 8-wave A/B (KVGPU_JIT_STORE=lane): the full record of a
-  // record that does not fit is written in the same pass, under a per-lane branch
-  if (!fits) {
-    uint4* x = (uint4*)(O.err + o);
-    x[0] = make_uint4(kind | (flags << 16), pn, key, res);
-    x[1] = make_uint4(i0, i1, i2, i3);
-  }
-#endif
   uint2 w;
   w.x = kind | (flags << 4) | ((fits ^ 1u) << 6) | (pn << 7);
   w.y = i0 | (i1 << 12) | (i2 << 22);
@@ -721,33 +712,6 @@ __device__ __forceinline__ void kv_count_status_lds(const uint32_t* w, unsigned 
   }
 }
 
-// histogram of one rule's KV_WG status bytes written whole (8 u32, zeros included) to the
-// workgroup's partial row (kv_part_reduce_kernel sums the rows)
-__device__ __forceinline__ void kv_count_status_part(const uint32_t* w, uint32_t* out) {
-  uint32_t c[KV_HIST] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-  uint32_t cx = 0u;
-#pragma unroll 8
-  for (uint32_t i = 0; i < KV_WG / 4u; i++) {
-    const uint32_t x = w[i];
-    c[ST_PASS] += kv_count_bytes(x, 0x00000000u);
-    c[ST_FAIL] += kv_count_bytes(x, 0x01010101u);
-    c[ST_NOMATCH] += kv_count_bytes(x, 0x05050505u);
-    cx += kv_count_bytes(x, 0xFFFFFFFFu);
-  }
-  if (c[ST_PASS] + c[ST_FAIL] + c[ST_NOMATCH] + cx < (uint32_t)KV_WG) {
-    for (uint32_t i = 0; i < KV_WG / 4u; i++) {
-      const uint32_t x = w[i];
-      c[ST_WARN] += kv_count_bytes(x, 0x02020202u);
-      c[ST_ERROR] += kv_count_bytes(x, 0x03030303u);
-      c[ST_SKIP] += kv_count_bytes(x, 0x04040404u);
-      c[ST_CPU] += kv_count_bytes(x, 0x06060606u);
-    }
-  }
-  uint4* o = (uint4*)out;
-  o[0] = make_uint4(c[0], c[1], c[2], c[3]);
-  o[1] = make_uint4(c[4], c[5], c[6], c[7]);
-}
-
 // status + error record (FAIL/ERROR/SKIP) + per-rule histogram with the
 // common statuses counted by one ballot each (fused specialized kernels)
 __device__ __forceinline__ void store_result2(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, bool valid,
@@ -758,9 +722,6 @@ __device__ __forceinline__ void store_result2(const DevOut& O, uint32_t ri, uint
     if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP))
       store_err(O, o, e.kind, e.flags, e.pn, e.key, e.res, e.i0, e.i1, e.i2, e.i3);
   }
-#ifdef KV_NOHIST
-  return;  // timing A/B only (KVGPU_JIT_NOHIST=1): no per-rule histogram
-#endif
   const uint64_t m_pass = __ballot(valid && st == ST_PASS), m_fail = __ballot(valid && st == ST_FAIL);
   const uint64_t m_nm = __ballot(valid && st == ST_NOMATCH);
   const uint64_t m_rest = __ballot(valid && st != ST_PASS && st != ST_FAIL && st != ST_NOMATCH);

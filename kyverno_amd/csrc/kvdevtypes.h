@@ -95,10 +95,6 @@ struct DevOut {
   ErrRec* err;                 // [rule][res] (only records flagged ERR8_WIDE)
   unsigned long long* counts;  // [rule][8]
   uint32_t full;               // bit0 status, bit1 error records, bit2 full 32 B records (not 8 B)
-  // per-workgroup partial histograms of the specialized kernels ([block][rule * 8 + status],
-  // u32, summed into counts by kv_part_reduce_kernel), or null: atomics into counts
-  uint32_t* part;
-  uint32_t part_pitch;
 };
 
 constexpr int KV_WG = 256;

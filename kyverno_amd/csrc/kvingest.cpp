@@ -627,14 +627,12 @@ bool scan_values(const char* p, size_t n, unsigned T, std::vector<size_t>* start
 // class-homogeneous: a wave whose values no predicate of the row applies to
 // exits after one load, and the rest run the same predicate code without
 // divergence. Buckets are ordered by key and stable inside (ingest order).
-// KVGPU_VAL_ORDER=0 keeps ingest order (A/B runs)
-const bool g_val_order = [] { const char* e = getenv("KVGPU_VAL_ORDER"); return !(e && e[0] == '0'); }();
 // class, type, then length bucket of the e-form bytes (16-byte steps up to 64, <= 128,
 // longer): kvj_ptab keeps values of <= 64 / <= 128 bytes in registers, so a wave of one
 // bucket runs one path, and its byte masks cover only the words its bucket occupies
 inline uint64_t val_order_key(const Val& v) {
   const uint32_t lb = v.e_len <= 64u ? (v.e_len + 15u) / 16u : v.e_len <= 128u ? 5u : 6u;
-  return g_val_order ? ((uint64_t)v.cls << 16 | (uint64_t)v.type << 8 | lb) : 0u;
+  return (uint64_t)v.cls << 16 | (uint64_t)v.type << 8 | lb;
 }
 
 using KeyCount = std::unordered_map<uint64_t, uint32_t>;

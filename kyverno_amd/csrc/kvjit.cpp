@@ -72,34 +72,18 @@ struct Gen {
   // value-predicate memo: a leaf predicate on a scalar is a pure function of the
   // (deduplicated) Val it reads, so each one is evaluated once per distinct value
   // of the batch (kvj_ptab) and the rule kernels test one bit of the table
-  bool memo = true;
   std::vector<uint32_t> mpreds;  // memo slot -> pred
   std::map<uint32_t, uint32_t> pslot;  // pred -> memo slot
-  // leaves on a hoisted scalar read their table word(s) through a load hoisted
-  // with the cursor (issued with the other lookups of the region instead of one
-  // dependent load per rule); KVGPU_JIT_PW=0 disables, for A/B runs
-  bool pw = true;
-  // the round-1 kvj_ptab (KVGPU_PTAB=words) stages each value's bytes in LDS before its
-  // row of predicates; KVGPU_PTAB_LDS=0 reads them from global memory per glob (A/B runs)
-  bool ptab_lds = !(getenv("KVGPU_PTAB_LDS") && getenv("KVGPU_PTAB_LDS")[0] == '0');
-  // kvj_ptab evaluates globs on a register copy of the value with shared byte masks
-  // (qglob_fn); KVGPU_PTAB=words keeps the per-glob word loops (A/B runs)
-  bool ptab_regs = !(getenv("KVGPU_PTAB") && std::string(getenv("KVGPU_PTAB")) == "words");
-  bool ptab_trim = !(getenv("KVGPU_PTAB_TRIM") && getenv("KVGPU_PTAB_TRIM")[0] == '0');
-  // hoisted lookups are branch-free (a failed guard reads cell 0 and discards it)
-  // and are all placed at the top of their chunk / fused-loop body, so the loads
-  // of one tree level issue together instead of one dependent wait per lookup;
-  // KVGPU_JIT_HOIST=lazy places each just before its first use, for A/B runs
-  bool early_hoist = !(getenv("KVGPU_JIT_HOIST") && std::string(getenv("KVGPU_JIT_HOIST")) == "lazy");
-  // fused array loops software-pipelined (next element's lookups issued before this
-  // element's rules); KVGPU_JIT_PIPE=1 enables, for A/B runs (C2: rule kernel +30 %)
-  bool pipe_loops = getenv("KVGPU_JIT_PIPE") && getenv("KVGPU_JIT_PIPE")[0] == '1';
+  // Leaves on a hoisted scalar read their table word(s) through a load hoisted with the
+  // cursor (issued with the other lookups of the region instead of one dependent load
+  // per rule). Hoisted lookups are branch-free (a failed guard reads cell 0 and discards
+  // it) and are placed at the top of their chunk / fused-loop body, so the loads of one
+  // tree level issue together instead of one dependent wait per lookup.
   explicit Gen(const PolicySet& p) : ps(p) {}
 
-  // call of leaf predicate `pi` on node `n` of type `t`
+  // call of leaf predicate `pi` on node `n` of type `t` (one bit of the value-predicate table)
   std::string pred_call(uint32_t pi, const std::string& t, const std::string& n) {
-    return std::string(memo ? "m_pred_" : "g_pred_") + std::to_string(pi) +
-           (memo ? "(P, V, S, pstr, " : "(V, S, S + (" + n + ").b, pstr, ") + t + ", " + n + ")";
+    return "m_pred_" + std::to_string(pi) + "(P, V, S, pstr, " + t + ", " + n + ")";
   }
 
   // ---------------------------------------------------------------- globs
@@ -487,7 +471,7 @@ struct Gen {
       default: o << "  return false;\n"; break;
     }
     o << "}\n";
-    if (memo) {
+    {
       const uint32_t slot = (uint32_t)mpreds.size();
       mpreds.push_back(pi);
       pslot[pi] = slot;
@@ -558,11 +542,6 @@ struct Gen {
   // kvj_ptab: one lane per distinct scalar Val of the batch; evaluates every memo
   // slot's predicate on the scalar node ingest builds for that value
   // (kvingest.cpp scalar(): a = val id, b = e_off, c = e_len | NC_* flags)
-  // One grid row per 16 predicates (half a table word, stored as a u16 half):
-  // keeps the code of a row (16 inlined globs / compares) within the
-  // instruction cache — 32-predicate rows stalled on instruction fetch.
-  // KVGPU_PTAB_ROW=32: one row per table word (A/B runs)
-  const uint32_t kPtabRow = getenv("KVGPU_PTAB_ROW") && atoi(getenv("KVGPU_PTAB_ROW")) == 32 ? 32u : 16u;
   // kernel texts (name, source): each one is compiled as its own hiprtc program
   // after the helpers every kernel may use (Gen::o, the common part)
   std::vector<std::pair<std::string, std::string>> kernels;
@@ -577,14 +556,10 @@ struct Gen {
     }
   };
 
-  // predicates per kvj_ptab thread: all of them (one grid row) on the register path
-  uint32_t ptab_row_out() const { return ptab_regs ? std::max<uint32_t>(1u, (uint32_t)mpreds.size()) : kPtabRow; }
+  // predicates per kvj_ptab thread: all of them (one grid row)
+  uint32_t ptab_row_out() const { return std::max<uint32_t>(1u, (uint32_t)mpreds.size()); }
 
   void ptab_kernel() {
-    if (!ptab_regs) {  // KVGPU_PTAB=words: 16-predicate grid rows with per-glob word loops (round 1; A/B runs)
-      ptab_kernel_words();
-      return;
-    }
     // register-path predicates (helpers: emitted before the kernel text)
     for (uint32_t k = 0; k < mpreds.size(); k++) qpred_fn(mpreds[k], kQ64);
     for (uint32_t k = 0; k < mpreds.size(); k++) qpred_fn(mpreds[k], kQ128);
@@ -632,9 +607,8 @@ struct Gen {
         << "#pragma unroll\n"
         << "    for (uint32_t i = 0; i < " << W << "u; i++) lw[i] = sw[i];\n"
         << "    lw[" << W << "] = src[lastw];\n"
-        // byte masks only over the words the wave's values occupy (KVGPU_PTAB_TRIM=0: all)
-        << "    const uint32_t nwu_ = " << (ptab_trim ? "kv_wave_words(lastw, " + std::to_string(W) + "u)" : std::to_string(W) + "u")
-        << ";\n";
+        // byte masks only over the words the wave's values occupy
+        << "    const uint32_t nwu_ = kv_wave_words(lastw, " << W << "u);\n";
       for (auto& [m, ks] : groups) {
         std::set<uint32_t> bytes;
         for (uint32_t k : ks) pred_bytes(mpreds[k], &bytes);
@@ -663,63 +637,6 @@ struct Gen {
     o << "  }\n  }\n";
     for (uint32_t i = 0; i < nw; i++) o << "  PT[(size_t)" << i << "u * NV + v] = w[" << i << "];\n";
     o << "}\n\n";
-  }
-
-  void ptab_kernel_words() {
-    KernelText kt(*this, "kvj_ptab");
-    o << "extern \"C\" __global__ __launch_bounds__(KV_WG) void kvj_ptab(const DevPS* __restrict__ Pp, "
-         "const Val* __restrict__ V, const uint8_t* __restrict__ S, uint32_t NV, uint32_t* __restrict__ PT) {\n"
-      << "  const uint32_t v = blockIdx.x * KV_WG + threadIdx.x;\n"
-      << "  if (v >= NV) return;\n"
-      << "  // Vals are numbered grouped by class (kvingest.cpp val_order_key): most waves\n"
-      << "  // are uniform in vc, and a wave no predicate of its row applies to stops here\n"
-      << "  const uint32_t vc = V[v].cls;\n"
-      << "  uint32_t rm = 0u;\n"
-      << "  switch (blockIdx.y) {\n";
-    auto pm = [&](uint32_t k) { auto it = pmask.find(mpreds[k]); return it == pmask.end() ? 0xFFFFFFFFu : it->second; };
-    for (uint32_t k0 = 0; k0 < mpreds.size(); k0 += kPtabRow) {
-      const uint32_t k1 = (uint32_t)std::min<size_t>(k0 + kPtabRow, mpreds.size());
-      uint32_t wm = 0;
-      for (uint32_t q = k0; q < k1; q++) wm |= pm(q);
-      o << "    case " << (k0 / kPtabRow) << "u: rm = " << u32(wm) << "; break;\n";
-    }
-    o << "    default: break;\n  }\n"
-      << "  uint32_t w = 0u;\n"
-      << "  if (" << (getenv("KVGPU_PTAB_EARLY") && getenv("KVGPU_PTAB_EARLY")[0] == '0' ? "true" : "vc & rm") << ") {\n"
-      << "  const uint8_t* __restrict__ pstr = Pp->pstr;\n"
-      << "  const Val& val = V[v];\n"
-      << "  const uint32_t type = val.type;\n"
-      << "  Node n{type, v, val.e_off, val.e_len};\n"
-      << "  if (val.flags & VF_ASCII_E) n.c |= NC_ASCII_E;\n"
-      << "  if (val.flags & VF_BOOLV) n.c |= NC_BOOLV;\n"
-      << "  if (val.flags & VF_NILLIKE) n.c |= NC_NILLIKE;\n"
-      << "  const uint8_t* __restrict__ E = S + val.e_off;\n";
-    if (ptab_lds) {
-      // Stage the value's bytes (<= 64 B, plus the one word the word-wise globs read
-      // past the end) in LDS once: the row's predicates then re-read them from LDS
-      // instead of re-issuing global loads per glob. Odd word stride: no bank conflicts.
-      o << "  __shared__ uint32_t lds_e[KV_WG * 17];\n"
-        << "  if (val.e_len <= 64u) {\n"
-        << "    const uint32_t* __restrict__ src = (const uint32_t*)E;\n"
-        << "    uint32_t* dst = lds_e + threadIdx.x * 17u;\n"
-        << "    const uint32_t nw = (val.e_len + 3u) / 4u + 1u;\n"
-        << "    for (uint32_t i = 0; i < nw; i++) dst[i] = src[i];\n"
-        << "    E = (const uint8_t*)dst;\n"
-        << "  }\n";
-    }
-    o << "  switch (blockIdx.y) {\n";
-    for (uint32_t k0 = 0; k0 < mpreds.size(); k0 += kPtabRow) {
-      const uint32_t k1 = (uint32_t)std::min<size_t>(k0 + kPtabRow, mpreds.size());
-      o << "    case " << (k0 / kPtabRow) << "u:\n";
-      for (uint32_t k = k0; k < k1; k++)
-        o << "      if ((vc & " << u32(pm(k)) << ") && g_pred_" << mpreds[k] << "(V, S, E, pstr, type, n)) w |= "
-          << u32(1u << (k % kPtabRow)) << ";\n";
-      o << "      break;\n";
-    }
-    o << "    default: break;\n  }\n  }\n"
-      << (kPtabRow == 32 ? "  PT[(size_t)blockIdx.y * NV + v] = w;\n}\n\n"
-                         : "  // row y = bits [16 (y % 2), +16) of table word y / 2 (little-endian u16 halves)\n"
-                           "  ((uint16_t*)PT)[((size_t)(blockIdx.y >> 1) * NV + v) * 2u + (blockIdx.y & 1u)] = (uint16_t)w;\n}\n\n");
   }
 
   // dynamic leaves (pattern variables, kvvars.cpp): the generic predicate evaluator on the
@@ -820,203 +737,6 @@ struct Gen {
     return pc;
   }
 
-  void rule_fn(uint32_t ri) {
-    const RuleRec& rr = ps.rules[ri];
-    const uint32_t b = rr.prog, e = prog_end(ps, rr.prog);
-    uint32_t maxd = 1;
-    for (uint32_t pc = b; pc <= e; pc++) {
-      const Inst& in = ps.prog[pc];
-      const uint32_t op = in.op & 0xFF, d = (in.op >> 8) & 0xFF;
-      maxd = std::max(maxd, d + 2);
-      if (op == OP_LEAF) pred_fn(in.a);
-    }
-    o << "__device__ __forceinline__ uint32_t g_rule_" << ri
-      << "(const DevPS& P, const DevBatch& B, const Node* __restrict__ N, const Val* __restrict__ V, "
-         "const uint8_t* __restrict__ S, uint32_t root, uint32_t r, EState& e) {\n"
-      << "  const uint32_t n_res = B.n_res; (void)n_res; (void)r;\n";
-    o << "  uint32_t c0 = root";
-    for (uint32_t d = 1; d < maxd; d++) o << ", c" << d << " = ABSENT";
-    o << ";\n  uint32_t lf0 = 0u, lf1 = 0u, lf2 = 0u, lf3 = 0u, ll0 = 0u, ll1 = 0u, ll2 = 0u, ll3 = 0u;\n"
-      << "  uint32_t li0 = 0u, li1 = 0u, li2 = 0u, li3 = 0u, keynode = ABSENT;\n"
-      << "  uint64_t areg = 0ull, apres = 0ull;\n"
-      << "  const uint8_t* __restrict__ pstr = P.pstr;\n"
-      << "  (void)P; (void)B; (void)pstr; (void)lf0; (void)lf1; (void)lf2; (void)lf3; (void)ll0; (void)ll1; (void)ll2; "
-         "(void)ll3; (void)keynode;\n";
-    auto C = [](uint32_t d) { return "c" + std::to_string(d); };
-    auto L = [](uint32_t pc) { return "L" + std::to_string(pc); };
-    auto raise = [&](const std::string& kind, uint32_t pn, const std::string& res, uint32_t catch_pc) {
-      if (catch_pc < b || catch_pc > e) throw std::runtime_error("kvjit: raising op without a catch target");
-      std::ostringstream r;
-      r << "{ e.kind = " << kind << "; e.flags = 0u; e.pn = " << u32(pn) << "; e.res = " << res
-        << "; e.key = keynode; e.i0 = li0; e.i1 = li1; e.i2 = li2; e.i3 = li3; goto " << L(catch_pc) << "; }";
-      return r.str();
-    };
-    for (uint32_t pc = b; pc <= e; pc++) {
-      const Inst& in = ps.prog[pc];
-      const uint32_t op = in.op & 0xFF, d = (in.op >> 8) & 0xFF, aux = (in.op >> 16) & 0xFF;
-      const std::string cd = C(d), cn = C(d + 1);
-      const std::string lv = std::to_string(aux & 3);
-      o << L(pc) << ":;\n";
-      switch (op) {
-        case OP_MAPCHK:
-        case OP_ARRCHK:
-          o << "  if (" << cd << " == ABSENT || node_type(N[" << cd << "].kt) != " << (op == OP_MAPCHK ? "NT_MAP" : "NT_ARR")
-            << ") " << raise(op == OP_MAPCHK ? "E_TYPE_MAP" : "E_TYPE_ARR", in.a, cd, in.c) << "\n";
-          break;
-        case OP_AREG: {
-          const std::string bit = "(1ull << " + std::to_string(aux & 63) + ")";
-          o << "  areg |= " << bit << "; if (lookup_op(N, " << cd << ", " << u32(in.a) << ", " << u32(aux)
-            << ") != ABSENT) apres |= " << bit << ";\n";
-          break;
-        }
-        case OP_KEY:
-          o << "  " << cn << " = lookup_op(N, " << cd << ", " << u32(in.a) << ", " << u32(aux) << "); if (" << cn
-            << " == ABSENT) goto " << L(in.b) << ";\n";
-          break;
-        case OP_KEYV:
-          o << "  " << cn << " = lookup_op(N, " << cd << ", " << u32(in.a) << ", " << u32(aux) << ");\n";
-          break;
-        case OP_KEYGLOB:
-          o << "  { uint32_t nd_; if (!keyglob_op(P, B, N, " << cd << ", " << u32(in.op) << ", " << u32(in.a) << ", "
-            << u32(in.c) << ", &nd_, &keynode)) goto " << L(in.b) << "; " << cn << " = nd_; }\n";
-          break;
-        case OP_SCOPE_END:
-          // c == 0: no wake-up target (interpreter: the lane keeps running)
-          if (in.c == 0) o << "  if (e.kind) e.flags |= " << u32(aux) << ";\n";
-          else o << "  if (e.kind) { e.flags |= " << u32(aux) << "; goto " << L(in.c) << "; }\n";
-          break;
-        case OP_POS_END:
-          o << "  if (e.kind) { if (e.flags & EF_COND) e.kind = 0u; else goto " << L(in.c) << "; }\n";
-          break;
-        case OP_NEG:
-          o << "  if (lookup_op(N, " << cd << ", " << u32(in.a) << ", " << u32(aux) << ") != ABSENT) "
-            << raise("E_NEG", in.b, "ABSENT", in.c) << "\n";
-          break;
-        case OP_STAR:
-          o << "  if (" << cn << " == ABSENT || node_type(N[" << cn << "].kt) == NT_NULL) "
-            << raise("E_STAR", in.b, "ABSENT", in.c) << "\n";
-          break;
-        case OP_LEAF:
-          o << "  { Node vn_{0u, 0u, 0u, 0u}; if (" << cd << " != ABSENT) vn_ = N[" << cd << "];\n"
-            << "    const uint32_t vt_ = node_type(vn_.kt); bool ok_;\n"
-            << "    if (vt_ == NT_ARR) { ok_ = true; for (uint32_t k_ = 0; k_ < vn_.b && ok_; k_++) { const Node en_ = N[ni(vn_.a + k_)]; "
-            << "ok_ = " << pred_call(in.a, "node_type(en_.kt)", "en_") << "; } }\n"
-            << "    else ok_ = " << pred_call(in.a, "vt_", "vn_") << ";\n"
-            << "    if (!ok_) " << raise("E_VALUE", in.b, cd, in.c) << " }\n";
-          break;
-        case OP_VLEAF:
-          dleaf_fn();
-          o << "  { Node vn_{0u, 0u, 0u, 0u}; if (" << cd << " != ABSENT) vn_ = N[" << cd << "];\n"
-            << "    if (!g_dleaf_0(B, N, B.dleaf[(size_t)" << u32(in.a) << " * n_res + r], vn_)) "
-            << raise("E_VALUE", in.b, cd, in.c) << " }\n";
-          break;
-        case OP_RAISE:
-          o << "  " << raise(u32(in.b), in.a, cd, in.c) << "\n";
-          break;
-        case OP_EXISTCHK:
-          o << "  if (" << cd << " == ABSENT || node_type(N[" << cd << "].kt) != NT_ARR) "
-            << raise("E_EXIST_RESTYPE", in.a, cd, in.c) << "\n";
-          break;
-        case OP_LENCHK:
-          o << "  if (N[" << cd << "].b < " << u32(in.a) << ") " << raise("E_LEN", in.b, cd, in.c) << "\n";
-          break;
-        case OP_INDEX:
-          o << "  " << cn << " = ni(N[" << cd << "].a + " << u32(in.a) << ");\n";
-          break;
-        case OP_LOOP_BEGIN:
-        case OP_EXIST_BEGIN:
-          o << "  { const Node an_ = N[" << cd << "]; lf" << lv << " = an_.a; ll" << lv << " = an_.b; li" << lv
-            << " = 0u;\n    if (an_.b == 0u) ";
-          if (op == OP_LOOP_BEGIN) o << "goto " << L(in.a + 1) << ";";
-          else o << raise("E_EXIST_FAIL", in.b, cd, in.c);
-          o << "\n    " << cn << " = ni(an_.a); }\n";
-          break;
-        case OP_LOOP_END:
-          o << "  if (e.kind) { if (e.flags & EF_COND) e.kind = 0u; else goto " << L(in.c) << "; }\n"
-            << "  if (li" << lv << " + 1u < ll" << lv << ") { li" << lv << "++; " << cn << " = ni(lf" << lv << " + li" << lv
-            << "); goto " << L(in.a + 1) << "; }\n";
-          break;
-        case OP_EXIST_END:
-          o << "  if (!e.kind) goto " << L(pc + 1) << ";\n  e.kind = 0u;\n"
-            << "  if (li" << lv << " + 1u < ll" << lv << ") { li" << lv << "++; " << cn << " = ni(lf" << lv << " + li" << lv
-            << "); goto " << L(in.a + 1) << "; }\n"
-            << "  " << raise("E_EXIST_FAIL", in.b, cd, in.c) << "\n";
-          break;
-        case OP_ALT_BEGIN:
-          o << "  e.kind = 0u; e.flags = 0u; areg = 0ull; apres = 0ull;\n";
-          break;
-        case OP_ALT_END:
-          o << "  if (e.kind == 0u) return ST_PASS;\n  if (e.kind == E_CPU) return ST_CPU;\n";
-          if (in.b) o << "  return ST_FAIL;\n";
-          else o << "  e.kind = 0u; e.flags = 0u; areg = 0ull; apres = 0ull;\n";
-          break;
-        case OP_DONE:
-          o << "  if (e.kind == 0u) return ST_PASS;\n"
-            << "  if (e.kind == E_CPU) return ST_CPU;\n"
-            << "  if (e.flags & (EF_COND | EF_GLOBAL)) return ST_SKIP;\n"
-            << "  if (areg & ~apres) return ST_ERROR;\n"
-            << "  if (e.kind == E_LEN) return ST_ERROR;\n"
-            << "  return ST_FAIL;\n";
-          break;
-        default:  // OP_NOP, OP_METACHK (handled per resource by RF_BAD_META)
-          break;
-      }
-    }
-    o << "}\n\n";
-  }
-
-  void chunk_kernel(const JitChunk& ch) {
-    KernelText kt(*this, ch.name);
-    const uint32_t nr = ch.rule_end - ch.rule_begin;
-    o << "extern \"C\" __global__ __launch_bounds__(KV_WG) void " << ch.name
-      << "(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp, const Node* __restrict__ N, "
-         "const Val* __restrict__ V, const uint8_t* __restrict__ S, DevOut O, uint32_t r0) {\n"
-      << "  __shared__ uint32_t s_hist[" << nr << "][KV_HIST];\n"
-      << "  const DevPS& P = *Pp;\n  const DevBatch& B = *Bp;\n"
-      << "  for (uint32_t q = threadIdx.x; q < " << nr << "u * KV_HIST; q += KV_WG) (&s_hist[0][0])[q] = 0u;\n"
-      << "  __syncthreads();\n"
-      << "  const uint32_t r = r0 + blockIdx.x * KV_WG + threadIdx.x;\n"
-      << "  const uint32_t n_res = B.n_res;\n"
-      << "  const bool valid = r < n_res;\n"
-      << "  const Res* __restrict__ R = B.res + (valid ? r : 0u);\n"
-      << "  uint32_t root = ABSENT, rkind = KEY_NONE, rflags = 0u;\n"
-      << "  if (valid) { root = ni(R->root); rkind = R->kind; rflags = R->flags; }\n";
-    for (uint32_t ri = ch.rule_begin; ri < ch.rule_end; ri++) {
-      const RuleRec& rr = ps.rules[ri];
-      o << "  { // rule " << ri << "\n"
-        << "    uint32_t st = ST_NOMATCH;\n"
-        << "    EState e{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u};\n"
-        << "    if (valid && g_match_" << ri << "(P, B, R, rkind, rflags)) {\n";
-      switch (rr.route) {
-        case 1: o << "      st = ST_CPU;\n"; break;
-        case 2: o << "      st = ST_NOMATCH;\n"; break;
-        case 3: o << "      st = " << u32(rr.const_status) << ";\n"; break;
-        default:
-          o << "      if (rflags & RF_MAGIC) st = ST_CPU;\n";
-          if (rr.flags & RR_META_EXPAND) o << "      else if (rflags & " << u32(meta_bad_flags(rr.flags)) << ") st = ST_CPU;\n";
-          if (rr.dyn) o << "      else if (B.dyn_st[(size_t)" << (rr.dyn - 1) << "u * n_res + r]) st = B.dyn_st[(size_t)"
-                        << (rr.dyn - 1) << "u * n_res + r];\n";
-          o << "      else st = g_rule_" << ri << "(P, B, N, V, S, root, r, e);\n";
-          break;
-      }
-      o << "    }\n"
-        << "    store_result(O, " << ri << "u, n_res, r, valid, st, e, &s_hist[" << (ri - ch.rule_begin) << "][0]);\n"
-        << "  }\n";
-    }
-    // KVGPU_JIT_NOATOMIC=1: no per-workgroup count flush (wrong counts; timing A/B only)
-    static const bool no_flush = getenv("KVGPU_JIT_NOATOMIC") && getenv("KVGPU_JIT_NOATOMIC")[0] == '1';
-    if (no_flush) {
-      o << "}\n\n";
-      hist_lds = false;
-      return;
-    }
-    o << "  __syncthreads();\n"
-      << "  for (uint32_t q = threadIdx.x; q < " << nr << "u * KV_HIST; q += KV_WG) {\n"
-      << "    const uint32_t v = (&s_hist[0][0])[q];\n"
-      << "    if (v) atomicAdd(&O.counts[(size_t)" << ch.rule_begin << "u * KV_HIST + q], (unsigned long long)v);\n"
-      << "  }\n}\n\n";
-  }
-
   // ================================================================ fused chunk kernels
   // All rules of a chunk run in one kernel body as interleaved sequential
   // programs. Rules never interact, so any interleaving that keeps each rule's
@@ -1073,21 +793,14 @@ struct Gen {
       c << "  if (node_type(" << p.node << ".kt) == NT_MAP) for (uint32_t q_ = 0u; q_ < " << p.node << ".b; q_++) { "
         << "const uint32_t c_ = ni(" << p.node << ".a + q_); const Node t_ = N[c_]; if (node_key(t_.kt) == " << u32(a)
         << ") { " << h.idx << " = c_; " << h.node << " = t_; break; } }\n";
-    } else if (early_hoist) {
+    } else {
       // the loaded node passes through v_perm (keep / zero) instead of a select,
       // which the compiler would turn into a branch around a narrowed reload
-      // below the root, a chunk's lookups run only on lanes where one of its rules matched
-      // (`ca_`): other lanes read cell 0 (one shared cached line) instead of their rows
-      const std::string guard = root_guard && p.node == "rootn" ? "ca_ && " : "";
-      c << "  { const bool ok_ = " << guard << "node_type(" << p.node << ".kt) == NT_MAP && " << u32(a) << " < " << p.node << ".b; "
+      c << "  { const bool ok_ = node_type(" << p.node << ".kt) == NT_MAP && " << u32(a) << " < " << p.node << ".b; "
         << "const uint32_t c_ = ok_ ? ni(" << p.node << ".a + " << u32(a) << ") : 0u; const Node t_ = N[c_]; "
         << "const bool hit_ = ok_ && node_type(t_.kt) != NT_ABSENT; const uint32_t m_ = hit_ ? 0x07060504u : 0x0c0c0c0cu; "
         << h.idx << " = hit_ ? c_ : ABSENT; " << h.node << " = Node{__builtin_amdgcn_perm(t_.kt, 0u, m_), "
         << "__builtin_amdgcn_perm(t_.a, 0u, m_), __builtin_amdgcn_perm(t_.b, 0u, m_), __builtin_amdgcn_perm(t_.c, 0u, m_)}; }\n";
-    } else {
-      c << "  if (node_type(" << p.node << ".kt) == NT_MAP && " << u32(a) << " < " << p.node << ".b) { "
-        << "const uint32_t c_ = ni(" << p.node << ".a + " << u32(a) << "); const Node t_ = N[c_]; "
-        << "if (node_type(t_.kt) != NT_ABSENT) { " << h.idx << " = c_; " << h.node << " = t_; } }\n";
     }
     T.code.push_back(c.str());
     T.vars.emplace(ex, h);
@@ -1107,17 +820,10 @@ struct Gen {
   };
 
   HoistTable* gT = nullptr;  // global (root-derived) hoist table of the current chunk
-  HoistTable* shared_global = nullptr;  // the group kernel's table (KVGPU_JIT_SHARED_HOIST=1)
-  // root lookups of a chunk guarded by its activity `ca_` (KVGPU_JIT_GUARD=1, A/B: C2 +1 %,
-  // C3 +3.6 %, C4 +0.6 % — the kernels are not bound by those loads)
-  bool root_guard = false;
-  bool guard_on = getenv("KVGPU_JIT_GUARD") && getenv("KVGPU_JIT_GUARD")[0] == '1';
   // per-rule histogram of a group kernel from its statuses staged in LDS (one byte per rule and
-  // lane, counted once at the end: kv_count_status_lds) instead of ballots + LDS atomics per
-  // rule and wave; KVGPU_JIT_HIST=ballot keeps the ballots (A/B runs)
+  // lane, counted once at the end: kv_count_status_lds); kernels of more than 192 rules (48 KB of
+  // status bytes) count with ballots + LDS atomics per rule and wave instead
   bool hist_lds = false;
-  bool hist_lds_on = !(getenv("KVGPU_JIT_HIST") && std::string(getenv("KVGPU_JIT_HIST")) == "ballot");
-  bool share_hoist = getenv("KVGPU_JIT_SHARED_HOIST") && getenv("KVGPU_JIT_SHARED_HOIST")[0] == '1';
 
   void emit_region(RGen& g, const Region& R, std::ostringstream& w) {
     const std::string& s = g.s;
@@ -1241,19 +947,15 @@ struct Gen {
             w << "  { const Node vn_ = " << NODE(d) << ";\n";
             auto sl = pslot.find(in.a);
             HoistTable* T = table_for(d);
-            if (memo && pw && sl != pslot.end() && T) {
+            if (sl != pslot.end() && T) {
               const uint32_t word = sl->second / 32;
               const std::string wv = g.hv[d].node + "_w" + std::to_string(word);
               const std::string hn = g.hv[d].node;
               if (T->words.insert(wv).second) {
                 const std::string off = std::to_string(word) + "u * P.n_vals + ";
-                if (early_hoist)
-                  T->code.push_back("  const uint32_t " + wv + " = __builtin_amdgcn_perm(kv_gld(P.ptab, (size_t)" + off +
-                                    "(node_type(" + hn + ".kt) - 1u < 4u ? " + hn + ".a : 0u)), 0u, node_type(" + hn +
-                                    ".kt) - 1u < 4u ? 0x07060504u : 0x0c0c0c0cu);\n");
-                else
-                  T->code.push_back("  const uint32_t " + wv + " = node_type(" + hn + ".kt) - 1u < 4u ? kv_gld(P.ptab, (size_t)" +
-                                    off + hn + ".a) : 0u;\n");
+                T->code.push_back("  const uint32_t " + wv + " = __builtin_amdgcn_perm(kv_gld(P.ptab, (size_t)" + off +
+                                  "(node_type(" + hn + ".kt) - 1u < 4u ? " + hn + ".a : 0u)), 0u, node_type(" + hn +
+                                  ".kt) - 1u < 4u ? 0x07060504u : 0x0c0c0c0cu);\n");
               }
               scalar = "(vt_ - 1u < 4u ? ((" + wv + " >> " + std::to_string(sl->second % 32) + "u) & 1u) != 0u : " +
                        "([&]() -> bool { __builtin_assume(vt_ - 1u >= 4u); return g_pred_" + std::to_string(in.a) +
@@ -1382,13 +1084,9 @@ struct Gen {
   std::string fused_block(const JitChunk& ch, uint32_t hbase) {
     const uint32_t nr = (uint32_t)ch.rules.size();
     std::vector<RGen> gs;
-    HoistTable local;
-    local.prefix = "g";
-    // group kernels may share one root-derived table over all their chunks (kernel-level
-    // declarations, loaded once per lane instead of once per chunk)
-    HoistTable& global = shared_global ? *shared_global : local;
+    HoistTable global;
+    global.prefix = "g";
     gT = &global;
-    root_guard = guard_on && early_hoist && !shared_global;
     size_t K = 0;
     for (uint32_t ri : ch.rules) {
       if (ps.rules[ri].route != 0) continue;
@@ -1438,8 +1136,6 @@ struct Gen {
         R.se = "R" + std::to_string(g.ri) + "_S" + std::to_string(k);
         std::ostringstream w;
         emit_region(g, R, w);
-        // hoisted lookups first used by this segment (lazy placement), then the resume dispatch
-        if (!early_hoist) seg << global.flush();
         seg << "  // rule " << g.ri << " stage " << k << "\n  switch (rs" << g.s << ") {\n";
         if (k == 0) seg << "    case " << u32(g.b) << ": goto R" << g.ri << "_L" << g.b << ";\n";
         for (uint32_t t : g.resume)
@@ -1447,7 +1143,7 @@ struct Gen {
         seg << "    default: goto " << R.se << ";\n  }\n" << w.str() << R.se << ":;\n";
         if (k == g.loops.size()) seg << store(g.ri);  // the rule has finished for every lane
       }
-      body << (shared_global ? std::string() : global.flush()) << seg.str();
+      body << global.flush() << seg.str();
       if (k == K) break;
       // fused loops of stage k: group rules by the symbolic array cursor
       std::map<std::string, std::vector<RGen*>> groups;
@@ -1488,7 +1184,6 @@ struct Gen {
           std::ostringstream w;
           emit_region(g, R, w);
           const Inst& end = ps.prog[le];
-          if (!early_hoist) bodies << T.flush();
           bodies << "    if (rs" << g.s << " & ACT_) {\n      c" << (d + 1) << g.s << " = el" << tag << ";\n"
                  << w.str() << "R" << g.ri << "_L" << le << ":;\n"
                  << "      if (ek" << g.s << " & 15u) { if (ek" << g.s << " & " << u32(EF_COND << 4) << ") ek" << g.s
@@ -1502,47 +1197,10 @@ struct Gen {
              << "    uint32_t fn" << tag << " = 0u, ff" << tag << " = 0u;\n    if ((0u";
         for (RGen* gp : grp) body << " | rs" << gp->s;
         body << ") & ACT_) { const Node an_ = " << arr_node << "; ff" << tag << " = an_.a; fn" << tag << " = an_.b; }\n";
-        if (!pipe_loops || !early_hoist || T.code.empty()) {
-          body << "    for (uint32_t fli" << tag << " = 0u; fli" << tag << " < fn" << tag << "; fli" << tag << "++) {\n"
-               << "      const uint32_t el" << tag << " = ni(ff" << tag << " + fli" << tag << ");\n"
-               << "      const Node eln" << tag << " = N[el" << tag << "];\n"
-               << T.flush() << bodies.str() << "    }\n";
-        } else {
-          // software-pipelined: the element node and the hoisted lookups of element i + 1 are
-          // issued before the rules run on element i (a second copy of the hoist statements
-          // under renamed variables, rotated at the end of the iteration), so one element's
-          // dependent loads overlap the previous element's compares instead of stalling the wave
-          const std::string hs = T.flush();
-          auto rename = [&](std::string t) {
-            auto repl = [&](const std::string& a, const std::string& b) {
-              for (size_t q = t.find(a); q != std::string::npos; q = t.find(a, q + b.size())) t.replace(q, a.size(), b);
-            };
-            repl(T.prefix, T.prefix + "n");
-            repl("eln" + tag, "elnX" + tag);
-            repl("el" + tag, "elX" + tag);
-            return t;
-          };
-          auto unconst = [&](std::string t) {  // word loads become assignable (rotated)
-            const std::string a = "const uint32_t " + T.prefix;
-            for (size_t q = t.find(a); q != std::string::npos; q = t.find(a, q + 1)) t.erase(q, 6);
-            return t;
-          };
-          body << "    uint32_t el" << tag << " = ni(ff" << tag << ");\n"
-               << "    Node eln" << tag << " = N[el" << tag << "];\n"
-               << unconst(hs)
-               << "    for (uint32_t fli" << tag << " = 0u; fli" << tag << " < fn" << tag << "; fli" << tag << "++) {\n"
-               << "      const uint32_t elX" << tag << " = ni(ff" << tag << " + (fli" << tag << " + 1u < fn" << tag
-               << " ? fli" << tag << " + 1u : fli" << tag << "));\n"
-               << "      const Node elnX" << tag << " = N[elX" << tag << "];\n"
-               << rename(hs) << bodies.str();
-          body << "      el" << tag << " = elX" << tag << "; eln" << tag << " = elnX" << tag << ";\n";
-          for (auto& [ex, hv] : T.vars) {
-            const std::string nidx = rename(hv.idx), nnode = rename(hv.node);
-            body << "      " << hv.idx << " = " << nidx << "; " << hv.node << " = " << nnode << ";\n";
-          }
-          for (const std::string& wv : T.words) body << "      " << wv << " = " << rename(wv) << ";\n";
-          body << "    }\n";
-        }
+        body << "    for (uint32_t fli" << tag << " = 0u; fli" << tag << " < fn" << tag << "; fli" << tag << "++) {\n"
+             << "      const uint32_t el" << tag << " = ni(ff" << tag << " + fli" << tag << ");\n"
+             << "      const Node eln" << tag << " = N[el" << tag << "];\n"
+             << T.flush() << bodies.str() << "    }\n";
         for (RGen* gp : grp) body << "    rs" << gp->s << " &= ~ACT_;\n";
         body << "  }\n";
       }
@@ -1602,12 +1260,6 @@ struct Gen {
     // rules of other routes are final after match / route
     for (uint32_t ri : ch.rules)
       if (ps.rules[ri].route != 0) k << store(ri);
-    if (root_guard) {  // some rule of the chunk still runs on this lane (rs below FIN)
-      k << "  const bool ca_ = ((FIN_";
-      for (uint32_t ri : ch.rules) k << " & rs_" << ri;
-      k << ") & FIN_) != FIN_;\n";
-    }
-    root_guard = false;
     k << body.str();
     return k.str();
   }
@@ -1618,17 +1270,13 @@ struct Gen {
   void group_kernel(const std::string& name, const std::vector<const JitChunk*>& chs, int waves) {
     std::vector<std::string> blocks;
     std::vector<uint32_t> rules;
-    HoistTable shared;
-    shared.prefix = "g";
-    if (share_hoist && early_hoist) shared_global = &shared;
     uint32_t nr_all = 0;
     for (const JitChunk* c : chs) nr_all += (uint32_t)c->rules.size();
-    hist_lds = hist_lds_on && nr_all * 256u <= 48u * 1024u;  // <= 48 KB of status bytes
+    hist_lds = nr_all * 256u <= 48u * 1024u;  // <= 48 KB of status bytes
     for (const JitChunk* c : chs) {
       blocks.push_back(fused_block(*c, (uint32_t)rules.size()));
       rules.insert(rules.end(), c->rules.begin(), c->rules.end());
     }
-    shared_global = nullptr;
     const uint32_t nr = (uint32_t)rules.size();
     KernelText kt(*this, name);
     o << "__device__ const uint32_t " << name << "_rules[" << nr << "] = {";
@@ -1651,37 +1299,23 @@ struct Gen {
     // Workgroup b runs tile (b % 8) * n/8 + b / 8, so each XCD (blocks b, b+8, ... share one)
     // walks a contiguous resource range and its L2 sees the values those resources share
     // (the value table and ptab lines are numbered by first occurrence): C2 -0.6 %, C3 -1 %
-    // per pass, traffic -1 %; KVGPU_JIT_XCD=0 keeps block b on tile b (A/B runs)
-    static const bool xcd_map = !(getenv("KVGPU_JIT_XCD") && getenv("KVGPU_JIT_XCD")[0] == '0');
-    if (xcd_map)
-      o << "  const uint32_t nb_ = gridDim.x, x_ = blockIdx.x & 7u, per_ = nb_ >> 3, rem_ = nb_ & 7u;\n"
-        << "  const uint32_t bx_ = x_ * per_ + (x_ < rem_ ? x_ : rem_) + (blockIdx.x >> 3);\n";
-    else
-      o << "  const uint32_t bx_ = blockIdx.x;\n";
+    // per pass, traffic -1 %
+    o << "  const uint32_t nb_ = gridDim.x, x_ = blockIdx.x & 7u, per_ = nb_ >> 3, rem_ = nb_ & 7u;\n"
+      << "  const uint32_t bx_ = x_ * per_ + (x_ < rem_ ? x_ : rem_) + (blockIdx.x >> 3);\n";
     o << "  const uint32_t r = r0 + bx_ * KV_WG + threadIdx.x;\n"
       << "  const uint32_t n_res = B.n_res;\n"
       << "  const bool valid = r < n_res;\n"
       << "  const Res* __restrict__ R = B.res + (valid ? r : 0u);\n"
       << "  uint32_t root = ABSENT, rkind = KEY_NONE, rflags = 0u;\n"
       << "  if (valid) { root = ni(R->root); rkind = R->kind; rflags = R->flags; }\n"
-      << "  Node rootn{0u, 0u, 0u, 0u};\n  if (valid) rootn = N[root];\n"
-      << shared.flush();
+      << "  Node rootn{0u, 0u, 0u, 0u};\n  if (valid) rootn = N[root];\n";
     for (const std::string& b : blocks) o << "  {\n" << b << "  }\n";
-    // KVGPU_JIT_NOATOMIC=1: no per-workgroup count flush (wrong counts; timing A/B only)
-    static const bool no_flush = getenv("KVGPU_JIT_NOATOMIC") && getenv("KVGPU_JIT_NOATOMIC")[0] == '1';
-    if (no_flush) {
-      o << "}\n\n";
-      hist_lds = false;
-      return;
-    }
     if (hist_lds) {
       // one thread per rule counts its 256 status bytes and adds the non-zero counts
       o << "  __syncthreads();\n"
         << "  if (threadIdx.x < " << nr << "u) {\n"
         << "    const uint32_t* w_ = s_stw + threadIdx.x * (KV_WG / 4u);\n"
-        << "    if (O.part) kv_count_status_part(w_, O.part + (size_t)(r0 / KV_WG + bx_) * O.part_pitch + " << name
-        << "_rules[threadIdx.x] * KV_HIST);\n"
-        << "    else kv_count_status_lds(w_, O.counts + (size_t)" << name << "_rules[threadIdx.x] * KV_HIST);\n"
+        << "    kv_count_status_lds(w_, O.counts + (size_t)" << name << "_rules[threadIdx.x] * KV_HIST);\n"
         << "  }\n}\n\n";
       hist_lds = false;
       return;
@@ -1753,71 +1387,27 @@ uint32_t jit_chunk_rules() {
 void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   auto t0 = std::chrono::steady_clock::now();
   Gen g(ps);
-  // KVGPU_JIT_STORE=lane: the per-lane-branch record store variant (8-wave A/B of DESIGN.md)
-  const bool lane_store = getenv("KVGPU_JIT_STORE") && std::string(getenv("KVGPU_JIT_STORE")) == "lane";
   const std::string prelude =
-      std::string(lane_store ? "#define KV_STORE_LANE_BRANCH 1\n" : "") +
-      std::string(getenv("KVGPU_JIT_NOHIST") && getenv("KVGPU_JIT_NOHIST")[0] == '1' ? "#define KV_NOHIST 1\n" : "") +
-      kPrelude + "\nusing namespace kv;\n\n" +
+      kPrelude + std::string("\nusing namespace kv;\n\n") +
       "__device__ __noinline__ bool kv_dleaf_impl(const DevBatch& B, const Node* __restrict__ N, uint32_t dp, Node vn);\n\n";
-  // KVGPU_JIT_FUSE=0: one device function per rule (no cross-rule sharing), for A/B runs
-  const char* fz = getenv("KVGPU_JIT_FUSE");
-  const bool fused = !(fz && fz[0] == '0');
-  // KVGPU_JIT_MEMO=0: evaluate every leaf predicate per pair (no value-predicate table), for A/B runs
-  const char* mz = getenv("KVGPU_JIT_MEMO");
-  g.memo = !(mz && mz[0] == '0');
-  const char* pz = getenv("KVGPU_JIT_PW");
-  g.pw = !(pz && pz[0] == '0');
   for (uint32_t ri = 0; ri < ps.rules.size(); ri++)
     if (ps.rules[ri].route == 0) g.leaf_classes(ri);
-  for (uint32_t ri = 0; ri < ps.rules.size(); ri++) {
-    g.match_fn(ri);
-    if (!fused && ps.rules[ri].route == 0) g.rule_fn(ri);
-  }
+  for (uint32_t ri = 0; ri < ps.rules.size(); ri++) g.match_fn(ri);
   out->chunks.clear();
   const uint32_t n = (uint32_t)ps.rules.size();
   if (chunk_rules == 0) chunk_rules = 32;
-  if (!fused) {
-    for (uint32_t b = 0; b < n; b += chunk_rules) {
-      JitChunk ch;
-      ch.rule_begin = b;
-      ch.rule_end = std::min(n, b + chunk_rules);
-      ch.name = "kvj_chunk_" + std::to_string(out->chunks.size());
-      g.chunk_kernel(ch);
-      out->chunks.push_back(ch);
-    }
-  } else {
+  {
     // rules that walk the same arrays and leaves share a kernel (and its hoisted lookups)
     std::vector<std::pair<std::string, uint32_t>> order;
     for (uint32_t ri = 0; ri < n; ri++)
       order.push_back({ps.rules[ri].route == 0 ? "0" + rule_signature(ps, ri) : "1", ri});
     std::stable_sort(order.begin(), order.end());
-    // chunks of chunk_rules rules; a run of rules with one signature (the same array walk and
-    // the same leaves: one set of hoisted loads, a few registers of state per rule) may grow
-    // to KVGPU_JIT_SIGCHUNK rules, so its array is walked fewer times
-    const char* sz = getenv("KVGPU_JIT_SIGCHUNK");
-    const uint32_t sigmax = std::max<uint32_t>(chunk_rules, sz ? (uint32_t)std::max(1, atoi(sz)) : chunk_rules);
+    // chunks of chunk_rules rules in signature order
     std::vector<JitChunk> chs;
-    {
+    for (uint32_t q = 0; q < n; q += chunk_rules) {
       JitChunk cur;
-      std::string cur_sig;
-      bool uniform = true;
-      for (uint32_t q = 0; q < n; q++) {
-        const std::string& sig = order[q].first;
-        if (!cur.rules.empty()) {
-          const bool same = uniform && sig == cur_sig;
-          if (cur.rules.size() >= sigmax || (cur.rules.size() >= chunk_rules && !same)) {
-            chs.push_back(cur);
-            cur = JitChunk();
-            uniform = true;
-          } else if (sig != cur_sig) {
-            uniform = false;
-          }
-        }
-        if (cur.rules.empty()) cur_sig = sig;
-        cur.rules.push_back(order[q].second);
-      }
-      if (!cur.rules.empty()) chs.push_back(cur);
+      for (uint32_t k = q; k < std::min(n, q + chunk_rules); k++) cur.rules.push_back(order[k].second);
+      chs.push_back(cur);
     }
     out->n_chunks = (uint32_t)chs.size();
     if (out->plan.empty()) {
@@ -1846,7 +1436,7 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   }
   out->memo_preds.clear();
   out->memo_words = 0;
-  if (g.memo && !g.mpreds.empty()) {
+  if (!g.mpreds.empty()) {
     g.ptab_kernel();
     out->memo_preds = g.mpreds;
     out->memo_words = (uint32_t)((g.mpreds.size() + 31) / 32);
@@ -1874,7 +1464,7 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   std::unordered_map<std::string, size_t> def_index;
   for (size_t i = 0; i < defs.size(); i++) def_index[defs[i].first] = i;
   auto refs = [&](const std::string& text, std::vector<size_t>* out_ids) {
-    static const char* prefixes[] = {"g_glob_", "g_atom_", "g_pred_", "m_pred_", "g_blk_", "g_match_", "g_rule_",
+    static const char* prefixes[] = {"g_glob_", "g_atom_", "g_pred_", "m_pred_", "g_blk_", "g_match_",
                                      "g_dleaf_", "q_glob_", "q_atom_", "q_pred_", "r_glob_", "r_atom_", "r_pred_"};
     for (const char* pf : prefixes) {
       const size_t pl = strlen(pf);
@@ -2118,7 +1708,11 @@ bool co_kernel_info(const std::vector<char>& co, const std::string& name, uint32
 }
 
 bool jit_plan_spills(JitImage* img) {
-  if (getenv("KVGPU_JIT_SPILL_SPLIT") && getenv("KVGPU_JIT_SPILL_SPLIT")[0] == '0') return false;
+  // No rule kernel ships with a private (scratch) segment, bounded or not (DESIGN.md §4
+  // *Register plan*: every faulting round-1 build had one). A kernel that spills under the
+  // wave bound is recompiled without the bound (it takes the registers it needs, at lower
+  // occupancy); an unbounded kernel that still spills is split in two; a single fused chunk
+  // that spills unbounded is an error.
   std::vector<JitKernelPlan> next;
   bool changed = false;
   img->kernel_scratch.assign(img->plan.size(), 0);
@@ -2132,22 +1726,20 @@ bool jit_plan_spills(JitImage* img) {
     if (ci == img->kernel_name.size() || !co_kernel_info(img->codes[ci], name, &priv, &code))
       throw std::runtime_error("kvjit: no kernel descriptor for " + name);
     img->kernel_scratch[k] = priv;
-    if (priv == 0 || kp.waves == 0) {
+    if (priv == 0) {
       next.push_back(kp);
       continue;
     }
     changed = true;
-    // A kernel that spills under the wave bound is recompiled without the bound (it takes the
-    // registers it needs, at lower occupancy). Splitting the group instead (KVGPU_JIT_SPILL=split)
-    // multiplies the kernels, each re-walking the resources: C4 1.73 ms (16 kernels) against
-    // 1.34 ms (2 unbounded kernels), C2 1.56 against 1.52 ms.
-    static const bool split = getenv("KVGPU_JIT_SPILL") && std::string(getenv("KVGPU_JIT_SPILL")) == "split";
-    if (split && kp.count > 1) {
-      const uint32_t h = kp.count / 2;
-      next.push_back({kp.first, h, kp.waves});
-      next.push_back({kp.first + h, kp.count - h, kp.waves});
-    } else {
+    if (kp.waves != 0) {
       next.push_back({kp.first, kp.count, 0});
+    } else if (kp.count > 1) {
+      const uint32_t h = kp.count / 2;
+      next.push_back({kp.first, h, 0});
+      next.push_back({kp.first + h, kp.count - h, 0});
+    } else {
+      throw std::runtime_error("kvjit: kernel " + name + " needs " + std::to_string(priv) +
+                               " B of scratch per lane even without a launch bound");
     }
   }
   if (changed) img->plan = next;

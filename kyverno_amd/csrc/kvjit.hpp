@@ -13,8 +13,7 @@
 namespace kvh {
 
 struct JitChunk {
-  uint32_t rule_begin = 0, rule_end = 0;  // unfused kernels: rules [begin, end) evaluated by kernel `name`
-  std::vector<uint32_t> rules;            // fused kernels: the rules evaluated by kernel `name`
+  std::vector<uint32_t> rules;  // the rules evaluated by kernel `name`
   std::string name;
 };
 
@@ -39,7 +38,7 @@ struct JitImage {
   // kernel "kvj_ptab" fills DevPS::ptab (memo_words words per value)
   std::vector<uint32_t> memo_preds;
   uint32_t memo_words = 0;
-  uint32_t ptab_row = 16;   // predicates per kvj_ptab grid row (16: u16 halves of a word, 32: whole words)
+  uint32_t ptab_row = 1;    // predicates per kvj_ptab grid row (one row: every predicate of a value)
   double gen_ms = 0, compile_ms = 0;
 };
 
@@ -55,10 +54,11 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out);
 // Throws std::runtime_error with the log on failure.
 void jit_compile(JitImage* img);
 uint64_t code_bytes(const JitImage& img);
-// Register budget of the plan: a kernel that spills under its wave bound (non-zero
-// private segment) is split in two, or, as a single fused chunk, compiled without
-// the bound. Returns true when the plan changed (regenerate + compile again; the
-// kernels that did not change come from the code-object cache).
+// Register budget of the plan: no kernel ships with a private (scratch) segment. A kernel
+// that spills under its wave bound is compiled without the bound; an unbounded kernel that
+// still spills is split in two (a single fused chunk that does: std::runtime_error).
+// Returns true when the plan changed (regenerate + compile again; the kernels that did not
+// change come from the code-object cache).
 bool jit_plan_spills(JitImage* img);
 bool co_kernel_info(const std::vector<char>& co, const std::string& name, uint32_t* private_seg, uint64_t* code);
 

@@ -588,24 +588,4 @@ hipError_t launch_expand_rows(const Node* pcells, const uint64_t* rmask, const u
   return hipGetLastError();
 }
 
-// Partial per-workgroup histograms of the specialized kernels -> counts: grid x over
-// columns (rule * 8 + status), grid y over row strides; one atomic per column and y.
-constexpr uint32_t KV_PART_Y = 16;
-__global__ __launch_bounds__(KV_WG) void kv_part_reduce_kernel(const uint32_t* __restrict__ part, uint32_t n_blocks,
-                                                               uint32_t pitch, unsigned long long* __restrict__ counts) {
-  const uint32_t c = blockIdx.x * KV_WG + threadIdx.x;
-  if (c >= pitch) return;
-  unsigned long long s = 0;
-  for (uint32_t b = blockIdx.y; b < n_blocks; b += KV_PART_Y) s += part[(size_t)b * pitch + c];
-  if (s) atomicAdd(&counts[c], s);
-}
-
-hipError_t launch_part_reduce(const uint32_t* part, uint32_t n_blocks, uint32_t pitch, unsigned long long* counts,
-                              hipStream_t stream) {
-  if (n_blocks == 0 || pitch == 0) return hipSuccess;
-  hipLaunchKernelGGL(kv_part_reduce_kernel, dim3((pitch + KV_WG - 1) / KV_WG, KV_PART_Y), dim3(KV_WG), 0, stream, part,
-                     n_blocks, pitch, counts);
-  return hipGetLastError();
-}
-
 }  // namespace kv

@@ -165,10 +165,12 @@ void labels(std::string& o, Rng& r) {
   o += "}";
 }
 
-void metadata(std::string& o, Rng& r, const char* prefix, uint64_t i) {
+// n_ns namespaces "ns-0" .. "ns-<n_ns - 1>" (one draw either way, so the rest of a
+// resource does not depend on n_ns)
+void metadata(std::string& o, Rng& r, const char* prefix, uint64_t i, uint32_t n_ns) {
   o += "\"metadata\":{\"name\":\"";
   o += prefix;
-  o += std::to_string(i) + "\",\"namespace\":\"ns-" + std::to_string(r.n(64)) + "\",";
+  o += std::to_string(i) + "\",\"namespace\":\"ns-" + std::to_string(r.n(n_ns)) + "\",";
   labels(o, r);
   if (r.u() < 0.05) o += ",\"annotations\":{\"container.apparmor.security.beta.kubernetes.io/c0\":\"runtime/default\"}";
   o += "}";
@@ -176,21 +178,24 @@ void metadata(std::string& o, Rng& r, const char* prefix, uint64_t i) {
 
 
 // resource i of stream `seed`: its own generator state, so any contiguous range
-// [first, first + n) of one stream is reproducible on its own (the shard of a rank)
+// [first, first + n) of one stream is reproducible on its own (the shard of a rank).
+// kind_mix 0: Pods, 64 namespaces (C2 / C4); 1: Pods/Deployments/Services 60/25/15,
+// 64 namespaces (C5); 2: the same kinds over 1 000 namespaces (C3)
 void resource(std::string& o, uint64_t seed, uint64_t i, uint32_t kind_mix) {
   Rng r{seed};
   r.s = r.next() ^ (i * 0xD1B54A32D192ED03ull);
   (void)r.next();
-  double k = kind_mix == 1 ? r.u() : 0.0;
+  const uint32_t n_ns = kind_mix == 2 ? 1000u : 64u;
+  double k = kind_mix != 0 ? r.u() : 0.0;
   if (k < 0.60) {
     o += "{\"apiVersion\":\"v1\",\"kind\":\"Pod\",";
-    metadata(o, r, "pod-", i);
+    metadata(o, r, "pod-", i, n_ns);
     o += ",\"spec\":";
     pod_spec(o, r);
     o += "}\n";
   } else if (k < 0.85) {
     o += "{\"apiVersion\":\"apps/v1\",\"kind\":\"Deployment\",";
-    metadata(o, r, "deploy-", i);
+    metadata(o, r, "deploy-", i, n_ns);
     o += ",\"spec\":{\"replicas\":" + std::to_string(1 + r.n(5)) + ",\"template\":{\"metadata\":{";
     labels(o, r);
     o += "},\"spec\":";
@@ -199,7 +204,7 @@ void resource(std::string& o, uint64_t seed, uint64_t i, uint32_t kind_mix) {
   } else {
     static const char* st[] = {"ClusterIP", "NodePort", "LoadBalancer"};
     o += "{\"apiVersion\":\"v1\",\"kind\":\"Service\",";
-    metadata(o, r, "svc-", i);
+    metadata(o, r, "svc-", i, n_ns);
     o += std::string(",\"spec\":{\"type\":\"") + st[r.n(3)] + "\",\"ports\":[{\"port\":" + std::to_string(80 + r.n(1000)) + "}]}}\n";
   }
 }
@@ -208,7 +213,7 @@ void resource(std::string& o, uint64_t seed, uint64_t i, uint32_t kind_mix) {
 
 extern "C" int kv_synth_range(uint64_t seed, uint64_t first, uint64_t n, uint32_t kind_mix, char** json_out,
                               size_t* len) {
-  if (!json_out || !len) return KV_E_INVALID;
+  if (!json_out || !len || kind_mix > 2) return KV_E_INVALID;
   const unsigned T = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(16, n / 4096));
   std::vector<std::string> parts(T);
   std::vector<std::thread> th;

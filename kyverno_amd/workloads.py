@@ -109,8 +109,13 @@ def c2_policies() -> list[dict]:
     return [_policy("c2-pod-rules", rules)]
 
 
+C3_KIND_MIX = 2  # kv_synth stream of C3: Pods/Deployments/Services 60/25/15 over 1 000 namespaces
+C3_NAMESPACES = 1000
+
+
 def c3_policies(n_policies: int = 1000, seed: int = SEED) -> list[dict]:
-    """Policies with 1-3 rules and varied match/exclude blocks (C3)."""
+    """Policies with 1-3 rules and varied match/exclude blocks (C3), namespace globs and
+    excludes over the C3 stream's 1 000 namespaces (``ns-0`` .. ``ns-999``)."""
     import random
 
     rnd = random.Random(seed)
@@ -127,7 +132,7 @@ def c3_policies(n_policies: int = 1000, seed: int = SEED) -> list[dict]:
             res = {"kinds": k}
             roll = rnd.random()
             if roll < 0.3:
-                res["namespaces"] = [f"ns-{rnd.randrange(64)}*"]
+                res["namespaces"] = [f"ns-{rnd.randrange(C3_NAMESPACES)}*"]
             elif roll < 0.5:
                 res["selector"] = {"matchLabels": {"app": rnd.choice(["web", "api", "*", "d?"])}}
             elif roll < 0.6:
@@ -141,7 +146,7 @@ def c3_policies(n_policies: int = 1000, seed: int = SEED) -> list[dict]:
                 match = {"any": [{"resources": res}, {"resources": {"kinds": ["Service"]}}]}
             exclude = None
             if rnd.random() < 0.25:
-                exclude = {"resources": {"namespaces": [f"ns-{rnd.randrange(64)}"]}}
+                exclude = {"resources": {"namespaces": [f"ns-{rnd.randrange(C3_NAMESPACES)}"]}}
             if "Service" in k:
                 pat = rnd.choice(pats_svc)
             elif "Deployment" in k or "apps/v1/Deployment" in k:

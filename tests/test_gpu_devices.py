@@ -96,3 +96,31 @@ def test_session_fetch_and_bulk_failures(c5):
     for i in idx:
         assert paths[pid[i]] == ref.path(int(rule[i]), int(res[i]))
     assert len(paths) < 1000  # paths are shared by pairs, not rendered per pair
+
+
+def _bench(*args):
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, "-u", os.path.join(root, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline", "--no-e2e", "--no-traffic", *args], capture_output=True, text=True,
+                       timeout=300, env=env, cwd=root)
+    assert p.returncode == 0, p.stderr[-2000:]
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c5"])
+def test_bench_in_process_parts_match_one_gpu(cfg):
+    """`bench.py --gpus N` without a launcher runs one kv_session_create_devices session over N
+    parts (here: N logical parts of device 0); its reduced counts equal one part over the same
+    [0, N * n) stream."""
+    n = 8192
+    one = _bench("--config", cfg, "--gpus", "1", "--n-res", str(4 * n))
+    four = _bench("--config", cfg, "--gpus", "4", "--parts-per-gpu", "4", "--n-res", str(n))
+    assert four["parts"] == 4 and four["n_gpus"] == 1 and "kv_session_create_devices" in four["config"]["parallelism"]
+    assert four["status_counts"] == one["status_counts"]
+    if "policy_reports" in one:
+        assert four["policy_reports"] == one["policy_reports"]

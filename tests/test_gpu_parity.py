@@ -74,7 +74,7 @@ def test_c3_synthetic_match_exclude(orc, spec):
     from kyverno_amd import batch, workloads
 
     pols = workloads.c3_policies(60)
-    data = batch.synth(workloads.SEED + 1, 1500, kind_mix=1).decode()
+    data = batch.synth(workloads.SEED + 1, 1500, kind_mix=workloads.C3_KIND_MIX).decode()
     ress = [json.loads(l) for l in data.strip().split("\n")]
     mism, r, ost = compare(orc, pols, ress, check_paths=True, max_path_checks=200, specialize=spec)
     assert not mism, "\n".join(mism)

@@ -3,7 +3,7 @@
 Full status matrices of the specialized kernels (the engine bench.py times)
 against the oracle run on every host core, plus sampled failing paths and
 error messages:
-* C3: the whole 1 000-policy / 1 978-rule set on mixed Pods/Deployments/Services,
+* C3: the whole 1 000-policy / 1 973-rule set on mixed Pods/Deployments/Services,
   at the shipped kernel grouping and at five fused chunks per kernel;
 * C2: 1 M Pods x 100 rules (the headline workload);
 * C4: 1 M Pods x 138 anchor-heavy rules.
@@ -69,14 +69,14 @@ def _check(orc, pols, data, env=None, n_paths=300, n_msgs=100, min_fail=100):
 
 @pytest.mark.parametrize("group", ["3", "5"])
 def test_c3_full_policy_set(orc, group):
-    """1 000 policies / 1 978 rules (match/exclude: kinds, namespace globs, wildcard matchLabels,
+    """1 000 policies / 1 973 rules (match/exclude: kinds, namespace globs, wildcard matchLabels,
     matchExpressions, any-blocks, exclude blocks) x 2 000 mixed resources."""
     from kyverno_amd import batch, workloads
 
     pols = workloads.c3_policies(1000)
-    data = batch.synth(workloads.SEED + 11, 2000, 1).strip()
+    data = batch.synth(workloads.SEED + 11, 2000, workloads.C3_KIND_MIX).strip()
     r = _check(orc, pols, data, env={"KVGPU_JIT_GROUP": group}, n_paths=200)
-    assert r.n_rules == 1978 and (r.status == 5).sum() > 0
+    assert r.n_rules == 1973 and (r.status == 5).sum() > 0
 
 
 def test_c2_full_scale(orc):
@@ -93,3 +93,26 @@ def test_c4_full_scale(orc):
 
     data = batch.synth(workloads.SEED + 4, 1_000_000).strip()
     _check(orc, workloads.c4_policies(), data)
+
+
+def test_c3_scope_counts_full_policy_set(orc):
+    """C3 in SCOPES mode (per-namespace PolicyReport counts, pkg/kyverno/apply/report.go:80-87): the
+    full 1 000-policy set over the C3 stream's 1 000 namespaces, device scope counts against the
+    oracle's per-pair statuses grouped by namespace."""
+    from kyverno_amd import batch, workloads
+
+    pols = workloads.c3_policies(1000)
+    data = batch.synth(workloads.SEED + 12, 2500, workloads.C3_KIND_MIX).strip()
+    ps = batch.PolicySet(pols, specialize=True)
+    b = batch.Batch(ps, data)
+    res = batch.validate(ps, b, mode=batch.MODE_SCOPES)
+    ost, _ = orc.validate_ndjson(json.dumps(pols), data, nthreads=_threads())
+    ost[ost == 7] = 6
+    nss = b.namespaces
+    idx = {n: i for i, n in enumerate(nss)}
+    want = np.zeros((len(nss), ost.shape[0], 8), np.int64)
+    for j, line in enumerate(data.split(b"\n")):
+        ns = json.loads(line)["metadata"].get("namespace", "")
+        np.add.at(want[idx[ns]], (np.arange(ost.shape[0]), ost[:, j]), 1)
+    assert len(nss) > 900  # the C3 stream spreads 2 500 resources over ~1 000 namespaces
+    assert np.array_equal(res.scope_counts, want)

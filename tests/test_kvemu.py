@@ -37,7 +37,7 @@ def test_generated_kernels_match_oracle(orc, cfg):
 
     pols, ress = {
         "c2": lambda: (workloads.c2_policies(), _synth(workloads.SEED, 1200)),
-        "c3": lambda: (workloads.c3_policies(120), _synth(workloads.SEED + 1, 1500, 1)),
+        "c3": lambda: (workloads.c3_policies(120), _synth(workloads.SEED + 1, 1500, workloads.C3_KIND_MIX)),
         "c4": lambda: (workloads.c4_policies(), _synth(workloads.SEED + 4, 1000)),
         "c5": lambda: (workloads.c5_policies(), _synth(workloads.SEED + 5, 1000, 1)),
     }[cfg]()

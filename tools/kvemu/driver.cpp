@@ -227,11 +227,6 @@ int main(int argc, char** argv) {
     O.err8 = err8.data();
     O.counts = counts.data();
     O.full = 3;
-    std::vector<ErrRec> lane_err;
-    if (getenv("KVGPU_JIT_STORE") && std::string(getenv("KVGPU_JIT_STORE")) == "lane") {
-      lane_err.assign(nr * nres, ErrRec{});  // the per-lane-branch variant writes full records every pass
-      O.err = lane_err.data();
-    }
     std::vector<chunk_fn> fns;
     for (const JitChunk& c : img.chunks) {
       auto f = (chunk_fn)dlsym(RTLD_DEFAULT, c.name.c_str());
