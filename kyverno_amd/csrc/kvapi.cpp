@@ -798,9 +798,9 @@ struct DevSession {
     P.fflags = (const uint32_t*)fflags.p;
     if (dp.ptab_fn) {  // value-predicate table of the specialized kernels: memo_words per distinct value
       nvals = (uint32_t)bt->b.vals.size();
-      ptab.alloc(std::max<size_t>((size_t)dp.memo_words * nvals, 1) * sizeof(uint32_t), device);
+      ptab.alloc((size_t)dp.memo_words * (nvals + KV_PTAB_PSEUDO) * sizeof(uint32_t), device);
       P.ptab = (const uint32_t*)ptab.p;
-      P.n_vals = nvals;
+      P.n_vals = nvals + KV_PTAB_PSEUDO;
     }
     {  // match tables: one allocation, three [word][entity] tables
       const PolicySet& pp = ps->ps;
@@ -889,12 +889,12 @@ struct DevSession {
     const Node* N = bhost->nodes;
     const Val* V = bhost->vals;
     const uint8_t* S = bhost->bstr;
-    if (dps->ptab_fn && nvals) {  // every leaf predicate once per distinct value, before the rule kernels
+    if (dps->ptab_fn) {  // every leaf predicate once per distinct value (+ pseudo columns), before the rule kernels
       uint32_t NV = nvals;
       uint32_t* PT = (uint32_t*)ptab.p;
       void* targs[] = {(void*)&P, (void*)&V, (void*)&S, (void*)&NV, (void*)&PT};
-      HIPCHK(hipModuleLaunchKernel(dps->ptab_fn, (NV + KV_WG - 1) / KV_WG, dps->ptab_rows, 1, KV_WG, 1, 1, 0, stream, targs,
-                                   nullptr));
+      HIPCHK(hipModuleLaunchKernel(dps->ptab_fn, (NV + KV_PTAB_PSEUDO + KV_WG - 1) / KV_WG, dps->ptab_rows, 1, KV_WG, 1, 1, 0,
+                                   stream, targs, nullptr));
     }
     DevOut Ov = O;
     uint32_t r0 = 0;

@@ -674,16 +674,43 @@ __device__ __forceinline__ uint32_t kv_count_bytes(uint32_t w, uint32_t b4) {
   return (uint32_t)__popc(~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu));
 }
 
-// status + error record (FAIL/ERROR/SKIP) of one rule, and this lane's status byte in
-// the workgroup's LDS row of the rule (0xFF: no resource), counted at the end of the
-// kernel by kv_count_status_lds
-__device__ __forceinline__ void store_result_lds(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, bool valid,
-                                                 uint32_t st, const EState& e, uint8_t* s_row) {
-  if (valid && (O.full & 1)) {
-    const size_t o = (size_t)ri * n_res + r;
-    O.status[o] = (uint8_t)st;
-    if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP))
-      store_err(O, o, e.kind, e.flags, e.pn, e.key, e.res, e.i0, e.i1, e.i2, e.i3);
+// ------------------------------------------------------------------ value-predicate table
+// column of the table holding the predicates of leaf node n: its Val for a scalar, else the
+// pseudo column of its type (null / map / array; an absent cursor reads as null)
+__device__ __forceinline__ uint32_t kv_ptab_col(const DevPS& P, uint32_t type, uint32_t a) {
+  if (type - 1u < 4u) return a;
+  return P.n_vals - KV_PTAB_PSEUDO + (type == NT_NULL ? 0u : type == NT_MAP ? 1u : 2u);
+}
+
+// table word `w` of the leaf predicates on node n: for an array every element must pass
+// (validateValueWithPattern per element), i.e. the AND of the elements' words (all ones
+// for an empty array)
+__device__ __forceinline__ uint32_t kv_leaf_word(const DevPS& P, const Node* __restrict__ N, const Node& n, uint32_t w) {
+  const uint32_t t = node_type(n.kt);
+  if (t != NT_ARR) return kv_gld(P.ptab, (size_t)w * P.n_vals + kv_ptab_col(P, t, n.a));
+  uint32_t x = 0xFFFFFFFFu;
+  for (uint32_t k = 0; k < n.b; k++) {
+    const Node e = N[ni(n.a + k)];
+    x &= kv_gld(P.ptab, (size_t)w * P.n_vals + kv_ptab_col(P, node_type(e.kt), e.a));
+  }
+  return x;
+}
+
+// final status of one rule on this lane: its byte in the workgroup's LDS row of the rule
+// (0xFF: no resource; copied to the status matrix and counted by kv_count_status_lds at
+// the end of the kernel) and, for FAIL / ERROR / SKIP, the error record
+// The record address is computed where the record is written: `r` and `ri` pass through
+// empty asm statements so the compiler cannot hoist one address per rule out of the element
+// loops (a wide fused block finalizes dozens of rules inside one loop; hoisted, their
+// addresses alone took 2-4 VGPRs or an SGPR pair per rule).
+__device__ __forceinline__ void kv_final(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, bool valid,
+                                         uint32_t st, const EState& e, uint8_t* s_row) {
+  if (valid && (O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP)) {
+#ifndef KVEMU
+    asm volatile("" : "+v"(r));
+    asm volatile("" : "+s"(ri));
+#endif
+    store_err(O, (size_t)ri * n_res + r, e.kind, e.flags, e.pn, e.key, e.res, e.i0, e.i1, e.i2, e.i3);
   }
   s_row[threadIdx.x] = valid ? (uint8_t)st : (uint8_t)0xFFu;
 }

@@ -48,7 +48,9 @@ struct DevPS {
   uint32_t n_filters, n_sels;
   // value-predicate table of the specialized kernels (per launch configuration):
   // ptab[word * n_vals + val] bit b = leaf predicate of memo slot 32*word+b on
-  // the scalar Val `val` (built each pass by kvj_ptab before the rule kernels)
+  // the scalar Val `val`, and on the three pseudo values after the batch's values: a
+  // null, a map and an array node (n_vals = values + KV_PTAB_PSEUDO; built each pass by
+  // kvj_ptab before the rule kernels)
   const uint32_t* ptab;
   uint32_t n_vals;
   // match tables (per launch configuration, built each pass by kv_mtab before the rule
@@ -98,6 +100,7 @@ struct DevOut {
 };
 
 constexpr int KV_WG = 256;
+constexpr uint32_t KV_PTAB_PSEUDO = 3;  // ptab columns of a null, a map and an array node
 constexpr int KV_HIST = 8;
 
 }  // namespace kv

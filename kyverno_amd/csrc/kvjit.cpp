@@ -81,9 +81,11 @@ struct Gen {
   // tree level issue together instead of one dependent wait per lookup.
   explicit Gen(const PolicySet& p) : ps(p) {}
 
-  // call of leaf predicate `pi` on node `n` of type `t` (one bit of the value-predicate table)
-  std::string pred_call(uint32_t pi, const std::string& t, const std::string& n) {
-    return "m_pred_" + std::to_string(pi) + "(P, V, S, pstr, " + t + ", " + n + ")";
+  // leaf predicate `pi` on node expression `n` (arrays: every element): one bit of the
+  // value-predicate table
+  std::string leaf_test(uint32_t pi, const std::string& n) const {
+    const uint32_t slot = pslot.at(pi);
+    return "((kv_leaf_word(P, N, " + n + ", " + u32(slot / 32) + ") >> " + u32(slot % 32) + ") & 1u) != 0u";
   }
 
   // ---------------------------------------------------------------- globs
@@ -471,20 +473,9 @@ struct Gen {
       default: o << "  return false;\n"; break;
     }
     o << "}\n";
-    {
-      const uint32_t slot = (uint32_t)mpreds.size();
-      mpreds.push_back(pi);
-      pslot[pi] = slot;
-      // scalars (BOOL/INT/FLOAT/STR carry a Val id in n.a): one bit of the table;
-      // null / map / array: the predicate itself (no value loads on those paths)
-      o << "__device__ __forceinline__ bool m_pred_" << pi
-        << "(const DevPS& P, const Val* __restrict__ V, const uint8_t* __restrict__ S, const uint8_t* __restrict__ pstr, "
-           "uint32_t type, const Node& n) {\n"
-        << "  if (type - 1u < 4u) return (kv_gld(P.ptab, (size_t)" << (slot / 32) << "u * P.n_vals + n.a) >> " << (slot % 32)
-        << "u) & 1u;\n"
-        << "  __builtin_assume(type - 1u >= 4u);  // null / map / array: the string and number code is dead here\n"
-        << "  return g_pred_" << pi << "(V, S, S + n.b, pstr, type, n);\n}\n";
-    }
+    const uint32_t slot = (uint32_t)mpreds.size();
+    mpreds.push_back(pi);
+    pslot[pi] = slot;
   }
 
   // Position classes of every leaf predicate: the projection-trie node of each
@@ -578,9 +569,18 @@ struct Gen {
     o << "extern \"C\" __global__ __launch_bounds__(KV_WG) void kvj_ptab(const DevPS* __restrict__ Pp, "
          "const Val* __restrict__ V, const uint8_t* __restrict__ S, uint32_t NV, uint32_t* __restrict__ PT) {\n"
       << "  const uint32_t v = blockIdx.x * KV_WG + threadIdx.x;\n"
-      << "  if (v >= NV) return;\n"
-      << "  const uint32_t vc = V[v].cls;\n"
+      << "  const uint32_t NP = NV + KV_PTAB_PSEUDO;  // table pitch\n"
+      << "  if (v >= NP) return;\n"
       << "  uint32_t w[" << nw << "] = {};\n"
+      << "  if (v >= NV) {  // pseudo columns: every predicate on a null / map / array node\n"
+      << "    const uint8_t* __restrict__ pstr = Pp->pstr;\n"
+      << "    const uint32_t type = v == NV ? NT_NULL : v == NV + 1u ? NT_MAP : NT_ARR;\n"
+      << "    const Node n{type, 0u, 0u, 0u};\n";
+    for (uint32_t k = 0; k < mpreds.size(); k++)
+      o << "    if (g_pred_" << mpreds[k] << "(V, S, S, pstr, type, n)) w[" << k / 32 << "] |= " << u32(1u << (k % 32)) << ";\n";
+    for (uint32_t i = 0; i < nw; i++) o << "    PT[(size_t)" << i << "u * NP + v] = w[" << i << "];\n";
+    o << "    return;\n  }\n"
+      << "  const uint32_t vc = V[v].cls;\n"
       << "  if (vc & " << u32(all) << ") {\n"
       << "  const uint8_t* __restrict__ pstr = Pp->pstr;\n"
       << "  const Val& val = V[v];\n"
@@ -635,7 +635,7 @@ struct Gen {
       o << "    }\n";
     }
     o << "  }\n  }\n";
-    for (uint32_t i = 0; i < nw; i++) o << "  PT[(size_t)" << i << "u * NV + v] = w[" << i << "];\n";
+    for (uint32_t i = 0; i < nw; i++) o << "  PT[(size_t)" << i << "u * NP + v] = w[" << i << "];\n";
     o << "}\n\n";
   }
 
@@ -775,6 +775,15 @@ struct Gen {
     std::vector<std::string> expr;                      // symbolic cursor per depth ("" = unknown)
     std::vector<HVar> hv;                               // hoisted vars per depth (when expr known)
     std::set<uint32_t> resume;                          // resume targets of later segments
+    // targets past the segment being emitted, reached without / with a pending error
+    std::set<uint32_t> seg_jumps, seg_err_jumps;
+    // per stage loop k: the rule is "lean" there (its state is one bit of the block's stage-k
+    // masks and a failing element decides its status at once), the status its post chain adds
+    // to the error (flags) and whether that chain ends at the last anyPattern alternative
+    std::vector<char> lean;
+    std::vector<uint32_t> post_flags, skip_to, skip_flags;
+    std::vector<char> post_alt, skip_alt;
+    uint32_t q = 0;                                     // position in the block (mask bit, LDS row)
     bool uses_anchor = false, uses_keyglob = false;
     uint32_t max_level = 0;
     std::string s;                                      // "_<ri>"
@@ -829,10 +838,12 @@ struct Gen {
     const std::string& s = g.s;
     auto C = [&](uint32_t d) { return "c" + std::to_string(d) + s; };
     auto L = [&](uint32_t pc) { return "R" + std::to_string(g.ri) + "_L" + std::to_string(pc); };
-    auto jump = [&](uint32_t t) -> std::string {
+    // err: the jump carries a pending error (a raise, or an error passed on by a scope end)
+    auto jump = [&](uint32_t t, bool err = false) -> std::string {
       if (t >= R.rb && t < R.jre) return "goto " + L(t) + ";";
       if (R.kind == 0 && t >= R.jre) {
         g.resume.insert(t);
+        (err ? g.seg_err_jumps : g.seg_jumps).insert(t);
         return "{ rs" + s + " = " + u32(t) + "; goto " + R.se + "; }";
       }
       throw std::runtime_error("kvjit: jump out of a fused region (rule " + std::to_string(g.ri) + ")");
@@ -848,7 +859,7 @@ struct Gen {
       r << "{ ek" << s << " = " << kind << " | " << u32(pn << 8) << ";";
       for (uint32_t lv = 0; lv <= g.max_level && lv < 4; lv++) r << " ei" << lv << s << " = " << li(lv) << ";";
       if (g.uses_keyglob) r << " ekn" << s << " = kn" << s << ";";
-      r << " " << jump(catch_pc) << " }";
+      r << " " << jump(catch_pc, true) << " }";
       return r.str();
     };
     auto known = [&](uint32_t d) {
@@ -927,11 +938,11 @@ struct Gen {
           break;
         case OP_SCOPE_END:
           if (in.c == 0) w << "  if (" << kindof << ") " << ek << " |= " << u32(aux << 4) << ";\n";
-          else w << "  if (" << kindof << ") { " << ek << " |= " << u32(aux << 4) << "; " << jump(in.c) << " }\n";
+          else w << "  if (" << kindof << ") { " << ek << " |= " << u32(aux << 4) << "; " << jump(in.c, true) << " }\n";
           break;
         case OP_POS_END:
           w << "  if (" << kindof << ") { if (" << ek << " & " << u32(EF_COND << 4) << ") " << ek << " = 0u; else "
-            << jump(in.c) << " }\n";
+            << jump(in.c, true) << " }\n";
           break;
         case OP_NEG:
           w << "  if (" << lookup(d, in.a, aux, false) << " != ABSENT) " << raise("E_NEG", in.b, in.c) << "\n";
@@ -942,34 +953,25 @@ struct Gen {
           w << raise("E_STAR", in.b, in.c) << "\n";
           break;
         case OP_LEAF: {
-          std::string scalar = pred_call(in.a, "vt_", "vn_");
-          if (known(d)) {
-            w << "  { const Node vn_ = " << NODE(d) << ";\n";
-            auto sl = pslot.find(in.a);
-            HoistTable* T = table_for(d);
-            if (sl != pslot.end() && T) {
-              const uint32_t word = sl->second / 32;
-              const std::string wv = g.hv[d].node + "_w" + std::to_string(word);
-              const std::string hn = g.hv[d].node;
-              if (T->words.insert(wv).second) {
-                const std::string off = std::to_string(word) + "u * P.n_vals + ";
-                T->code.push_back("  const uint32_t " + wv + " = __builtin_amdgcn_perm(kv_gld(P.ptab, (size_t)" + off +
-                                  "(node_type(" + hn + ".kt) - 1u < 4u ? " + hn + ".a : 0u)), 0u, node_type(" + hn +
-                                  ".kt) - 1u < 4u ? 0x07060504u : 0x0c0c0c0cu);\n");
-              }
-              scalar = "(vt_ - 1u < 4u ? ((" + wv + " >> " + std::to_string(sl->second % 32) + "u) & 1u) != 0u : " +
-                       "([&]() -> bool { __builtin_assume(vt_ - 1u >= 4u); return g_pred_" + std::to_string(in.a) +
-                       "(V, S, S + vn_.b, pstr, vt_, vn_); })())";
-            }
+          // one bit of the leaf's table word: hoisted leaves read the word loaded (and, for an
+          // array, AND-ed over its elements) once per region; others load it here
+          const uint32_t slot = pslot.at(in.a);
+          const uint32_t word = slot / 32;
+          HoistTable* T = known(d) ? table_for(d) : nullptr;
+          std::string test;
+          if (T) {
+            const std::string hn = g.hv[d].node;
+            const std::string wv = hn + "_w" + std::to_string(word);
+            if (T->words.insert(wv).second)
+              T->code.push_back("  const uint32_t " + wv + " = kv_leaf_word(P, N, " + hn + ", " + u32(word) + ");\n");
+            test = "((" + wv + " >> " + u32(slot % 32) + ") & 1u) != 0u";
           } else {
             w << "  { Node vn_{0u, 0u, 0u, 0u}; if (" << cd << " != ABSENT) vn_ = N[" << cd << "];\n";
+            test = leaf_test(in.a, "vn_");
+            w << "    if (!(" << test << ")) " << raise("E_VALUE", in.b, in.c) << " }\n";
+            break;
           }
-          w << "    const uint32_t vt_ = node_type(vn_.kt); bool ok_;\n"
-            << "    if (vt_ == NT_ARR) { ok_ = true; for (uint32_t k_ = 0; k_ < vn_.b && ok_; k_++) { const Node en_ = "
-               "N[ni(vn_.a + k_)]; ok_ = "
-            << pred_call(in.a, "node_type(en_.kt)", "en_") << "; } }\n"
-            << "    else ok_ = " << scalar << ";\n"
-            << "    if (!ok_) " << raise("E_VALUE", in.b, in.c) << " }\n";
+          w << "  if (!(" << test << ")) " << raise("E_VALUE", in.b, in.c) << "\n";
           break;
         }
         case OP_VLEAF:  // pattern variables: the resource's substituted value (kvvars.cpp)
@@ -1011,7 +1013,7 @@ struct Gen {
           break;
         case OP_LOOP_END:
           w << "  if (" << kindof << ") { if (" << ek << " & " << u32(EF_COND << 4) << ") " << ek << " = 0u; else "
-            << jump(in.c) << " }\n"
+            << jump(in.c, true) << " }\n"
             << "  if (li" << L_lv << s << " + 1u < ll" << L_lv << s << ") { li" << L_lv << s << "++; " << cn << " = ni(lf"
             << L_lv << s << " + li" << L_lv << s << "); " << jump(in.a + 1) << " }\n";
           set_unknown(d + 1);
@@ -1079,8 +1081,72 @@ struct Gen {
     return g;
   }
 
+  // The ops a lane runs after leaving stage loop k of `g` with a (non-condition) error,
+  // from the LOOP_END's catch target: pure when it only carries the error through scope
+  // ends to DONE (or to the end of the last anyPattern alternative), adding `flags`. The
+  // rule's status is then a function of the error alone, decided at the failing element.
+  struct PostChain {
+    bool pure = false, alt = false;
+    uint32_t flags = 0;
+  };
+  PostChain post_chain(const RGen& g, uint32_t pc, bool cond = false) const {
+    PostChain r;
+    for (int steps = 0; steps < 100000 && pc >= g.b && pc <= g.e; steps++) {
+      const Inst& in = ps.prog[pc];
+      const uint32_t op = in.op & 0xFF, aux = (in.op >> 16) & 0xFF;
+      switch (op) {
+        case OP_SCOPE_END:
+          r.flags |= aux;
+          cond |= (aux & EF_COND) != 0;
+          pc = in.c ? in.c : pc + 1;
+          continue;
+        case OP_POS_END:
+        case OP_LOOP_END:
+          if (cond) return r;  // a condition error is cleared there: the walk goes on
+          pc = in.c;
+          continue;
+        case OP_NOP:
+        case OP_METACHK:
+          pc++;
+          continue;
+        case OP_DONE:
+          r.pure = true;
+          return r;
+        case OP_ALT_END:
+          if (in.b) r.pure = r.alt = true;  // the last alternative: FAIL (or CPU)
+          return r;
+        default:
+          return r;
+      }
+    }
+    return r;
+  }
+
+  // Status of a rule whose error `ekx` reached DONE (or the last alternative's end): the
+  // MatchPattern epilogue as one select chain
+  std::string done_status(const RGen& g, const std::string& ekx, bool alt) const {
+    std::ostringstream w;
+    const std::string k = "(" + ekx + " & 15u)";
+    if (alt) {
+      w << "(" << k << " == 0u ? ST_PASS : " << k << " == E_CPU ? ST_CPU : ST_FAIL)";
+      return w.str();
+    }
+    w << "(" << k << " == 0u ? ST_PASS : " << k << " == E_CPU ? ST_CPU : (" << ekx << " & "
+      << u32((EF_COND | EF_GLOBAL) << 4) << ") ? ST_SKIP : ";
+    if (g.uses_anchor) w << "(areg" << g.s << " & ~apres" << g.s << ") ? ST_ERROR : ";
+    w << k << " == E_LEN ? ST_ERROR : ST_FAIL)";
+    return w.str();
+  }
+
   // Code block of one fused chunk inside a kernel body (its own C++ scope); the
-  // chunk's histogram rows are s_hist[hbase, hbase + rules).
+  // chunk's status rows are s_stw rows [hbase, hbase + rules).
+  //
+  // Lean rules (hist_lds kernels): at the end of stage segment k a rule that enters stage
+  // loop k keeps only one bit (am<k>_<w>, bit q of its block position), one that jumps past
+  // the loop one bit of sk<k>_<w> (its single target), and one that finished stores its
+  // status at once; inside the fused loop its error state is local to the element and an
+  // element that fails decides the status there (post_chain), so no per-rule register lives
+  // across the loop. After the loops the resume pc is rebuilt from the bits.
   std::string fused_block(const JitChunk& ch, uint32_t hbase) {
     const uint32_t nr = (uint32_t)ch.rules.size();
     std::vector<RGen> gs;
@@ -1088,37 +1154,83 @@ struct Gen {
     global.prefix = "g";
     gT = &global;
     size_t K = 0;
-    for (uint32_t ri : ch.rules) {
+    for (uint32_t q = 0; q < nr; q++) {
+      const uint32_t ri = ch.rules[q];
       if (ps.rules[ri].route != 0) continue;
       RGen g = analyze(ri);
+      g.q = q;
       for (uint32_t pc = g.b; pc <= g.e; pc++)
         if ((ps.prog[pc].op & 0xFF) == OP_LEAF) pred_fn(ps.prog[pc].a);
       K = std::max(K, g.loops.size());
+      g.lean.assign(g.loops.size(), 0);
+      g.post_flags.assign(g.loops.size(), 0);
+      g.post_alt.assign(g.loops.size(), 0);
+      g.skip_to.assign(g.loops.size(), 0xFFFFFFFFu);
+      g.skip_flags.assign(g.loops.size(), 0);
+      g.skip_alt.assign(g.loops.size(), 0);
       gs.push_back(std::move(g));
     }
-    // status + error record + histogram of rule `ri` (chunk position q): emitted as
-    // soon as the rule's last segment has run, so its state registers die there
-    auto store = [&](uint32_t ri) {
-      const uint32_t q = (uint32_t)(std::find(ch.rules.begin(), ch.rules.end(), ri) - ch.rules.begin());
+    const uint32_t nw = (nr + 31) / 32;
+    auto mword = [&](const char* m, size_t k, uint32_t q) {
+      return std::string(m) + std::to_string(k) + "_" + std::to_string(q / 32);
+    };
+    auto mbit = [&](uint32_t q) { return u32(1u << (q % 32)); };
+    auto row = [&](uint32_t q) { return "(uint8_t*)s_stw + " + u32((hbase + q) * 256u); };
+    // EState of rule g from its registers (error kind / flags / pattern node in `ekx`)
+    auto estate = [&](const RGen* g, const std::string& ekx) {
+      std::ostringstream k;
+      if (!g) return std::string("EState e_{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u};");
+      k << "EState e_{" << ekx << " & 15u, (" << ekx << " >> 4) & 15u, " << ekx << " >> 8, "
+        << (g->uses_keyglob ? "ekn" + g->s : std::string("ABSENT")) << ", ABSENT";
+      for (uint32_t lv = 0; lv < 4; lv++) k << ", " << (lv <= g->max_level ? "ei" + std::to_string(lv) + g->s : "0u");
+      k << "};";
+      return k.str();
+    };
+    // status + error record of rule `ri` (block position q): LDS status byte (copied to the
+    // status matrix at the end of the kernel) + the error record, or the ballot histogram
+    auto store_st = [&](uint32_t q, const RGen* g, const std::string& st, const std::string& ekx) {
+      const uint32_t ri = ch.rules[q];
+      std::ostringstream k;
+      k << "  { " << estate(g, ekx) << "\n";
+      if (hist_lds)
+        k << "    kv_final(O, " << ri << "u, n_res, r, valid, " << st << ", e_, " << row(q) << "); }\n";
+      else
+        k << "    store_result2(O, " << ri << "u, n_res, r, valid, " << st << ", e_, &s_hist[" << (hbase + q)
+          << "][0]); }\n";
+      return k.str();
+    };
+    auto store = [&](uint32_t q) {
+      const uint32_t ri = ch.rules[q];
       const std::string s = "_" + std::to_string(ri);
       const RGen* g = nullptr;
       for (const RGen& x : gs)
         if (x.ri == ri) g = &x;
+      const std::string st = "rs" + s + " & 0xFFu";
+      if (!g) return store_st(q, g, st, "0u");
+      return "  if ((rs" + s + " & 0xFFu) != ST_STORED_) {\n" + store_st(q, g, st, "ek" + s) + "  }\n";
+    };
+    // match / route of rule q (rs = its first pc, or FIN | status)
+    auto match_code = [&](uint32_t q) {
+      const uint32_t ri = ch.rules[q];
+      const RuleRec& rr = ps.rules[ri];
+      const std::string s = "_" + std::to_string(ri);
       std::ostringstream k;
-      if (g) {
-        k << "  { EState e_{ek" << s << " & 15u, (ek" << s << " >> 4) & 15u, ek" << s << " >> 8, "
-          << (g->uses_keyglob ? "ekn" + s : std::string("ABSENT")) << ", ABSENT";
-        for (uint32_t lv = 0; lv < 4; lv++) k << ", " << (lv <= g->max_level ? "ei" + std::to_string(lv) + s : "0u");
-        k << "};\n";
-      } else {
-        k << "  { EState e_{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u};\n";
+      k << "  if (valid && g_match_" << ri << "(P, B, R, rkind, rflags)) {\n";
+      switch (rr.route) {
+        case 1: k << "    rs" << s << " = FIN_ | ST_CPU;\n"; break;
+        case 2: k << "    rs" << s << " = FIN_ | ST_NOMATCH;\n"; break;
+        case 3: k << "    rs" << s << " = FIN_ | " << u32(rr.const_status) << ";\n"; break;
+        default:
+          k << "    if (rflags & RF_MAGIC) rs" << s << " = FIN_ | ST_CPU;\n";
+          if (rr.flags & RR_META_EXPAND)
+            k << "    else if (rflags & " << u32(meta_bad_flags(rr.flags)) << ") rs" << s << " = FIN_ | ST_CPU;\n";
+          if (rr.dyn)
+            k << "    else if (B.dyn_st[(size_t)" << (rr.dyn - 1) << "u * n_res + r]) rs" << s << " = FIN_ | B.dyn_st[(size_t)"
+              << (rr.dyn - 1) << "u * n_res + r];\n";
+          k << "    else rs" << s << " = " << u32(rr.prog) << ";\n";
+          break;
       }
-      if (hist_lds)
-        k << "    store_result_lds(O, " << ri << "u, n_res, r, valid, rs" << s << " & 0xFFu, e_, (uint8_t*)s_stw + "
-          << u32((hbase + q) * 256u) << "); }\n";
-      else
-        k << "    store_result2(O, " << ri << "u, n_res, r, valid, rs" << s << " & 0xFFu, e_, &s_hist[" << (hbase + q)
-          << "][0]); }\n";
+      k << "  }\n";
       return k.str();
     };
     std::ostringstream body;  // everything after the per-rule declarations
@@ -1135,13 +1247,76 @@ struct Gen {
         R.jre = se;
         R.se = "R" + std::to_string(g.ri) + "_S" + std::to_string(k);
         std::ostringstream w;
+        g.seg_jumps.clear();
+        g.seg_err_jumps.clear();
         emit_region(g, R, w);
+        if (k == 0) seg << match_code(g.q);  // just before its first segment: rs is born here
+        if (k > 0 && g.lean[k - 1]) {  // resume pc of a lean rule from its stage-(k-1) bits
+          const uint32_t le = g.loops[k - 1].second;
+          seg << "  rs" << g.s << " = (" << mword("am", k - 1, g.q) << " & " << mbit(g.q) << ") ? " << u32(le + 1) << " : ";
+          if (g.skip_to[k - 1] != 0xFFFFFFFFu)
+            seg << "(" << mword("sk", k - 1, g.q) << " & " << mbit(g.q) << ") ? " << u32(g.skip_to[k - 1]) << " : ";
+          seg << "FIN_ | ST_STORED_;\n";
+          // the error state of a lane that left the loop clean (no register of the rule lives
+          // across the loop)
+          seg << "  ek" << g.s << " = 0u;";
+          for (uint32_t lv = 0; lv <= g.max_level && lv < 4; lv++) seg << " ei" << lv << g.s << " = 0u;";
+          if (g.uses_keyglob) seg << " ekn" << g.s << " = ABSENT;";
+          seg << "\n";
+        }
         seg << "  // rule " << g.ri << " stage " << k << "\n  switch (rs" << g.s << ") {\n";
         if (k == 0) seg << "    case " << u32(g.b) << ": goto R" << g.ri << "_L" << g.b << ";\n";
         for (uint32_t t : g.resume)
           if (t >= sb && t < se) seg << "    case " << u32(t) << ": goto R" << g.ri << "_L" << t << ";\n";
         seg << "    default: goto " << R.se << ";\n  }\n" << w.str() << R.se << ":;\n";
-        if (k == g.loops.size()) seg << store(g.ri);  // the rule has finished for every lane
+        if (k == g.loops.size()) {
+          seg << store(g.q);  // the rule has finished for every lane
+          continue;
+        }
+        // stage loop k follows: lean when the kernel stages statuses in LDS, the post chain of
+        // the loop is pure, and the segment leaves at most one way past the loop, whose chain
+        // is pure for any pending error (a lane that jumps there with an error is decided at
+        // once; one without resumes there after the loop)
+        const uint32_t le = g.loops[k].second;
+        const PostChain pcn = post_chain(g, ps.prog[le].c);
+        bool lean = hist_lds && pcn.pure && g.seg_jumps.size() <= 1;
+        std::vector<std::pair<uint32_t, PostChain>> errc;  // chains of the error targets
+        for (uint32_t t : g.seg_err_jumps) {
+          errc.push_back({t, post_chain(g, t, true)});
+          lean &= errc.back().second.pure;
+        }
+        bool alt0 = !errc.empty() && errc[0].second.alt;
+        for (auto& e : errc) lean &= e.second.alt == alt0;
+        g.lean[k] = lean;
+        g.post_flags[k] = pcn.flags;
+        g.post_alt[k] = pcn.alt;
+        if (!lean) continue;
+        const std::string ek = "ek" + g.s;
+        seg << "  if (rs" << g.s << " & ACT_) " << mword("am", k, g.q) << " |= " << mbit(g.q) << ";\n";
+        if (!g.seg_jumps.empty() || !errc.empty()) {
+          // past the loop: with an error the status is decided now, else resume there later
+          seg << "  else if (rs" << g.s << " < FIN_) {\n";
+          if (!errc.empty()) {
+            std::string fl = "0u";
+            for (auto it = errc.rbegin(); it != errc.rend(); ++it)
+              fl = "(rs" + g.s + " == " + u32(it->first) + " ? " + u32(it->second.flags << 4) + " : " + fl + ")";
+            const std::string ekx = "(" + ek + " | " + fl + ")";
+            seg << "    if (" << ek << " & 15u) {\n" << store_st(g.q, &g, done_status(g, ekx, alt0), ekx) << "    }\n";
+          }
+          if (!g.seg_jumps.empty()) {
+            g.skip_to[k] = *g.seg_jumps.begin();
+            seg << "    " << (errc.empty() ? "" : "else ") << mword("sk", k, g.q) << " |= " << mbit(g.q) << ";\n";
+          }
+          seg << "  }\n";
+        }
+        seg << "  else {\n" << store(g.q) << "  }\n";
+      }
+      if (k < K) {  // stage-k masks of the lean rules
+        std::ostringstream mk;
+        mk << "  uint32_t";
+        for (uint32_t w = 0; w < nw; w++) mk << (w ? "," : "") << " am" << k << "_" << w << " = 0u, sk" << k << "_" << w << " = 0u";
+        mk << ";\n";
+        body << mk.str();
       }
       body << global.flush() << seg.str();
       if (k == K) break;
@@ -1167,6 +1342,7 @@ struct Gen {
         T.prefix = "l" + tag + "_";
         const std::string troot = "E" + tag;
         std::ostringstream bodies;
+        std::vector<uint32_t> gmask(nw, 0);  // lean rules of the group, per mask word
         for (RGen* gp : grp) {
           RGen& g = *gp;
           const uint32_t lb = g.loops[k].first, le = g.loops[k].second;
@@ -1184,24 +1360,44 @@ struct Gen {
           std::ostringstream w;
           emit_region(g, R, w);
           const Inst& end = ps.prog[le];
-          bodies << "    if (rs" << g.s << " & ACT_) {\n      c" << (d + 1) << g.s << " = el" << tag << ";\n"
-                 << w.str() << "R" << g.ri << "_L" << le << ":;\n"
-                 << "      if (ek" << g.s << " & 15u) { if (ek" << g.s << " & " << u32(EF_COND << 4) << ") ek" << g.s
-                 << " = 0u; else rs" << g.s << " = " << u32(end.c) << "; }\n    }\n";
           if (end.c <= le) throw std::runtime_error("kvjit: loop exit target inside the loop");
-          g.resume.insert(end.c);
+          const std::string ek = "ek" + g.s;
+          if (g.lean[k]) {
+            gmask[g.q / 32] |= 1u << (g.q % 32);
+            // element-local error state; an error that leaves the loop decides the status now
+            bodies << "    if (" << mword("am", k, g.q) << " & " << mbit(g.q) << ") {\n      " << ek << " = 0u;";
+            for (uint32_t lv = 0; lv <= g.max_level && lv < 4; lv++) bodies << " ei" << lv << g.s << " = 0u;";
+            if (g.uses_keyglob) bodies << " ekn" << g.s << " = ABSENT;";
+            bodies << "\n      c" << (d + 1) << g.s << " = el" << tag << ";\n"
+                   << w.str() << "R" << g.ri << "_L" << le << ":;\n"
+                   << "      if (" << ek << " & 15u) { if (" << ek << " & " << u32(EF_COND << 4) << ") " << ek
+                   << " = 0u; else {\n        " << mword("am", k, g.q) << " &= ~" << mbit(g.q) << ";\n";
+            const std::string ekx = g.post_flags[k] ? "(" + ek + " | " + u32(g.post_flags[k] << 4) + ")" : ek;
+            bodies << "  " << store_st(g.q, &g, done_status(g, ekx, g.post_alt[k]), ekx) << "      } }\n    }\n";
+          } else {
+            bodies << "    if (rs" << g.s << " & ACT_) {\n      c" << (d + 1) << g.s << " = el" << tag << ";\n"
+                   << w.str() << "R" << g.ri << "_L" << le << ":;\n"
+                   << "      if (" << ek << " & 15u) { if (" << ek << " & " << u32(EF_COND << 4) << ") " << ek
+                   << " = 0u; else rs" << g.s << " = " << u32(end.c) << "; }\n    }\n";
+            g.resume.insert(end.c);
+          }
           g.resume.insert(le + 1);
           for (uint32_t x = d + 1; x < g.expr.size(); x++) g.expr[x].clear();  // loop-local exprs end here
         }
         body << "  { // fused loop " << tag << " over " << key << " (" << grp.size() << " rules)\n"
-             << "    uint32_t fn" << tag << " = 0u, ff" << tag << " = 0u;\n    if ((0u";
-        for (RGen* gp : grp) body << " | rs" << gp->s;
-        body << ") & ACT_) { const Node an_ = " << arr_node << "; ff" << tag << " = an_.a; fn" << tag << " = an_.b; }\n";
+             << "    uint32_t fn" << tag << " = 0u, ff" << tag << " = 0u;\n    if (((0u";
+        for (RGen* gp : grp)
+          if (!gp->lean[k]) body << " | rs" << gp->s;
+        body << ") & ACT_)";
+        for (uint32_t w = 0; w < nw; w++)
+          if (gmask[w]) body << " | (am" << k << "_" << w << " & " << u32(gmask[w]) << ")";
+        body << ") { const Node an_ = " << arr_node << "; ff" << tag << " = an_.a; fn" << tag << " = an_.b; }\n";
         body << "    for (uint32_t fli" << tag << " = 0u; fli" << tag << " < fn" << tag << "; fli" << tag << "++) {\n"
              << "      const uint32_t el" << tag << " = ni(ff" << tag << " + fli" << tag << ");\n"
              << "      const Node eln" << tag << " = N[el" << tag << "];\n"
              << T.flush() << bodies.str() << "    }\n";
-        for (RGen* gp : grp) body << "    rs" << gp->s << " &= ~ACT_;\n";
+        for (RGen* gp : grp)
+          if (!gp->lean[k]) body << "    rs" << gp->s << " &= ~ACT_;\n";
         body << "  }\n";
       }
     }
@@ -1236,30 +1432,9 @@ struct Gen {
         k << (l ? "," : "") << " li" << l << s << " = 0u, lf" << l << s << " = 0u, ll" << l << s << " = 0u";
       k << ";\n";
     }
-    // match / route
-    for (uint32_t ri : ch.rules) {
-      const RuleRec& rr = ps.rules[ri];
-      const std::string s = "_" + std::to_string(ri);
-      k << "  if (valid && g_match_" << ri << "(P, B, R, rkind, rflags)) {\n";
-      switch (rr.route) {
-        case 1: k << "    rs" << s << " = FIN_ | ST_CPU;\n"; break;
-        case 2: k << "    rs" << s << " = FIN_ | ST_NOMATCH;\n"; break;
-        case 3: k << "    rs" << s << " = FIN_ | " << u32(rr.const_status) << ";\n"; break;
-        default:
-          k << "    if (rflags & RF_MAGIC) rs" << s << " = FIN_ | ST_CPU;\n";
-          if (rr.flags & RR_META_EXPAND)
-            k << "    else if (rflags & " << u32(meta_bad_flags(rr.flags)) << ") rs" << s << " = FIN_ | ST_CPU;\n";
-          if (rr.dyn)
-            k << "    else if (B.dyn_st[(size_t)" << (rr.dyn - 1) << "u * n_res + r]) rs" << s << " = FIN_ | B.dyn_st[(size_t)"
-              << (rr.dyn - 1) << "u * n_res + r];\n";
-          k << "    else rs" << s << " = " << u32(rr.prog) << ";\n";
-          break;
-      }
-      k << "  }\n";
-    }
     // rules of other routes are final after match / route
-    for (uint32_t ri : ch.rules)
-      if (ps.rules[ri].route != 0) k << store(ri);
+    for (uint32_t q = 0; q < nr; q++)
+      if (ps.rules[ch.rules[q]].route != 0) k << match_code(q) << store(q);
     k << body.str();
     return k.str();
   }
@@ -1289,7 +1464,7 @@ struct Gen {
     o << "extern \"C\" __global__ __launch_bounds__(" << lb << ") void " << name
       << "(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp, const Node* __restrict__ N, "
          "const Val* __restrict__ V, const uint8_t* __restrict__ S, DevOut O, uint32_t r0) {\n"
-      << "  constexpr uint32_t FIN_ = " << u32(FIN) << ", ACT_ = " << u32(ACT) << ";\n"
+      << "  constexpr uint32_t FIN_ = " << u32(FIN) << ", ACT_ = " << u32(ACT) << ", ST_STORED_ = 0x7Eu;\n"
       << (hist_lds ? "  __shared__ uint32_t s_stw[" + std::to_string(nr * 256u / 4) + "];\n"
                    : "  __shared__ uint32_t s_hist[" + std::to_string(nr) + "][KV_HIST];\n")
       << "  const DevPS& P = *Pp;\n  const DevBatch& B = *Bp;\n  const uint8_t* __restrict__ pstr = P.pstr;\n";
@@ -1311,8 +1486,16 @@ struct Gen {
       << "  Node rootn{0u, 0u, 0u, 0u};\n  if (valid) rootn = N[root];\n";
     for (const std::string& b : blocks) o << "  {\n" << b << "  }\n";
     if (hist_lds) {
-      // one thread per rule counts its 256 status bytes and adds the non-zero counts
+      // the status rows staged in LDS go to the status matrix (one byte per rule and lane,
+      // 64 B per wave and rule); one thread per rule counts its 256 status bytes and adds the
+      // non-zero counts
       o << "  __syncthreads();\n"
+        << "  if ((O.full & 1u) && valid) {\n"
+        << "    const uint8_t* s_b = (const uint8_t*)s_stw + threadIdx.x;\n"
+        << "#pragma unroll 4\n"
+        << "    for (uint32_t q = 0; q < " << nr << "u; q++) O.status[(size_t)" << name
+        << "_rules[q] * n_res + r] = s_b[q * KV_WG];\n"
+        << "  }\n"
         << "  if (threadIdx.x < " << nr << "u) {\n"
         << "    const uint32_t* w_ = s_stw + threadIdx.x * (KV_WG / 4u);\n"
         << "    kv_count_status_lds(w_, O.counts + (size_t)" << name << "_rules[threadIdx.x] * KV_HIST);\n"
@@ -1381,7 +1564,7 @@ std::string rule_signature(const PolicySet& ps, uint32_t ri) {
 
 uint32_t jit_chunk_rules() {
   const char* ch = getenv("KVGPU_JIT_CHUNK");
-  return ch && atoi(ch) > 0 ? (uint32_t)atoi(ch) : 4u;
+  return ch && atoi(ch) > 0 ? (uint32_t)atoi(ch) : 128u;
 }
 
 void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
@@ -1395,42 +1578,32 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   for (uint32_t ri = 0; ri < ps.rules.size(); ri++) g.match_fn(ri);
   out->chunks.clear();
   const uint32_t n = (uint32_t)ps.rules.size();
-  if (chunk_rules == 0) chunk_rules = 32;
+  if (chunk_rules == 0) chunk_rules = 128;
   {
     // rules that walk the same arrays and leaves share a kernel (and its hoisted lookups)
     std::vector<std::pair<std::string, uint32_t>> order;
     for (uint32_t ri = 0; ri < n; ri++)
       order.push_back({ps.rules[ri].route == 0 ? "0" + rule_signature(ps, ri) : "1", ri});
     std::stable_sort(order.begin(), order.end());
-    // chunks of chunk_rules rules in signature order
-    std::vector<JitChunk> chs;
-    for (uint32_t q = 0; q < n; q += chunk_rules) {
-      JitChunk cur;
-      for (uint32_t k = q; k < std::min(n, q + chunk_rules); k++) cur.rules.push_back(order[k].second);
-      chs.push_back(cur);
-    }
-    out->n_chunks = (uint32_t)chs.size();
-    if (out->plan.empty()) {
-      // KVGPU_JIT_GROUP: fused chunks run back to back inside one kernel (default 25: C2 1.56 ms
-      // vs 1.58 at 5, C3 22.6 ms vs 27.3, C4 1.73 vs 1.90; compile 11-13 s);
-      // KVGPU_JIT_WAVES: launch bound in waves per SIMD (default 8, 0: none)
-      const char* gz = getenv("KVGPU_JIT_GROUP");
-      const uint32_t group = gz ? (uint32_t)std::max(1, atoi(gz)) : 25u;
+    // One kernel per range of the signature order: its rules run as one fused block (every
+    // array they walk is walked once per resource, all rules of the range in one loop over
+    // it). Default: ceil(n / chunk_rules) ranges of near-equal size.
+    // KVGPU_JIT_WAVES: launch bound in waves per SIMD (default 8, 0: none)
+    if (out->plan.empty() && n) {
       const char* wz = getenv("KVGPU_JIT_WAVES");
       const int waves = wz ? atoi(wz) : 8;
-      for (uint32_t b = 0; b < chs.size(); b += group)
-        out->plan.push_back({b, std::min<uint32_t>(group, (uint32_t)chs.size() - b), waves});
+      const uint32_t parts = (n + chunk_rules - 1) / chunk_rules;
+      for (uint32_t k = 0; k < parts; k++) {
+        const uint32_t a = (uint32_t)((uint64_t)n * k / parts), e = (uint32_t)((uint64_t)n * (k + 1) / parts);
+        out->plan.push_back({a, e - a, waves});
+      }
     }
     for (const JitKernelPlan& kp : out->plan) {
       JitChunk kc;
-      // named by its first chunk and chunk count: stable when other groups are re-planned
-      kc.name = "kvj_c" + std::to_string(kp.first) + "_" + std::to_string(kp.count) + (kp.waves ? "" : "u");
-      std::vector<const JitChunk*> part;
-      for (uint32_t q = kp.first; q < kp.first + kp.count; q++) {
-        part.push_back(&chs.at(q));
-        kc.rules.insert(kc.rules.end(), chs[q].rules.begin(), chs[q].rules.end());
-      }
-      g.group_kernel(kc.name, part, kp.waves);
+      // named by its rule range: stable when other ranges are re-planned
+      kc.name = "kvj_r" + std::to_string(kp.first) + "_" + std::to_string(kp.count) + (kp.waves ? "" : "u");
+      for (uint32_t q = kp.first; q < kp.first + kp.count; q++) kc.rules.push_back(order.at(q).second);
+      g.group_kernel(kc.name, {&kc}, kp.waves);
       out->chunks.push_back(kc);
     }
   }
@@ -1464,7 +1637,7 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   std::unordered_map<std::string, size_t> def_index;
   for (size_t i = 0; i < defs.size(); i++) def_index[defs[i].first] = i;
   auto refs = [&](const std::string& text, std::vector<size_t>* out_ids) {
-    static const char* prefixes[] = {"g_glob_", "g_atom_", "g_pred_", "m_pred_", "g_blk_", "g_match_",
+    static const char* prefixes[] = {"g_glob_", "g_atom_", "g_pred_", "g_blk_", "g_match_",
                                      "g_dleaf_", "q_glob_", "q_atom_", "q_pred_", "r_glob_", "r_atom_", "r_pred_"};
     for (const char* pf : prefixes) {
       const size_t pl = strlen(pf);

@@ -17,8 +17,8 @@ struct JitChunk {
   std::string name;
 };
 
-// One specialized rule kernel: fused chunks [first, first + count) of the
-// signature-sorted rule order, compiled with a `waves`-per-SIMD launch bound (0: none).
+// One specialized rule kernel: rules [first, first + count) of the signature-sorted
+// rule order as one fused block, compiled with a `waves`-per-SIMD launch bound (0: none).
 struct JitKernelPlan {
   uint32_t first, count;
   int waves;
@@ -27,7 +27,6 @@ struct JitKernelPlan {
 struct JitImage {
   std::vector<JitKernelPlan> plan;     // kernel grouping (empty: default groups; kept across re-plans)
   std::vector<uint32_t> kernel_scratch;  // private segment bytes per lane of each planned kernel
-  uint32_t n_chunks = 0;
   std::string source;       // generated HIP source, all of it (diagnostics, tools/kvemu)
   std::string common;       // prelude + helper functions shared by the kernels
   std::vector<std::string> kernel_name, kernel_src;  // one hiprtc program per kernel: common + kernel_src[i]
@@ -44,7 +43,7 @@ struct JitImage {
 
 // Generate the specialized source for every rule of `ps` (chunks of at most
 // `chunk_rules` rules per kernel).
-// rules per fused chunk: KVGPU_JIT_CHUNK (experiments), default 4 (C2 sweep)
+// most rules per kernel (one fused block): KVGPU_JIT_CHUNK, default 128
 uint32_t jit_chunk_rules();
 void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out);
 // Compile every kernel program with hiprtc for gfx950, on parallel host threads

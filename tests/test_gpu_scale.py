@@ -4,7 +4,7 @@ Full status matrices of the specialized kernels (the engine bench.py times)
 against the oracle run on every host core, plus sampled failing paths and
 error messages:
 * C3: the whole 1 000-policy / 1 973-rule set on mixed Pods/Deployments/Services,
-  at the shipped kernel grouping and at five fused chunks per kernel;
+  at the shipped kernel plan and at 40 rules per kernel;
 * C2: 1 M Pods x 100 rules (the headline workload);
 * C4: 1 M Pods x 138 anchor-heavy rules.
 Reference semantics: pkg/engine/validation.go:26-106 (oracle/src/engine.cpp).
@@ -67,15 +67,16 @@ def _check(orc, pols, data, env=None, n_paths=300, n_msgs=100, min_fail=100):
     return r
 
 
-@pytest.mark.parametrize("group", ["3", "5"])
-def test_c3_full_policy_set(orc, group):
+@pytest.mark.parametrize("chunk", ["40", "128"])
+def test_c3_full_policy_set(orc, chunk):
     """1 000 policies / 1 973 rules (match/exclude: kinds, namespace globs, wildcard matchLabels,
-    matchExpressions, any-blocks, exclude blocks) x 2 000 mixed resources."""
+    matchExpressions, any-blocks, exclude blocks) x 2 000 mixed resources, at the shipped kernel
+    plan (128 rules per fused kernel) and at 40."""
     from kyverno_amd import batch, workloads
 
     pols = workloads.c3_policies(1000)
     data = batch.synth(workloads.SEED + 11, 2000, workloads.C3_KIND_MIX).strip()
-    r = _check(orc, pols, data, env={"KVGPU_JIT_GROUP": group}, n_paths=200)
+    r = _check(orc, pols, data, env={"KVGPU_JIT_CHUNK": chunk}, n_paths=200)
     assert r.n_rules == 1973 and (r.status == 5).sum() > 0
 
 

@@ -118,7 +118,7 @@ int main(int argc, char** argv) {
     std::string ks;
     key_table(ps, b, &koff, &klen, &ks);
     const uint32_t NV = (uint32_t)b.vals.size();
-    std::vector<uint32_t> ptab((size_t)std::max<uint32_t>(img.memo_words, 1) * std::max<uint32_t>(NV, 1), 0u);
+    std::vector<uint32_t> ptab((size_t)std::max<uint32_t>(img.memo_words, 1) * (NV + KV_PTAB_PSEUDO), 0u);
     DevPS P{};
     P.prog = ps.prog.data();
     P.preds = ps.preds.data();
@@ -144,7 +144,7 @@ int main(int argc, char** argv) {
     P.n_filters = (uint32_t)ps.filters.size();
     P.n_sels = (uint32_t)ps.selectors.size();
     P.ptab = ptab.data();
-    P.n_vals = NV;
+    P.n_vals = NV + KV_PTAB_PSEUDO;
     DevBatch B{};
     B.nodes = b.nodes.data();
     // merged batches carry the packed transfer form of their rows (what kv_validate
@@ -212,11 +212,11 @@ int main(int argc, char** argv) {
                std::max({B.n_nsm, B.n_asets, B.n_lsets}), mt.data(), mt.data() + n_ns, mt.data() + n_ns + n_an);
     const uint64_t nr = ps.rules.size(), nres = b.res.size();
 
-    if (img.memo_words && NV) {
+    if (img.memo_words) {
       auto f = (ptab_fn)dlsym(RTLD_DEFAULT, "kvj_ptab");
       if (!f) throw std::runtime_error("kvj_ptab not linked in");
       const uint32_t rows = (uint32_t)((img.memo_preds.size() + img.ptab_row - 1) / img.ptab_row);
-      grid((NV + KV_WG - 1) / KV_WG, rows, [&]() { f(&P, B.vals, B.bstr, NV, ptab.data()); });
+      grid((NV + KV_PTAB_PSEUDO + KV_WG - 1) / KV_WG, rows, [&]() { f(&P, B.vals, B.bstr, NV, ptab.data()); });
     }
     std::vector<uint8_t> status(nr * nres, 0xEE);
     std::vector<ErrRec8> err8(nr * nres);

@@ -10,6 +10,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#define KVEMU 1  // host emulation: no AMDGPU inline asm (kvdevfn.h)
 #define __device__
 #define __host__
 #define __global__
