@@ -777,6 +777,9 @@ struct Gen {
     std::set<uint32_t> resume;                          // resume targets of later segments
     // targets past the segment being emitted, reached without / with a pending error
     std::set<uint32_t> seg_jumps, seg_err_jumps;
+    // resume targets set by earlier stages and not consumed yet (the segment holding them lies
+    // further on), reached without / with a pending error
+    std::set<uint32_t> carry_ok, carry_err;
     // per stage loop k: the rule is "lean" there (its state is one bit of the block's stage-k
     // masks and a failing element decides its status at once), the status its post chain adds
     // to the error (flags) and whether that chain ends at the last anyPattern alternative
@@ -1279,21 +1282,36 @@ struct Gen {
         // once; one without resumes there after the loop)
         const uint32_t le = g.loops[k].second;
         const PostChain pcn = post_chain(g, ps.prog[le].c);
-        bool lean = hist_lds && pcn.pure && g.seg_jumps.size() <= 1;
+        // every way past loop k: this segment's jumps and the targets of earlier stages that lie
+        // beyond this segment (they pass through it)
+        std::set<uint32_t> okset = g.seg_jumps, errset = g.seg_err_jumps;
+        for (uint32_t t : g.carry_ok)
+          if (t >= se) okset.insert(t);
+        for (uint32_t t : g.carry_err)
+          if (t >= se) errset.insert(t);
+        bool lean = hist_lds && pcn.pure && okset.size() <= 1;
         std::vector<std::pair<uint32_t, PostChain>> errc;  // chains of the error targets
-        for (uint32_t t : g.seg_err_jumps) {
+        for (uint32_t t : errset) {
           errc.push_back({t, post_chain(g, t, true)});
           lean &= errc.back().second.pure;
         }
         bool alt0 = !errc.empty() && errc[0].second.alt;
         for (auto& e : errc) lean &= e.second.alt == alt0;
+        g.carry_ok = okset;
+        if (lean) {
+          g.carry_err.clear();  // errors past the loop are decided at the segment end
+        } else {
+          g.carry_ok.insert(le + 1);
+          g.carry_err = errset;
+          g.carry_err.insert(ps.prog[le].c);
+        }
         g.lean[k] = lean;
         g.post_flags[k] = pcn.flags;
         g.post_alt[k] = pcn.alt;
         if (!lean) continue;
         const std::string ek = "ek" + g.s;
         seg << "  if (rs" << g.s << " & ACT_) " << mword("am", k, g.q) << " |= " << mbit(g.q) << ";\n";
-        if (!g.seg_jumps.empty() || !errc.empty()) {
+        if (!okset.empty() || !errc.empty()) {
           // past the loop: with an error the status is decided now, else resume there later
           seg << "  else if (rs" << g.s << " < FIN_) {\n";
           if (!errc.empty()) {
@@ -1303,8 +1321,8 @@ struct Gen {
             const std::string ekx = "(" + ek + " | " + fl + ")";
             seg << "    if (" << ek << " & 15u) {\n" << store_st(g.q, &g, done_status(g, ekx, alt0), ekx) << "    }\n";
           }
-          if (!g.seg_jumps.empty()) {
-            g.skip_to[k] = *g.seg_jumps.begin();
+          if (!okset.empty()) {
+            g.skip_to[k] = *okset.begin();
             seg << "    " << (errc.empty() ? "" : "else ") << mword("sk", k, g.q) << " |= " << mbit(g.q) << ";\n";
           }
           seg << "  }\n";
