@@ -652,11 +652,13 @@ struct EState {
 // compact form, flagged `wide` when the indices / key do not fit. Passes with
 // O.full bit 2 (re-run by the host only when some record was wide) write the
 // full 32 B form instead; the flag is uniform, so this is a scalar branch.
-__device__ __forceinline__ void store_err(const DevOut& O, size_t o, uint32_t kind, uint32_t flags, uint32_t pn,
-                                          uint32_t key, uint32_t res, uint32_t i0, uint32_t i1, uint32_t i2,
-                                          uint32_t i3) {
+// Record of rule ri on resource r: the rule's row base is uniform and r the only per-lane
+// part of the address (a scalar base + 32-bit vector offset store).
+__device__ __forceinline__ void store_err(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, uint32_t kind,
+                                          uint32_t flags, uint32_t pn, uint32_t key, uint32_t res, uint32_t i0,
+                                          uint32_t i1, uint32_t i2, uint32_t i3) {
   if (O.full & 4) {
-    uint4* x = (uint4*)(O.err + o);
+    uint4* x = (uint4*)(O.err + (size_t)ri * n_res) + 2u * r;
     x[0] = make_uint4(kind | (flags << 16), pn, key, res);
     x[1] = make_uint4(i0, i1, i2, i3);
     return;
@@ -665,7 +667,7 @@ __device__ __forceinline__ void store_err(const DevOut& O, size_t o, uint32_t ki
   uint2 w;
   w.x = kind | (flags << 4) | ((fits ^ 1u) << 6) | (pn << 7);
   w.y = i0 | (i1 << 12) | (i2 << 22);
-  *(uint2*)(O.err8 + o) = w;
+  ((uint2*)(O.err8 + (size_t)ri * n_res))[r] = w;
 }
 
 // number of bytes of w equal to the byte replicated in b4 (exact SWAR zero-byte count)
@@ -699,20 +701,41 @@ __device__ __forceinline__ uint32_t kv_leaf_word(const DevPS& P, const Node* __r
 // final status of one rule on this lane: its byte in the workgroup's LDS row of the rule
 // (0xFF: no resource; copied to the status matrix and counted by kv_count_status_lds at
 // the end of the kernel) and, for FAIL / ERROR / SKIP, the error record
-// The record address is computed where the record is written: `r` and `ri` pass through
-// empty asm statements so the compiler cannot hoist one address per rule out of the element
-// loops (a wide fused block finalizes dozens of rules inside one loop; hoisted, their
-// addresses alone took 2-4 VGPRs or an SGPR pair per rule).
+// The record address is computed where the record is written: `r` and `ri` (uniform: every
+// caller passes a constant or a wave-uniform member index) pass through empty asm statements
+// so the compiler cannot hoist one address per rule out of the element loops (a wide fused
+// block finalizes dozens of rules inside one loop; hoisted, their addresses alone took 2-4
+// VGPRs or an SGPR pair per rule).
 __device__ __forceinline__ void kv_final(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, bool valid,
                                          uint32_t st, const EState& e, uint8_t* s_row) {
   if (valid && (O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP)) {
+    uint32_t z = 0u;  // an opaque zero: the site's constant record words are built here, not
+                      // hoisted out of the loops as one constant register tuple per site
 #ifndef KVEMU
-    asm volatile("" : "+v"(r));
+    asm volatile("" : "+v"(r), "+v"(z));
     asm volatile("" : "+s"(ri));
 #endif
-    store_err(O, (size_t)ri * n_res + r, e.kind, e.flags, e.pn, e.key, e.res, e.i0, e.i1, e.i2, e.i3);
+    store_err(O, ri, n_res, r, e.kind + z, e.flags, e.pn + z, e.key + z, e.res + z, e.i0, e.i1, e.i2, e.i3);
   }
   s_row[threadIdx.x] = valid ? (uint8_t)st : (uint8_t)0xFFu;
+}
+
+// final status `st` of the members `m` of a rule group (kvjit.cpp: rules whose programs differ
+// only in their leaf predicates and pattern-node ids, evaluated once with one bit per member):
+// member j is rule tab[j] (or ri0 + j * sri), its pattern nodes are the group's shifted by
+// tab[n + j] (or j * spn), its status row is s_row0 + j * KV_WG; `ekx` is the error of the
+// group's representative (kind | flags << 4 | node << 8; 0: none)
+__device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_t r, bool valid, uint32_t m, uint32_t st,
+                                        uint32_t ekx, uint32_t i0, uint32_t i1, uint32_t i2, uint32_t i3,
+                                        uint8_t* s_row0, const uint32_t* tab, uint32_t n, uint32_t ri0, uint32_t sri,
+                                        uint32_t spn) {
+  for (uint32_t j = 0; j < n; j++) {  // uniform over the members (scalar rule ids and rows)
+    if (!((m >> j) & 1u)) continue;
+    const uint32_t ri = tab ? tab[j] : ri0 + j * sri;
+    const uint32_t ek = ekx ? ekx + ((tab ? tab[n + j] : j * spn) << 8) : 0u;
+    const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
+    kv_final(O, ri, n_res, r, valid, st, e, s_row0 + j * (uint32_t)KV_WG);
+  }
 }
 
 // histogram of one rule's KV_WG status bytes (64 words in LDS) added to counts[KV_HIST]
@@ -747,7 +770,7 @@ __device__ __forceinline__ void store_result2(const DevOut& O, uint32_t ri, uint
     const size_t o = (size_t)ri * n_res + r;
     O.status[o] = (uint8_t)st;
     if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP))
-      store_err(O, o, e.kind, e.flags, e.pn, e.key, e.res, e.i0, e.i1, e.i2, e.i3);
+      store_err(O, ri, n_res, r, e.kind, e.flags, e.pn, e.key, e.res, e.i0, e.i1, e.i2, e.i3);
   }
   const uint64_t m_pass = __ballot(valid && st == ST_PASS), m_fail = __ballot(valid && st == ST_FAIL);
   const uint64_t m_nm = __ballot(valid && st == ST_NOMATCH);
@@ -774,7 +797,7 @@ __device__ __forceinline__ void store_result(const DevOut& O, uint32_t ri, uint3
     const size_t o = (size_t)ri * n_res + r;
     O.status[o] = (uint8_t)st;
     if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP))
-      store_err(O, o, e.kind, e.flags, e.pn, e.key, e.res, e.i0, e.i1, e.i2, e.i3);
+      store_err(O, ri, n_res, r, e.kind, e.flags, e.pn, e.key, e.res, e.i0, e.i1, e.i2, e.i3);
   }
   for (uint32_t s = 0; s < 7; s++) {
     const uint64_t bm = __ballot(valid && st == s);

@@ -83,8 +83,8 @@ struct Gen {
 
   // leaf predicate `pi` on node expression `n` (arrays: every element): one bit of the
   // value-predicate table
-  std::string leaf_test(uint32_t pi, const std::string& n) const {
-    const uint32_t slot = pslot.at(pi);
+  std::string leaf_test(uint32_t pi, const std::string& n) {
+    const uint32_t slot = slot_for(pi);
     return "((kv_leaf_word(P, N, " + n + ", " + u32(slot / 32) + ") >> " + u32(slot % 32) + ") & 1u) != 0u";
   }
 
@@ -473,9 +473,25 @@ struct Gen {
       default: o << "  return false;\n"; break;
     }
     o << "}\n";
+  }
+
+  // memo slot of leaf predicate `pi` (one per predicate for single rules, assigned on first use)
+  uint32_t slot_for(uint32_t pi) {
+    auto it = pslot.find(pi);
+    if (it != pslot.end()) return it->second;
     const uint32_t slot = (uint32_t)mpreds.size();
     mpreds.push_back(pi);
     pslot[pi] = slot;
+    return slot;
+  }
+  // consecutive memo slots inside one table word for the leaf predicates of a rule group's
+  // members (member j = bit base + j; a word's unused tail is padded with the first predicate)
+  uint32_t group_slots(const std::vector<uint32_t>& preds) {
+    if ((mpreds.size() % 32) + preds.size() > 32)
+      while (mpreds.size() % 32) mpreds.push_back(preds[0]);
+    const uint32_t base = (uint32_t)mpreds.size();
+    for (uint32_t p : preds) mpreds.push_back(p);
+    return base;
   }
 
   // Position classes of every leaf predicate: the projection-trie node of each
@@ -788,6 +804,13 @@ struct Gen {
     std::vector<char> post_alt, skip_alt;
     uint32_t q = 0;                                     // position in the block (mask bit, LDS row)
     bool uses_anchor = false, uses_keyglob = false;
+    // rule group: the representative's program run once for all members (bit j of `al` = member
+    // j alive on this lane); every error is decided where it is raised (kv_gfin)
+    bool grp = false;
+    uint32_t gn = 1, grow = 0, gsri = 0, gspn = 0;      // members, LDS row offset of member 0, steps
+    std::vector<uint32_t> gri, gdpn;                    // member rule ids, pattern-node shifts
+    std::map<uint32_t, uint32_t> gslot;                 // representative LEAF pc -> slot of member 0
+    std::string gtab;                                   // member table (empty: arithmetic)
     uint32_t max_level = 0;
     std::string s;                                      // "_<ri>"
   };
@@ -856,10 +879,37 @@ struct Gen {
       return "{ rs" + s + " = FIN_ | " + st + "; goto " + R.se + "; }";
     };
     auto li = [&](uint32_t lv) { return lv == 0 && R.kind == 1 ? R.li0 : "li" + std::to_string(lv) + s; };
-    auto raise = [&](const std::string& kind, uint32_t pn, uint32_t catch_pc) {
-      if (pn >= (1u << 24)) throw std::runtime_error("kvjit: pattern node id exceeds 24 bits");
+    const bool G = g.grp;
+    const std::string al = "al" + s;
+    // a group with no member left on this lane leaves the region
+    auto gdone = [&]() -> std::string {
+      if (R.kind == 0) return "{ rs" + s + " = FIN_ | ST_STORED_; goto " + R.se + "; }";
+      return "goto " + L(R.re) + ";";
+    };
+    // members `m` of a group fail with the representative's error (kind, pn) raised here: their
+    // status is the error's, carried statically through the scope ends to DONE (post_chain)
+    auto gfin = [&](const std::string& m, uint32_t kind, uint32_t pn, uint32_t catch_pc) {
+      const PostChain pcn = post_chain(g, catch_pc);
+      if (!pcn.pure || pcn.alt) throw std::runtime_error("kvjit: impure error chain in rule group");
+      std::string st;
+      if (kind == E_CPU) st = "ST_CPU";
+      else if (pcn.flags & (EF_COND | EF_GLOBAL)) st = "ST_SKIP";
+      else {
+        st = kind == E_LEN ? "ST_ERROR" : "ST_FAIL";
+        if (g.uses_anchor) st = "((areg" + s + " & ~apres" + s + ") ? ST_ERROR : " + st + ")";
+      }
       std::ostringstream r;
-      r << "{ ek" << s << " = " << kind << " | " << u32(pn << 8) << ";";
+      r << "kv_gfin(O, n_res, r, valid, " << m << ", " << st << ", " << u32(kind | (pcn.flags << 4) | (pn << 8));
+      for (uint32_t lv = 0; lv < 4; lv++) r << ", " << (lv <= g.max_level ? li(lv) : std::string("0u"));
+      r << ", (uint8_t*)s_stw + " << u32(g.grow) << ", " << (g.gtab.empty() ? std::string("nullptr") : g.gtab) << ", "
+        << u32(g.gn) << ", " << u32(g.gri[0]) << ", " << u32(g.gsri) << ", " << u32(g.gspn) << ");";
+      return r.str();
+    };
+    auto raise = [&](uint32_t kind, uint32_t pn, uint32_t catch_pc) {
+      if (pn >= (1u << 24)) throw std::runtime_error("kvjit: pattern node id exceeds 24 bits");
+      if (G) return "{ " + gfin(al, kind, pn, catch_pc) + " " + al + " = 0u; " + gdone() + " }";
+      std::ostringstream r;
+      r << "{ ek" << s << " = " << u32(kind) << " | " << u32(pn << 8) << ";";
       for (uint32_t lv = 0; lv <= g.max_level && lv < 4; lv++) r << " ei" << lv << s << " = " << li(lv) << ";";
       if (g.uses_keyglob) r << " ekn" << s << " = kn" << s << ";";
       r << " " << jump(catch_pc, true) << " }";
@@ -915,7 +965,7 @@ struct Gen {
           const char* t = op == OP_MAPCHK ? "NT_MAP" : "NT_ARR";
           if (known(d)) w << "  if (node_type(" << NODE(d) << ".kt) != " << t << ") ";
           else w << "  if (" << cd << " == ABSENT || node_type(N[" << cd << "].kt) != " << t << ") ";
-          w << raise(op == OP_MAPCHK ? "E_TYPE_MAP" : "E_TYPE_ARR", in.a, in.c) << "\n";
+          w << raise(op == OP_MAPCHK ? E_TYPE_MAP : E_TYPE_ARR, in.a, in.c) << "\n";
           break;
         }
         case OP_AREG: {
@@ -935,65 +985,73 @@ struct Gen {
           break;
         }
         case OP_KEYGLOB:
+          if (G) throw std::runtime_error("kvjit: KEYGLOB in a rule group");
           set_unknown(d + 1);
           w << "  { uint32_t nd_; if (!keyglob_op(P, B, N, " << cd << ", " << u32(in.op) << ", " << u32(in.a) << ", "
             << u32(in.c) << ", &nd_, &kn" << s << ")) " << jump(in.b) << " " << cn << " = nd_; }\n";
           break;
         case OP_SCOPE_END:
+          if (G) break;  // groups carry no pending error (decided where raised)
           if (in.c == 0) w << "  if (" << kindof << ") " << ek << " |= " << u32(aux << 4) << ";\n";
           else w << "  if (" << kindof << ") { " << ek << " |= " << u32(aux << 4) << "; " << jump(in.c, true) << " }\n";
           break;
         case OP_POS_END:
+          if (G) throw std::runtime_error("kvjit: POS_END in a rule group");
           w << "  if (" << kindof << ") { if (" << ek << " & " << u32(EF_COND << 4) << ") " << ek << " = 0u; else "
             << jump(in.c, true) << " }\n";
           break;
         case OP_NEG:
-          w << "  if (" << lookup(d, in.a, aux, false) << " != ABSENT) " << raise("E_NEG", in.b, in.c) << "\n";
+          w << "  if (" << lookup(d, in.a, aux, false) << " != ABSENT) " << raise(E_NEG, in.b, in.c) << "\n";
           break;
         case OP_STAR:
           if (known(d + 1)) w << "  if (node_type(" << NODE(d + 1) << ".kt) == NT_NULL) ";
           else w << "  if (" << cn << " == ABSENT || node_type(N[" << cn << "].kt) == NT_NULL) ";
-          w << raise("E_STAR", in.b, in.c) << "\n";
+          w << raise(E_STAR, in.b, in.c) << "\n";
           break;
         case OP_LEAF: {
-          // one bit of the leaf's table word: hoisted leaves read the word loaded (and, for an
-          // array, AND-ed over its elements) once per region; others load it here
-          const uint32_t slot = pslot.at(in.a);
+          // one bit of the leaf's table word (a group: one bit per member, consecutive): hoisted
+          // leaves read the word loaded (and, for an array, AND-ed over its elements) once per
+          // region; others load it here
+          const uint32_t slot = G ? g.gslot.at(pc) : slot_for(in.a);
           const uint32_t word = slot / 32;
           HoistTable* T = known(d) ? table_for(d) : nullptr;
-          std::string test;
+          std::string wx;
           if (T) {
             const std::string hn = g.hv[d].node;
-            const std::string wv = hn + "_w" + std::to_string(word);
-            if (T->words.insert(wv).second)
-              T->code.push_back("  const uint32_t " + wv + " = kv_leaf_word(P, N, " + hn + ", " + u32(word) + ");\n");
-            test = "((" + wv + " >> " + u32(slot % 32) + ") & 1u) != 0u";
+            wx = hn + "_w" + std::to_string(word);
+            if (T->words.insert(wx).second)
+              T->code.push_back("  const uint32_t " + wx + " = kv_leaf_word(P, N, " + hn + ", " + u32(word) + ");\n");
           } else {
-            w << "  { Node vn_{0u, 0u, 0u, 0u}; if (" << cd << " != ABSENT) vn_ = N[" << cd << "];\n";
-            test = leaf_test(in.a, "vn_");
-            w << "    if (!(" << test << ")) " << raise("E_VALUE", in.b, in.c) << " }\n";
-            break;
+            wx = "kv_leaf_word(P, N, (" + cd + " != ABSENT ? N[" + cd + "] : Node{0u, 0u, 0u, 0u}), " + u32(word) + ")";
           }
-          w << "  if (!(" << test << ")) " << raise("E_VALUE", in.b, in.c) << "\n";
+          if (G) {
+            const uint32_t mask = g.gn >= 32 ? 0xFFFFFFFFu : (1u << g.gn) - 1u;
+            w << "  { const uint32_t f_ = " << al << " & ~((" << wx << " >> " << u32(slot % 32) << ") & " << hex32(mask)
+              << ");\n    if (f_) { " << gfin("f_", E_VALUE, in.b, in.c) << " " << al << " &= ~f_; if (!" << al << ") "
+              << gdone() << " } }\n";
+          } else {
+            w << "  if (!(((" << wx << " >> " << u32(slot % 32) << ") & 1u) != 0u)) " << raise(E_VALUE, in.b, in.c) << "\n";
+          }
           break;
         }
         case OP_VLEAF:  // pattern variables: the resource's substituted value (kvvars.cpp)
+          if (G) throw std::runtime_error("kvjit: VLEAF in a rule group");
           if (known(d)) w << "  { const Node vn_ = " << NODE(d) << ";\n";
           else w << "  { Node vn_{0u, 0u, 0u, 0u}; if (" << cd << " != ABSENT) vn_ = N[" << cd << "];\n";
           dleaf_fn();
           w << "    if (!g_dleaf_0(B, N, B.dleaf[(size_t)" << u32(in.a) << " * n_res + r], vn_)) "
-            << raise("E_VALUE", in.b, in.c) << " }\n";
+            << raise(E_VALUE, in.b, in.c) << " }\n";
           break;
         case OP_RAISE:
-          w << "  " << raise(u32(in.b), in.a, in.c) << "\n";
+          w << "  " << raise(in.b, in.a, in.c) << "\n";
           break;
         case OP_EXISTCHK:
           if (known(d)) w << "  if (node_type(" << NODE(d) << ".kt) != NT_ARR) ";
           else w << "  if (" << cd << " == ABSENT || node_type(N[" << cd << "].kt) != NT_ARR) ";
-          w << raise("E_EXIST_RESTYPE", in.a, in.c) << "\n";
+          w << raise(E_EXIST_RESTYPE, in.a, in.c) << "\n";
           break;
         case OP_LENCHK:
-          w << "  if (" << NODE(d) << ".b < " << u32(in.a) << ") " << raise("E_LEN", in.b, in.c) << "\n";
+          w << "  if (" << NODE(d) << ".b < " << u32(in.a) << ") " << raise(E_LEN, in.b, in.c) << "\n";
           break;
         case OP_INDEX:
           w << "  " << cn << " = ni(" << NODE(d) << ".a + " << u32(in.a) << ");\n";
@@ -1007,33 +1065,38 @@ struct Gen {
           }
           [[fallthrough]];  // nested loop, per rule
         case OP_EXIST_BEGIN:
+          if (G && op == OP_EXIST_BEGIN) throw std::runtime_error("kvjit: EXIST in a rule group");
           set_unknown(d + 1);
           w << "  { const Node an_ = " << NODE(d) << "; lf" << L_lv << s << " = an_.a; ll" << L_lv << s << " = an_.b; li"
             << L_lv << s << " = 0u;\n    if (an_.b == 0u) ";
           if (op == OP_LOOP_BEGIN) w << jump(in.a + 1);
-          else w << raise("E_EXIST_FAIL", in.b, in.c);
+          else w << raise(E_EXIST_FAIL, in.b, in.c);
           w << "\n    " << cn << " = ni(an_.a); }\n";
           break;
         case OP_LOOP_END:
-          w << "  if (" << kindof << ") { if (" << ek << " & " << u32(EF_COND << 4) << ") " << ek << " = 0u; else "
-            << jump(in.c, true) << " }\n"
-            << "  if (li" << L_lv << s << " + 1u < ll" << L_lv << s << ") { li" << L_lv << s << "++; " << cn << " = ni(lf"
+          if (!G)  // groups carry no pending error
+            w << "  if (" << kindof << ") { if (" << ek << " & " << u32(EF_COND << 4) << ") " << ek << " = 0u; else "
+              << jump(in.c, true) << " }\n";
+          w << "  if (li" << L_lv << s << " + 1u < ll" << L_lv << s << ") { li" << L_lv << s << "++; " << cn << " = ni(lf"
             << L_lv << s << " + li" << L_lv << s << "); " << jump(in.a + 1) << " }\n";
           set_unknown(d + 1);
           break;
         case OP_EXIST_END:
+          if (G) throw std::runtime_error("kvjit: EXIST in a rule group");
           w << "  if (!" << kindof << ") " << jump(pc + 1) << "\n  " << ek << " = 0u;\n"
             << "  if (li" << L_lv << s << " + 1u < ll" << L_lv << s << ") { li" << L_lv << s << "++; " << cn << " = ni(lf"
             << L_lv << s << " + li" << L_lv << s << "); " << jump(in.a + 1) << " }\n"
-            << "  " << raise("E_EXIST_FAIL", in.b, in.c) << "\n";
+            << "  " << raise(E_EXIST_FAIL, in.b, in.c) << "\n";
           set_unknown(d + 1);
           break;
         case OP_ALT_BEGIN:
+          if (G) throw std::runtime_error("kvjit: anyPattern in a rule group");
           w << "  " << ek << " = 0u;";
           if (g.uses_anchor) w << " areg" << s << " = 0ull; apres" << s << " = 0ull;";
           w << "\n";
           break;
         case OP_ALT_END:
+          if (G) throw std::runtime_error("kvjit: anyPattern in a rule group");
           w << "  if (" << kindof << " == 0u) " << finish("ST_PASS") << "\n  if (" << kindof << " == E_CPU) "
             << finish("ST_CPU") << "\n";
           if (in.b) w << "  " << finish("ST_FAIL") << "\n";
@@ -1045,6 +1108,10 @@ struct Gen {
           break;
         case OP_DONE:  // the MatchPattern epilogue as one select chain (no per-lane branches)
           if (R.kind != 0) throw std::runtime_error("kvjit: rule end inside a fused loop");
+          if (G) {  // the members alive here passed (no error: the anchor-key check does not apply)
+            w << "  { rs" << s << " = FIN_ | ST_PASS; goto " << R.se << "; }\n";
+            break;
+          }
           w << "  { const uint32_t k_ = " << kindof << ";\n    rs" << s << " = FIN_ | (k_ == 0u ? ST_PASS : k_ == E_CPU ? ST_CPU : ("
             << ek << " & " << u32((EF_COND | EF_GLOBAL) << 4) << ") ? ST_SKIP : ";
           if (g.uses_anchor) w << "(areg" << s << " & ~apres" << s << ") ? ST_ERROR : ";
@@ -1141,6 +1208,58 @@ struct Gen {
     return w.str();
   }
 
+  // Structural form of rule ri's program for rule groups: its ops with their operands, jump
+  // targets relative to the program start; the pattern nodes and leaf predicates are left out
+  // (listed in pns / preds, the LEAF pcs relative to the start in leafpcs). Empty when the
+  // program holds an op a group cannot run: condition anchors (errors cleared later), existence
+  // anchors, anyPattern, wildcard keys, pattern variables.
+  std::string group_form(uint32_t ri, std::vector<uint32_t>* preds, std::vector<uint32_t>* pns,
+                         std::vector<uint32_t>* leafpcs) const {
+    const RuleRec& rr = ps.rules[ri];
+    if (rr.route != 0) return "";
+    const uint32_t b = rr.prog, e = prog_end(ps, b);
+    std::ostringstream f;
+    auto rel = [&](uint32_t t) { return (int64_t)t - (int64_t)b; };
+    for (uint32_t pc = b; pc <= e; pc++) {
+      const Inst& in = ps.prog[pc];
+      const uint32_t op = in.op & 0xFF, aux = (in.op >> 16) & 0xFF;
+      f << (in.op & 0xFFFFFFu) << ':';  // op | depth << 8 | aux << 16
+      switch (op) {
+        case OP_MAPCHK:
+        case OP_ARRCHK: pns->push_back(in.a); f << rel(in.c); break;
+        case OP_AREG:
+        case OP_KEYV:
+        case OP_INDEX: f << in.a; break;
+        case OP_KEY: f << in.a << ',' << rel(in.b); break;
+        case OP_SCOPE_END:
+          if (aux & EF_COND) return "";
+          f << (in.c ? rel(in.c) : -1);
+          break;
+        case OP_NEG: f << in.a << ','; pns->push_back(in.b); f << rel(in.c); break;
+        case OP_STAR: pns->push_back(in.b); f << rel(in.c); break;
+        case OP_LEAF:
+          preds->push_back(in.a);
+          leafpcs->push_back(pc - b);
+          pns->push_back(in.b);
+          f << rel(in.c);
+          break;
+        case OP_RAISE: f << in.b << ','; pns->push_back(in.a); f << rel(in.c); break;
+        case OP_LENCHK: f << in.a << ','; pns->push_back(in.b); f << rel(in.c); break;
+        case OP_LOOP_BEGIN: f << rel(in.a); break;
+        case OP_LOOP_END: f << rel(in.a) << ',' << rel(in.c); break;
+        case OP_DONE:
+        case OP_NOP:
+        case OP_METACHK: break;
+        default: return "";
+      }
+      f << ';';
+    }
+    return f.str();
+  }
+
+  uint32_t gtab_n = 0;          // member tables emitted so far (per generated program text)
+  std::string block_decls;      // declarations the current kernel's blocks need (member tables)
+
   // Code block of one fused chunk inside a kernel body (its own C++ scope); the
   // chunk's status rows are s_stw rows [hbase, hbase + rules).
   //
@@ -1150,7 +1269,59 @@ struct Gen {
   // status at once; inside the fused loop its error state is local to the element and an
   // element that fails decides the status there (post_chain), so no per-rule register lives
   // across the loop. After the loops the resume pc is rebuilt from the bits.
-  std::string fused_block(const JitChunk& ch, uint32_t hbase) {
+  //
+  // Rule groups (hist_lds kernels): rules of one structural form (group_form) whose pattern
+  // nodes differ by one constant run the representative's program once, with one bit per
+  // member; their leaf predicates take consecutive bits of one table word, so a leaf tests
+  // every member with one shift and mask. The members take consecutive block positions.
+  // `order` receives the block's rules in block position order.
+  std::string fused_block(const JitChunk& ch_in, uint32_t hbase, std::vector<uint32_t>* order) {
+    struct GInfo {
+      std::vector<uint32_t> members, pns0, leafpcs;
+      std::vector<uint32_t> dpn;                 // pattern-node shift of each member
+      std::vector<std::vector<uint32_t>> preds;  // leaf predicates of each member
+    };
+    std::vector<GInfo> ginfo;
+    std::map<uint32_t, size_t> gof;  // rule -> group
+    if (hist_lds) {
+      std::map<std::string, size_t> open;
+      for (uint32_t ri : ch_in.rules) {
+        std::vector<uint32_t> pr, pn, lp;
+        const std::string f = group_form(ri, &pr, &pn, &lp);
+        if (f.empty()) continue;
+        auto it = open.find(f);
+        if (it != open.end()) {
+          GInfo& G = ginfo[it->second];
+          const uint32_t dp = pn.empty() ? 0u : pn[0] - G.pns0[0];
+          bool ok = G.members.size() < 32;
+          for (size_t i = 0; i < pn.size() && ok; i++) ok = pn[i] - G.pns0[i] == dp;
+          if (ok) {
+            G.members.push_back(ri);
+            G.dpn.push_back(dp);
+            G.preds.push_back(pr);
+            gof[ri] = it->second;
+            continue;
+          }
+        }
+        GInfo G;
+        G.members = {ri};
+        G.pns0 = pn;
+        G.leafpcs = lp;
+        G.dpn = {0u};
+        G.preds = {pr};
+        open[f] = ginfo.size();
+        gof[ri] = ginfo.size();
+        ginfo.push_back(std::move(G));
+      }
+    }
+    JitChunk ch;  // block order: a group's members together, at its first member's place
+    for (uint32_t ri : ch_in.rules) {
+      auto it = gof.find(ri);
+      if (it == gof.end()) ch.rules.push_back(ri);
+      else if (ginfo[it->second].members[0] == ri)
+        ch.rules.insert(ch.rules.end(), ginfo[it->second].members.begin(), ginfo[it->second].members.end());
+    }
+    *order = ch.rules;
     const uint32_t nr = (uint32_t)ch.rules.size();
     std::vector<RGen> gs;
     HoistTable global;
@@ -1160,10 +1331,42 @@ struct Gen {
     for (uint32_t q = 0; q < nr; q++) {
       const uint32_t ri = ch.rules[q];
       if (ps.rules[ri].route != 0) continue;
+      auto git = gof.find(ri);
+      if (git != gof.end() && ginfo[git->second].members[0] != ri) continue;  // a group member
       RGen g = analyze(ri);
       g.q = q;
       for (uint32_t pc = g.b; pc <= g.e; pc++)
         if ((ps.prog[pc].op & 0xFF) == OP_LEAF) pred_fn(ps.prog[pc].a);
+      if (git != gof.end()) {
+        const GInfo& G = ginfo[git->second];
+        g.grp = true;
+        g.s = "_G" + std::to_string(hbase + q);
+        g.gn = (uint32_t)G.members.size();
+        g.gri = G.members;
+        g.gdpn = G.dpn;
+        g.grow = (hbase + q) * 256u;
+        for (const auto& m : G.preds)
+          for (uint32_t pi : m) pred_fn(pi);
+        for (size_t i = 0; i < G.leafpcs.size(); i++) {
+          std::vector<uint32_t> lp;
+          for (const auto& m : G.preds) lp.push_back(m[i]);
+          g.gslot[g.b + G.leafpcs[i]] = group_slots(lp);
+        }
+        // members as arithmetic progressions (rule ids, node shifts), else a table
+        bool arith = true;
+        g.gsri = g.gn > 1 ? g.gri[1] - g.gri[0] : 0u;
+        g.gspn = g.gn > 1 ? g.gdpn[1] : 0u;
+        for (uint32_t j = 0; j < g.gn && arith; j++) arith = g.gri[j] == g.gri[0] + j * g.gsri && g.gdpn[j] == j * g.gspn;
+        if (!arith) {
+          g.gtab = "kvg_t" + std::to_string(gtab_n++);
+          std::ostringstream t;
+          t << "__device__ const uint32_t " << g.gtab << "[" << 2 * g.gn << "] = {";
+          for (uint32_t j = 0; j < g.gn; j++) t << u32(g.gri[j]) << ", ";
+          for (uint32_t j = 0; j < g.gn; j++) t << u32(g.gdpn[j]) << (j + 1 < g.gn ? ", " : "");
+          t << "};\n";
+          block_decls += t.str();
+        }
+      }
       K = std::max(K, g.loops.size());
       g.lean.assign(g.loops.size(), 0);
       g.post_flags.assign(g.loops.size(), 0);
@@ -1203,17 +1406,46 @@ struct Gen {
       return k.str();
     };
     auto store = [&](uint32_t q) {
-      const uint32_t ri = ch.rules[q];
-      const std::string s = "_" + std::to_string(ri);
       const RGen* g = nullptr;
       for (const RGen& x : gs)
-        if (x.ri == ri) g = &x;
+        if (x.q == q) g = &x;
+      const std::string s = g ? g->s : "_" + std::to_string(ch.rules[q]);
       const std::string st = "rs" + s + " & 0xFFu";
       if (!g) return store_st(q, g, st, "0u");
+      if (g->grp)  // the members alive here end with the group's status (no error record)
+        return "  if ((rs" + s + " & 0xFFu) != ST_STORED_)\n    kv_gfin(O, n_res, r, valid, al" + s + ", rs" + s +
+               " & 0xFFu, 0u, 0u, 0u, 0u, 0u, (uint8_t*)s_stw + " + u32(g->grow) + ", " +
+               (g->gtab.empty() ? std::string("nullptr") : g->gtab) + ", " + u32(g->gn) + ", " + u32(g->gri[0]) + ", " +
+               u32(g->gsri) + ", " + u32(g->gspn) + ");\n";
       return "  if ((rs" + s + " & 0xFFu) != ST_STORED_) {\n" + store_st(q, g, st, "ek" + s) + "  }\n";
     };
-    // match / route of rule q (rs = its first pc, or FIN | status)
+    // match / route of rule q (rs = its first pc, or FIN | status); of a group: every member's,
+    // the matched ones alive (al), the others stored
     auto match_code = [&](uint32_t q) {
+      const RGen* gp = nullptr;
+      for (const RGen& x : gs)
+        if (x.q == q && x.grp) gp = &x;
+      if (gp) {
+        const RGen& g = *gp;
+        std::ostringstream k;
+        for (uint32_t j = 0; j < g.gn; j++) {
+          const uint32_t ri = g.gri[j];
+          const RuleRec& rr = ps.rules[ri];
+          const std::string rw = "(uint8_t*)s_stw + " + u32(g.grow + j * 256u);
+          auto st = [&](const std::string& x) {
+            return "{ const EState e_{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u}; kv_final(O, " + u32(ri) +
+                   ", n_res, r, valid, " + x + ", e_, " + rw + "); }";
+          };
+          k << "  if (valid && g_match_" << ri << "(P, B, R, rkind, rflags)) {\n"
+            << "    if (rflags & RF_MAGIC) " << st("ST_CPU") << "\n";
+          if (rr.flags & RR_META_EXPAND) k << "    else if (rflags & " << u32(meta_bad_flags(rr.flags)) << ") " << st("ST_CPU") << "\n";
+          if (rr.dyn)
+            k << "    else if (B.dyn_st[(size_t)" << (rr.dyn - 1) << "u * n_res + r]) " << st("B.dyn_st[(size_t)" + std::to_string(rr.dyn - 1) + "u * n_res + r]") << "\n";
+          k << "    else al" << g.s << " |= " << u32(1u << j) << ";\n  } else " << st("ST_NOMATCH") << "\n";
+        }
+        k << "  rs" << g.s << " = al" << g.s << " ? " << u32(g.b) << " : FIN_ | ST_STORED_;\n";
+        return k.str();
+      }
       const uint32_t ri = ch.rules[q];
       const RuleRec& rr = ps.rules[ri];
       const std::string s = "_" + std::to_string(ri);
@@ -1380,7 +1612,14 @@ struct Gen {
           const Inst& end = ps.prog[le];
           if (end.c <= le) throw std::runtime_error("kvjit: loop exit target inside the loop");
           const std::string ek = "ek" + g.s;
-          if (g.lean[k]) {
+          if (g.grp) {  // errors were decided where raised: a group with no member left stops
+            const std::string act = g.lean[k] ? mword("am", k, g.q) + " & " + mbit(g.q) : "rs" + g.s + " & ACT_";
+            if (g.lean[k]) gmask[g.q / 32] |= 1u << (g.q % 32);
+            bodies << "    if (" << act << ") {\n      c" << (d + 1) << g.s << " = el" << tag << ";\n"
+                   << w.str() << "R" << g.ri << "_L" << le << ":;\n      if (!al" << g.s << ") ";
+            if (g.lean[k]) bodies << mword("am", k, g.q) << " &= ~" << mbit(g.q) << ";\n    }\n";
+            else bodies << "rs" << g.s << " = FIN_ | ST_STORED_;\n    }\n";
+          } else if (g.lean[k]) {
             gmask[g.q / 32] |= 1u << (g.q % 32);
             // element-local error state; an error that leaves the loop decides the status now
             bodies << "    if (" << mword("am", k, g.q) << " & " << mbit(g.q) << ") {\n      " << ek << " = 0u;";
@@ -1433,10 +1672,13 @@ struct Gen {
       }
 
     std::ostringstream k;
-    // per-rule state (rules of other routes only carry rs = FIN | status)
-    for (uint32_t ri : ch.rules) k << "  uint32_t rs_" << ri << " = FIN_ | ST_NOMATCH;\n";
+    // per-rule state (rules of other routes only carry rs = FIN | status); a group's: rs and the
+    // alive members
+    for (uint32_t ri : ch.rules)
+      if (!gof.count(ri)) k << "  uint32_t rs_" << ri << " = FIN_ | ST_NOMATCH;\n";
     for (const RGen& g : gs) {
       const std::string& s = g.s;
+      if (g.grp) k << "  uint32_t rs" << s << " = FIN_ | ST_STORED_, al" << s << " = 0u;\n";
       k << "  uint32_t ek" << s << " = 0u";
       for (uint32_t lv = 0; lv <= g.max_level && lv < 4; lv++) k << ", ei" << lv << s << " = 0u";
       if (g.uses_keyglob) k << ", kn" << s << " = ABSENT, ekn" << s << " = ABSENT";
@@ -1466,12 +1708,15 @@ struct Gen {
     uint32_t nr_all = 0;
     for (const JitChunk* c : chs) nr_all += (uint32_t)c->rules.size();
     hist_lds = nr_all * 256u <= 48u * 1024u;  // <= 48 KB of status bytes
+    block_decls.clear();
     for (const JitChunk* c : chs) {
-      blocks.push_back(fused_block(*c, (uint32_t)rules.size()));
-      rules.insert(rules.end(), c->rules.begin(), c->rules.end());
+      std::vector<uint32_t> ord;
+      blocks.push_back(fused_block(*c, (uint32_t)rules.size(), &ord));
+      rules.insert(rules.end(), ord.begin(), ord.end());
     }
     const uint32_t nr = (uint32_t)rules.size();
     KernelText kt(*this, name);
+    o << block_decls;
     o << "__device__ const uint32_t " << name << "_rules[" << nr << "] = {";
     for (uint32_t q = 0; q < nr; q++) o << (q ? ", " : "") << u32(rules[q]);
     o << "};\n";

@@ -310,7 +310,7 @@ extern "C" __global__ __launch_bounds__(KV_WG) __attribute__((amdgpu_waves_per_e
         const size_t o = (size_t)ri * n_res + r;
         O.status[o] = (uint8_t)st;
         if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP))
-          store_err(O, o, ekind, eflags, epn, ekey, eres, eidx0, eidx1, eidx2, eidx3);
+          store_err(O, ri, n_res, r, ekind, eflags, epn, ekey, eres, eidx0, eidx1, eidx2, eidx3);
       }
       // histogram: one LDS atomic per (wave, status) via ballot popcount
       for (uint32_t s = 0; s < 7; s++) {
