@@ -858,13 +858,15 @@ struct DevSession {
     if (stream) (void)hipStreamDestroy(stream);
   }
   // enqueue `iters` passes, wait, return HIP-event milliseconds of all passes
-  double run(int iters) {
+  // vm: run the passes on the bytecode engine even when the policy set has specialized kernels
+  // (the full-record re-run of fetch: the specialized kernels write compact records only)
+  double run(int iters, bool vm = false) {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipEventRecord(e0, stream));
     for (int i = 0; i < iters; i++) {
       HIPCHK(hipMemsetAsync(cn.p, 0, cn.n, stream));
       HIPCHK(launch_mtab((const DevPS*)pview.p, bview, mt_words, mt_entities, mt_ns, mt_ann, mt_sel, stream));
-      if (dps->specialized()) {
+      if (dps->specialized() && !vm) {
         launch_specialized();
       } else {
         HIPCHK(launch_validate((const DevPS*)pview.p, bview, (uint32_t)nres, O, 0, (uint32_t)nrules, stream));
@@ -966,7 +968,7 @@ struct DevSession {
         if (!er.p) er.alloc(nrules * nres * sizeof(ErrRec), device);
         O.err = (ErrRec*)er.p;
         O.full |= 4;
-        run(1);
+        run(1, true);
         O.full &= ~4u;
         if (r_outw.n < total * sizeof(ErrRec)) r_outw.alloc(std::max<uint64_t>(total, 1) * sizeof(ErrRec), device);
         HIPCHK(launch_rec_compact(O.status, O.err8, O.err, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
@@ -1209,7 +1211,7 @@ int kv_compile(const char* policies_json, size_t len, uint32_t flags, kv_policys
         }
         if (!getenv("KVGPU_JIT_SKIP_COMPILE")) {  // (dump-only analysis runs skip it)
           double ms = 0;
-          for (int round = 0; round < 8; round++) {  // register budget: re-plan kernels that spill
+          for (int round = 0; round < 16; round++) {  // register budget: re-plan kernels that spill
             jit_compile(s->jit.get());
             ms += s->jit->compile_ms;
             if (!jit_plan_spills(s->jit.get())) break;

@@ -657,12 +657,19 @@ struct EState {
 __device__ __forceinline__ void store_err(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, uint32_t kind,
                                           uint32_t flags, uint32_t pn, uint32_t key, uint32_t res, uint32_t i0,
                                           uint32_t i1, uint32_t i2, uint32_t i3) {
+#if defined(KV_JIT_PRELUDE) && !defined(KVEMU)
+  // specialized kernels write compact records only: the host re-runs a pass that needs full
+  // records on the bytecode engine (kvapi.cpp DevSession::fetch), which keeps the code of
+  // every record site of these kernels small
+  if (O.full & 4) return;
+#else
   if (O.full & 4) {
     uint4* x = (uint4*)(O.err + (size_t)ri * n_res) + 2u * r;
     x[0] = make_uint4(kind | (flags << 16), pn, key, res);
     x[1] = make_uint4(i0, i1, i2, i3);
     return;
   }
+#endif
   const uint32_t fits = (i0 < 4096u) & (i1 < 1024u) & (i2 < 1024u) & (i3 == 0u) & (key == ABSENT) & (pn < (1u << 25));
   uint2 w;
   w.x = kind | (flags << 4) | ((fits ^ 1u) << 6) | (pn << 7);

@@ -563,6 +563,22 @@ struct Gen {
     }
   };
 
+  // the slots `ks` by predicate (a predicate holds several slots when rule groups share it):
+  // predicate -> (table word -> bits), in first-slot order
+  std::vector<std::pair<uint32_t, std::map<uint32_t, uint32_t>>> pred_words(const std::vector<uint32_t>& ks) const {
+    std::vector<std::pair<uint32_t, std::map<uint32_t, uint32_t>>> out;
+    std::map<uint32_t, size_t> at;
+    for (uint32_t k : ks) {
+      auto it = at.find(mpreds[k]);
+      if (it == at.end()) {
+        it = at.emplace(mpreds[k], out.size()).first;
+        out.push_back({mpreds[k], {}});
+      }
+      out[it->second].second[k / 32] |= 1u << (k % 32);
+    }
+    return out;
+  }
+
   // predicates per kvj_ptab thread: all of them (one grid row)
   uint32_t ptab_row_out() const { return std::max<uint32_t>(1u, (uint32_t)mpreds.size()); }
 
@@ -592,8 +608,15 @@ struct Gen {
       << "    const uint8_t* __restrict__ pstr = Pp->pstr;\n"
       << "    const uint32_t type = v == NV ? NT_NULL : v == NV + 1u ? NT_MAP : NT_ARR;\n"
       << "    const Node n{type, 0u, 0u, 0u};\n";
-    for (uint32_t k = 0; k < mpreds.size(); k++)
-      o << "    if (g_pred_" << mpreds[k] << "(V, S, S, pstr, type, n)) w[" << k / 32 << "] |= " << u32(1u << (k % 32)) << ";\n";
+    {
+      std::vector<uint32_t> all_k(mpreds.size());
+      for (uint32_t k = 0; k < mpreds.size(); k++) all_k[k] = k;
+      for (const auto& [pi, wb] : pred_words(all_k)) {
+        o << "    if (g_pred_" << pi << "(V, S, S, pstr, type, n)) {";
+        for (const auto& [wi, bits] : wb) o << " w[" << wi << "] |= " << u32(bits) << ";";
+        o << " }\n";
+      }
+    }
     for (uint32_t i = 0; i < nw; i++) o << "    PT[(size_t)" << i << "u * NP + v] = w[" << i << "];\n";
     o << "    return;\n  }\n"
       << "  const uint32_t vc = V[v].cls;\n"
@@ -636,18 +659,22 @@ struct Gen {
         } else {
           o << "      const " << qv->mt << "* bm = nullptr;\n";
         }
-        for (uint32_t k : ks)
-          o << "      w[" << k / 32 << "] |= " << qv->pfx << "_pred_" << mpreds[k] << "(V, S, sw, lw, bm, pstr, type, n) ? "
-            << u32(1u << (k % 32)) << " : 0u;\n";
+        for (const auto& [pi, wb] : pred_words(ks)) {  // each predicate once, into every slot it has
+          o << "      { const bool p_ = " << qv->pfx << "_pred_" << pi << "(V, S, sw, lw, bm, pstr, type, n);";
+          for (const auto& [wi, bits] : wb) o << " w[" << wi << "] |= p_ ? " << u32(bits) << " : 0u;";
+          o << " }\n";
+        }
         o << "    }\n";
       }
     }
     o << "  } else {\n";
     for (auto& [m, ks] : groups) {
       o << "    if (vc & " << u32(m) << ") {\n";
-      for (uint32_t k : ks)
-        o << "      if (g_pred_" << mpreds[k] << "(V, S, E, pstr, type, n)) w[" << k / 32 << "] |= " << u32(1u << (k % 32))
-          << ";\n";
+      for (const auto& [pi, wb] : pred_words(ks)) {
+        o << "      if (g_pred_" << pi << "(V, S, E, pstr, type, n)) {";
+        for (const auto& [wi, bits] : wb) o << " w[" << wi << "] |= " << u32(bits) << ";";
+        o << " }\n";
+      }
       o << "    }\n";
     }
     o << "  }\n  }\n";
@@ -1853,12 +1880,14 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
     // it). Default: ceil(n / chunk_rules) ranges of near-equal size.
     // KVGPU_JIT_WAVES: launch bound in waves per SIMD (default 8, 0: none)
     if (out->plan.empty() && n) {
+      // first bound: 8 waves, or what the kernel's LDS status rows (256 B per rule) leave of a
+      // CU's 160 KB (one workgroup = one wave per SIMD); the spill plan lowers it if needed
       const char* wz = getenv("KVGPU_JIT_WAVES");
-      const int waves = wz ? atoi(wz) : 8;
       const uint32_t parts = (n + chunk_rules - 1) / chunk_rules;
       for (uint32_t k = 0; k < parts; k++) {
         const uint32_t a = (uint32_t)((uint64_t)n * k / parts), e = (uint32_t)((uint64_t)n * (k + 1) / parts);
-        out->plan.push_back({a, e - a, waves});
+        const int lds_waves = (int)std::max<uint32_t>(1u, (160u * 1024u) / std::max<uint32_t>(1u, (e - a) * 256u));
+        out->plan.push_back({a, e - a, wz ? atoi(wz) : std::min(8, lds_waves)});
       }
     }
     for (const JitKernelPlan& kp : out->plan) {
@@ -2099,7 +2128,8 @@ void compile_in_children(JitImage* img, const std::vector<size_t>& todo, const s
 // object: the kernel descriptor `<name>.kd` (offset 4: private_segment_fixed_size)
 // and the size of the function symbol. A non-zero private segment in these
 // kernels means register spills (they keep no arrays on the stack).
-bool co_kernel_info(const std::vector<char>& co, const std::string& name, uint32_t* private_seg, uint64_t* code) {
+bool co_kernel_info(const std::vector<char>& co, const std::string& name, uint32_t* private_seg, uint64_t* code,
+                    uint32_t* vgprs) {
   auto rd = [&](size_t off, size_t n, void* out) {
     if (off + n > co.size()) return false;
     memcpy(out, co.data() + off, n);
@@ -2134,6 +2164,10 @@ bool co_kernel_info(const std::vector<char>& co, const std::string& name, uint32
       if (sym == name + ".kd" && shndx < shnum) {
         const Sh& sec = sh[shndx];
         kd = rd(sec.off + (value - sec.addr) + 4, 4, private_seg);
+        // compute_pgm_rsrc1 (descriptor offset 48): granulated VGPR count, 8-register granules
+        // of the unified (arch + acc) file on gfx950
+        uint32_t rsrc1 = 0;
+        if (kd && vgprs && rd(sec.off + (value - sec.addr) + 48, 4, &rsrc1)) *vgprs = ((rsrc1 & 0x3Fu) + 1u) * 8u;
       } else if (sym == name) {
         *code = size;
         fn = true;
@@ -2145,29 +2179,32 @@ bool co_kernel_info(const std::vector<char>& co, const std::string& name, uint32
 
 bool jit_plan_spills(JitImage* img) {
   // No rule kernel ships with a private (scratch) segment, bounded or not (DESIGN.md §4
-  // *Register plan*: every faulting round-1 build had one). A kernel that spills under the
-  // wave bound is recompiled without the bound (it takes the registers it needs, at lower
-  // occupancy); an unbounded kernel that still spills is split in two; a single fused chunk
-  // that spills unbounded is an error.
+  // *Register plan*: every faulting round-1 build had one), and a bound is only kept when the
+  // compiler met it. A kernel that spills under its bound of w waves per SIMD, or that takes
+  // more than 512 / w registers, is recompiled at w - 1 (w = 1: without a bound); an unbounded
+  // kernel that still spills is split in two; a single rule range that does is an error.
   std::vector<JitKernelPlan> next;
   bool changed = false;
   img->kernel_scratch.assign(img->plan.size(), 0);
   for (size_t k = 0; k < img->plan.size(); k++) {
     const JitKernelPlan& kp = img->plan[k];
     const std::string& name = img->chunks[k].name;
-    uint32_t priv = 0;
+    uint32_t priv = 0, vgprs = 0;
     uint64_t code = 0;
     size_t ci = 0;
     while (ci < img->kernel_name.size() && img->kernel_name[ci] != name) ci++;
-    if (ci == img->kernel_name.size() || !co_kernel_info(img->codes[ci], name, &priv, &code))
+    if (ci == img->kernel_name.size() || !co_kernel_info(img->codes[ci], name, &priv, &code, &vgprs))
       throw std::runtime_error("kvjit: no kernel descriptor for " + name);
     img->kernel_scratch[k] = priv;
-    if (priv == 0) {
+    const bool met = kp.waves == 0 || vgprs <= 512u / (uint32_t)kp.waves;
+    if (priv == 0 && met) {
       next.push_back(kp);
       continue;
     }
     changed = true;
-    if (kp.waves != 0) {
+    if (kp.waves > 1) {
+      next.push_back({kp.first, kp.count, kp.waves - 1});
+    } else if (kp.waves == 1) {
       next.push_back({kp.first, kp.count, 0});
     } else if (kp.count > 1) {
       const uint32_t h = kp.count / 2;

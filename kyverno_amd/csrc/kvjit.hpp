@@ -53,12 +53,14 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out);
 // Throws std::runtime_error with the log on failure.
 void jit_compile(JitImage* img);
 uint64_t code_bytes(const JitImage& img);
-// Register budget of the plan: no kernel ships with a private (scratch) segment. A kernel
-// that spills under its wave bound is compiled without the bound; an unbounded kernel that
-// still spills is split in two (a single fused chunk that does: std::runtime_error).
+// Register budget of the plan: no kernel ships with a private (scratch) segment, and a wave
+// bound is kept only when the compiler met it. A kernel that spills (or exceeds the registers)
+// under w waves per SIMD is compiled at w - 1, then without a bound; an unbounded kernel that
+// still spills is split in two (a single rule range that does: std::runtime_error).
 // Returns true when the plan changed (regenerate + compile again; the kernels that did not
 // change come from the code-object cache).
 bool jit_plan_spills(JitImage* img);
-bool co_kernel_info(const std::vector<char>& co, const std::string& name, uint32_t* private_seg, uint64_t* code);
+bool co_kernel_info(const std::vector<char>& co, const std::string& name, uint32_t* private_seg, uint64_t* code,
+                    uint32_t* vgprs = nullptr);
 
 }  // namespace kvh
