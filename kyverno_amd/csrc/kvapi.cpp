@@ -504,19 +504,19 @@ DevBatchRes& dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
   if (it != bt->dev.end()) return *it->second;
   auto d = std::make_unique<DevBatchRes>();
   const Batch& b = bt->b;
-  if (!b.rmask.empty() && b.rmask.size() == b.n_rows && b.nodes.size() == b.n_rows * KV_LANES) {
-    // packed rows (merged batches): upload the non-zero cells, masks and row offsets, then
-    // expand to the wave-group layout on the device
+  if (b.rmask.size() != b.n_rows || b.roff.size() != b.n_rows)
+    throw std::runtime_error("batch: packed row arrays do not match the row count");
+  {
+    // packed rows: upload the non-zero cells, masks and row offsets, then expand to the
+    // wave-group layout on the device
     DevBuf pc, rm, ro;
     pc.upload(b.pcells, device);
     rm.upload(b.rmask, device);
     ro.upload(b.roff, device);
-    d->nodes.alloc(b.nodes.size() * sizeof(Node), device);
+    d->nodes.alloc(b.n_cells() * sizeof(Node), device);
     HIPCHK(launch_expand_rows((const Node*)pc.p, (const uint64_t*)rm.p, (const uint32_t*)ro.p, b.n_rows,
                               (Node*)d->nodes.p, nullptr));
     HIPCHK(hipStreamSynchronize(nullptr));
-  } else {
-    d->nodes.upload(b.nodes, device);
   }
   d->vals.upload(b.vals, device);
   d->res.upload(b.res, device);
@@ -597,8 +597,8 @@ std::vector<PathSeg> path_segs(const PolicySet& ps, const Batch& b, const ErrRec
       case SEG_LOOP: segs.push_back({true, std::to_string(e.idx[n.level & 3])}); break;
       case SEG_CONST_INDEX: segs.push_back({true, std::to_string(n.level)}); break;
       case SEG_RESOLVED: {
-        if (e.keynode != ABSENT && e.keynode < b.nodes.size()) {
-          uint32_t k = node_key(b.nodes[e.keynode].kt);
+        if (e.keynode != ABSENT && e.keynode < b.n_cells()) {
+          uint32_t k = node_key(b.cell(e.keynode).kt);
           segs.push_back({false, k < ps.keys.size() ? ps.keys[k] : b.dyn_keys[k - ps.keys.size()]});
         } else {
           segs.push_back({false, n.key});
@@ -1287,8 +1287,8 @@ int kv_ingest(const kv_policyset* ps, const char* resources_json, size_t len, co
       throw;
     }
     if (getenv("KVGPU_VERBOSE"))
-      fprintf(stderr, "[kvgpu] ingest: %zu resources, %zu nodes, %zu vals, %zu string bytes\n", b->b.res.size(),
-              b->b.nodes.size(), b->b.vals.size(), b->b.strs.size());
+      fprintf(stderr, "[kvgpu] ingest: %zu resources, %zu cells, %zu vals, %zu string bytes\n", b->b.res.size(),
+              (size_t)b->b.cells_used, b->b.vals.size(), b->b.strs.size());
     *out = b;
     return 0;
   } catch (const std::exception& e) {

@@ -13,6 +13,7 @@
 //   pkg/engine/variables/vars.go:20-28,253-309,450-554  $() references (resolved here, once)
 //   pkg/engine/utils.go:37-369            match/exclude blocks
 // Go map iteration order is replaced by the canonical order of DESIGN.md.
+#include <cmath>
 #include <algorithm>
 #include <cstring>
 #include <functional>

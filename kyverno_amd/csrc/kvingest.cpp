@@ -36,43 +36,43 @@ struct Ingest {
   // a hit is confirmed against the bytes already stored in the heap / the value record, so
   // no key string is built or kept per lookup)
   struct Probe {
-    std::vector<uint64_t> h;   // 0 = empty slot
-    std::vector<uint32_t> id;
+    struct Slot {
+      uint64_t h;    // 0 = empty
+      uint32_t id;   // entry id
+      uint32_t aux;  // entry length (string heap) or 0
+    };
+    std::vector<Slot> t;  // one cache line holds 4 slots: a miss costs one line
     size_t n = 0;
     void init(size_t cap) {
-      size_t c = 1024;
+      size_t c = 64;
       while (c < cap * 2) c <<= 1;
-      h.assign(c, 0);
-      id.assign(c, 0);
+      t.assign(c, Slot{0, 0, 0});
       n = 0;
     }
+    // id of the entry with hash hv that eq(slot) confirms, -1 when absent
     template <class Eq>
     int64_t find(uint64_t hv, Eq eq) const {
-      const size_t m = h.size() - 1;
+      const size_t m = t.size() - 1;
       for (size_t i = hv & m;; i = (i + 1) & m) {
-        if (h[i] == 0) return -1;
-        if (h[i] == hv && eq(id[i])) return id[i];
+        if (t[i].h == 0) return -1;
+        if (t[i].h == hv && eq(t[i])) return t[i].id;
       }
     }
-    void insert(uint64_t hv, uint32_t v) {
-      if ((n + 1) * 2 > h.size()) grow();
-      const size_t m = h.size() - 1;
+    void insert(uint64_t hv, uint32_t v, uint32_t aux = 0) {
+      if ((n + 1) * 2 > t.size()) grow();
+      const size_t m = t.size() - 1;
       size_t i = hv & m;
-      while (h[i] != 0) i = (i + 1) & m;
-      h[i] = hv;
-      id[i] = v;
+      while (t[i].h != 0) i = (i + 1) & m;
+      t[i] = Slot{hv, v, aux};
       n++;
     }
     void grow() {
-      std::vector<uint64_t> oh;
-      std::vector<uint32_t> oi;
-      oh.swap(h);
-      oi.swap(id);
-      h.assign(oh.size() * 2, 0);
-      id.assign(oh.size() * 2, 0);
+      std::vector<Slot> o;
+      o.swap(t);
+      t.assign(o.size() * 2, Slot{0, 0, 0});
       n = 0;
-      for (size_t i = 0; i < oh.size(); i++)
-        if (oh[i]) insert(oh[i], oi[i]);
+      for (const Slot& x : o)
+        if (x.h) insert(x.h, x.id, x.aux);
     }
   };
   static uint64_t hash_bytes(const void* p, size_t len, uint64_t seed) {
@@ -91,48 +91,73 @@ struct Ingest {
     h ^= h >> 32;
     return h ? h : 1;
   }
-  Probe str_off;  // string heap offsets (id = offset; length checked against the stored bytes)
+  Probe str_off;  // string heap offsets (id = offset, aux = length; confirmed against the heap)
   Probe val_id;   // scalars (id = value index; type and bytes checked against the Val)
-  std::unordered_map<std::string, uint32_t> dyn_key;   // batch-local key ids
-  std::unordered_map<std::string, uint32_t> ns_index;
+  Probe dict;     // the policy set's key dictionary (id = static key id)
+  Probe dyn_key;  // batch-local key ids (id = index into b.dyn_keys)
+  Probe ns_probe, nsm_probe, lset_probe, aset_probe;  // namespaces, match inputs (confirmed by key)
   uint32_t nstatic;
   std::vector<std::vector<uint32_t>> slot_ids;  // per trie node: key ids of its slots
+  std::vector<Probe> slot_tab;                  // per trie node: slot of a key (built on first use)
 
-  Ingest(const PolicySet& p, Batch& bb) : ps(p), b(bb), nstatic((uint32_t)p.keys.size()), slot_ids(p.trie.nodes.size()) {
+  Ingest(const PolicySet& p, Batch& bb) : ps(p), b(bb), nstatic((uint32_t)p.keys.size()), slot_ids(p.trie.nodes.size()),
+                                          slot_tab(p.trie.nodes.size()) {
     str_off.init(1 << 14);
     val_id.init(1 << 14);
+    dict.init(p.keys.size());
+    for (uint32_t i = 0; i < (uint32_t)p.keys.size(); i++) dict.insert(hash_bytes(p.keys[i].data(), p.keys[i].size(), 'K'), i);
+    dyn_key.init(64);
+    ns_probe.init(1024);
+    nsm_probe.init(1024);
+    lset_probe.init(1024);
+    aset_probe.init(1024);
     // offset 0 holds "0": convertNumberToString(nil) for the device glob (kvkernel.hip atom_eval)
     str("0");
   }
 
-  std::vector<std::pair<uint32_t, uint32_t>> str_ents;  // (offset, length) per interned string
-
   uint32_t str(std::string_view s) {
     const uint64_t hv = hash_bytes(s.data(), s.size(), 0x5354u);
-    const int64_t e = str_off.find(hv, [&](uint32_t x) {
-      return str_ents[x].second == s.size() && memcmp(b.strs.data() + str_ents[x].first, s.data(), s.size()) == 0;
+    const int64_t e = str_off.find(hv, [&](const Probe::Slot& x) {
+      return x.aux == s.size() && memcmp(b.strs.data() + x.id, s.data(), s.size()) == 0;
     });
-    if (e >= 0) return str_ents[(size_t)e].first;
+    if (e >= 0) return (uint32_t)e;
     // 4-byte aligned: the device glob compares whole words (kvkernel.hip seg_at)
     while (b.strs.size() & 3) b.strs.push_back('\0');
     uint32_t off = (uint32_t)b.strs.size();
     b.strs.append(s.data(), s.size());
-    str_off.insert(hv, (uint32_t)str_ents.size());
-    str_ents.push_back({off, (uint32_t)s.size()});
+    str_off.insert(hv, off, (uint32_t)s.size());
     return off;
   }
 
+  // static key id of k (KEY_NONE when the policy set does not know it)
+  uint32_t lookup(std::string_view k) const {
+    const int64_t id = dict.find(hash_bytes(k.data(), k.size(), 'K'), [&](const Probe::Slot& x) { return ps.keys[x.id] == k; });
+    return id >= 0 ? (uint32_t)id : KEY_NONE;
+  }
+
   uint32_t key_of(std::string_view k) {
-    uint32_t id = ps.lookup(k);
+    uint32_t id = lookup(k);
     if (id != KEY_NONE) return id;
-    std::string ks(k);
-    auto it = dyn_key.find(ks);
-    if (it != dyn_key.end()) return it->second;
+    const uint64_t hv = hash_bytes(k.data(), k.size(), 'D');
+    const int64_t hit = dyn_key.find(hv, [&](const Probe::Slot& x) { return b.dyn_keys[x.id] == k; });
+    if (hit >= 0) return nstatic + (uint32_t)hit;
     uint32_t nid = nstatic + (uint32_t)b.dyn_keys.size();
     if (nid >= KEY_NONE28) throw std::runtime_error("ingest: too many distinct keys in one batch");
-    b.dyn_keys.push_back(ks);
-    dyn_key.emplace(ks, nid);
+    dyn_key.insert(hv, (uint32_t)b.dyn_keys.size());
+    b.dyn_keys.emplace_back(k);
     return nid;
+  }
+
+  // id of `k` among `keys` (interned through `pr`), appending it when new
+  static uint32_t intern(Probe& pr, std::vector<std::string>& keys, std::string_view k, bool* fresh) {
+    const uint64_t hv = hash_bytes(k.data(), k.size(), 'I');
+    const int64_t hit = pr.find(hv, [&](const Probe::Slot& x) { return keys[x.id] == k; });
+    *fresh = hit < 0;
+    if (hit >= 0) return (uint32_t)hit;
+    const uint32_t id = (uint32_t)keys.size();
+    keys.emplace_back(k);
+    pr.insert(hv, id);
+    return id;
   }
 
   uint32_t val(const JDoc& d, const JNode& n) {
@@ -144,8 +169,8 @@ struct Ingest {
       case J_FLOAT: hv = hash_bytes(&n.f, 8, 'f'); break;
       default: sv = d.sval(n); hv = hash_bytes(sv.data(), sv.size(), 's'); break;
     }
-    const int64_t hit = val_id.find(hv, [&](uint32_t x) {
-      const Val& v = b.vals[x];
+    const int64_t hit = val_id.find(hv, [&](const Probe::Slot& x) {
+      const Val& v = b.vals[x.id];
       switch (n.t) {
         case J_BOOL: return v.type == NT_BOOL && ((v.flags & VF_BOOLV) != 0) == n.b;
         case J_INT: return v.type == NT_INT && v.i == n.i;
@@ -156,7 +181,11 @@ struct Ingest {
     });
     if (hit >= 0) return (uint32_t)hit;
     Val v{};
-    std::string e, num;
+    // e: the validateString form; num: the number-with-string form (same bytes except for
+    // floats, where they are FormatFloat 'E' and %f)
+    std::string_view e, num;
+    std::string fe, fnum;
+    char ibuf[24];
     bool nvalid = true;
     switch (n.t) {
       case J_BOOL:
@@ -165,25 +194,26 @@ struct Ingest {
         nvalid = false;
         v.flags |= n.b ? VF_BOOLV : VF_NILLIKE;
         break;
-      case J_INT:
+      case J_INT: {
         v.type = NT_INT;
         v.i = n.i;
-        e = std::to_string(n.i);
-        num = e;
+        const int len = snprintf(ibuf, sizeof ibuf, "%lld", (long long)n.i);
+        e = num = std::string_view(ibuf, (size_t)len);
         if (n.i == 0) v.flags |= VF_NILLIKE;
         break;
+      }
       case J_FLOAT:
         v.type = NT_FLOAT;
         v.f = n.f;
-        e = go_format_E(n.f);
-        num = go_format_f6(n.f);
+        fe = go_format_E(n.f);
+        fnum = go_format_f6(n.f);
+        e = fe;
+        num = fnum;
         if (n.f == 0.0) v.flags |= VF_NILLIKE;
         break;
       default: {
         v.type = NT_STR;
-        std::string_view sv = d.sval(n);
-        e = std::string(sv);
-        num = e;
+        e = num = sv;
         double f;
         if (go_parse_float(sv, &f)) { v.flags |= VF_PF_OK; v.f = f; }
         if (sv.empty()) v.flags |= VF_NILLIKE;
@@ -192,12 +222,14 @@ struct Ingest {
     }
     v.e_off = str(e);
     v.e_len = (uint32_t)e.size();
-    if (utf8_ascii(e)) v.flags |= VF_ASCII_E;
+    const bool e_ascii = utf8_ascii(e);
+    if (e_ascii) v.flags |= VF_ASCII_E;
     if (nvalid) {
       v.flags |= VF_N_VALID;
-      v.n_off = str(num);
+      const bool same = num.data() == e.data();
+      v.n_off = same ? v.e_off : str(num);
       v.n_len = (uint32_t)num.size();
-      if (utf8_ascii(num)) v.flags |= VF_ASCII_N;
+      if (same ? e_ascii : utf8_ascii(num)) v.flags |= VF_ASCII_N;
       QCanon q = parse_quantity(num);
       if (q.valid) {
         v.flags |= VF_Q_VALID;
@@ -227,22 +259,36 @@ struct Ingest {
     uint32_t row = 0;          // row within the group
     bool has_map = false, has_arr = false, keep_all = false;
     uint32_t map_row = 0, arr_row = 0;
-    std::vector<Shape> kids;   // map block (slot-addressed: one per slot key; keep-all: max count)
-    std::vector<Shape> elems;  // array block (max length)
-  };
-
-  // slot of key k in a slot-addressed trie node (binary search of its byte-sorted keys,
-  // no string built per lookup), -1 when the key is not projected
-  static int32_t slot_of(const Trie::N& tn, std::string_view k) {
-    size_t lo = 0, hi = tn.slot_keys.size();
-    while (lo < hi) {
-      const size_t mid = (lo + hi) / 2;
-      const int c = std::string_view(tn.slot_keys[mid]).compare(k);
-      if (c == 0) return (int32_t)mid;
-      if (c < 0) lo = mid + 1;
-      else hi = mid;
+    // map block (slot-addressed: one per slot key; keep-all: max count) and array block (max
+    // length): the first nk / ne entries; the vectors are pools kept across groups
+    uint32_t nk = 0, ne = 0;
+    std::vector<Shape> kids;
+    std::vector<Shape> elems;
+    void reset(int32_t trie) {
+      t = trie;
+      row = map_row = arr_row = 0;
+      has_map = has_arr = keep_all = false;
+      nk = ne = 0;
     }
-    return -1;
+  };
+  Shape shape_root;  // the current group's shape (reused)
+  // slot of each map child at a slot-addressed trie node, found by unite and reused by put:
+  // per lane, indexed by the child's node index in its document
+  std::vector<int32_t> jslot[KV_LANES];
+  std::vector<uint32_t> kids_sorted;  // (reused)
+
+  // slot of key k in slot-addressed trie node t (a hash table of its slot keys, built on
+  // first use; no string built per lookup), -1 when the key is not projected
+  int32_t slot_of(int32_t t, std::string_view k) {
+    const Trie::N& tn = ps.trie.nodes[t];
+    Probe& tab = slot_tab[t];
+    if (tab.t.empty()) {
+      tab.init(tn.slot_keys.size());
+      for (uint32_t i = 0; i < (uint32_t)tn.slot_keys.size(); i++)
+        tab.insert(hash_bytes(tn.slot_keys[i].data(), tn.slot_keys[i].size(), 'S'), i);
+    }
+    return (int32_t)tab.find(hash_bytes(k.data(), k.size(), 'S'),
+                             [&](const Probe::Slot& x) { return tn.slot_keys[x.id] == k; });
   }
 
   void sorted_children(const JDoc& d, const JNode& n, std::vector<uint32_t>* out) {
@@ -251,7 +297,7 @@ struct Ingest {
     std::sort(out->begin(), out->end(), [&](uint32_t x, uint32_t y) { return d.key(d.at(x)) < d.key(d.at(y)); });
   }
 
-  void unite(Shape& s, const JDoc& d, uint32_t jn) {
+  void unite(Shape& s, const JDoc& d, uint32_t jn, std::vector<int32_t>& js) {
     const JNode& n = d.at(jn);
     if (n.t == J_MAP) {
       if (s.t < 0) return;
@@ -260,46 +306,53 @@ struct Ingest {
         s.has_map = true;
         s.keep_all = tn.keep_all;
         if (!tn.keep_all) {
-          s.kids.resize(tn.slot_keys.size());
-          for (size_t i = 0; i < tn.slot_keys.size(); i++) s.kids[i].t = (int32_t)tn.kids.at(tn.slot_keys[i]);
+          const uint32_t K = (uint32_t)tn.slot_keys.size();
+          if (s.kids.size() < K) s.kids.resize(K);
+          for (uint32_t i = 0; i < K; i++) s.kids[i].reset((int32_t)tn.kids.at(tn.slot_keys[i]));
+          s.nk = K;
         }
       }
       if (tn.keep_all) {
-        if (s.kids.size() < n.count) s.kids.resize(n.count);  // children leaf-only (t = -1)
+        if (s.nk < n.count) {  // children leaf-only (t = -1)
+          if (s.kids.size() < n.count) s.kids.resize(n.count);
+          for (uint32_t i = s.nk; i < n.count; i++) s.kids[i].reset(-1);
+          s.nk = n.count;
+        }
         std::vector<uint32_t> ch;
         sorted_children(d, n, &ch);
-        for (size_t i = 0; i < ch.size(); i++) unite(s.kids[i], d, ch[i]);
+        for (size_t i = 0; i < ch.size(); i++) unite(s.kids[i], d, ch[i], js);
       } else {
         for (uint32_t c = n.first; c < n.first + n.count; c++) {
-          const int32_t si = slot_of(tn, d.key(d.at(c)));
-          if (si >= 0) unite(s.kids[si], d, c);
+          const int32_t si = slot_of(s.t, d.key(d.at(c)));
+          js[c] = si;
+          if (si >= 0) unite(s.kids[si], d, c, js);
         }
       }
     } else if (n.t == J_ARR) {
       s.has_arr = true;
       const int32_t et = s.t >= 0 ? ps.trie.nodes[s.t].elem : -1;
-      if (s.elems.size() < n.count) {
-        size_t old = s.elems.size();
-        s.elems.resize(n.count);
-        for (size_t j = old; j < n.count; j++) s.elems[j].t = et;
+      if (s.ne < n.count) {
+        if (s.elems.size() < n.count) s.elems.resize(n.count);
+        for (uint32_t j = s.ne; j < n.count; j++) s.elems[j].reset(et);
+        s.ne = n.count;
       }
-      for (uint32_t j = 0; j < n.count; j++) unite(s.elems[j], d, n.first + j);
+      for (uint32_t j = 0; j < n.count; j++) unite(s.elems[j], d, n.first + j, js);
     }
   }
 
   void assign(Shape& s, uint32_t* next) {
     if (s.has_map) {
       s.map_row = *next;
-      *next += (uint32_t)s.kids.size();
-      for (size_t i = 0; i < s.kids.size(); i++) s.kids[i].row = s.map_row + (uint32_t)i;
+      *next += s.nk;
+      for (uint32_t i = 0; i < s.nk; i++) s.kids[i].row = s.map_row + i;
     }
     if (s.has_arr) {
       s.arr_row = *next;
-      *next += (uint32_t)s.elems.size();
-      for (size_t j = 0; j < s.elems.size(); j++) s.elems[j].row = s.arr_row + (uint32_t)j;
+      *next += s.ne;
+      for (uint32_t j = 0; j < s.ne; j++) s.elems[j].row = s.arr_row + j;
     }
-    for (auto& k : s.kids) assign(k, next);
-    for (auto& e : s.elems) assign(e, next);
+    for (uint32_t i = 0; i < s.nk; i++) assign(s.kids[i], next);
+    for (uint32_t j = 0; j < s.ne; j++) assign(s.elems[j], next);
   }
 
   Node scalar(const JDoc& d, const JNode& n, uint32_t type, uint32_t key, int32_t pos) {
@@ -315,11 +368,18 @@ struct Ingest {
   }
 
   uint64_t base_row = 0;  // first row of the current group
-  Node& cell(uint32_t row, uint32_t lane) { return b.nodes[(size_t)(base_row + row) * KV_LANES + lane]; }
+  // the current group's padded rows (reused, cache-resident); packed into b.pcells at its end
+  std::vector<Node> gcells;
+  std::vector<uint64_t> gmask;  // lanes written per row of the group
+  void set_cell(uint32_t row, uint32_t lane, const Node& v) {
+    gcells[(size_t)row * KV_LANES + lane] = v;
+    gmask[row] |= 1ull << lane;
+  }
 
   // Write lane's value at shape position s (key = key id in the parent map)
   // pos: position class id of this value (kv_pos_*; Val::cls)
   void put(const Shape& s, const JDoc& d, uint32_t jn, uint32_t lane, uint32_t key, int32_t pos) {
+    const std::vector<int32_t>& js = jslot[lane];
     const JNode& n = d.at(jn);
     Node out{(key & KEY_NONE28) << 4 | NT_NULL, 0, 0, 0};
     switch (n.t) {
@@ -343,9 +403,9 @@ struct Ingest {
           out.b = K;
           auto& ids = slot_ids[s.t];
           for (uint32_t i = (uint32_t)ids.size(); i < K; i++) ids.push_back(key_of(tn.slot_keys[i]));
-          for (uint32_t i = 0; i < K; i++) cell(s.map_row + i, lane) = Node{(ids[i] & KEY_NONE28) << 4 | NT_ABSENT, 0, 0, 0};
+          for (uint32_t i = 0; i < K; i++) set_cell(s.map_row + i, lane, Node{(ids[i] & KEY_NONE28) << 4 | NT_ABSENT, 0, 0, 0});
           for (uint32_t c = n.first; c < n.first + n.count; c++) {
-            const int32_t si = slot_of(tn, d.key(d.at(c)));
+            const int32_t si = js[c];
             if (si >= 0) put(s.kids[si], d, c, lane, ids[si], s.kids[si].t);
           }
         }
@@ -359,7 +419,7 @@ struct Ingest {
         break;
       }
     }
-    cell(s.row, lane) = out;
+    set_cell(s.row, lane, out);
   }
 
   std::vector<JDoc> group;
@@ -368,29 +428,65 @@ struct Ingest {
 
   void flush_group() {
     if (group_n == 0) return;
-    Shape root;
-    root.t = 0;
-    for (uint32_t l = 0; l < group_n; l++) unite(root, group[l], group[l].root);
+    Shape& root = shape_root;
+    root.reset(0);
+    for (uint32_t l = 0; l < group_n; l++) {
+      if (jslot[l].size() < group[l].nodes.size()) jslot[l].resize(group[l].nodes.size());
+      unite(root, group[l], group[l].root, jslot[l]);
+    }
     uint32_t rows = 1;
     root.row = 0;
     assign(root, &rows);
     base_row = b.n_rows;
     b.n_rows += rows;
     if (b.n_rows * KV_LANES >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: batch too large for 32-bit node indices");
-    // capacity for the rest of the part from the rows per group so far (+1/8), instead of
-    // the vector's doubling (each doubling copies every cell written so far)
-    const size_t want = (size_t)b.n_rows * KV_LANES;
-    if (want > b.nodes.capacity() && expected_res > b.res.size()) {
-      const double per_res = (double)b.n_rows / (double)b.res.size();
-      b.nodes.reserve(std::max(want, (size_t)(per_res * (double)expected_res * 1.125) * KV_LANES));
-    }
-    b.nodes.resize(want, Node{NT_NULL, 0, 0, 0});
+    if (gcells.size() < (size_t)rows * KV_LANES) gcells.resize((size_t)rows * KV_LANES);
+    gmask.assign(rows, 0);
     for (uint32_t l = 0; l < group_n; l++) {
       put(root, group[l], group[l].root, l, KEY_NONE, 0);
       b.res[b.res.size() - group_n + l].root = (uint32_t)base_row;
     }
-    for (size_t c = (size_t)base_row * KV_LANES; c < b.nodes.size(); c++)
-      if (b.nodes[c].kt | b.nodes[c].a | b.nodes[c].b | b.nodes[c].c) b.cells_used++;
+    // capacity for the rest of the part from the cells per group so far (+1/8), instead of
+    // the vector's doubling (each doubling copies every cell written so far)
+    const size_t want = b.pcells.size() + gcells.size();
+    if (want > b.pcells.capacity()) {
+      size_t cap = want;
+      if (expected_res > b.res.size())
+        cap = std::max(cap, (size_t)((double)want / (double)b.res.size() * (double)expected_res * 1.125));
+      b.pcells.reserve(std::max(cap, b.pcells.capacity() * 2));
+      if (expected_res > b.res.size()) {  // values, strings and headers grow in proportion
+        const double f = (double)expected_res / (double)b.res.size() * 1.125;
+        if (b.vals.capacity() < (size_t)(b.vals.size() * f)) b.vals.reserve((size_t)(b.vals.size() * f));
+        if (b.strs.capacity() < (size_t)(b.strs.size() * f)) b.strs.reserve((size_t)(b.strs.size() * f));
+        if (b.res.capacity() < expected_res) b.res.reserve(expected_res);
+      }
+      b.rmask.reserve(std::max<size_t>(b.rmask.capacity() * 2, cap / KV_LANES + rows));
+      b.roff.reserve(std::max<size_t>(b.roff.capacity() * 2, cap / KV_LANES + rows));
+    }
+    // packed rows: the non-zero cells of each row, its lane mask and first packed cell
+    size_t pc = b.pcells.size(), nw = 0;
+    for (uint32_t row = 0; row < rows; row++) nw += (size_t)__builtin_popcountll(gmask[row]);
+    b.pcells.resize(pc + nw);
+    const size_t r0 = b.rmask.size();
+    b.rmask.resize(r0 + rows);
+    b.roff.resize(r0 + rows);
+    Node* out = b.pcells.data();
+    for (uint32_t row = 0; row < rows; row++) {
+      const Node* c = &gcells[(size_t)row * KV_LANES];
+      uint64_t m = 0;
+      b.roff[r0 + row] = (uint32_t)pc;
+      for (uint64_t w = gmask[row]; w; w &= w - 1) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(w);
+        if (c[l].kt | c[l].a | c[l].b | c[l].c) {
+          m |= 1ull << l;
+          out[pc++] = c[l];
+        }
+      }
+      b.rmask[r0 + row] = m;
+    }
+    b.pcells.resize(pc);
+    if (b.pcells.size() >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: batch too large for 32-bit cell offsets");
+    b.cells_used = b.pcells.size();
     group_n = 0;
   }
 
@@ -426,26 +522,28 @@ struct Ingest {
   // Interned label / annotation list of a resource: identical lists (same pairs, same
   // validity bits) share one KVSet, so the match tables evaluate a selector or an
   // annotation filter once per distinct list.
-  std::unordered_map<std::string, uint32_t> lset_id, aset_id, nsm_id;
+  std::vector<std::pair<std::string_view, std::string_view>> pairs;  // (reused)
+  std::string kbuf;                                                  // (reused)
   uint32_t kvset(const JDoc& d, int64_t mapnode, bool labels) {
-    std::vector<std::pair<std::string_view, std::string_view>> pairs;
+    pairs.clear();
     if (mapnode >= 0) {
       const JNode& m = d.at((uint32_t)mapnode);
       if (is_str_map(d, m))  // else NestedStringMap error -> nil map
         for (uint32_t c = m.first; c < m.first + m.count; c++) pairs.push_back({d.key(d.at(c)), d.sval(d.at(c))});
     }
     std::sort(pairs.begin(), pairs.end());
-    std::string key;
+    std::string& key = kbuf;
+    key.clear();
     for (auto& p : pairs) {
       key.append(p.first.data(), p.first.size());
       key.push_back('\0');
       key.append(p.second.data(), p.second.size());
       key.push_back('\0');
     }
-    auto& ids = labels ? lset_id : aset_id;
     auto& sets = labels ? b.lsets : b.asets;
-    auto it = ids.find(key);
-    if (it != ids.end()) return it->second;
+    bool fresh = false;
+    const uint32_t id = intern(labels ? lset_probe : aset_probe, labels ? b.lset_keys : b.aset_keys, key, &fresh);
+    if (!fresh) return id;
     KVSet set{(uint32_t)b.kvs.size(), (uint32_t)pairs.size()};
     for (auto& p : pairs) {
       KV kv{};
@@ -459,21 +557,14 @@ struct Ingest {
       }
       b.kvs.push_back(kv);
     }
-    const uint32_t id = (uint32_t)sets.size();
     sets.push_back(set);
-    (labels ? b.lset_keys : b.aset_keys).push_back(key);
-    ids.emplace(std::move(key), id);
     return id;
   }
 
   uint32_t nsm(std::string_view s) {
-    std::string k(s);
-    auto it = nsm_id.find(k);
-    if (it != nsm_id.end()) return it->second;
-    const uint32_t id = (uint32_t)b.nsms.size();
-    b.nsms.push_back(StrRef{str(s), (uint32_t)s.size()});
-    b.nsm_keys.push_back(k);
-    nsm_id.emplace(std::move(k), id);
+    bool fresh = false;
+    const uint32_t id = intern(nsm_probe, b.nsm_keys, s, &fresh);
+    if (fresh) b.nsms.push_back(StrRef{str(s), (uint32_t)s.size()});
     return id;
   }
 
@@ -496,34 +587,32 @@ struct Ingest {
       labels = d.get((uint32_t)md, "labels");
       ann = d.get((uint32_t)md, "annotations");
     }
-    r.kind = ps.lookup(kind);
+    r.kind = lookup(kind);
     std::string_view grp, ver;
     if (!apiv.empty() && apiv != "/") {
       size_t c = std::count(apiv.begin(), apiv.end(), '/');
       if (c == 0) ver = apiv;
       else if (c == 1) { size_t i = apiv.find('/'); grp = apiv.substr(0, i); ver = apiv.substr(i + 1); }
     }
-    r.group = ps.lookup(grp);
-    r.version = ps.lookup(ver);
+    r.group = lookup(grp);
+    r.version = lookup(ver);
     r.name_off = str(name);
     r.name_len = (uint32_t)name.size();
-    if (utf8_ascii(std::string(name))) r.flags |= RF_NAME_ASCII;
+    if (utf8_ascii(name)) r.flags |= RF_NAME_ASCII;
     bool isns = kind == "Namespace";
     r.nsm = nsm(isns ? name : ns);
     if (isns) r.flags |= RF_KIND_NAMESPACE;
     if (kind.empty()) r.flags |= RF_KIND_EMPTY;
     r.lset = kvset(d, labels, true);
     r.aset = kvset(d, ann, false);
-    std::string nss(ns);
-    auto it = ns_index.find(nss);
-    if (it == ns_index.end()) {
-      it = ns_index.emplace(nss, (uint32_t)b.namespaces.size()).first;
-      b.namespaces.push_back(nss);
-    }
-    r.ns_index = it->second;
+    bool fresh = false;
+    r.ns_index = intern(ns_probe, b.namespaces, ns, &fresh);
     if (const uint32_t bm = bad_meta(d)) r.flags |= RF_BAD_META | bm;
-    if (d.strs.find("conditional anchor mismatch") != std::string::npos ||
-        d.strs.find("global anchor mismatch") != std::string::npos)
+    // the anchor-mismatch error substrings (common/anchorKey.go:12-19): both end in
+    // "anchor mismatch", so one search finds any candidate
+    if (memmem(d.strs.data(), d.strs.size(), "anchor mismatch", 15) &&
+        (d.strs.find("conditional anchor mismatch") != std::string::npos ||
+         d.strs.find("global anchor mismatch") != std::string::npos))
       r.flags |= RF_MAGIC;
     b.res.push_back(r);  // root row assigned by flush_group
     // pattern variables: every distinct (string, path) resolved on this resource (kvvars.cpp)
@@ -673,7 +762,7 @@ void order_vals(Batch& b) {
     out[perm[i]] = b.vals[i];
   }
   b.vals.swap(out);
-  for (Node& nd : b.nodes) {
+  for (Node& nd : b.pcells) {
     const uint32_t t = node_type(nd.kt);
     if (t == NT_BOOL || t == NT_INT || t == NT_FLOAT || t == NT_STR) nd.a = perm[nd.a];
   }
@@ -683,13 +772,13 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
   const size_t P = parts.size();
   std::unordered_map<std::string, uint32_t> dyn, nsi, gnsm, glset, gaset;
   std::vector<std::vector<uint32_t>> dmap(P), nmap(P), nsmmap(P), lmap(P), amap(P);
-  std::vector<uint64_t> hb(P), vb(P), kb(P), rb(P), nb(P), resb(P);
-  uint64_t H = 0, V = 0, K = 0, R = 0, N = 0, RS = 0;
+  std::vector<uint64_t> hb(P), vb(P), kb(P), rb(P), resb(P);
+  uint64_t H = 0, V = 0, K = 0, R = 0, RS = 0;
   for (size_t k = 0; k < P; k++) {  // offsets and id remaps (serial, small)
     Batch& q = parts[k];
     H = (H + 3) & ~3ull;
-    hb[k] = H; vb[k] = V; kb[k] = K; rb[k] = R; nb[k] = N; resb[k] = RS;
-    H += q.strs.size(); V += q.vals.size(); K += q.kvs.size(); R += q.n_rows; N += q.nodes.size(); RS += q.res.size();
+    hb[k] = H; vb[k] = V; kb[k] = K; rb[k] = R; resb[k] = RS;
+    H += q.strs.size(); V += q.vals.size(); K += q.kvs.size(); R += q.n_rows; RS += q.res.size();
     for (const std::string& s : q.dyn_keys) {
       auto it = dyn.find(s);
       if (it == dyn.end()) {
@@ -753,17 +842,16 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
   }
   if (H >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: string heap exceeds 4 GiB");
   if (R * KV_LANES >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: batch too large for 32-bit node indices");
-  b.pin_store(true);
+  b.pin_store();
   std::vector<uint64_t> pcb(P + 1, 0);  // packed-cell base of each part (its non-zero cells)
-  for (size_t k = 0; k < P; k++) pcb[k + 1] = pcb[k] + parts[k].cells_used;
+  for (size_t k = 0; k < P; k++) pcb[k + 1] = pcb[k] + parts[k].pcells.size();
+  if (pcb[P] >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: batch too large for 32-bit cell offsets");
   b.pcells.resize(pcb[P]);
   b.rmask.resize(R);
   b.roff.resize(R);
-  std::vector<std::string> perr(P);
   b.strs.assign(H, '\0');
   b.vals.resize(V);
   b.kvs.resize(K);
-  b.nodes.resize(N);
   b.res.resize(RS);
   b.n_rows = R;
   std::vector<KeyCount> hists(P);
@@ -791,9 +879,11 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
         x.v_off += h;
         b.kvs[kb[k] + i] = x;
       }
-      Node* out = &b.nodes[nb[k]];
-      for (size_t i = 0; i < q.nodes.size(); i++) {
-        Node nd = q.nodes[i];
+      // packed cells with key ids, rows, values and string offsets rebased (a remapped cell
+      // stays non-zero: its row masks and offsets carry over, offset by the part's base)
+      Node* out = &b.pcells[pcb[k]];
+      for (size_t i = 0; i < q.pcells.size(); i++) {
+        Node nd = q.pcells[i];
         const uint32_t t = node_type(nd.kt);
         uint32_t key = node_key(nd.kt);
         if (key >= nstatic && key != KEY_NONE28) key = dmap[k][key - nstatic];
@@ -802,28 +892,8 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
         else if (t == NT_BOOL || t == NT_INT || t == NT_FLOAT || t == NT_STR) { nd.a = perm[nd.a]; nd.b += h; }
         out[i] = nd;
       }
-      // packed transfer form of the part's rows (remapping keeps zero cells zero and
-      // non-zero cells non-zero, so the part's count from ingest sizes its range)
-      uint64_t pc = pcb[k];
-      for (uint64_t row = 0; row < q.n_rows; row++) {
-        const Node* cells = out + row * KV_LANES;
-        uint64_t m = 0;
-        b.roff[r0 + row] = (uint32_t)pc;
-        for (uint32_t l = 0; l < KV_LANES; l++)
-          if (cells[l].kt | cells[l].a | cells[l].b | cells[l].c) {
-            if (pc >= pcb[k + 1]) {
-              perr[k] = "ingest: packed cell count mismatch";
-              return;
-            }
-            m |= 1ull << l;
-            b.pcells[pc++] = cells[l];
-          }
-        b.rmask[r0 + row] = m;
-      }
-      if (pc != pcb[k + 1]) {
-        perr[k] = "ingest: packed cell count mismatch";
-        return;
-      }
+      memcpy(&b.rmask[r0], q.rmask.data(), q.n_rows * sizeof(uint64_t));
+      for (uint64_t row = 0; row < q.n_rows; row++) b.roff[r0 + row] = q.roff[row] + (uint32_t)pcb[k];
       for (size_t i = 0; i < q.res.size(); i++) {
         Res r = q.res[i];
         r.root += r0;
@@ -834,11 +904,9 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
         r.ns_index = nmap[k][r.ns_index];
         b.res[resb[k] + i] = r;
       }
-      Batch().nodes.swap(q.nodes);
+      StoreVec<Node>().swap(q.pcells);
     });
   for (auto& t : th) t.join();
-  for (auto& e : perr)
-    if (!e.empty()) throw std::runtime_error(e);
 }
 
 }  // namespace
@@ -896,7 +964,7 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
     Ingest in(ps, *b);
     parse_json_stream(json, len, NUM_UNSTRUCTURED, [&](JDoc& d) { in.take(d); });
     in.flush_group();
-    ns_index = std::move(in.ns_index);
+    for (size_t i = 0; i < b->namespaces.size(); i++) ns_index.emplace(b->namespaces[i], (uint32_t)i);
     order_vals(*b);
   }
   // namespace labels (CLI --values-file namespaceSelector map / cluster namespaces)

@@ -239,23 +239,28 @@ using StoreVec = std::vector<T, StoreAlloc<T>>;
 
 // Ingested batch (host mirror of the HBM store)
 struct Batch {
-  StoreVec<kv::Node> nodes;          // [n_rows][KV_LANES] (wave-group layout, kvingest.cpp)
+  // Node rows in packed form: the wave-group layout (kvingest.cpp) has n_rows rows of
+  // KV_LANES cells (node index = row * KV_LANES + lane); the host keeps only the non-zero
+  // cells of every row in row order (`pcells`), a 64-bit lane mask per row (`rmask`) and
+  // the first packed cell of each row (`roff`). kv_validate uploads these and expands the
+  // rows on the device (kv_expand_rows_kernel), so the row padding (40+ % of the cells at
+  // C2) is never written on the host nor sent over PCIe.
   uint64_t n_rows = 0;
-  uint64_t cells_used = 0;           // populated cells (incl. absent-slot markers)
+  uint64_t cells_used = 0;           // populated cells (incl. absent-slot markers) = pcells.size()
   StoreVec<kv::Val> vals;
   StoreVec<kv::Res> res;
-  // Transfer form of `nodes` (merged batches): the non-zero cells of every row in row
-  // order, a 64-bit lane mask per row and the first packed cell of each row. kv_validate
-  // uploads these and expands the rows on the device (kv_expand_rows_kernel), so the row
-  // padding of the wave-group layout (40+ % of the cells at C2) does not cross PCIe.
   StoreVec<kv::Node> pcells;
   StoreVec<uint64_t> rmask;
   StoreVec<uint32_t> roff;
-  // the arrays that cross PCIe in page-locked memory when g_hostmem provides it: the
-  // merged batch uploads the packed rows (its padded `nodes` stay pageable), a shard its
-  // padded rows
-  void pin_store(bool packed_rows) {
-    nodes = StoreVec<kv::Node>(StoreAlloc<kv::Node>(!packed_rows));
+  // cell `idx` of the padded layout (zero Node where the row has no cell in that lane)
+  kv::Node cell(uint64_t idx) const {
+    const uint64_t row = idx / kv::KV_LANES, lane = idx % kv::KV_LANES;
+    if (row >= n_rows || !((rmask[row] >> lane) & 1ull)) return kv::Node{0u, 0u, 0u, 0u};
+    return pcells[(uint64_t)roff[row] + (uint64_t)__builtin_popcountll(rmask[row] & ((1ull << lane) - 1ull))];
+  }
+  uint64_t n_cells() const { return n_rows * kv::KV_LANES; }
+  // the arrays that cross PCIe in page-locked memory when g_hostmem provides it
+  void pin_store() {
     vals = StoreVec<kv::Val>(StoreAlloc<kv::Val>(true));
     res = StoreVec<kv::Res>(StoreAlloc<kv::Res>(true));
     pcells = StoreVec<kv::Node>(StoreAlloc<kv::Node>(true));

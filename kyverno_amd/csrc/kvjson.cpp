@@ -1,28 +1,33 @@
 // Arena JSON parser (see kvjson.hpp).
 #include "kvjson.hpp"
 
+#include <algorithm>
 #include <cstring>
 
 namespace kvh {
 
 namespace {
 
-inline void put_utf8(std::string& out, uint32_t cp) {
+// UTF-8 bytes of code point cp at out (returns the count, 1..4)
+inline size_t put_utf8(char* out, uint32_t cp) {
   if (cp < 0x80) {
-    out.push_back((char)cp);
+    out[0] = (char)cp;
+    return 1;
   } else if (cp < 0x800) {
-    out.push_back((char)(0xC0 | (cp >> 6)));
-    out.push_back((char)(0x80 | (cp & 0x3F)));
+    out[0] = (char)(0xC0 | (cp >> 6));
+    out[1] = (char)(0x80 | (cp & 0x3F));
+    return 2;
   } else if (cp < 0x10000) {
-    out.push_back((char)(0xE0 | (cp >> 12)));
-    out.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
-    out.push_back((char)(0x80 | (cp & 0x3F)));
-  } else {
-    out.push_back((char)(0xF0 | (cp >> 18)));
-    out.push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
-    out.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
-    out.push_back((char)(0x80 | (cp & 0x3F)));
+    out[0] = (char)(0xE0 | (cp >> 12));
+    out[1] = (char)(0x80 | ((cp >> 6) & 0x3F));
+    out[2] = (char)(0x80 | (cp & 0x3F));
+    return 3;
   }
+  out[0] = (char)(0xF0 | (cp >> 18));
+  out[1] = (char)(0x80 | ((cp >> 12) & 0x3F));
+  out[2] = (char)(0x80 | ((cp >> 6) & 0x3F));
+  out[3] = (char)(0x80 | (cp & 0x3F));
+  return 4;
 }
 
 // Width of a valid UTF-8 sequence at p (1..4), or 0 if invalid.
@@ -52,7 +57,19 @@ struct P {
   size_t i = 0;
   NumMode mode;
   JDoc* d;
-  std::vector<JNode> scratch;  // children staging (stack discipline)
+  std::vector<JNode>& scratch;  // children staging (stack discipline), reused per thread
+  // decoded string bytes go to d->strs[o..] through a raw cursor (strs is kept longer than
+  // o and grown on demand; parse_one trims it to o at the end)
+  char* sb = nullptr;
+  size_t o = 0;
+  inline void room(size_t k) {
+    if (o + k > d->strs.size()) {
+      d->strs.resize(std::max(2 * d->strs.size(), o + k + 256));
+      sb = &d->strs[0];
+    }
+  }
+  inline void put1(char c) { room(1); sb[o++] = c; }
+  inline void putn(const char* p, size_t k) { room(k); memcpy(sb + o, p, k); o += k; }
 
   [[noreturn]] void fail(const char* w) { throw std::runtime_error(std::string("json: ") + w); }
   inline void ws() {
@@ -80,8 +97,7 @@ struct P {
   void str(uint32_t* off, uint32_t* len) {
     if (i >= n || s[i] != '"') fail("expected string");
     i++;
-    std::string& out = d->strs;
-    size_t start = out.size();
+    const size_t start = o;
     // fast path: plain ASCII run
     while (true) {
       size_t j = i;
@@ -90,7 +106,7 @@ struct P {
         if (c == '"' || c == '\\' || c < 0x20 || c >= 0x80) break;
         j++;
       }
-      out.append(s + i, j - i);
+      putn(s + i, j - i);
       i = j;
       if (i >= n) fail("unterminated string");
       unsigned char c = (unsigned char)s[i];
@@ -101,14 +117,14 @@ struct P {
         if (i >= n) fail("bad escape");
         char e = s[i++];
         switch (e) {
-          case '"': out.push_back('"'); break;
-          case '\\': out.push_back('\\'); break;
-          case '/': out.push_back('/'); break;
-          case 'b': out.push_back('\b'); break;
-          case 'f': out.push_back('\f'); break;
-          case 'n': out.push_back('\n'); break;
-          case 'r': out.push_back('\r'); break;
-          case 't': out.push_back('\t'); break;
+          case '"': put1('"'); break;
+          case '\\': put1('\\'); break;
+          case '/': put1('/'); break;
+          case 'b': put1('\b'); break;
+          case 'f': put1('\f'); break;
+          case 'n': put1('\n'); break;
+          case 'r': put1('\r'); break;
+          case 't': put1('\t'); break;
           case 'u': {
             uint32_t cp = hex4();
             if (cp >= 0xD800 && cp < 0xDC00) {
@@ -124,7 +140,8 @@ struct P {
             } else if (cp >= 0xDC00 && cp < 0xE000) {
               cp = 0xFFFD;
             }
-            put_utf8(out, cp);
+            room(4);
+            o += put_utf8(sb + o, cp);
             break;
           }
           default: fail("bad escape");
@@ -133,11 +150,11 @@ struct P {
       }
       // non-ASCII
       size_t w = valid_utf8((const unsigned char*)s + i, n - i);
-      if (w == 0) { put_utf8(out, 0xFFFD); i++; }
-      else { out.append(s + i, w); i += w; }
+      if (w == 0) { room(4); o += put_utf8(sb + o, 0xFFFD); i++; }
+      else { putn(s + i, w); i += w; }
     }
     *off = (uint32_t)start;
-    *len = (uint32_t)(out.size() - start);
+    *len = (uint32_t)(o - start);
   }
   void num(JNode& v) {
     size_t st = i;
@@ -192,9 +209,9 @@ struct P {
         value(ch, depth + 1);
         // duplicate key: last one wins (replace in place)
         bool dup = false;
-        std::string_view k = d->str(ch.key_off, ch.key_len);
+        const std::string_view k(sb + ch.key_off, ch.key_len);
         for (size_t q = base; q < scratch.size(); q++) {
-          if (d->str(scratch[q].key_off, scratch[q].key_len) == k) { scratch[q] = ch; dup = true; break; }
+          if (std::string_view(sb + scratch[q].key_off, scratch[q].key_len) == k) { scratch[q] = ch; dup = true; break; }
         }
         if (!dup) scratch.push_back(ch);
         ws();
@@ -240,9 +257,21 @@ struct P {
 }  // namespace
 
 size_t parse_one(const char* s, size_t n, NumMode mode, JDoc* doc) {
-  P p{s, n, 0, mode, doc, {}};
+  static thread_local std::vector<JNode> scratch;
+  scratch.clear();
+  P p{s, n, 0, mode, doc, scratch};
+  const size_t base = doc->strs.size();
+  doc->strs.resize(std::max(doc->strs.capacity(), base + 1024));
+  p.sb = &doc->strs[0];
+  p.o = base;
   JNode root;
-  p.value(root, 0);
+  try {
+    p.value(root, 0);
+  } catch (...) {
+    doc->strs.resize(base);
+    throw;
+  }
+  doc->strs.resize(p.o);
   doc->root = (uint32_t)doc->nodes.size();
   doc->nodes.push_back(root);
   return p.i;

@@ -20,14 +20,17 @@ void make_shard(const Batch& b, uint64_t lo, uint64_t hi, Batch* out) {
     throw std::runtime_error("shard: range must start at a multiple of 64 resources");
   Batch& s = *out;
   s = Batch();
-  s.pin_store(false);
+  s.pin_store();
   const uint64_t row_lo = lo < b.res.size() ? b.res[lo].root : b.n_rows;
   const uint64_t row_hi = hi < b.res.size() ? b.res[hi].root : b.n_rows;
   s.n_rows = row_hi - row_lo;
+  // the shard's packed cells: rows [row_lo, row_hi)
+  const uint64_t c_lo = row_lo < b.n_rows ? b.roff[row_lo] : b.pcells.size();
+  const uint64_t c_hi = row_hi < b.n_rows ? b.roff[row_hi] : b.pcells.size();
+  const Node* src = b.pcells.data() + c_lo;
+  const size_t ncell = (size_t)(c_hi - c_lo);
   // values referenced by the shard, renumbered in global order
   std::vector<uint32_t> vmap(b.vals.size(), 0xFFFFFFFFu);
-  const Node* src = b.nodes.data() + row_lo * KV_LANES;
-  const size_t ncell = (size_t)s.n_rows * KV_LANES;
   auto scalar = [](uint32_t t) { return t == NT_BOOL || t == NT_INT || t == NT_FLOAT || t == NT_STR; };
   for (size_t i = 0; i < ncell; i++)
     if (scalar(node_type(src[i].kt))) vmap[src[i].a] = 0;
@@ -39,15 +42,18 @@ void make_shard(const Batch& b, uint64_t lo, uint64_t hi, Batch* out) {
       vmap[v] = (uint32_t)s.vals.size();
       s.vals.push_back(b.vals[v]);
     }
-  s.nodes.resize(ncell);
+  s.pcells.resize(ncell);
   for (size_t i = 0; i < ncell; i++) {
     Node n = src[i];
     const uint32_t t = node_type(n.kt);
     if (t == NT_MAP || t == NT_ARR) n.a -= (uint32_t)row_lo;
     else if (scalar(t)) n.a = vmap[n.a];
-    if (n.kt | n.a | n.b | n.c) s.cells_used++;
-    s.nodes[i] = n;
+    s.pcells[i] = n;
   }
+  s.cells_used = ncell;
+  s.rmask.assign(b.rmask.begin() + row_lo, b.rmask.begin() + row_hi);
+  s.roff.resize(s.n_rows);
+  for (uint64_t r = 0; r < s.n_rows; r++) s.roff[r] = b.roff[row_lo + r] - (uint32_t)c_lo;
   s.res.assign(b.res.begin() + lo, b.res.begin() + hi);
   for (Res& r : s.res) r.root -= (uint32_t)row_lo;
   s.kvs = b.kvs;

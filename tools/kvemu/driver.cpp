@@ -146,26 +146,18 @@ int main(int argc, char** argv) {
     P.ptab = ptab.data();
     P.n_vals = NV + KV_PTAB_PSEUDO;
     DevBatch B{};
-    B.nodes = b.nodes.data();
-    // merged batches carry the packed transfer form of their rows (what kv_validate
-    // uploads): expand it as kv_expand_rows_kernel does and run on that copy, after
-    // checking it equals the padded rows
-    std::vector<Node> expanded;
-    if (!b.rmask.empty()) {
-      if (b.rmask.size() != b.n_rows || b.roff.size() != b.n_rows || b.nodes.size() != b.n_rows * KV_LANES)
-        throw std::runtime_error("kvemu: packed row arrays do not match the batch");
-      expanded.assign(b.nodes.size(), Node{0u, 0u, 0u, 0u});
-      for (uint64_t row = 0; row < b.n_rows; row++)
-        for (uint32_t l = 0; l < KV_LANES; l++)
-          if ((b.rmask[row] >> l) & 1ull) {
-            const uint64_t at = (uint64_t)b.roff[row] + (uint64_t)__builtin_popcountll(b.rmask[row] & ((1ull << l) - 1ull));
-            if (at >= b.pcells.size()) throw std::runtime_error("kvemu: packed cell index out of range");
-            expanded[row * KV_LANES + l] = b.pcells[at];
-          }
-      if (memcmp(expanded.data(), b.nodes.data(), expanded.size() * sizeof(Node)) != 0)
-        throw std::runtime_error("kvemu: expanded packed rows differ from the padded rows");
-      B.nodes = expanded.data();
-    }
+    // the packed rows (what kv_validate uploads), expanded as kv_expand_rows_kernel does
+    if (b.rmask.size() != b.n_rows || b.roff.size() != b.n_rows)
+      throw std::runtime_error("kvemu: packed row arrays do not match the batch");
+    std::vector<Node> expanded(b.n_cells(), Node{0u, 0u, 0u, 0u});
+    for (uint64_t row = 0; row < b.n_rows; row++)
+      for (uint32_t l = 0; l < KV_LANES; l++)
+        if ((b.rmask[row] >> l) & 1ull) {
+          const uint64_t at = (uint64_t)b.roff[row] + (uint64_t)__builtin_popcountll(b.rmask[row] & ((1ull << l) - 1ull));
+          if (at >= b.pcells.size()) throw std::runtime_error("kvemu: packed cell index out of range");
+          expanded[row * KV_LANES + l] = b.pcells[at];
+        }
+    B.nodes = expanded.data();
     B.vals = b.vals.data();
     B.res = b.res.data();
     B.kvs = b.kvs.data();
