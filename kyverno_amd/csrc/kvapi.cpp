@@ -1210,8 +1210,11 @@ int kv_compile(const char* policies_json, size_t len, uint32_t flags, kv_policys
           }
         }
         if (!getenv("KVGPU_JIT_SKIP_COMPILE")) {  // (dump-only analysis runs skip it)
-          double ms = 0;
-          for (int round = 0; round < 16; round++) {  // register budget: re-plan kernels that spill
+          // block sizes from probe compiles of each block, then the kernels themselves
+          jit_refine_blocks(s->ps, chunk, s->jit.get());
+          double ms = s->jit->compile_ms;
+          jit_generate(s->ps, chunk, s->jit.get());
+          for (int round = 0; round < 40; round++) {  // register budget: re-plan kernels that spill
             jit_compile(s->jit.get());
             ms += s->jit->compile_ms;
             if (!jit_plan_spills(s->jit.get())) break;

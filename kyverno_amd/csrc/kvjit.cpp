@@ -1729,7 +1729,7 @@ struct Gen {
   // One kernel running the fused chunks `chs` one after the other for each
   // resource: a workgroup re-reads its resources' node rows per chunk while they
   // are still cache-resident, instead of one grid-wide pass per chunk.
-  void group_kernel(const std::string& name, const std::vector<const JitChunk*>& chs, int waves) {
+  std::vector<uint32_t> group_kernel(const std::string& name, const std::vector<const JitChunk*>& chs, int waves) {
     std::vector<std::string> blocks;
     std::vector<uint32_t> rules;
     uint32_t nr_all = 0;
@@ -1791,7 +1791,7 @@ struct Gen {
         << "    kv_count_status_lds(w_, O.counts + (size_t)" << name << "_rules[threadIdx.x] * KV_HIST);\n"
         << "  }\n}\n\n";
       hist_lds = false;
-      return;
+      return rules;
     }
     o << "  __syncthreads();\n"
       << "  for (uint32_t q = threadIdx.x; q < " << nr << "u * KV_HIST; q += KV_WG) {\n"
@@ -1799,6 +1799,48 @@ struct Gen {
       << "    if (v) atomicAdd(&O.counts[(size_t)" << name << "_rules[q / KV_HIST] * KV_HIST + q % KV_HIST], "
          "(unsigned long long)v);\n"
       << "  }\n}\n\n";
+    return rules;
+  }
+
+  // Register weight of rule ri in a fused block: the state it keeps across the block (status
+  // / resume pc, error kind, cursors per depth, loop counters and error indices per loop
+  // level, anchor bitsets, wildcard-key node); 0 for rules of other routes.
+  uint32_t rule_weight(uint32_t ri) {
+    if (ps.rules[ri].route != 0) return 0;
+    const RGen g = analyze(ri);
+    uint32_t w = 2 + g.maxd;
+    if (!g.loops.empty()) w += 4 * (g.max_level + 1);
+    if (g.uses_anchor) w += 4;
+    if (g.uses_keyglob) w += 3;
+    return w;
+  }
+
+  // First block sizes of the kernel of sorted rules [a, e): greedy runs whose weight stays
+  // within KVGPU_JIT_BLOCK_W (default 160); a rule of the same structural form as an
+  // earlier rule of the run joins it for free (rule groups run its program once).
+  std::vector<uint32_t> initial_blocks(const std::vector<uint32_t>& sorted, uint32_t a, uint32_t e) {
+    const char* bw = getenv("KVGPU_JIT_BLOCK_W");
+    const uint32_t budget = bw && atoi(bw) > 0 ? (uint32_t)atoi(bw) : 160u;
+    std::vector<uint32_t> out;
+    std::set<std::string> forms;
+    uint32_t cur = 0, w = 0;
+    for (uint32_t q = a; q < e; q++) {
+      const uint32_t ri = sorted[q];
+      std::vector<uint32_t> pr, pn, lp;
+      const std::string f = group_form(ri, &pr, &pn, &lp);
+      const uint32_t rw = !f.empty() && forms.count(f) ? 0u : rule_weight(ri);
+      if (cur > 0 && w + rw > budget) {
+        out.push_back(cur);
+        cur = 0;
+        w = 0;
+        forms.clear();
+      }
+      cur++;
+      w += !f.empty() && forms.count(f) ? 0u : rule_weight(ri);
+      if (!f.empty()) forms.insert(f);
+    }
+    if (cur) out.push_back(cur);
+    return out;
   }
 };
 
@@ -1881,21 +1923,37 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
     // KVGPU_JIT_WAVES: launch bound in waves per SIMD (default 8, 0: none)
     if (out->plan.empty() && n) {
       // first bound: 8 waves, or what the kernel's LDS status rows (256 B per rule) leave of a
-      // CU's 160 KB (one workgroup = one wave per SIMD); the spill plan lowers it if needed
+      // CU's 160 KB (one workgroup = one wave per SIMD); the spill plan splits blocks (or
+      // lowers the bound) until the compiler meets it
       const char* wz = getenv("KVGPU_JIT_WAVES");
       const uint32_t parts = (n + chunk_rules - 1) / chunk_rules;
+      std::vector<uint32_t> sorted;
+      for (auto& o : order) sorted.push_back(o.second);
       for (uint32_t k = 0; k < parts; k++) {
         const uint32_t a = (uint32_t)((uint64_t)n * k / parts), e = (uint32_t)((uint64_t)n * (k + 1) / parts);
         const int lds_waves = (int)std::max<uint32_t>(1u, (160u * 1024u) / std::max<uint32_t>(1u, (e - a) * 256u));
-        out->plan.push_back({a, e - a, wz ? atoi(wz) : std::min(8, lds_waves)});
+        out->plan.push_back({a, e - a, wz ? atoi(wz) : std::min(8, lds_waves), g.initial_blocks(sorted, a, e)});
       }
     }
     for (const JitKernelPlan& kp : out->plan) {
       JitChunk kc;
-      // named by its rule range: stable when other ranges are re-planned
-      kc.name = "kvj_r" + std::to_string(kp.first) + "_" + std::to_string(kp.count) + (kp.waves ? "" : "u");
+      // named by its rule range and block count: stable when other ranges are re-planned
+      kc.name = "kvj_r" + std::to_string(kp.first) + "_" + std::to_string(kp.count) +
+                (kp.blocks.size() > 1 ? "_b" + std::to_string(kp.blocks.size()) : "") + (kp.waves ? "" : "u");
       for (uint32_t q = kp.first; q < kp.first + kp.count; q++) kc.rules.push_back(order.at(q).second);
-      g.group_kernel(kc.name, {&kc}, kp.waves);
+      std::vector<JitChunk> bl;
+      uint32_t at = 0;
+      for (uint32_t c : kp.blocks) {
+        JitChunk b;
+        b.rules.assign(kc.rules.begin() + at, kc.rules.begin() + at + c);
+        at += c;
+        bl.push_back(std::move(b));
+      }
+      if (at != kp.count) throw std::runtime_error("kvjit: kernel plan blocks do not cover its rules");
+      std::vector<const JitChunk*> bp;
+      for (auto& b : bl) bp.push_back(&b);
+      // the kernel's rules in LDS-row order (blocks reorder rule-group members)
+      kc.rules = g.group_kernel(kc.name, bp, kp.waves);
       out->chunks.push_back(kc);
     }
   }
@@ -2202,21 +2260,88 @@ bool jit_plan_spills(JitImage* img) {
       continue;
     }
     changed = true;
-    if (kp.waves > 1) {
-      next.push_back({kp.first, kp.count, kp.waves - 1});
+    JitKernelPlan np = kp;
+    size_t big = 0;
+    for (size_t b = 1; b < np.blocks.size(); b++)
+      if (np.blocks[b] > np.blocks[big]) big = b;
+    if (!np.blocks.empty() && np.blocks[big] > 1) {  // the largest block in two halves
+      const uint32_t c = np.blocks[big], h = c / 2;
+      np.blocks[big] = h;
+      np.blocks.insert(np.blocks.begin() + big + 1, c - h);
+    } else if (kp.waves > 1) {
+      np.waves = kp.waves - 1;
     } else if (kp.waves == 1) {
-      next.push_back({kp.first, kp.count, 0});
+      np.waves = 0;
     } else if (kp.count > 1) {
       const uint32_t h = kp.count / 2;
-      next.push_back({kp.first, h, 0});
-      next.push_back({kp.first + h, kp.count - h, 0});
+      next.push_back({kp.first, h, 0, std::vector<uint32_t>(h, 1u)});
+      next.push_back({kp.first + h, kp.count - h, 0, std::vector<uint32_t>(kp.count - h, 1u)});
+      continue;
     } else {
       throw std::runtime_error("kvjit: kernel " + name + " needs " + std::to_string(priv) +
                                " B of scratch per lane even without a launch bound");
     }
+    next.push_back(np);
   }
   if (changed) img->plan = next;
   return changed;
+}
+
+void jit_refine_blocks(const PolicySet& ps, uint32_t chunk_rules, JitImage* img) {
+  // Each block of the plan compiled alone as a probe kernel under its kernel's bound (small
+  // programs, compiled in parallel); a block whose probe spills or exceeds the bound's
+  // registers is split in two, and its halves are probed in the next round.
+  for (int round = 0; round < 12; round++) {
+    JitImage probe;
+    std::vector<std::pair<size_t, size_t>> at;  // (kernel, block) of each probe
+    for (size_t k = 0; k < img->plan.size(); k++) {
+      const JitKernelPlan& kp = img->plan[k];
+      if (kp.blocks.size() < 2 || kp.waves == 0) continue;
+      uint32_t first = kp.first;
+      for (size_t b = 0; b < kp.blocks.size(); b++) {
+        if (kp.blocks[b] > 1) {
+          probe.plan.push_back({first, kp.blocks[b], kp.waves, {kp.blocks[b]}});
+          at.push_back({k, b});
+        }
+        first += kp.blocks[b];
+      }
+    }
+    if (probe.plan.empty()) return;
+    jit_generate(ps, chunk_rules, &probe);
+    jit_compile(&probe);
+    img->compile_ms += probe.compile_ms;
+    std::vector<std::vector<char>> split(img->plan.size());
+    bool any = false;
+    for (size_t i = 0; i < probe.plan.size(); i++) {
+      const std::string& name = probe.chunks[i].name;
+      size_t ci = 0;
+      while (ci < probe.kernel_name.size() && probe.kernel_name[ci] != name) ci++;
+      uint32_t priv = 0, vgprs = 0;
+      uint64_t code = 0;
+      if (ci == probe.kernel_name.size() || !co_kernel_info(probe.codes[ci], name, &priv, &code, &vgprs))
+        throw std::runtime_error("kvjit: no kernel descriptor for probe " + name);
+      if (priv != 0 || vgprs > 512u / (uint32_t)probe.plan[i].waves) {
+        split[at[i].first].resize(img->plan[at[i].first].blocks.size(), 0);
+        split[at[i].first][at[i].second] = 1;
+        any = true;
+      }
+    }
+    if (!any) return;
+    for (size_t k = 0; k < img->plan.size(); k++) {
+      if (split[k].empty()) continue;
+      std::vector<uint32_t> nb;
+      for (size_t b = 0; b < img->plan[k].blocks.size(); b++) {
+        const uint32_t c = img->plan[k].blocks[b];
+        if (split[k][b]) {
+          nb.push_back(c / 2);
+          nb.push_back(c - c / 2);
+        } else {
+          nb.push_back(c);
+        }
+      }
+      img->plan[k].blocks = nb;
+    }
+  }
 }
 
 uint64_t code_bytes(const JitImage& img) {

@@ -18,10 +18,14 @@ struct JitChunk {
 };
 
 // One specialized rule kernel: rules [first, first + count) of the signature-sorted
-// rule order as one fused block, compiled with a `waves`-per-SIMD launch bound (0: none).
+// rule order as consecutive fused blocks of `blocks[i]` rules (sum = count), compiled with
+// a `waves`-per-SIMD launch bound (0: none). Every array a block's rules walk is walked
+// once per resource and block; the rules of a block keep their state in registers across
+// the whole block, so the block sizes bound the kernel's register use.
 struct JitKernelPlan {
   uint32_t first, count;
   int waves;
+  std::vector<uint32_t> blocks;
 };
 
 struct JitImage {
@@ -55,11 +59,16 @@ void jit_compile(JitImage* img);
 uint64_t code_bytes(const JitImage& img);
 // Register budget of the plan: no kernel ships with a private (scratch) segment, and a wave
 // bound is kept only when the compiler met it. A kernel that spills (or exceeds the registers)
-// under w waves per SIMD is compiled at w - 1, then without a bound; an unbounded kernel that
-// still spills is split in two (a single rule range that does: std::runtime_error).
+// under its bound of w waves per SIMD has its largest block split in two; a kernel of
+// one-rule blocks is compiled at w - 1, then without a bound (a one-rule kernel that still
+// spills: std::runtime_error).
 // Returns true when the plan changed (regenerate + compile again; the kernels that did not
 // change come from the code-object cache).
 bool jit_plan_spills(JitImage* img);
+// Block sizes of the plan from probe compiles: every multi-rule block of a multi-block kernel
+// is compiled alone under its kernel's bound, and the blocks that spill or exceed the bound's
+// registers are split in two, until every probe meets its bound (then regenerate the image).
+void jit_refine_blocks(const PolicySet& ps, uint32_t chunk_rules, JitImage* img);
 bool co_kernel_info(const std::vector<char>& co, const std::string& name, uint32_t* private_seg, uint64_t* code,
                     uint32_t* vgprs = nullptr);
 

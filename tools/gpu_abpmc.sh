@@ -1,7 +1,7 @@
 #!/bin/bash
-# PMC A/B of kernel variants: for each argument (env list "K=V,K2=V2", "-" for none) two
-# rocprofv3 --pmc passes of a short bench ($CFG, default c2): FETCH_SIZE / WRITE_SIZE, and the
-# SQ wave / instruction / wait counters; prints per-kernel means per dispatch.
+# PMC A/B of kernel variants: for each argument (env list "K=V,K2=V2", "-" for none) one
+# rocprofv3 --pmc pass per counter group of a short bench ($CFG, default c2): FETCH_SIZE, WRITE_SIZE,
+# L2 hits / misses, and the SQ wave / instruction / wait counters; prints per-kernel means per dispatch.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"; A=gpurun_out/${OUTDIR:-abpmc}; mkdir -p $A
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
@@ -10,7 +10,7 @@ for spec in "$@"; do
   i=$((i+1))
   envs=""; [ "$spec" != "-" ] && envs=$(echo "$spec" | tr ',' ' ')
   j=0
-  for grp in "FETCH_SIZE WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY"; do
+  for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY"; do
     j=$((j+1))
     (cd /tmp && env $envs timeout -s KILL 300 rocprofv3 --pmc $grp --kernel-trace --stats -d "$R/$A/v$i" -o pass$j --output-format csv -- \
        python -u "$R/bench.py" --config ${CFG:-c2} --steps 2 --warmup 0 --no-cpu-baseline --no-e2e --no-traffic ${BENCH_ARGS} \
