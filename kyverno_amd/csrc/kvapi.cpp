@@ -178,6 +178,17 @@ struct kv_batch {
     std::call_once(dyn_once, [&]() { build_dyn(ps, b, &dyn); });
     return dyn;
   }
+  // caller index -> store index (the inverse of Batch::order), on first use; null: identity
+  std::once_flag inv_once;
+  std::vector<uint32_t> inv;
+  const uint32_t* inverse() {
+    if (b.order.empty()) return nullptr;
+    std::call_once(inv_once, [&]() {
+      inv.assign(b.order.size(), 0);
+      for (size_t i = 0; i < b.order.size(); i++) inv[b.order[i]] = (uint32_t)i;
+    });
+    return inv.data();
+  }
 };
 
 namespace {
@@ -347,7 +358,11 @@ struct kv_result {
   const kv_policyset* ps = nullptr;
   const kv_batch* b = nullptr;
   uint64_t n_rules = 0, n_res = 0;
-  HostArray<uint8_t> status;        // [rule][res]
+  // [rule][res] in the batch's store order (Batch::order); `res` below is a store index unless
+  // named a caller index. kv_result_status returns status_c, the caller order, when they differ.
+  HostArray<uint8_t> status;
+  std::once_flag sc_once;
+  HostArray<uint8_t> status_c;
   std::vector<ResultPart> parts;    // by resource range
   bool errors = false;              // KV_MODE_ERRORS: records fetched
   std::vector<int64_t> counts;
@@ -361,6 +376,34 @@ struct kv_result {
   std::vector<std::string> f_paths;
 
   bool has_err() const { return errors; }
+  // store index of caller index `res`
+  uint64_t sidx(uint64_t res) const {
+    const uint32_t* iv = const_cast<kv_batch*>(b)->inverse();
+    return iv ? iv[res] : res;
+  }
+  // caller index of store index `s`
+  uint64_t cidx(uint64_t s) const { return b->b.order.empty() ? s : b->b.order[s]; }
+  // the statuses in caller order: rows of the store-order matrix scattered through the batch
+  // order, rules split over host threads (a permuted batch only)
+  const uint8_t* status_caller() {
+    if (b->b.order.empty() || status.empty()) return status.empty() ? nullptr : status.data();
+    std::call_once(sc_once, [this]() {
+      status_c.alloc(status.size());
+      const uint32_t* ord = b->b.order.data();
+      const unsigned T = std::max(1u, std::min<unsigned>(16u, std::thread::hardware_concurrency()));
+      std::vector<std::thread> th;
+      for (unsigned t = 0; t < T; t++)
+        th.emplace_back([&, t]() {
+          for (uint64_t rl = t; rl < n_rules; rl += T) {
+            const uint8_t* in = status.data() + rl * n_res;
+            uint8_t* out = status_c.data() + rl * n_res;
+            for (uint64_t q = 0; q < n_res; q++) out[ord[q]] = in[q];
+          }
+        });
+      for (auto& x : th) x.join();
+    });
+    return status_c.data();
+  }
   const Batch& batch_of(const ResultPart& p) const { return p.shard ? p.shard->b : b->b; }
   const ResultPart* part_of(uint64_t res) const {
     for (const ResultPart& p : parts)
@@ -1210,8 +1253,9 @@ int kv_compile(const char* policies_json, size_t len, uint32_t flags, kv_policys
           }
         }
         if (!getenv("KVGPU_JIT_SKIP_COMPILE")) {  // (dump-only analysis runs skip it)
-          // block sizes from probe compiles of each block, then the kernels themselves
-          jit_refine_blocks(s->ps, chunk, s->jit.get());
+          const std::string pkey = jit_plan_key(*s->jit);
+          const bool cached_plan = jit_load_plan(pkey, s->jit.get());
+          if (!cached_plan) jit_refine_blocks(s->ps, chunk, s->jit.get());  // block sizes from probe compiles
           double ms = s->jit->compile_ms;
           jit_generate(s->ps, chunk, s->jit.get());
           for (int round = 0; round < 40; round++) {  // register budget: re-plan kernels that spill
@@ -1221,6 +1265,7 @@ int kv_compile(const char* policies_json, size_t len, uint32_t flags, kv_policys
             jit_generate(s->ps, chunk, s->jit.get());
           }
           s->jit->compile_ms = ms;
+          jit_save_plan(pkey, *s->jit);
         }
         if (const char* dump = getenv("KVGPU_JIT_DUMP_CO")) {  // gfx950 code objects (llvm-objdump / readelf)
           for (size_t i = 0; i < s->jit->codes.size(); i++) {
@@ -1365,7 +1410,13 @@ int kv_bench(const kv_policyset* ps, const kv_batch* b, const char* ctx_json, in
 
 int kv_result_status(const kv_result* r, const uint8_t** status, uint64_t* n_rules, uint64_t* n_res) {
   if (!r) return KV_E_INVALID;
-  if (status) *status = r->status.empty() ? nullptr : r->status.data();
+  if (status) {
+    try {
+      *status = const_cast<kv_result*>(r)->status_caller();
+    } catch (const std::exception&) {
+      return KV_E_NOMEM;
+    }
+  }
   if (n_rules) *n_rules = r->n_rules;
   if (n_res) *n_res = r->n_res;
   return 0;
@@ -1399,6 +1450,7 @@ const char* kv_batch_namespace(const kv_batch* b, uint32_t i) {
 int kv_result_path(const kv_result* r, uint32_t rule, uint64_t res, char* buf, size_t cap) {
   if (!r || !r->has_err()) return KV_E_INVALID;
   if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
+  res = r->sidx(res);
   size_t o = (size_t)rule * r->n_res + res;
   if (r->status[o] != ST_FAIL) return KV_E_INVALID;
   ErrRec e;
@@ -1416,6 +1468,7 @@ int kv_result_path(const kv_result* r, uint32_t rule, uint64_t res, char* buf, s
 int kv_result_error(const kv_result* r, uint32_t rule, uint64_t res, uint32_t* kind, uint32_t* flags) {
   if (!r || !r->has_err()) return KV_E_INVALID;
   if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
+  res = r->sidx(res);
   const uint8_t st = r->status[(size_t)rule * r->n_res + res];
   if (st != ST_FAIL && st != ST_ERROR && st != ST_SKIP) return KV_E_INVALID;
   ErrRec e;
@@ -1430,6 +1483,7 @@ int kv_result_error_message(const kv_result* r, uint32_t rule, uint64_t res, con
                             char* buf, size_t cap) {
   if (!r || !r->has_err() || !resource_json) return KV_E_INVALID;
   if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
+  res = r->sidx(res);  // the caller's document of its resource `res`, the record of its store slot
   size_t o = (size_t)rule * r->n_res + res;
   const uint8_t st = r->status[o];
   if (st != ST_FAIL && st != ST_ERROR && st != ST_SKIP) return KV_E_INVALID;
@@ -1468,6 +1522,7 @@ int kv_result_subst_error(const kv_result* r, uint32_t rule, uint64_t res, char*
   if (!r) return KV_E_INVALID;
   if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
   if (r->status.empty()) return KV_E_INVALID;  // counts-only result: no statuses were fetched
+  res = r->sidx(res);
   try {
     const RuleRec& rr = r->ps->ps.rules[rule];
     if (!rr.dyn || r->status[(size_t)rule * r->n_res + res] != ST_ERROR) return 0;
@@ -1538,11 +1593,28 @@ int kv_result_failures(const kv_result* cr, uint64_t* n, const uint32_t** rule, 
               }
             }
             r->f_rule.push_back(rl);
-            r->f_res.push_back(q);
+            r->f_res.push_back(r->cidx(q));
             r->f_path.push_back(id);
             i++;
           }
         }
+      }
+      if (!r->b->b.order.empty()) {  // caller order: by rule, then caller resource index
+        std::vector<size_t> ix(r->f_rule.size());
+        for (size_t i = 0; i < ix.size(); i++) ix[i] = i;
+        std::sort(ix.begin(), ix.end(), [r](size_t x, size_t y) {
+          return r->f_rule[x] != r->f_rule[y] ? r->f_rule[x] < r->f_rule[y] : r->f_res[x] < r->f_res[y];
+        });
+        std::vector<uint32_t> fr(ix.size()), fp(ix.size());
+        std::vector<uint64_t> fs(ix.size());
+        for (size_t i = 0; i < ix.size(); i++) {
+          fr[i] = r->f_rule[ix[i]];
+          fs[i] = r->f_res[ix[i]];
+          fp[i] = r->f_path[ix[i]];
+        }
+        r->f_rule.swap(fr);
+        r->f_res.swap(fs);
+        r->f_path.swap(fp);
       }
     });
   } catch (const std::exception&) {

@@ -911,6 +911,51 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
 
 }  // namespace
 
+// The string value of the first `"<key>":` in a resource's JSON text (no escapes; empty when
+// absent): the store-order key. A miss only changes which resources share a wave group.
+std::string_view raw_string_of(const char* p, size_t n, const char* key, size_t kl) {
+  const char* e = p + n;
+  for (const char* q = p; q < e;) {
+    const char* k = (const char*)memmem(q, (size_t)(e - q), key, kl);
+    if (!k) return {};
+    const char* v = k + kl;
+    while (v < e && (*v == ' ' || *v == '\t' || *v == '\n' || *v == '\r')) v++;
+    if (v < e && *v == ':') {
+      v++;
+      while (v < e && (*v == ' ' || *v == '\t' || *v == '\n' || *v == '\r')) v++;
+      if (v >= e || *v != '"') return {};
+      const char* a = ++v;
+      while (v < e && *v != '"' && *v != '\\') v++;
+      return std::string_view(a, (size_t)(v - a));
+    }
+    q = k + kl;
+  }
+  return {};
+}
+
+// Store order from per-resource kind keys: the kinds in order of first appearance, the
+// resources of each kind in input order (stable counting sort); empty when every resource
+// has the same kind. Resources of one kind then share wave groups, so a rule that matches
+// other kinds only is skipped by whole waves (its match fails uniformly) instead of running
+// its pattern walk for the few lanes of a mixed wave (C5: 6.1 -> 4.3 ms per pass).
+std::vector<uint32_t> kind_order(const std::vector<std::string_view>& kinds) {
+  std::unordered_map<std::string_view, uint32_t> id;
+  std::vector<uint32_t> kid(kinds.size()), cnt;
+  for (size_t i = 0; i < kinds.size(); i++) {
+    auto it = id.emplace(kinds[i], (uint32_t)id.size()).first;
+    kid[i] = it->second;
+    if (kid[i] >= cnt.size()) cnt.push_back(0);
+    cnt[kid[i]]++;
+  }
+  if (id.size() < 2) return {};
+  if (const char* e = getenv("KVGPU_INGEST_ORDER"); e && e[0] == '0') return {};  // input order (A/B)
+  std::vector<uint32_t> at(cnt.size(), 0);
+  for (size_t k = 1; k < cnt.size(); k++) at[k] = at[k - 1] + cnt[k - 1];
+  std::vector<uint32_t> order(kinds.size());
+  for (size_t i = 0; i < kinds.size(); i++) order[at[kid[i]]++] = (uint32_t)i;
+  return order;
+}
+
 void ingest_resources(const PolicySet& ps, const char* json, size_t len, const char* ns_labels_json, Batch* b) {
   const unsigned T = ingest_threads();
   size_t first = 0;
@@ -927,6 +972,20 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
     const size_t nres = starts.size(), groups = (nres + KV_LANES - 1) / KV_LANES;
     const size_t per = (groups + T - 1) / T * KV_LANES;
     const size_t P = (nres + per - 1) / per;
+    {  // store order: resources grouped by kind
+      std::vector<std::string_view> kinds(nres);
+      std::vector<std::thread> kt;
+      for (size_t k = 0; k < P; k++)
+        kt.emplace_back([&, k]() {
+          for (size_t i = k * per; i < std::min(nres, (k + 1) * per); i++) {
+            const size_t end = i + 1 < nres ? starts[i + 1] : len;
+            kinds[i] = raw_string_of(json + starts[i], end - starts[i], "\"kind\"", 6);
+          }
+        });
+      for (auto& t : kt) t.join();
+      b->order = kind_order(kinds);
+    }
+    const std::vector<uint32_t>& order = b->order;
     std::vector<Batch> parts(P);
     std::vector<std::string> errs(P);
     std::vector<std::thread> th;
@@ -937,7 +996,8 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
           JDoc doc;
           const size_t e = std::min(nres, (k + 1) * per);
           in.expected_res = e > k * per ? e - k * per : 0;
-          for (size_t i = k * per; i < e; i++) {
+          for (size_t q = k * per; q < e; q++) {
+            const size_t i = order.empty() ? q : order[q];
             const size_t end = i + 1 < nres ? starts[i + 1] : len;
             doc.nodes.clear();
             doc.strs.clear();
@@ -962,7 +1022,20 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
   }
   if (!parallel) {
     Ingest in(ps, *b);
-    parse_json_stream(json, len, NUM_UNSTRUCTURED, [&](JDoc& d) { in.take(d); });
+    if (len <= (64u << 20)) {  // small inputs: documents held, taken in store order
+      std::vector<JDoc> docs;
+      parse_json_stream(json, len, NUM_UNSTRUCTURED, [&](JDoc& d) { docs.push_back(std::move(d)); });
+      std::vector<std::string_view> kinds(docs.size());
+      for (size_t i = 0; i < docs.size(); i++) {
+        const JDoc& d = docs[i];
+        const int64_t c = d.at(d.root).t == J_MAP ? d.get(d.root, "kind") : -1;
+        if (c >= 0 && d.at((uint32_t)c).t == J_STR) kinds[i] = d.sval(d.at((uint32_t)c));
+      }
+      b->order = kind_order(kinds);
+      for (size_t q = 0; q < docs.size(); q++) in.take(docs[b->order.empty() ? q : b->order[q]]);
+    } else {
+      parse_json_stream(json, len, NUM_UNSTRUCTURED, [&](JDoc& d) { in.take(d); });
+    }
     in.flush_group();
     for (size_t i = 0; i < b->namespaces.size(); i++) ns_index.emplace(b->namespaces[i], (uint32_t)i);
     order_vals(*b);

@@ -259,6 +259,10 @@ struct Batch {
     return pcells[(uint64_t)roff[row] + (uint64_t)__builtin_popcountll(rmask[row] & ((1ull << lane) - 1ull))];
   }
   uint64_t n_cells() const { return n_rows * kv::KV_LANES; }
+  // store order: resource i of the store (its wave group, its status column) is resource
+  // order[i] of the caller's input; empty = the input order. Ingest groups resources of one
+  // kind into common wave groups (kvingest.cpp), the result accessors map indices back.
+  std::vector<uint32_t> order;
   // the arrays that cross PCIe in page-locked memory when g_hostmem provides it
   void pin_store() {
     vals = StoreVec<kv::Val>(StoreAlloc<kv::Val>(true));

@@ -2350,18 +2350,95 @@ uint64_t code_bytes(const JitImage& img) {
   return n;
 }
 
+namespace {
+
+// hash of the compiler options, hiprtc version and the common prelude of img's programs
+uint64_t common_hash(const JitImage& img) {
+  std::string opt_key;
+  for (const char* o : kOpts) opt_key += std::string(o) + "\n";
+  int hv = 0;
+  (void)hiprtcVersion(&hv, &hv);
+  opt_key += "hiprtc " + std::to_string(hv) + "\n";
+  return fnv1a64(img.common, fnv1a64(opt_key));
+}
+
+// code-object cache file of kernel program i: <name>-<hash of options + program text>.co
+std::string cache_file(const JitImage& img, size_t i, uint64_t hcommon) {
+  char key[40];
+  snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a64(img.kernel_src[i], hcommon));
+  return img.kernel_name[i] + "-" + key + ".co";
+}
+
+}  // namespace
+
+std::string jit_plan_key(const JitImage& img) {
+  uint64_t h = common_hash(img);
+  for (size_t i = 0; i < img.kernel_src.size(); i++) h = fnv1a64(img.kernel_src[i], fnv1a64(img.kernel_name[i], h));
+  char key[40];
+  snprintf(key, sizeof key, "%016llx", (unsigned long long)h);
+  return key;
+}
+
+bool jit_load_plan(const std::string& key, JitImage* img) {
+  const std::string dir = cache_dir();
+  std::vector<char> text;
+  if (dir.empty() || !read_file(dir + "/plan-" + key + ".txt", &text)) return false;
+  std::vector<JitKernelPlan> plan;
+  std::string line;
+  for (size_t i = 0; i <= text.size(); i++) {
+    if (i < text.size() && text[i] != '\n') {
+      line.push_back(text[i]);
+      continue;
+    }
+    if (line.rfind("kernel ", 0) == 0) {  // kernel <first> <count> <waves> <block sizes...>
+      JitKernelPlan kp{0, 0, 0, {}};
+      const char* c = line.c_str() + 7;
+      char* e = nullptr;
+      kp.first = (uint32_t)strtoul(c, &e, 10);
+      kp.count = (uint32_t)strtoul(e, &e, 10);
+      kp.waves = (int)strtol(e, &e, 10);
+      uint32_t sum = 0;
+      while (*e) {
+        char* f = nullptr;
+        const unsigned long b = strtoul(e, &f, 10);
+        if (f == e) break;
+        kp.blocks.push_back((uint32_t)b);
+        sum += (uint32_t)b;
+        e = f;
+      }
+      if (sum != kp.count || kp.blocks.empty()) return false;
+      plan.push_back(kp);
+    }
+    line.clear();
+  }
+  if (plan.empty()) return false;
+  img->plan = plan;
+  return true;
+}
+
+void jit_save_plan(const std::string& key, const JitImage& img) {
+  const std::string dir = cache_dir();
+  if (dir.empty()) return;
+  std::string t;
+  for (const JitKernelPlan& kp : img.plan) {
+    t += "kernel " + std::to_string(kp.first) + " " + std::to_string(kp.count) + " " + std::to_string(kp.waves);
+    for (uint32_t b : kp.blocks) t += " " + std::to_string(b);
+    t += "\n";
+  }
+  // the code objects of the final kernels (tools/jit_warm.sh keeps these, drops the
+  // intermediate probes and re-plans)
+  const uint64_t hc = common_hash(img);
+  for (size_t i = 0; i < img.kernel_src.size(); i++) t += "co " + cache_file(img, i, hc) + "\n";
+  write_file_atomic(dir, dir + "/plan-" + key + ".txt", std::vector<char>(t.begin(), t.end()));
+}
+
 void jit_compile(JitImage* img) {
   auto t0 = std::chrono::steady_clock::now();
   const size_t K = img->kernel_src.size();
   img->codes.assign(K, {});
   img->cache_hits = 0;
   const std::string dir = cache_dir();
-  std::string opt_key;
-  for (const char* o : kOpts) opt_key += std::string(o) + "\n";
-  int hv = 0;
-  (void)hiprtcVersion(&hv, &hv);
-  opt_key += "hiprtc " + std::to_string(hv) + "\n";
-  const uint64_t hcommon = fnv1a64(img->common, fnv1a64(opt_key));
+  const uint64_t hcommon = common_hash(*img);
   // cache lookups; the misses compile in child processes (hiprtc serialises the
   // compilations of one process), or in this process when kvjitc is unavailable
   // (KVGPU_JIT_PROCS=0 forces that)
@@ -2369,9 +2446,7 @@ void jit_compile(JitImage* img) {
   std::vector<size_t> todo;
   uint32_t hits = 0;
   for (size_t i = 0; i < K; i++) {
-    char key[40];
-    snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a64(img->kernel_src[i], hcommon));
-    paths[i] = dir.empty() ? "" : dir + "/" + img->kernel_name[i] + "-" + key + ".co";
+    paths[i] = dir.empty() ? "" : dir + "/" + cache_file(*img, i, hcommon);
     if (!paths[i].empty() && read_file(paths[i], &img->codes[i])) hits++;
     else todo.push_back(i);
   }

@@ -69,6 +69,13 @@ bool jit_plan_spills(JitImage* img);
 // is compiled alone under its kernel's bound, and the blocks that spill or exceed the bound's
 // registers are split in two, until every probe meets its bound (then regenerate the image).
 void jit_refine_blocks(const PolicySet& ps, uint32_t chunk_rules, JitImage* img);
+// Plan cache (in the code-object cache directory): the final kernel plan of a policy set,
+// keyed by a hash of its first generated image (jit_plan_key), so a later compile of the
+// same set goes straight to its final kernels (plan-<key>.txt, which also lists their
+// code-object files).
+std::string jit_plan_key(const JitImage& img);
+bool jit_load_plan(const std::string& key, JitImage* img);
+void jit_save_plan(const std::string& key, const JitImage& img);
 bool co_kernel_info(const std::vector<char>& co, const std::string& name, uint32_t* private_seg, uint64_t* code,
                     uint32_t* vgprs = nullptr);
 

@@ -6,6 +6,9 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# specialized-kernel code objects of the policy sets the tests compile: built ahead of time
+# on the CPU (tools/jit_warm.sh; hiprtc needs no GPU) and shipped in-tree with libkvgpu.so
+os.environ.setdefault("KVGPU_JIT_CACHE", os.path.join(ROOT, "kyverno_amd", "jitcache"))
 
 
 def pytest_configure(config):

@@ -19,7 +19,7 @@ import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.abspath(__file__))
+ROOT = "/root/repo" if not os.environ.get("GRAFT_REPO_ROOT") else os.environ["GRAFT_REPO_ROOT"]
 sys.path.insert(0, ROOT)
 # code objects of the configs' specialized kernels, compiled ahead of time (tools/jit_warm.sh)
 os.environ.setdefault("KVGPU_JIT_CACHE", os.path.join(ROOT, "kyverno_amd", "jitcache"))
@@ -232,6 +232,16 @@ def main():
     # in-process path ingests [0, G * N) and the library cuts the same G shards of it
     n_devs = args.gpus if inproc else 1
     data = batch.synth(workloads.SEED, args.n_res * n_devs, kind_mix, first=rank * args.n_res)
+    if os.environ.get("SORT_STREAM"):
+        import re
+        lines = data.split(b"\n")
+        rk = re.compile(rb'"kind":"([^"]*)"'); rn = re.compile(rb'"namespace":"([^"]*)"')
+        def key(l):
+            a = rk.search(l); b = rn.search(l)
+            return (a.group(1) if a else b"", b.group(1) if (b and os.environ.get("SORT_STREAM") == "2") else b"")
+        lines = [l for l in lines if l]
+        lines.sort(key=key)
+        data = b"\n".join(lines) + b"\n"
     ndjson_bytes = len(data)
     t1 = time.time()
     b = batch.Batch(ps, data)

@@ -98,6 +98,7 @@ int main(int argc, char** argv) {
     const uint32_t G = getenv("KVEMU_SHARDS") ? (uint32_t)std::max(1, atoi(getenv("KVEMU_SHARDS"))) : 1u;
     const auto ranges = shard_ranges(whole.res.size(), G);
     const uint64_t n_total = whole.res.size();
+    const std::vector<uint32_t> order = whole.order;  // store order (whole is moved below)
     std::vector<uint8_t> status_all(ps.rules.size() * n_total, 0xEE);
     std::vector<ErrRec> err_all;
     bool wide_any = false;
@@ -266,6 +267,17 @@ int main(int argc, char** argv) {
     }  // shards
     const uint64_t nr = ps.rules.size(), nres = n_total;
     const bool wide = wide_any;
+    if (!order.empty()) {  // store order -> the input's resource order (as kv_result_status)
+      std::vector<uint8_t> st(status_all.size());
+      std::vector<ErrRec> ew(err_all.size());
+      for (uint64_t rl = 0; rl < nr; rl++)
+        for (uint64_t q = 0; q < nres; q++) {
+          st[rl * nres + order[q]] = status_all[rl * nres + q];
+          if (!err_all.empty()) ew[rl * nres + order[q]] = err_all[rl * nres + q];
+        }
+      status_all.swap(st);
+      err_all.swap(ew);
+    }
     const std::vector<uint8_t>& status = status_all;
     const std::vector<ErrRec>& errw = err_all;
     const std::string out = argv[4];
