@@ -104,7 +104,9 @@ struct Res {
   uint32_t nsm, lset, aset;
   uint32_t ns_index;      // index into the batch namespace table (namespaceSelector bits, report scope)
   uint32_t flags;         // RF_*
-  uint32_t pad[5];
+  uint32_t tup;           // match tuple: resources with equal match inputs (every field above
+                          // but root and name) share one (Batch::tup_rep, kvj_mtup)
+  uint32_t pad[4];
 };
 
 // a label / annotation list of a batch: kvs[first, first + count), sorted by key bytes

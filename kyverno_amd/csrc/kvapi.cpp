@@ -135,6 +135,8 @@ struct DevPolicySet {
   std::vector<hipModule_t> mods;
   std::vector<hipFunction_t> fns;
   hipFunction_t ptab_fn = nullptr;  // value-predicate table builder (kvj_ptab)
+  hipFunction_t mtup_fn = nullptr;  // match bits per tuple (kvj_mtup)
+  uint32_t mtup_words = 0;
   uint32_t memo_words = 0, ptab_rows = 0;
   int dev = -1;
   bool specialized() const { return !mods.empty(); }
@@ -151,7 +153,7 @@ struct DevPolicySet {
 };
 
 struct DevBatchRes {
-  DevBuf nodes, vals, res, kvs, bstr, nsbits, koff, klen, kstr, nsms, lsets, asets, view_dev;
+  DevBuf nodes, vals, res, kvs, bstr, nsbits, koff, klen, kstr, nsms, lsets, asets, tuprep, view_dev;
   // pattern variables (kvvars.cpp): the batch predicate table (a DevPS with its pred tables),
   // outcome ids per [dynamic leaf][res], statuses per [dynamic rule][res]
   DevBuf dpreds, dalts, dconjs, datoms, dgsegs, dgwords, dpstr, dps, dleaf, dynst;
@@ -530,6 +532,10 @@ DevPolicySet& dev_ps(kv_policyset* s, int device) {
                 local);
       }
     }
+    if (J.mtup_words) {
+      d->mtup_fn = byname.at("kvj_mtup");
+      d->mtup_words = J.mtup_words;
+    }
     if (J.memo_words) {
       d->ptab_fn = byname.at("kvj_ptab");
       d->memo_words = J.memo_words;
@@ -576,6 +582,7 @@ DevBatchRes& dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
   d->nsms.upload(b.nsms, device);
   d->lsets.upload(b.lsets, device);
   d->asets.upload(b.asets, device);
+  d->tuprep.upload(b.tup_rep, device);
   DevBatch& v = d->view;
   v.nodes = (const Node*)d->nodes.p;
   v.vals = (const Val*)d->vals.p;
@@ -594,6 +601,8 @@ DevBatchRes& dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
   v.n_asets = (uint32_t)b.asets.size();
   v.ns_words = b.ns_words;
   v.n_res = (uint32_t)b.res.size();
+  v.tup_rep = (const uint32_t*)d->tuprep.p;
+  v.n_tup = (uint32_t)b.tup_rep.size();
   {  // pattern variables: every pointer valid (16-byte buffers when the policy set has none)
     const DynHost& h = bt->dyn_host(ps);
     d->dpreds.upload(h.tbl.preds, device);
@@ -812,7 +821,7 @@ struct DevSession {
   int device = 0;
   uint32_t mode = 0;
   uint64_t nrules = 0, nres = 0;
-  DevBuf fflags, pview, st, er8, er, cn, scope, scn, ptab, mtab, mtbf;
+  DevBuf fflags, pview, st, er8, er, cn, scope, scn, ptab, mtab, mtbf, mtup;
   DevBuf r_offs, r_tot, r_base, r_out8, r_outw, r_wide;  // record compaction (fetch)
   uint32_t mt_words = 0, mt_entities = 0;
   uint32_t *mt_ns = nullptr, *mt_ann = nullptr, *mt_sel = nullptr;
@@ -864,6 +873,11 @@ struct DevSession {
       P.mt_sel = mt_sel;
       mt_words = P.mt_ns_words + P.mt_ann_words + P.mt_sel_words;
       mt_entities = (uint32_t)std::max({bb.nsms.size(), bb.asets.size(), bb.lsets.size()});
+    }
+    if (dp.mtup_fn) {  // match bits of every rule per match tuple: mtup_words per tuple
+      mtup.alloc(std::max<size_t>((size_t)dp.mtup_words * bt->b.tup_rep.size(), 1) * sizeof(uint32_t), device);
+      P.mtup = (const uint32_t*)mtup.p;
+      P.mtup_words = dp.mtup_words;
     }
     pview.upload_raw(&P, sizeof(DevPS), device);  // read through a uniform pointer (scalar loads)
     nrules = ps->ps.rules.size();
@@ -940,6 +954,12 @@ struct DevSession {
       void* targs[] = {(void*)&P, (void*)&V, (void*)&S, (void*)&NV, (void*)&PT};
       HIPCHK(hipModuleLaunchKernel(dps->ptab_fn, (NV + KV_PTAB_PSEUDO + KV_WG - 1) / KV_WG, dps->ptab_rows, 1, KV_WG, 1, 1, 0,
                                    stream, targs, nullptr));
+    }
+    if (dps->mtup_fn && bt->b.tup_rep.size()) {  // every rule's match bit per tuple (after kv_mtab)
+      uint32_t* MT = (uint32_t*)mtup.p;
+      void* margs[] = {(void*)&P, (void*)&bview, (void*)&MT};
+      HIPCHK(hipModuleLaunchKernel(dps->mtup_fn, (uint32_t)((bt->b.tup_rep.size() + KV_WG - 1) / KV_WG),
+                                   dps->mtup_words, 1, KV_WG, 1, 1, 0, stream, margs, nullptr));
     }
     DevOut Ov = O;
     uint32_t r0 = 0;

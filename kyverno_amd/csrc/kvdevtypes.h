@@ -62,6 +62,12 @@ struct DevPS {
   const uint32_t* mt_ns;
   const uint32_t* mt_ann;
   const uint32_t* mt_sel;
+  // match bits of the specialized kernels per match tuple (Res::tup): mtup[tup * mtup_words +
+  // w] bit b = rule at bit position 32*w+b (kernel order, kvjit.cpp) matches the tuple's
+  // resources (1 for rules with name filters: evaluated per resource); built each pass by
+  // kvj_mtup after kv_mtab
+  const uint32_t* mtup;
+  uint32_t mtup_words;
   // filter of each namespace-glob bit (mt_ns_words * 32 entries), then of each annotation bit
   // (mt_ann_words * 32); KV_SENT for unused bits (mtab_bit_filters, kvfold.cpp)
   const uint32_t* mt_bitf;
@@ -83,6 +89,8 @@ struct DevBatch {
   uint32_t n_nsm, n_lsets, n_asets;
   uint32_t ns_words;
   uint32_t n_res;
+  const uint32_t* tup_rep;  // a resource of each match tuple (its Res is the tuple's inputs)
+  uint32_t n_tup;
   // pattern variables (kvvars.cpp build_dyn): predicate table of the batch's distinct
   // substituted leaves, outcome (= predicate) id per [dynamic leaf][res], and the status
   // substitution decides per [dynamic rule][res] (0: evaluate, ST_ERROR, ST_CPU)

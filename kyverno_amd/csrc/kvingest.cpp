@@ -956,6 +956,41 @@ std::vector<uint32_t> kind_order(const std::vector<std::string_view>& kinds) {
   return order;
 }
 
+void match_tuples(Batch* b) {
+  // open addressing over 64-bit hashes of the match inputs, confirmed field by field against
+  // the tuple's first resource
+  auto key = [](const Res& r, uint32_t* k) {
+    k[0] = r.kind; k[1] = r.group; k[2] = r.version; k[3] = r.nsm;
+    k[4] = r.lset; k[5] = r.aset; k[6] = r.ns_index; k[7] = r.flags;
+  };
+  size_t cap = 1024;
+  while (cap < b->res.size() * 2) cap <<= 1;
+  std::vector<uint64_t> hs(cap, 0);
+  std::vector<uint32_t> ids(cap, 0);
+  b->tup_rep.clear();
+  for (size_t i = 0; i < b->res.size(); i++) {
+    uint32_t k[8], q[8];
+    key(b->res[i], k);
+    uint64_t h = 1469598103934665603ull;
+    for (uint32_t x : k) h = (h ^ x) * 1099511628211ull, h ^= h >> 29;
+    h = h ? h : 1;
+    size_t at = h & (cap - 1);
+    for (;; at = (at + 1) & (cap - 1)) {
+      if (hs[at] == 0) {
+        hs[at] = h;
+        ids[at] = (uint32_t)b->tup_rep.size();
+        b->tup_rep.push_back((uint32_t)i);
+        break;
+      }
+      if (hs[at] == h) {
+        key(b->res[b->tup_rep[ids[at]]], q);
+        if (memcmp(k, q, sizeof k) == 0) break;
+      }
+    }
+    b->res[i].tup = ids[at];
+  }
+}
+
 void ingest_resources(const PolicySet& ps, const char* json, size_t len, const char* ns_labels_json, Batch* b) {
   const unsigned T = ingest_threads();
   size_t first = 0;
@@ -1067,6 +1102,7 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
       if (selector_eval_host(ps.nsselectors[s], b->ns_labels[n]) == 1) b->ns_bits[n * b->ns_words + s / 32] |= 1u << (s % 32);
   // word-granular readers may touch up to 8 bytes past the last string
   b->strs.append(16, '\0');
+  match_tuples(b);
   // interning keys are only needed while ingesting
   std::unordered_map<std::string, uint32_t>().swap(b->vout_id);
   std::vector<std::string>().swap(b->nsm_keys);

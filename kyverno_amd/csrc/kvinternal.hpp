@@ -263,6 +263,8 @@ struct Batch {
   // order[i] of the caller's input; empty = the input order. Ingest groups resources of one
   // kind into common wave groups (kvingest.cpp), the result accessors map indices back.
   std::vector<uint32_t> order;
+  // match tuples (Res::tup): a store index of each tuple's first resource
+  std::vector<uint32_t> tup_rep;
   // the arrays that cross PCIe in page-locked memory when g_hostmem provides it
   void pin_store() {
     vals = StoreVec<kv::Val>(StoreAlloc<kv::Val>(true));
@@ -310,6 +312,10 @@ uint32_t compile_leaf_pred(PolicySet& tbl, const PV& value);  // kvcompile.cpp
 std::string pattern_go_v(const PV& p);                         // Go %v of a scalar pattern value
 
 void ingest_resources(const PolicySet& ps, const char* json, size_t len, const char* ns_labels_json, Batch* b);
+// Res::tup and Batch::tup_rep: resources whose match inputs (kind, group, version, checkNameSpace
+// string, label / annotation lists, namespace, flags) are equal share a tuple id, numbered in
+// store order (kvingest.cpp)
+void match_tuples(Batch* b);
 
 // Launch-time folding (kvfold.cpp): per-filter flags with the batch-constant
 // user-info criteria folded in (ctx_json: AdmissionInfo / ExcludeGroupRole, or

@@ -1284,6 +1284,27 @@ struct Gen {
     return f.str();
   }
 
+  // Match bits (kvj_mtup): the rule at LDS row q of the kernel being generated has bit
+  // position 32 * mt_kbase + q; mt_bits[p] = the rule at bit position p (KV_SENT: padding).
+  // A rule whose match reads the resource name is evaluated per resource behind its bit (which
+  // the tuple kernel sets to 1).
+  uint32_t mt_kbase = 0;
+  std::vector<uint32_t> mt_bits;
+  bool name_dependent(uint32_t ri) const {
+    const RuleRec& rr = ps.rules[ri];
+    for (uint32_t f = rr.m_first; f < rr.m_first + rr.m_count; f++)
+      if (ps.filters[f].flags & (MF_NAME | MF_NAMES)) return true;
+    for (uint32_t f = rr.x_first; f < rr.x_first + rr.x_count; f++)
+      if (ps.filters[f].flags & (MF_NAME | MF_NAMES)) return true;
+    return false;
+  }
+  std::string mt_cond(uint32_t ri, uint32_t row) const {
+    const uint32_t p = mt_kbase * 32u + row;
+    std::string c = "((mw" + std::to_string(p / 32u) + " >> " + std::to_string(p % 32u) + "u) & 1u)";
+    if (name_dependent(ri)) c += " && g_match_" + std::to_string(ri) + "(P, B, R, rkind, rflags)";
+    return c;
+  }
+
   uint32_t gtab_n = 0;          // member tables emitted so far (per generated program text)
   std::string block_decls;      // declarations the current kernel's blocks need (member tables)
 
@@ -1463,7 +1484,7 @@ struct Gen {
             return "{ const EState e_{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u}; kv_final(O, " + u32(ri) +
                    ", n_res, r, valid, " + x + ", e_, " + rw + "); }";
           };
-          k << "  if (valid && g_match_" << ri << "(P, B, R, rkind, rflags)) {\n"
+          k << "  if (" << mt_cond(ri, hbase + g.q + j) << ") {\n"
             << "    if (rflags & RF_MAGIC) " << st("ST_CPU") << "\n";
           if (rr.flags & RR_META_EXPAND) k << "    else if (rflags & " << u32(meta_bad_flags(rr.flags)) << ") " << st("ST_CPU") << "\n";
           if (rr.dyn)
@@ -1477,7 +1498,7 @@ struct Gen {
       const RuleRec& rr = ps.rules[ri];
       const std::string s = "_" + std::to_string(ri);
       std::ostringstream k;
-      k << "  if (valid && g_match_" << ri << "(P, B, R, rkind, rflags)) {\n";
+      k << "  if (" << mt_cond(ri, hbase + q) << ") {\n";
       switch (rr.route) {
         case 1: k << "    rs" << s << " = FIN_ | ST_CPU;\n"; break;
         case 2: k << "    rs" << s << " = FIN_ | ST_NOMATCH;\n"; break;
@@ -1731,16 +1752,21 @@ struct Gen {
   // are still cache-resident, instead of one grid-wide pass per chunk.
   std::vector<uint32_t> group_kernel(const std::string& name, const std::vector<const JitChunk*>& chs, int waves) {
     std::vector<std::string> blocks;
+    std::vector<std::pair<uint32_t, uint32_t>> rows;  // LDS rows [first, first + count) of each block
     std::vector<uint32_t> rules;
     uint32_t nr_all = 0;
     for (const JitChunk* c : chs) nr_all += (uint32_t)c->rules.size();
     hist_lds = nr_all * 256u <= 48u * 1024u;  // <= 48 KB of status bytes
     block_decls.clear();
+    mt_kbase = (uint32_t)(mt_bits.size() / 32u);
     for (const JitChunk* c : chs) {
       std::vector<uint32_t> ord;
+      rows.push_back({(uint32_t)rules.size(), (uint32_t)c->rules.size()});
       blocks.push_back(fused_block(*c, (uint32_t)rules.size(), &ord));
       rules.insert(rules.end(), ord.begin(), ord.end());
     }
+    mt_bits.insert(mt_bits.end(), rules.begin(), rules.end());
+    while (mt_bits.size() % 32u) mt_bits.push_back(0xFFFFFFFFu);
     const uint32_t nr = (uint32_t)rules.size();
     KernelText kt(*this, name);
     o << block_decls;
@@ -1771,10 +1797,33 @@ struct Gen {
       << "  const uint32_t n_res = B.n_res;\n"
       << "  const bool valid = r < n_res;\n"
       << "  const Res* __restrict__ R = B.res + (valid ? r : 0u);\n"
-      << "  uint32_t root = ABSENT, rkind = KEY_NONE, rflags = 0u;\n"
-      << "  if (valid) { root = ni(R->root); rkind = R->kind; rflags = R->flags; }\n"
-      << "  Node rootn{0u, 0u, 0u, 0u};\n  if (valid) rootn = N[root];\n";
-    for (const std::string& b : blocks) o << "  {\n" << b << "  }\n";
+      << "  uint32_t root = ABSENT, rkind = KEY_NONE, rflags = 0u, rtup = 0u;\n"
+      << "  if (valid) { root = ni(R->root); rkind = R->kind; rflags = R->flags; rtup = R->tup; }\n"
+      << "  Node rootn{0u, 0u, 0u, 0u};\n  if (valid) rootn = N[root];\n"
+      << "  const uint32_t* __restrict__ mtr_ = P.mtup + (size_t)rtup * P.mtup_words;\n";
+    for (size_t bi = 0; bi < blocks.size(); bi++) {
+      // the block's match words (bits of its rules, kvj_mtup); a wave none of whose resources
+      // matches any rule of the block skips it whole (every rule NOMATCH on every lane)
+      const uint32_t r0 = rows[bi].first, rn = rows[bi].second;
+      const uint32_t p0 = mt_kbase * 32u + r0, p1 = p0 + rn;  // bit positions [p0, p1)
+      o << "  {\n";
+      std::string any = "0u";
+      for (uint32_t w = p0 / 32u; w * 32u < p1; w++) {
+        const uint32_t lo = std::max(p0, w * 32u) - w * 32u, hi = std::min(p1, w * 32u + 32u) - w * 32u;
+        const uint32_t m = hi - lo == 32u ? 0xFFFFFFFFu : ((1u << (hi - lo)) - 1u) << lo;
+        o << "  const uint32_t mw" << w << " = valid ? mtr_[" << w << "] : 0u;\n";
+        any += " | (mw" + std::to_string(w) + " & " + u32(m) + ")";
+      }
+      if (hist_lds) {
+        o << "  if (__ballot((" << any << ") != 0u) == 0ull) {\n"
+          << "    for (uint32_t q_ = " << r0 << "u; q_ < " << r0 + rn << "u; q_++) ((uint8_t*)s_stw)[q_ * KV_WG + threadIdx.x] = "
+          << "valid ? (uint8_t)ST_NOMATCH : (uint8_t)0xFFu;\n"
+          << "  } else {\n" << blocks[bi] << "  }\n";
+      } else {
+        o << blocks[bi];
+      }
+      o << "  }\n";
+    }
     if (hist_lds) {
       // the status rows staged in LDS go to the status matrix (one byte per rule and lane,
       // 64 B per wave and rule); one thread per rule counts its 256 status bytes and adds the
@@ -1800,6 +1849,33 @@ struct Gen {
          "(unsigned long long)v);\n"
       << "  }\n}\n\n";
     return rules;
+  }
+
+  // kvj_mtup: the match bits of every rule for every match tuple (one thread per tuple and
+  // 32-rule word): g_match of the word's rules on the tuple's representative resource; a rule
+  // whose match reads the name gets bit 1 (its kernel evaluates it per resource)
+  void mtup_kernel() {
+    const uint32_t W = (uint32_t)(mt_bits.size() / 32u);
+    KernelText kt(*this, "kvj_mtup");
+    o << "extern \"C\" __global__ __launch_bounds__(KV_WG) void kvj_mtup(const DevPS* __restrict__ Pp, "
+         "const DevBatch* __restrict__ Bp, uint32_t* __restrict__ out) {\n"
+      << "  const DevPS& P = *Pp;\n  const DevBatch& B = *Bp;\n"
+      << "  const uint32_t t = blockIdx.x * KV_WG + threadIdx.x;\n"
+      << "  if (t >= B.n_tup) return;\n"
+      << "  const Res* __restrict__ R = B.res + B.tup_rep[t];\n"
+      << "  const uint32_t rkind = R->kind, rflags = R->flags;\n"
+      << "  uint32_t m = 0u;\n  switch (blockIdx.y) {\n";
+    for (uint32_t w = 0; w < W; w++) {
+      o << "    case " << w << "u:\n";
+      for (uint32_t b = 0; b < 32u; b++) {
+        const uint32_t ri = mt_bits[w * 32u + b];
+        if (ri == 0xFFFFFFFFu) continue;
+        if (name_dependent(ri)) o << "      m |= " << u32(1u << b) << ";\n";
+        else o << "      if (g_match_" << ri << "(P, B, R, rkind, rflags)) m |= " << u32(1u << b) << ";\n";
+      }
+      o << "      break;\n";
+    }
+    o << "  }\n  out[(size_t)t * " << W << "u + blockIdx.y] = m;\n}\n\n";
   }
 
   // Register weight of rule ri in a fused block: the state it keeps across the block (status
@@ -1957,9 +2033,11 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
       out->chunks.push_back(kc);
     }
   }
+  out->mtup_words = (uint32_t)(g.mt_bits.size() / 32u);
+  if (out->mtup_words && !out->probe) g.mtup_kernel();
   out->memo_preds.clear();
   out->memo_words = 0;
-  if (!g.mpreds.empty()) {
+  if (!g.mpreds.empty() && !out->probe) {
     g.ptab_kernel();
     out->memo_preds = g.mpreds;
     out->memo_words = (uint32_t)((g.mpreds.size() + 31) / 32);
@@ -2293,6 +2371,7 @@ void jit_refine_blocks(const PolicySet& ps, uint32_t chunk_rules, JitImage* img)
   // registers is split in two, and its halves are probed in the next round.
   for (int round = 0; round < 12; round++) {
     JitImage probe;
+    probe.probe = true;
     std::vector<std::pair<size_t, size_t>> at;  // (kernel, block) of each probe
     for (size_t k = 0; k < img->plan.size(); k++) {
       const JitKernelPlan& kp = img->plan[k];

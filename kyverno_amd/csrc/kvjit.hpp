@@ -42,6 +42,9 @@ struct JitImage {
   std::vector<uint32_t> memo_preds;
   uint32_t memo_words = 0;
   uint32_t ptab_row = 1;    // predicates per kvj_ptab grid row (one row: every predicate of a value)
+  // match bits per tuple (kvj_mtup, DevPS::mtup): words of 32 rules in kernel order
+  uint32_t mtup_words = 0;
+  bool probe = false;       // a block-probe image (jit_refine_blocks): rule kernels only
   double gen_ms = 0, compile_ms = 0;
 };
 

@@ -56,6 +56,7 @@ void make_shard(const Batch& b, uint64_t lo, uint64_t hi, Batch* out) {
   for (uint64_t r = 0; r < s.n_rows; r++) s.roff[r] = b.roff[row_lo + r] - (uint32_t)c_lo;
   s.res.assign(b.res.begin() + lo, b.res.begin() + hi);
   for (Res& r : s.res) r.root -= (uint32_t)row_lo;
+  match_tuples(&s);  // the shard's own tuples (its table holds only those)
   s.kvs = b.kvs;
   s.strs = b.strs;
   s.dyn_keys = b.dyn_keys;

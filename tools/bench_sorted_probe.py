@@ -207,6 +207,13 @@ def main():
         workload = "C2: synthetic Pods x 100 validate.pattern rules (image globs, ?*, quantities, |-lists)"
     elif args.config == "c3":
         pols = workloads.c3_policies(1000)
+        if os.environ.get("C3_KINDS_ONLY"):  # probe: match blocks reduced to their kinds
+            for p in pols:
+                for r in p["spec"]["rules"]:
+                    m = r["match"]
+                    res = m["resources"] if "resources" in m else m["any"][0]["resources"]
+                    r["match"] = {"resources": {"kinds": res["kinds"]}}
+                    r.pop("exclude", None)
         kind_mix = workloads.C3_KIND_MIX  # 1 000 namespaces
         workload = "C3: Pods/Deployments/Services 60/25/15 over 1000 namespaces x 1000 policies with match/exclude"
     elif args.config == "c4":

@@ -40,6 +40,7 @@ extern "C" void kvemu_mtab(const DevPS* P, const DevBatch* B, uint32_t words, ui
                            uint32_t* an, uint32_t* sl);
 
 typedef void (*ptab_fn)(const DevPS*, const Val*, const uint8_t*, uint32_t, uint32_t*);
+typedef void (*mtup_fn)(const DevPS*, const DevBatch*, uint32_t*);
 typedef void (*chunk_fn)(const DevPS*, const DevBatch*, const Node*, const Val*, const uint8_t*, DevOut, uint32_t);
 
 static std::string slurp(const char* p) {
@@ -175,6 +176,11 @@ int main(int argc, char** argv) {
     B.n_asets = (uint32_t)b.asets.size();
     B.ns_words = b.ns_words;
     B.n_res = (uint32_t)b.res.size();
+    B.tup_rep = b.tup_rep.data();
+    B.n_tup = (uint32_t)b.tup_rep.size();
+    std::vector<uint32_t> mtup(std::max<size_t>((size_t)img.mtup_words * b.tup_rep.size(), 1), 0xA5A5A5A5u);
+    P.mtup = mtup.data();
+    P.mtup_words = img.mtup_words;
     // pattern variables (as dev_batch in kvapi.cpp)
     DynHost dyn;
     build_dyn(ps, b, &dyn);
@@ -210,6 +216,11 @@ int main(int argc, char** argv) {
       if (!f) throw std::runtime_error("kvj_ptab not linked in");
       const uint32_t rows = (uint32_t)((img.memo_preds.size() + img.ptab_row - 1) / img.ptab_row);
       grid((NV + KV_PTAB_PSEUDO + KV_WG - 1) / KV_WG, rows, [&]() { f(&P, B.vals, B.bstr, NV, ptab.data()); });
+    }
+    if (img.mtup_words && B.n_tup) {  // match bits per tuple (as kv_session, after the match tables)
+      auto f = (mtup_fn)dlsym(RTLD_DEFAULT, "kvj_mtup");
+      if (!f) throw std::runtime_error("kvj_mtup not linked in");
+      grid((B.n_tup + KV_WG - 1) / KV_WG, img.mtup_words, [&]() { f(&P, &B, mtup.data()); });
     }
     std::vector<uint8_t> status(nr * nres, 0xEE);
     std::vector<ErrRec8> err8(nr * nres);
