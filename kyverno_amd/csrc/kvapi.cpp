@@ -959,7 +959,7 @@ struct DevSession {
       uint32_t* MT = (uint32_t*)mtup.p;
       void* margs[] = {(void*)&P, (void*)&bview, (void*)&MT};
       HIPCHK(hipModuleLaunchKernel(dps->mtup_fn, (uint32_t)((bt->b.tup_rep.size() + KV_WG - 1) / KV_WG),
-                                   1, 1, KV_WG, 1, 1, 0, stream, margs, nullptr));
+                                   dps->mtup_words, 1, KV_WG, 1, 1, 0, stream, margs, nullptr));
     }
     DevOut Ov = O;
     uint32_t r0 = 0;

@@ -1851,10 +1851,9 @@ struct Gen {
     return rules;
   }
 
-  // kvj_mtup: the match bits of every rule for every match tuple (one thread per tuple, every
-  // word): g_match of each rule on the tuple's representative resource, straight-line, so the
-  // match-table words the rules test are loaded once per tuple (no store in between may alias
-  // them); a rule whose match reads the name gets bit 1 (its kernel evaluates it per resource)
+  // kvj_mtup: the match bits of every rule for every match tuple (one thread per tuple and
+  // 32-rule word): g_match of the word's rules on the tuple's representative resource; a rule
+  // whose match reads the name gets bit 1 (its kernel evaluates it per resource)
   void mtup_kernel() {
     const uint32_t W = (uint32_t)(mt_bits.size() / 32u);
     KernelText kt(*this, "kvj_mtup");
@@ -1865,18 +1864,18 @@ struct Gen {
       << "  if (t >= B.n_tup) return;\n"
       << "  const Res* __restrict__ R = B.res + B.tup_rep[t];\n"
       << "  const uint32_t rkind = R->kind, rflags = R->flags;\n"
-      << "  uint32_t* __restrict__ o_ = out + (size_t)t * " << W << "u;\n  uint32_t m;\n";
+      << "  uint32_t m = 0u;\n  switch (blockIdx.y) {\n";
     for (uint32_t w = 0; w < W; w++) {
-      o << "  m = 0u;\n";
+      o << "    case " << w << "u:\n";
       for (uint32_t b = 0; b < 32u; b++) {
         const uint32_t ri = mt_bits[w * 32u + b];
         if (ri == 0xFFFFFFFFu) continue;
-        if (name_dependent(ri)) o << "  m |= " << u32(1u << b) << ";\n";
-        else o << "  if (g_match_" << ri << "(P, B, R, rkind, rflags)) m |= " << u32(1u << b) << ";\n";
+        if (name_dependent(ri)) o << "      m |= " << u32(1u << b) << ";\n";
+        else o << "      if (g_match_" << ri << "(P, B, R, rkind, rflags)) m |= " << u32(1u << b) << ";\n";
       }
-      o << "  o_[" << w << "] = m;\n";
+      o << "      break;\n";
     }
-    o << "}\n\n";
+    o << "  }\n  out[(size_t)t * " << W << "u + blockIdx.y] = m;\n}\n\n";
   }
 
   // Register weight of rule ri in a fused block: the state it keeps across the block (status

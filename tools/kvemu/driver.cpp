@@ -220,7 +220,7 @@ int main(int argc, char** argv) {
     if (img.mtup_words && B.n_tup) {  // match bits per tuple (as kv_session, after the match tables)
       auto f = (mtup_fn)dlsym(RTLD_DEFAULT, "kvj_mtup");
       if (!f) throw std::runtime_error("kvj_mtup not linked in");
-      grid((B.n_tup + KV_WG - 1) / KV_WG, 1, [&]() { f(&P, &B, mtup.data()); });
+      grid((B.n_tup + KV_WG - 1) / KV_WG, img.mtup_words, [&]() { f(&P, &B, mtup.data()); });
     }
     std::vector<uint8_t> status(nr * nres, 0xEE);
     std::vector<ErrRec8> err8(nr * nres);
