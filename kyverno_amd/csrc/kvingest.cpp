@@ -706,6 +706,46 @@ bool scan_values(const char* p, size_t n, unsigned T, std::vector<size_t>* start
   return true;
 }
 
+// Start offsets of the documents of NDJSON input, one object per line (the usual form of
+// a resource dump): a memchr per line over parallel pieces, no byte-by-byte scan. The parse
+// threads check that each document ends its line; any other form (pretty-printed objects,
+// several values on a line) fails that check and goes through scan_values.
+struct NotLines {};
+
+bool split_lines(const char* p, size_t n, unsigned T, std::vector<size_t>* starts) {
+  std::vector<size_t> cut{0};
+  for (unsigned k = 1; k < T; k++) {
+    const size_t x = std::max(cut.back(), n / T * k);
+    const char* nl = x < n ? (const char*)memchr(p + x, '\n', n - x) : nullptr;
+    if (!nl) break;
+    cut.push_back((size_t)(nl - p) + 1);
+  }
+  cut.push_back(n);
+  const size_t P = cut.size() - 1;
+  std::vector<std::vector<size_t>> part(P);
+  std::vector<char> ok(P, 1);
+  std::vector<std::thread> th;
+  for (size_t k = 0; k < P; k++)
+    th.emplace_back([&, k]() {
+      for (size_t q = cut[k], e = cut[k + 1]; q < e;) {
+        while (q < e && (p[q] == ' ' || p[q] == '\t' || p[q] == '\r' || p[q] == '\n')) q++;
+        if (q >= e) break;
+        if (p[q] != '{') {
+          ok[k] = 0;
+          return;
+        }
+        part[k].push_back(q);
+        const char* nl = (const char*)memchr(p + q, '\n', e - q);
+        q = nl ? (size_t)(nl - p) + 1 : e;
+      }
+    });
+  for (auto& t : th) t.join();
+  for (size_t k = 0; k < P; k++)
+    if (!ok[k]) return false;
+  for (auto& v : part) starts->insert(starts->end(), v.begin(), v.end());
+  return true;
+}
+
 // Concatenate per-thread batches (each a whole number of 64-resource wave
 // groups, in input order): heaps, values, KV pairs and rows are appended with
 // their offsets rebased; batch-local key ids and namespace indices are remapped
@@ -1001,8 +1041,17 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
   const auto t0 = std::chrono::steady_clock::now();
   auto ms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
   const bool verbose = getenv("KVGPU_VERBOSE") != nullptr;
-  if (T > 1 && len >= (1u << 20) && first < len && json[first] == '{' && scan_values(json, len, T, &starts)) {
-    if (verbose) fprintf(stderr, "[kvgpu] ingest: scan %.1f ms (%zu values)\n", ms(), starts.size());
+  // NDJSON first (documents = lines); when a document does not end its line, the values are
+  // found again by the full scan
+  bool lines = T > 1 && len >= (1u << 20) && first < len && json[first] == '{' && split_lines(json, len, T, &starts);
+  for (int attempt = 0; attempt < 2 && !parallel; attempt++) {
+    if (attempt == 1 || !lines) {
+      starts.clear();
+      lines = false;
+      b->order.clear();
+      if (!(T > 1 && len >= (1u << 20) && first < len && json[first] == '{' && scan_values(json, len, T, &starts))) break;
+    }
+    if (verbose) fprintf(stderr, "[kvgpu] ingest: %s %.1f ms (%zu values)\n", lines ? "lines" : "scan", ms(), starts.size());
     // whole wave groups per thread, so lane = resource index % 64 holds in the merged batch
     const size_t nres = starts.size(), groups = (nres + KV_LANES - 1) / KV_LANES;
     const size_t per = (groups + T - 1) / T * KV_LANES;
@@ -1036,15 +1085,23 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
             const size_t end = i + 1 < nres ? starts[i + 1] : len;
             doc.nodes.clear();
             doc.strs.clear();
-            parse_one(json + starts[i], end - starts[i], NUM_UNSTRUCTURED, &doc);
+            const size_t used = parse_one(json + starts[i], end - starts[i], NUM_UNSTRUCTURED, &doc);
+            if (lines)  // the document must end its line
+              for (size_t x = starts[i] + used; x < end; x++)
+                if (json[x] != ' ' && json[x] != '\t' && json[x] != '\r' && json[x] != '\n') throw NotLines();
             in.take(doc);
           }
           in.flush_group();
+        } catch (const NotLines&) {
+          errs[k] = "\x01";
         } catch (const std::exception& ex) {
-          errs[k] = ex.what();
+          errs[k] = lines ? "\x01" : ex.what();  // (a line-split document may be a fragment)
         }
       });
     for (auto& t : th) t.join();
+    bool relines = false;
+    for (auto& e : errs) relines |= e == "\x01";
+    if (relines) continue;  // not one document per line: scan
     for (auto& e : errs)
       if (!e.empty()) throw std::runtime_error(e);
     if (verbose) fprintf(stderr, "[kvgpu] ingest: %zu threads %.1f ms\n", P, ms());

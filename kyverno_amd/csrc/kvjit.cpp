@@ -1968,6 +1968,27 @@ std::string rule_signature(const PolicySet& ps, uint32_t ri) {
   return sig;
 }
 
+// The kinds rule ri's match blocks admit ("*" when any block admits every kind): rules of
+// one kind set then share blocks, which the kind-grouped store order lets whole waves skip
+std::string rule_kind_key(const PolicySet& ps, uint32_t ri) {
+  const RuleRec& rr = ps.rules[ri];
+  std::vector<std::string> ks;
+  for (uint32_t f = rr.m_first; f < rr.m_first + rr.m_count; f++) {
+    const MFilter& F = ps.filters[f];
+    if (!(F.flags & MF_KINDS)) return "*";
+    for (uint32_t i = F.kinds_first; i < F.kinds_first + F.kinds_count; i++) {
+      const KindSpec& k = ps.kinds[i];
+      if (k.form == 3) return "*";
+      ks.push_back(std::to_string(k.kind));
+    }
+  }
+  std::sort(ks.begin(), ks.end());
+  ks.erase(std::unique(ks.begin(), ks.end()), ks.end());
+  std::string key;
+  for (auto& k : ks) key += k + ",";
+  return key;
+}
+
 }  // namespace
 
 uint32_t jit_chunk_rules() {
@@ -1990,8 +2011,13 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   {
     // rules that walk the same arrays and leaves share a kernel (and its hoisted lookups)
     std::vector<std::pair<std::string, uint32_t>> order;
+    // KVGPU_JIT_KINDSORT=1: rules grouped by the kinds they match first, walk signature second
+    const bool kind_first = getenv("KVGPU_JIT_KINDSORT") && getenv("KVGPU_JIT_KINDSORT")[0] == '1';
     for (uint32_t ri = 0; ri < n; ri++)
-      order.push_back({ps.rules[ri].route == 0 ? "0" + rule_signature(ps, ri) : "1", ri});
+      order.push_back({ps.rules[ri].route == 0 ? "0" + (kind_first ? rule_kind_key(ps, ri) + "#" : std::string()) +
+                                                     rule_signature(ps, ri)
+                                               : "1",
+                       ri});
     std::stable_sort(order.begin(), order.end());
     // One kernel per range of the signature order: its rules run as one fused block (every
     // array they walk is walked once per resource, all rules of the range in one loop over
@@ -2333,12 +2359,21 @@ bool jit_plan_spills(JitImage* img) {
       throw std::runtime_error("kvjit: no kernel descriptor for " + name);
     img->kernel_scratch[k] = priv;
     const bool met = kp.waves == 0 || vgprs <= 512u / (uint32_t)kp.waves;
-    if (priv == 0 && met) {
+    // the out-of-line dynamic-leaf evaluator (pattern variables) keeps a call frame in
+    // scratch: allowed in a kernel without a launch bound (the round-1 fault was spill code
+    // under a bound), so such a kernel drops its bound instead of splitting blocks
+    const bool calls = img->kernel_src[ci].find("kv_dleaf_impl") != std::string::npos;
+    if ((priv == 0 || (calls && kp.waves == 0)) && met) {
       next.push_back(kp);
       continue;
     }
     changed = true;
     JitKernelPlan np = kp;
+    if (calls && met && priv != 0) {
+      np.waves = 0;
+      next.push_back(np);
+      continue;
+    }
     size_t big = 0;
     for (size_t b = 1; b < np.blocks.size(); b++)
       if (np.blocks[b] > np.blocks[big]) big = b;
@@ -2399,7 +2434,8 @@ void jit_refine_blocks(const PolicySet& ps, uint32_t chunk_rules, JitImage* img)
       uint64_t code = 0;
       if (ci == probe.kernel_name.size() || !co_kernel_info(probe.codes[ci], name, &priv, &code, &vgprs))
         throw std::runtime_error("kvjit: no kernel descriptor for probe " + name);
-      if (priv != 0 || vgprs > 512u / (uint32_t)probe.plan[i].waves) {
+      const bool calls = probe.kernel_src[ci].find("kv_dleaf_impl") != std::string::npos;
+      if ((priv != 0 && !calls) || vgprs > 512u / (uint32_t)probe.plan[i].waves) {
         split[at[i].first].resize(img->plan[at[i].first].blocks.size(), 0);
         split[at[i].first][at[i].second] = 1;
         any = true;

@@ -139,3 +139,24 @@ def test_register_path_globs_long_and_unicode(orc):
     bad = np.argwhere(st != ost)
     assert not len(bad), [(int(a), int(b), int(st[a, b]), int(ost[a, b])) for a, b in bad[:20]]
     assert (st == 0).sum() > 0 and (st == 1).sum() > 0
+
+
+def test_ingest_paths_agree(orc):
+    """The three ingest paths give the same store: NDJSON split at newlines on 8 threads,
+    pretty-printed documents (the line split fails its check, the byte scan finds the
+    values) on 8 threads, and the serial parser; mixed kinds, so the kind store order is on."""
+    from kyverno_amd import workloads
+
+    pols = workloads.c5_policies()
+    ress = _synth(workloads.SEED + 9, 3000, 1)
+    exe = kvemu.build(pols, os.path.join(WORK, "ingest_paths"))
+    nd = b"\n".join(json.dumps(r).encode() for r in ress)
+    pretty = b"\n".join(json.dumps(r, indent=1).encode() for r in ress)
+    assert len(nd) >= (1 << 20)  # the parallel paths need >= 1 MiB
+    got = {}
+    for tag, data, threads in (("lines", nd, "8"), ("scan", pretty, "8"), ("serial", nd, "1")):
+        st, _ = kvemu.run(exe, data, os.path.join(WORK, "ingest_paths"), env={"KVGPU_INGEST_THREADS": threads})
+        got[tag] = st
+    ost = oracle_status(orc, pols, ress)
+    for tag, st in got.items():
+        assert np.array_equal(st, ost), tag

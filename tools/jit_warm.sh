@@ -20,7 +20,7 @@ ps = batch.PolicySet(pols, specialize=True)
 print(c, ps.jit_info["kernels"], "kernels", round(time.time() - t, 1), "s", flush=True)
 PY
 done
-timeout 3000 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600 -n 4 > /tmp/jit_warm_tests.log 2>&1
+timeout 5400 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 1200 -n 4 > /tmp/jit_warm_tests.log 2>&1
 tail -1 /tmp/jit_warm_tests.log
 python tools/jit_prune.py "$KVGPU_JIT_CACHE"
 du -sh "$KVGPU_JIT_CACHE"
