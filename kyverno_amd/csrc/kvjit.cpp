@@ -2011,8 +2011,9 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   {
     // rules that walk the same arrays and leaves share a kernel (and its hoisted lookups)
     std::vector<std::pair<std::string, uint32_t>> order;
-    // KVGPU_JIT_KINDSORT=1: rules grouped by the kinds they match first, walk signature second
-    const bool kind_first = getenv("KVGPU_JIT_KINDSORT") && getenv("KVGPU_JIT_KINDSORT")[0] == '1';
+    // rules grouped by the kinds they match first, walk signature second (C5 4.07 -> 3.72 ms,
+    // C3 10.19 -> 10.32; KVGPU_JIT_KINDSORT=0: signature only, for A/B)
+    const bool kind_first = !(getenv("KVGPU_JIT_KINDSORT") && getenv("KVGPU_JIT_KINDSORT")[0] == '0');
     for (uint32_t ri = 0; ri < n; ri++)
       order.push_back({ps.rules[ri].route == 0 ? "0" + (kind_first ? rule_kind_key(ps, ri) + "#" : std::string()) +
                                                      rule_signature(ps, ri)
