@@ -14,7 +14,8 @@ struct ErrRec {
 };
 
 // Compact error record (8 B per FAIL / ERROR / SKIP pair, the one written per pass):
-//   w0 = kind | flags << 4 | wide << 6 | pnode << 7          (pnode < 2^25)
+//   w0 = kind | flags << 4 | wide << 6 | lane << 7 | pnode << 13   (pnode < 2^19; lane: the
+//        resource's lane in its wave, which places a slotted record, kv_final)
 //   w1 = idx0 | idx1 << 12 | idx2 << 22    (idx0 < 4096, idx1 / idx2 < 1024, idx3 == 0)
 // A record that does not fit (larger loop indices, a fourth loop level, a resolved
 // wildcard key) sets `wide`; the host then re-runs the pass with full records
@@ -62,8 +63,8 @@ struct DevPS {
   const uint32_t* mt_ns;
   const uint32_t* mt_ann;
   const uint32_t* mt_sel;
-  // match bits of the specialized kernels per match tuple (Res::tup): mtup[tup * mtup_words +
-  // w] bit b = rule at bit position 32*w+b (kernel order, kvjit.cpp) matches the tuple's
+  // match bits of the specialized kernels per match tuple (Res::tup): mtup[w * n_tup + tup]
+  // bit b = rule at bit position 32*w+b (kernel order, kvjit.cpp) matches the tuple's
   // resources (1 for rules with name filters: evaluated per resource); built each pass by
   // kvj_mtup after kv_mtab
   const uint32_t* mtup;

@@ -928,7 +928,8 @@ struct Gen {
       std::ostringstream r;
       r << "kv_gfin(O, n_res, r, valid, " << m << ", " << st << ", " << u32(kind | (pcn.flags << 4) | (pn << 8));
       for (uint32_t lv = 0; lv < 4; lv++) r << ", " << (lv <= g.max_level ? li(lv) : std::string("0u"));
-      r << ", (uint8_t*)s_stw + " << u32(g.grow) << ", " << (g.gtab.empty() ? std::string("nullptr") : g.gtab) << ", "
+      r << ", (uint8_t*)s_stw + " << u32(g.grow) << ", s_rc + " << u32(g.grow / 256u * 4u) << ", "
+        << (g.gtab.empty() ? std::string("nullptr") : g.gtab) << ", "
         << u32(g.gn) << ", " << u32(g.gri[0]) << ", " << u32(g.gsri) << ", " << u32(g.gspn) << ");";
       return r.str();
     };
@@ -1447,7 +1448,8 @@ struct Gen {
       std::ostringstream k;
       k << "  { " << estate(g, ekx) << "\n";
       if (hist_lds)
-        k << "    kv_final(O, " << ri << "u, n_res, r, valid, " << st << ", e_, " << row(q) << "); }\n";
+        k << "    kv_final(O, " << ri << "u, n_res, r, valid, " << st << ", e_, " << row(q) << ", s_rc + "
+          << u32((hbase + q) * 4u) << "); }\n";
       else
         k << "    store_result2(O, " << ri << "u, n_res, r, valid, " << st << ", e_, &s_hist[" << (hbase + q)
           << "][0]); }\n";
@@ -1462,10 +1464,12 @@ struct Gen {
       if (!g) return store_st(q, g, st, "0u");
       if (g->grp)  // the members alive here end with the group's status (no error record)
         return "  if ((rs" + s + " & 0xFFu) != ST_STORED_)\n    kv_gfin(O, n_res, r, valid, al" + s + ", rs" + s +
-               " & 0xFFu, 0u, 0u, 0u, 0u, 0u, (uint8_t*)s_stw + " + u32(g->grow) + ", " +
+               " & 0xFFu, 0u, 0u, 0u, 0u, 0u, (uint8_t*)s_stw + " + u32(g->grow) + ", s_rc + " + u32(g->grow / 256u * 4u) +
+               ", " +
                (g->gtab.empty() ? std::string("nullptr") : g->gtab) + ", " + u32(g->gn) + ", " + u32(g->gri[0]) + ", " +
                u32(g->gsri) + ", " + u32(g->gspn) + ");\n";
-      return "  if ((rs" + s + " & 0xFFu) != ST_STORED_) {\n" + store_st(q, g, st, "ek" + s) + "  }\n";
+      return "  if ((rs" + s + " & 0xFFu) != ST_STORED_" + (hist_lds ? std::string(" && (rs" + s + " & 0xFFu) != ST_NOMATCH") : "") +
+             ") {\n" + store_st(q, g, st, "ek" + s) + "  }\n";
     };
     // match / route of rule q (rs = its first pc, or FIN | status); of a group: every member's,
     // the matched ones alive (al), the others stored
@@ -1479,7 +1483,7 @@ struct Gen {
         for (uint32_t j = 0; j < g.gn; j++) {
           const uint32_t ri = g.gri[j];
           const RuleRec& rr = ps.rules[ri];
-          const std::string rw = "(uint8_t*)s_stw + " + u32(g.grow + j * 256u);
+          const std::string rw = "(uint8_t*)s_stw + " + u32(g.grow + j * 256u) + ", s_rc + " + u32((g.grow / 256u + j) * 4u);
           auto st = [&](const std::string& x) {
             return "{ const EState e_{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u}; kv_final(O, " + u32(ri) +
                    ", n_res, r, valid, " + x + ", e_, " + rw + "); }";
@@ -1489,7 +1493,10 @@ struct Gen {
           if (rr.flags & RR_META_EXPAND) k << "    else if (rflags & " << u32(meta_bad_flags(rr.flags)) << ") " << st("ST_CPU") << "\n";
           if (rr.dyn)
             k << "    else if (B.dyn_st[(size_t)" << (rr.dyn - 1) << "u * n_res + r]) " << st("B.dyn_st[(size_t)" + std::to_string(rr.dyn - 1) + "u * n_res + r]") << "\n";
-          k << "    else al" << g.s << " |= " << u32(1u << j) << ";\n  } else " << st("ST_NOMATCH") << "\n";
+          // (hist_lds: the row was prefilled with NOMATCH)
+          k << "    else al" << g.s << " |= " << u32(1u << j) << ";\n  }";
+          if (hist_lds) k << "\n";
+          else k << " else " << st("ST_NOMATCH") << "\n";
         }
         k << "  rs" << g.s << " = al" << g.s << " ? " << u32(g.b) << " : FIN_ | ST_STORED_;\n";
         return k.str();
@@ -1757,6 +1764,8 @@ struct Gen {
     uint32_t nr_all = 0;
     for (const JitChunk* c : chs) nr_all += (uint32_t)c->rules.size();
     hist_lds = nr_all * 256u <= 48u * 1024u;  // <= 48 KB of status bytes
+    if (!hist_lds)  // (record slots and the NOMATCH prefill live beside the LDS status rows)
+      throw std::runtime_error("kvjit: at most 192 rules per kernel (KVGPU_JIT_CHUNK)");
     block_decls.clear();
     mt_kbase = (uint32_t)(mt_bits.size() / 32u);
     for (const JitChunk* c : chs) {
@@ -1781,7 +1790,8 @@ struct Gen {
       << "(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp, const Node* __restrict__ N, "
          "const Val* __restrict__ V, const uint8_t* __restrict__ S, DevOut O, uint32_t r0) {\n"
       << "  constexpr uint32_t FIN_ = " << u32(FIN) << ", ACT_ = " << u32(ACT) << ", ST_STORED_ = 0x7Eu;\n"
-      << (hist_lds ? "  __shared__ uint32_t s_stw[" + std::to_string(nr * 256u / 4) + "];\n"
+      << (hist_lds ? "  __shared__ uint32_t s_stw[" + std::to_string(nr * 256u / 4) + "], s_rc[" + std::to_string(nr * 4u) +
+                         "];\n"
                    : "  __shared__ uint32_t s_hist[" + std::to_string(nr) + "][KV_HIST];\n")
       << "  const DevPS& P = *Pp;\n  const DevBatch& B = *Bp;\n  const uint8_t* __restrict__ pstr = P.pstr;\n";
     if (!hist_lds)
@@ -1800,7 +1810,9 @@ struct Gen {
       << "  uint32_t root = ABSENT, rkind = KEY_NONE, rflags = 0u, rtup = 0u;\n"
       << "  if (valid) { root = ni(R->root); rkind = R->kind; rflags = R->flags; rtup = R->tup; }\n"
       << "  Node rootn{0u, 0u, 0u, 0u};\n  if (valid) rootn = N[root];\n"
-      << "  const uint32_t* __restrict__ mtr_ = P.mtup + (size_t)rtup * P.mtup_words;\n";
+      << "  const uint32_t* __restrict__ mtr_ = P.mtup + rtup;\n  const uint32_t ntup_ = B.n_tup;\n";
+    if (hist_lds)  // every status row starts as NOMATCH (0xFF past the batch): only matched lanes store
+      o << "  kv_prefill_rows(s_stw, s_rc, " << nr << "u, r - threadIdx.x, n_res);\n";
     for (size_t bi = 0; bi < blocks.size(); bi++) {
       // the block's match words (bits of its rules, kvj_mtup); a wave none of whose resources
       // matches any rule of the block skips it whole (every rule NOMATCH on every lane)
@@ -1811,14 +1823,12 @@ struct Gen {
       for (uint32_t w = p0 / 32u; w * 32u < p1; w++) {
         const uint32_t lo = std::max(p0, w * 32u) - w * 32u, hi = std::min(p1, w * 32u + 32u) - w * 32u;
         const uint32_t m = hi - lo == 32u ? 0xFFFFFFFFu : ((1u << (hi - lo)) - 1u) << lo;
-        o << "  const uint32_t mw" << w << " = valid ? mtr_[" << w << "] : 0u;\n";
+        o << "  const uint32_t mw" << w << " = valid ? mtr_[(size_t)" << w << "u * ntup_] : 0u;\n";
         any += " | (mw" + std::to_string(w) + " & " + u32(m) + ")";
       }
       if (hist_lds) {
-        o << "  if (__ballot((" << any << ") != 0u) == 0ull) {\n"
-          << "    for (uint32_t q_ = " << r0 << "u; q_ < " << r0 + rn << "u; q_++) ((uint8_t*)s_stw)[q_ * KV_WG + threadIdx.x] = "
-          << "valid ? (uint8_t)ST_NOMATCH : (uint8_t)0xFFu;\n"
-          << "  } else {\n" << blocks[bi] << "  }\n";
+        // (the rows of a skipped block keep their NOMATCH prefill)
+        o << "  if (__ballot((" << any << ") != 0u) != 0ull) {\n" << blocks[bi] << "  }\n";
       } else {
         o << blocks[bi];
       }
@@ -1875,7 +1885,7 @@ struct Gen {
       }
       o << "      break;\n";
     }
-    o << "  }\n  out[(size_t)t * " << W << "u + blockIdx.y] = m;\n}\n\n";
+    o << "  }\n  out[(size_t)blockIdx.y * B.n_tup + t] = m;\n}\n\n";
   }
 
   // Register weight of rule ri in a fused block: the state it keeps across the block (status
