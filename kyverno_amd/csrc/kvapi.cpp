@@ -415,7 +415,7 @@ struct kv_result {
   static ErrRec decode(const ErrRec8& c) {
     ErrRec e{};
     e.kind_flags = (c.w0 & 15u) | (((c.w0 >> 4) & 3u) << 16);
-    e.pnode = c.w0 >> 13;
+    e.pnode = c.w0 >> 7;
     e.keynode = ABSENT;
     e.resnode = ABSENT;
     e.idx[0] = c.w1 & 4095u;
@@ -1005,7 +1005,7 @@ struct DevSession {
       }
       HIPCHK(launch_rec_compact(O.status, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                 (unsigned long long*)r_tot.p, (unsigned long long*)r_base.p, nullptr, nullptr, nullptr,
-                                0, false, stream));
+                                0, stream));
       part->base.resize(nrules + 1);
       part->offs.resize((size_t)nrules * tiles);
       HIPCHK(hipMemcpyAsync(part->base.data(), r_base.p, part->base.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
@@ -1017,10 +1017,9 @@ struct DevSession {
       const uint64_t total = part->base[nrules];
       if (r_out8.n < total * sizeof(ErrRec8)) r_out8.alloc(std::max<uint64_t>(total, 1) * sizeof(ErrRec8), device);
       HIPCHK(hipMemsetAsync(r_wide.p, 0, sizeof(uint32_t), stream));
-      // the passes' records: slotted when the specialized kernels wrote them
       HIPCHK(launch_rec_compact(O.status, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                 nullptr, (unsigned long long*)r_base.p, (ErrRec8*)r_out8.p, nullptr,
-                                (uint32_t*)r_wide.p, 1, dps->specialized(), stream));
+                                (uint32_t*)r_wide.p, 1, stream));
       part->rec.alloc(total);
       if (total)
         HIPCHK(hipMemcpyAsync(part->rec.data(), r_out8.p, total * sizeof(ErrRec8), hipMemcpyDeviceToHost, stream));
@@ -1037,7 +1036,7 @@ struct DevSession {
         if (r_outw.n < total * sizeof(ErrRec)) r_outw.alloc(std::max<uint64_t>(total, 1) * sizeof(ErrRec), device);
         HIPCHK(launch_rec_compact(O.status, O.err8, O.err, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                   nullptr, (unsigned long long*)r_base.p, (ErrRec8*)r_out8.p, (ErrRec*)r_outw.p,
-                                  (uint32_t*)r_wide.p, 1, false, stream));  // the re-run is the bytecode engine
+                                  (uint32_t*)r_wide.p, 1, stream));
         part->recw.alloc(total);
         HIPCHK(hipMemcpyAsync(part->recw.data(), r_outw.p, total * sizeof(ErrRec), hipMemcpyDeviceToHost, stream));
       }

@@ -654,12 +654,9 @@ struct EState {
 // full 32 B form instead; the flag is uniform, so this is a scalar branch.
 // Record of rule ri on resource r: the rule's row base is uniform and r the only per-lane
 // part of the address (a scalar base + 32-bit vector offset store).
-// `pos`: the record's slot in the rule's row (the resource index for the bytecode engine; for
-// the specialized kernels the next free slot of the resource's wave, the lane kept in the
-// record: every wave's records are contiguous from its first slot, kv_final)
-__device__ __forceinline__ void store_err(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, uint32_t pos,
-                                          uint32_t kind, uint32_t flags, uint32_t pn, uint32_t key, uint32_t res,
-                                          uint32_t i0, uint32_t i1, uint32_t i2, uint32_t i3) {
+__device__ __forceinline__ void store_err(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, uint32_t kind,
+                                          uint32_t flags, uint32_t pn, uint32_t key, uint32_t res, uint32_t i0,
+                                          uint32_t i1, uint32_t i2, uint32_t i3) {
 #if defined(KV_JIT_PRELUDE) && !defined(KVEMU)
   // specialized kernels write compact records only: the host re-runs a pass that needs full
   // records on the bytecode engine (kvapi.cpp DevSession::fetch), which keeps the code of
@@ -673,11 +670,11 @@ __device__ __forceinline__ void store_err(const DevOut& O, uint32_t ri, uint32_t
     return;
   }
 #endif
-  const uint32_t fits = (i0 < 4096u) & (i1 < 1024u) & (i2 < 1024u) & (i3 == 0u) & (key == ABSENT) & (pn < (1u << 19));
+  const uint32_t fits = (i0 < 4096u) & (i1 < 1024u) & (i2 < 1024u) & (i3 == 0u) & (key == ABSENT) & (pn < (1u << 25));
   uint2 w;
-  w.x = kind | (flags << 4) | ((fits ^ 1u) << 6) | ((r & 63u) << 7) | (pn << 13);
+  w.x = kind | (flags << 4) | ((fits ^ 1u) << 6) | (pn << 7);
   w.y = i0 | (i1 << 12) | (i2 << 22);
-  ((uint2*)(O.err8 + (size_t)ri * n_res))[pos] = w;
+  ((uint2*)(O.err8 + (size_t)ri * n_res))[r] = w;
 }
 
 // number of bytes of w equal to the byte replicated in b4 (exact SWAR zero-byte count)
@@ -716,12 +713,8 @@ __device__ __forceinline__ uint32_t kv_leaf_word(const DevPS& P, const Node* __r
 // so the compiler cannot hoist one address per rule out of the element loops (a wide fused
 // block finalizes dozens of rules inside one loop; hoisted, their addresses alone took 2-4
 // VGPRs or an SGPR pair per rule).
-// The record goes to the next free slot of the rule's wave segment ([r & ~63, +64) of its row;
-// `s_rc` = the rule's four per-wave slot counters in LDS), so the records of a wave are written
-// contiguously instead of scattered over its 512 B (a partial line per record); the
-// fetch-time compaction (kv_rec_scatter) puts them back in resource order by their lane.
 __device__ __forceinline__ void kv_final(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, bool valid,
-                                         uint32_t st, const EState& e, uint8_t* s_row, uint32_t* s_rc) {
+                                         uint32_t st, const EState& e, uint8_t* s_row) {
   if (valid && (O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP)) {
     uint32_t z = 0u;  // an opaque zero: the site's constant record words are built here, not
                       // hoisted out of the loops as one constant register tuple per site
@@ -729,9 +722,7 @@ __device__ __forceinline__ void kv_final(const DevOut& O, uint32_t ri, uint32_t 
     asm volatile("" : "+v"(r), "+v"(z));
     asm volatile("" : "+s"(ri));
 #endif
-    const uint32_t slot = atomicAdd(&s_rc[threadIdx.x >> 6], 1u);
-    store_err(O, ri, n_res, r, (r & ~63u) + slot, e.kind + z, e.flags, e.pn + z, e.key + z, e.res + z, e.i0, e.i1,
-              e.i2, e.i3);
+    store_err(O, ri, n_res, r, e.kind + z, e.flags, e.pn + z, e.key + z, e.res + z, e.i0, e.i1, e.i2, e.i3);
   }
   s_row[threadIdx.x] = valid ? (uint8_t)st : (uint8_t)0xFFu;
 }
@@ -743,32 +734,27 @@ __device__ __forceinline__ void kv_final(const DevOut& O, uint32_t ri, uint32_t 
 // group's representative (kind | flags << 4 | node << 8; 0: none)
 __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_t r, bool valid, uint32_t m, uint32_t st,
                                         uint32_t ekx, uint32_t i0, uint32_t i1, uint32_t i2, uint32_t i3,
-                                        uint8_t* s_row0, uint32_t* s_rc0, const uint32_t* tab, uint32_t n, uint32_t ri0,
+                                        uint8_t* s_row0, const uint32_t* tab, uint32_t n, uint32_t ri0,
                                         uint32_t sri, uint32_t spn) {
   for (uint32_t j = 0; j < n; j++) {  // uniform over the members (scalar rule ids and rows)
     if (!((m >> j) & 1u)) continue;
     const uint32_t ri = tab ? tab[j] : ri0 + j * sri;
     const uint32_t ek = ekx ? ekx + ((tab ? tab[n + j] : j * spn) << 8) : 0u;
     const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
-    kv_final(O, ri, n_res, r, valid, st, e, s_row0 + j * (uint32_t)KV_WG, s_rc0 + j * 4u);
+    kv_final(O, ri, n_res, r, valid, st, e, s_row0 + j * (uint32_t)KV_WG);
   }
 }
 
 // the workgroup's LDS status rows (nr rules x KV_WG lanes, one byte each) set to NOMATCH for
 // the lanes holding a resource (0xFF past the batch), with 32-bit stores spread over the
 // workgroup; the rule code then stores only the statuses of matched lanes
-__device__ __forceinline__ void kv_prefill_rows(uint32_t* s_stw, uint32_t* s_rc, uint32_t nr, uint32_t base,
-                                                uint32_t n_res) {
+__device__ __forceinline__ void kv_prefill_rows(uint32_t* s_stw, uint32_t nr, uint32_t base, uint32_t n_res) {
   const uint32_t nv = n_res > base ? n_res - base : 0u;
 #ifdef KVEMU
-  // host emulation runs the lanes one after another: each lane fills its own bytes (and the
-  // first lane of the workgroup clears the record slot counters)
+  // host emulation runs the lanes one after another: each lane fills its own bytes
   for (uint32_t q = 0; q < nr; q++)
     ((uint8_t*)s_stw)[q * (uint32_t)KV_WG + threadIdx.x] = threadIdx.x < nv ? (uint8_t)ST_NOMATCH : (uint8_t)0xFFu;
-  if (threadIdx.x == 0)
-    for (uint32_t i = 0; i < nr * 4u; i++) s_rc[i] = 0u;
 #else
-  for (uint32_t i = threadIdx.x; i < nr * 4u; i += (uint32_t)KV_WG) s_rc[i] = 0u;
   for (uint32_t i = threadIdx.x; i < nr * ((uint32_t)KV_WG / 4u); i += (uint32_t)KV_WG) {
     const uint32_t l = (i % ((uint32_t)KV_WG / 4u)) * 4u;
     uint32_t w = 0u;
@@ -811,7 +797,7 @@ __device__ __forceinline__ void store_result2(const DevOut& O, uint32_t ri, uint
     const size_t o = (size_t)ri * n_res + r;
     O.status[o] = (uint8_t)st;
     if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP))
-      store_err(O, ri, n_res, r, r, e.kind, e.flags, e.pn, e.key, e.res, e.i0, e.i1, e.i2, e.i3);
+      store_err(O, ri, n_res, r, e.kind, e.flags, e.pn, e.key, e.res, e.i0, e.i1, e.i2, e.i3);
   }
   const uint64_t m_pass = __ballot(valid && st == ST_PASS), m_fail = __ballot(valid && st == ST_FAIL);
   const uint64_t m_nm = __ballot(valid && st == ST_NOMATCH);
@@ -838,7 +824,7 @@ __device__ __forceinline__ void store_result(const DevOut& O, uint32_t ri, uint3
     const size_t o = (size_t)ri * n_res + r;
     O.status[o] = (uint8_t)st;
     if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP))
-      store_err(O, ri, n_res, r, r, e.kind, e.flags, e.pn, e.key, e.res, e.i0, e.i1, e.i2, e.i3);
+      store_err(O, ri, n_res, r, e.kind, e.flags, e.pn, e.key, e.res, e.i0, e.i1, e.i2, e.i3);
   }
   for (uint32_t s = 0; s < 7; s++) {
     const uint64_t bm = __ballot(valid && st == s);

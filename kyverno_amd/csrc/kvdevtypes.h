@@ -14,8 +14,7 @@ struct ErrRec {
 };
 
 // Compact error record (8 B per FAIL / ERROR / SKIP pair, the one written per pass):
-//   w0 = kind | flags << 4 | wide << 6 | lane << 7 | pnode << 13   (pnode < 2^19; lane: the
-//        resource's lane in its wave, which places a slotted record, kv_final)
+//   w0 = kind | flags << 4 | wide << 6 | pnode << 7          (pnode < 2^25)
 //   w1 = idx0 | idx1 << 12 | idx2 << 22    (idx0 < 4096, idx1 / idx2 < 1024, idx3 == 0)
 // A record that does not fit (larger loop indices, a fourth loop level, a resolved
 // wildcard key) sets `wide`; the host then re-runs the pass with full records

@@ -928,8 +928,7 @@ struct Gen {
       std::ostringstream r;
       r << "kv_gfin(O, n_res, r, valid, " << m << ", " << st << ", " << u32(kind | (pcn.flags << 4) | (pn << 8));
       for (uint32_t lv = 0; lv < 4; lv++) r << ", " << (lv <= g.max_level ? li(lv) : std::string("0u"));
-      r << ", (uint8_t*)s_stw + " << u32(g.grow) << ", s_rc + " << u32(g.grow / 256u * 4u) << ", "
-        << (g.gtab.empty() ? std::string("nullptr") : g.gtab) << ", "
+      r << ", (uint8_t*)s_stw + " << u32(g.grow) << ", " << (g.gtab.empty() ? std::string("nullptr") : g.gtab) << ", "
         << u32(g.gn) << ", " << u32(g.gri[0]) << ", " << u32(g.gsri) << ", " << u32(g.gspn) << ");";
       return r.str();
     };
@@ -1448,8 +1447,7 @@ struct Gen {
       std::ostringstream k;
       k << "  { " << estate(g, ekx) << "\n";
       if (hist_lds)
-        k << "    kv_final(O, " << ri << "u, n_res, r, valid, " << st << ", e_, " << row(q) << ", s_rc + "
-          << u32((hbase + q) * 4u) << "); }\n";
+        k << "    kv_final(O, " << ri << "u, n_res, r, valid, " << st << ", e_, " << row(q) << "); }\n";
       else
         k << "    store_result2(O, " << ri << "u, n_res, r, valid, " << st << ", e_, &s_hist[" << (hbase + q)
           << "][0]); }\n";
@@ -1464,8 +1462,7 @@ struct Gen {
       if (!g) return store_st(q, g, st, "0u");
       if (g->grp)  // the members alive here end with the group's status (no error record)
         return "  if ((rs" + s + " & 0xFFu) != ST_STORED_)\n    kv_gfin(O, n_res, r, valid, al" + s + ", rs" + s +
-               " & 0xFFu, 0u, 0u, 0u, 0u, 0u, (uint8_t*)s_stw + " + u32(g->grow) + ", s_rc + " + u32(g->grow / 256u * 4u) +
-               ", " +
+               " & 0xFFu, 0u, 0u, 0u, 0u, 0u, (uint8_t*)s_stw + " + u32(g->grow) + ", " +
                (g->gtab.empty() ? std::string("nullptr") : g->gtab) + ", " + u32(g->gn) + ", " + u32(g->gri[0]) + ", " +
                u32(g->gsri) + ", " + u32(g->gspn) + ");\n";
       return "  if ((rs" + s + " & 0xFFu) != ST_STORED_" + (hist_lds ? std::string(" && (rs" + s + " & 0xFFu) != ST_NOMATCH") : "") +
@@ -1483,7 +1480,7 @@ struct Gen {
         for (uint32_t j = 0; j < g.gn; j++) {
           const uint32_t ri = g.gri[j];
           const RuleRec& rr = ps.rules[ri];
-          const std::string rw = "(uint8_t*)s_stw + " + u32(g.grow + j * 256u) + ", s_rc + " + u32((g.grow / 256u + j) * 4u);
+          const std::string rw = "(uint8_t*)s_stw + " + u32(g.grow + j * 256u);
           auto st = [&](const std::string& x) {
             return "{ const EState e_{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u}; kv_final(O, " + u32(ri) +
                    ", n_res, r, valid, " + x + ", e_, " + rw + "); }";
@@ -1764,7 +1761,7 @@ struct Gen {
     uint32_t nr_all = 0;
     for (const JitChunk* c : chs) nr_all += (uint32_t)c->rules.size();
     hist_lds = nr_all * 256u <= 48u * 1024u;  // <= 48 KB of status bytes
-    if (!hist_lds)  // (record slots and the NOMATCH prefill live beside the LDS status rows)
+    if (!hist_lds)  // (the NOMATCH prefill and the histogram use the LDS status rows)
       throw std::runtime_error("kvjit: at most 192 rules per kernel (KVGPU_JIT_CHUNK)");
     block_decls.clear();
     mt_kbase = (uint32_t)(mt_bits.size() / 32u);
@@ -1790,8 +1787,7 @@ struct Gen {
       << "(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp, const Node* __restrict__ N, "
          "const Val* __restrict__ V, const uint8_t* __restrict__ S, DevOut O, uint32_t r0) {\n"
       << "  constexpr uint32_t FIN_ = " << u32(FIN) << ", ACT_ = " << u32(ACT) << ", ST_STORED_ = 0x7Eu;\n"
-      << (hist_lds ? "  __shared__ uint32_t s_stw[" + std::to_string(nr * 256u / 4) + "], s_rc[" + std::to_string(nr * 4u) +
-                         "];\n"
+      << (hist_lds ? "  __shared__ uint32_t s_stw[" + std::to_string(nr * 256u / 4) + "];\n"
                    : "  __shared__ uint32_t s_hist[" + std::to_string(nr) + "][KV_HIST];\n")
       << "  const DevPS& P = *Pp;\n  const DevBatch& B = *Bp;\n  const uint8_t* __restrict__ pstr = P.pstr;\n";
     if (!hist_lds)
@@ -1812,7 +1808,7 @@ struct Gen {
       << "  Node rootn{0u, 0u, 0u, 0u};\n  if (valid) rootn = N[root];\n"
       << "  const uint32_t* __restrict__ mtr_ = P.mtup + rtup;\n  const uint32_t ntup_ = B.n_tup;\n";
     if (hist_lds)  // every status row starts as NOMATCH (0xFF past the batch): only matched lanes store
-      o << "  kv_prefill_rows(s_stw, s_rc, " << nr << "u, r - threadIdx.x, n_res);\n";
+      o << "  kv_prefill_rows(s_stw, " << nr << "u, r - threadIdx.x, n_res);\n";
     for (size_t bi = 0; bi < blocks.size(); bi++) {
       // the block's match words (bits of its rules, kvj_mtup); a wave none of whose resources
       // matches any rule of the block skips it whole (every rule NOMATCH on every lane)

@@ -310,7 +310,7 @@ extern "C" __global__ __launch_bounds__(KV_WG) __attribute__((amdgpu_waves_per_e
         const size_t o = (size_t)ri * n_res + r;
         O.status[o] = (uint8_t)st;
         if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP))
-          store_err(O, ri, n_res, r, r, ekind, eflags, epn, ekey, eres, eidx0, eidx1, eidx2, eidx3);
+          store_err(O, ri, n_res, r, ekind, eflags, epn, ekey, eres, eidx0, eidx1, eidx2, eidx3);
       }
       // histogram: one LDS atomic per (wave, status) via ballot popcount
       for (uint32_t s = 0; s < 7; s++) {
@@ -461,7 +461,7 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_scatter_kernel(const uint8_t* __
                                                                 uint32_t tiles, const uint32_t* __restrict__ offs,
                                                                 const unsigned long long* __restrict__ base,
                                                                 ErrRec8* __restrict__ out8, ErrRec* __restrict__ outw,
-                                                                uint32_t* __restrict__ wide, uint32_t slotted) {
+                                                                uint32_t* __restrict__ wide) {
   __shared__ uint32_t s_w[KV_WG / 64];
   const uint32_t rule = blockIdx.y, r = blockIdx.x * KV_WG + threadIdx.x, lane = threadIdx.x & 63;
   const size_t o = (size_t)rule * n_res + r;
@@ -469,21 +469,10 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_scatter_kernel(const uint8_t* __
   const uint64_t m = __ballot(f);
   if (lane == 0) s_w[threadIdx.x >> 6] = (uint32_t)__popcll(m);
   __syncthreads();
-  uint32_t prior = 0;
-  for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) prior += s_w[w];
-  const unsigned long long at = base[rule] + offs[(size_t)rule * tiles + blockIdx.x] + prior;
-  if (slotted) {
-    // specialized kernels: the wave's records fill its first slots, each holding its lane
-    // (kv_final); this thread moves slot `lane` to its resource-order rank
-    if (lane >= (uint32_t)__popcll(m)) return;
-    const ErrRec8 e = err8[o];
-    const uint32_t l = (e.w0 >> 7) & 63u;
-    out8[at + (uint32_t)__popcll(m & ((1ull << l) - 1ull))] = e;
-    if (e.w0 & ERR8_WIDE) atomicOr(wide, 1u);
-    return;
-  }
   if (!f) return;
-  const unsigned long long idx = at + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+  uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+  for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) rank += s_w[w];
+  const unsigned long long idx = base[rule] + offs[(size_t)rule * tiles + blockIdx.x] + rank;
   const ErrRec8 e = err8[o];
   out8[idx] = e;
   if (outw) outw[idx] = errw[o];
@@ -492,7 +481,7 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_scatter_kernel(const uint8_t* __
 
 hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const ErrRec* errw, uint32_t n_res,
                               uint32_t n_rules, uint32_t* offs, unsigned long long* totals, unsigned long long* base,
-                              ErrRec8* out8, ErrRec* outw, uint32_t* wide, int phase, bool slotted, hipStream_t stream) {
+                              ErrRec8* out8, ErrRec* outw, uint32_t* wide, int phase, hipStream_t stream) {
   if (n_res == 0 || n_rules == 0) return hipSuccess;
   const uint32_t tiles = (n_res + KV_WG - 1) / KV_WG;
   if (phase == 0) {  // offsets and bases
@@ -501,7 +490,7 @@ hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const 
     hipLaunchKernelGGL(kv_rec_base_kernel, dim3(1), dim3(KV_WG), 0, stream, totals, n_rules, base);
   } else {
     hipLaunchKernelGGL(kv_rec_scatter_kernel, dim3(tiles, n_rules), dim3(KV_WG), 0, stream, status, err8, errw, n_res,
-                       tiles, offs, base, out8, outw, wide, slotted ? 1u : 0u);
+                       tiles, offs, base, out8, outw, wide);
   }
   return hipGetLastError();
 }

@@ -242,24 +242,6 @@ int main(int argc, char** argv) {
       for (chunk_fn f : fns) grid(blocks, 1, [&]() { f(&P, &B, B.nodes, B.vals, B.bstr, O, 0u); });
     };
     if (nres) pass();
-    // the kernels write each wave's records into its first slots with the lane in the record
-    // (kv_final): put them at their resources' positions (as kv_rec_scatter does at fetch)
-    {
-      std::vector<ErrRec8> d8(err8.size(), ErrRec8{0u, 0u});
-      auto has = [](uint8_t s) { return s == ST_FAIL || s == ST_ERROR || s == ST_SKIP; };
-      for (uint64_t rl = 0; rl < nr; rl++)
-        for (uint64_t w0 = 0; w0 < nres; w0 += 64) {
-          uint32_t k = 0;
-          for (uint64_t q = w0; q < std::min<uint64_t>(nres, w0 + 64); q++) k += has(status[rl * nres + q]);
-          for (uint32_t s = 0; s < k; s++) {
-            const ErrRec8 c = err8[rl * nres + w0 + s];
-            const uint64_t at = w0 + ((c.w0 >> 7) & 63u);
-            if (at >= nres || !has(status[rl * nres + at])) throw std::runtime_error("kvemu: record slot holds a lane without a record");
-            d8[rl * nres + at] = c;
-          }
-        }
-      err8.swap(d8);
-    }
     bool wide = false;
     for (size_t o = 0; o < status.size() && !wide; o++) {
       const uint8_t s = status[o];
@@ -279,7 +261,7 @@ int main(int argc, char** argv) {
       const ErrRec8 c = err8[o];
       ErrRec e{};
       e.kind_flags = (c.w0 & 15u) | (((c.w0 >> 4) & 3u) << 16);
-      e.pnode = c.w0 >> 13;
+      e.pnode = c.w0 >> 7;
       e.keynode = ABSENT;
       e.resnode = ABSENT;
       e.idx[0] = c.w1 & 4095u;
