@@ -92,7 +92,16 @@ struct Ingest {
     return h ? h : 1;
   }
   Probe str_off;  // string heap offsets (id = offset, aux = length; confirmed against the heap)
-  Probe val_id;   // scalars (id = value index; type and bytes checked against the Val)
+  // scalars: a slot carries what a node needs (id, e_off, e_len | NC_* flags, position
+  // classes so far) and the value's first 8 bytes, so a hit is confirmed and answered from
+  // the slot alone (strings longer than 8 bytes compare their tail in the heap)
+  struct VSlot {
+    uint64_t h;     // 0 = empty
+    uint64_t key8;  // INT / FLOAT bits, BOOL, or a string's first 8 bytes (zero padded)
+    uint32_t id, e_off, c, cls, type;
+  };
+  std::vector<VSlot> vtab;
+  size_t vn = 0;
   Probe dict;     // the policy set's key dictionary (id = static key id)
   Probe dyn_key;  // batch-local key ids (id = index into b.dyn_keys)
   Probe ns_probe, nsm_probe, lset_probe, aset_probe;  // namespaces, match inputs (confirmed by key)
@@ -103,7 +112,7 @@ struct Ingest {
   Ingest(const PolicySet& p, Batch& bb) : ps(p), b(bb), nstatic((uint32_t)p.keys.size()), slot_ids(p.trie.nodes.size()),
                                           slot_tab(p.trie.nodes.size()) {
     str_off.init(1 << 14);
-    val_id.init(1 << 14);
+    vtab.assign(1 << 15, VSlot{});
     dict.init(p.keys.size());
     for (uint32_t i = 0; i < (uint32_t)p.keys.size(); i++) dict.insert(hash_bytes(p.keys[i].data(), p.keys[i].size(), 'K'), i);
     dyn_key.init(64);
@@ -160,26 +169,8 @@ struct Ingest {
     return id;
   }
 
-  uint32_t val(const JDoc& d, const JNode& n) {
-    uint64_t hv;
-    std::string_view sv;
-    switch (n.t) {
-      case J_BOOL: hv = hash_bytes(n.b ? "1" : "0", 1, 'b'); break;
-      case J_INT: hv = hash_bytes(&n.i, 8, 'i'); break;
-      case J_FLOAT: hv = hash_bytes(&n.f, 8, 'f'); break;
-      default: sv = d.sval(n); hv = hash_bytes(sv.data(), sv.size(), 's'); break;
-    }
-    const int64_t hit = val_id.find(hv, [&](const Probe::Slot& x) {
-      const Val& v = b.vals[x.id];
-      switch (n.t) {
-        case J_BOOL: return v.type == NT_BOOL && ((v.flags & VF_BOOLV) != 0) == n.b;
-        case J_INT: return v.type == NT_INT && v.i == n.i;
-        case J_FLOAT: return v.type == NT_FLOAT && memcmp(&v.f, &n.f, 8) == 0;
-        default:
-          return v.type == NT_STR && v.e_len == sv.size() && memcmp(b.strs.data() + v.e_off, sv.data(), sv.size()) == 0;
-      }
-    });
-    if (hit >= 0) return (uint32_t)hit;
+  // new Val for scalar n (sv: its bytes when a string)
+  uint32_t val_new(const JNode& n, std::string_view sv) {
     Val v{};
     // e: the validateString form; num: the number-with-string form (same bytes except for
     // floats, where they are FormatFloat 'E' and %f)
@@ -242,8 +233,19 @@ struct Ingest {
     }
     uint32_t id = (uint32_t)b.vals.size();
     b.vals.push_back(v);
-    val_id.insert(hv, id);
     return id;
+  }
+
+  void vgrow() {
+    std::vector<VSlot> o(vtab.size() * 2, VSlot{});
+    o.swap(vtab);
+    const size_t m = vtab.size() - 1;
+    for (const VSlot& x : o)
+      if (x.h) {
+        size_t i = x.h & m;
+        while (vtab[i].h) i = (i + 1) & m;
+        vtab[i] = x;
+      }
   }
 
   // ---------------------------------------------------------------- wave-group layout
@@ -356,15 +358,45 @@ struct Ingest {
   }
 
   Node scalar(const JDoc& d, const JNode& n, uint32_t type, uint32_t key, int32_t pos) {
-    const uint32_t vid = val(d, n);
-    b.vals[vid].cls |= kv_tcls(pos);
-    const Val& v = b.vals[vid];
-    Node out{(key & KEY_NONE28) << 4 | type, vid, v.e_off, v.e_len};
+    uint64_t k8 = 0, hv;
+    std::string_view sv;
+    switch (n.t) {
+      case J_BOOL: k8 = n.b ? 1 : 0; hv = hash_bytes(&k8, 8, 'b'); break;
+      case J_INT: memcpy(&k8, &n.i, 8); hv = hash_bytes(&k8, 8, 'i'); break;
+      case J_FLOAT: memcpy(&k8, &n.f, 8); hv = hash_bytes(&k8, 8, 'f'); break;
+      default:
+        sv = d.sval(n);
+        memcpy(&k8, sv.data(), std::min<size_t>(8, sv.size()));
+        hv = hash_bytes(sv.data(), sv.size(), 's');
+        break;
+    }
+    const uint32_t bit = kv_tcls(pos);
+    const size_t m = vtab.size() - 1;
+    size_t i = hv & m;
+    for (;; i = (i + 1) & m) {
+      VSlot& x = vtab[i];
+      if (x.h == 0) break;
+      if (x.h != hv || x.key8 != k8 || x.type != type) continue;
+      if (type == NT_STR && ((x.c & NC_LEN_MASK) != sv.size() ||
+                             (sv.size() > 8 && memcmp(b.strs.data() + x.e_off + 8, sv.data() + 8, sv.size() - 8) != 0)))
+        continue;
+      if (!(x.cls & bit)) {
+        x.cls |= bit;
+        b.vals[x.id].cls |= bit;
+      }
+      return Node{(key & KEY_NONE28) << 4 | type, x.id, x.e_off, x.c};
+    }
+    const uint32_t vid = val_new(n, sv);
+    Val& v = b.vals[vid];
+    v.cls |= bit;
     if (v.e_len > NC_LEN_MASK) throw std::runtime_error("ingest: string value too long");
-    if (v.flags & VF_ASCII_E) out.c |= NC_ASCII_E;
-    if (v.flags & VF_BOOLV) out.c |= NC_BOOLV;
-    if (v.flags & VF_NILLIKE) out.c |= NC_NILLIKE;
-    return out;
+    uint32_t c = v.e_len;
+    if (v.flags & VF_ASCII_E) c |= NC_ASCII_E;
+    if (v.flags & VF_BOOLV) c |= NC_BOOLV;
+    if (v.flags & VF_NILLIKE) c |= NC_NILLIKE;
+    vtab[i] = VSlot{hv, k8, vid, v.e_off, c, v.cls, type};
+    if (++vn * 2 > vtab.size()) vgrow();
+    return Node{(key & KEY_NONE28) << 4 | type, vid, v.e_off, c};
   }
 
   uint64_t base_row = 0;  // first row of the current group
