@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <stdexcept>
 #include <thread>
 #include <unordered_map>
@@ -293,6 +294,15 @@ struct Ingest {
                              [&](const Probe::Slot& x) { return tn.slot_keys[x.id] == k; });
   }
 
+  // sorted-children buffers of the keep-all maps being walked, one per nesting depth (a
+  // deque: growing it keeps the outer frames' references valid)
+  std::deque<std::vector<uint32_t>> ch_pool;
+  size_t ch_depth = 0;
+  std::vector<uint32_t>& child_buf() {
+    if (ch_pool.size() <= ch_depth) ch_pool.emplace_back();
+    return ch_pool[ch_depth++];
+  }
+
   void sorted_children(const JDoc& d, const JNode& n, std::vector<uint32_t>* out) {
     out->clear();
     for (uint32_t c = n.first; c < n.first + n.count; c++) out->push_back(c);
@@ -320,9 +330,10 @@ struct Ingest {
           for (uint32_t i = s.nk; i < n.count; i++) s.kids[i].reset(-1);
           s.nk = n.count;
         }
-        std::vector<uint32_t> ch;
+        std::vector<uint32_t>& ch = child_buf();
         sorted_children(d, n, &ch);
         for (size_t i = 0; i < ch.size(); i++) unite(s.kids[i], d, ch[i], js);
+        ch_depth--;
       } else {
         for (uint32_t c = n.first; c < n.first + n.count; c++) {
           const int32_t si = slot_of(s.t, d.key(d.at(c)));
@@ -427,9 +438,10 @@ struct Ingest {
         out.a = (uint32_t)(base_row + s.map_row);
         if (tn.keep_all) {
           out.b = n.count;
-          std::vector<uint32_t> ch;
+          std::vector<uint32_t>& ch = child_buf();
           sorted_children(d, n, &ch);
           for (size_t i = 0; i < ch.size(); i++) put(s.kids[i], d, ch[i], lane, key_of(d.key(d.at(ch[i]))), -1);
+          ch_depth--;
         } else {
           const uint32_t K = (uint32_t)tn.slot_keys.size();
           out.b = K;
