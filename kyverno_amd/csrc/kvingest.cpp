@@ -933,6 +933,7 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
   b.pcells.resize(pcb[P]);
   b.rmask.resize(R);
   b.roff.resize(R);
+  b.strs.reserve(H + 16);  // + the word-reader pad appended after the merge (no 2nd copy)
   b.strs.assign(H, '\0');
   b.vals.resize(V);
   b.kvs.resize(K);
@@ -1040,39 +1041,91 @@ std::vector<uint32_t> kind_order(const std::vector<std::string_view>& kinds) {
   return order;
 }
 
+static void tuple_key(const Res& r, uint32_t* k) {
+  k[0] = r.kind; k[1] = r.group; k[2] = r.version; k[3] = r.nsm;
+  k[4] = r.lset; k[5] = r.aset; k[6] = r.ns_index; k[7] = r.flags;
+}
+
 void match_tuples(Batch* b) {
   // open addressing over 64-bit hashes of the match inputs, confirmed field by field against
-  // the tuple's first resource
-  auto key = [](const Res& r, uint32_t* k) {
-    k[0] = r.kind; k[1] = r.group; k[2] = r.version; k[3] = r.nsm;
-    k[4] = r.lset; k[5] = r.aset; k[6] = r.ns_index; k[7] = r.flags;
-  };
-  size_t cap = 1024;
-  while (cap < b->res.size() * 2) cap <<= 1;
-  std::vector<uint64_t> hs(cap, 0);
-  std::vector<uint32_t> ids(cap, 0);
-  b->tup_rep.clear();
-  for (size_t i = 0; i < b->res.size(); i++) {
-    uint32_t k[8], q[8];
-    key(b->res[i], k);
+  // the tuple's first resource; tables sized by the tuples found (grown at half load), so a
+  // few thousand tuples over a million resources stay cache-resident
+  auto key = tuple_key;
+  auto hash = [](const uint32_t* k) {
     uint64_t h = 1469598103934665603ull;
-    for (uint32_t x : k) h = (h ^ x) * 1099511628211ull, h ^= h >> 29;
-    h = h ? h : 1;
-    size_t at = h & (cap - 1);
-    for (;; at = (at + 1) & (cap - 1)) {
-      if (hs[at] == 0) {
-        hs[at] = h;
-        ids[at] = (uint32_t)b->tup_rep.size();
-        b->tup_rep.push_back((uint32_t)i);
-        break;
-      }
-      if (hs[at] == h) {
-        key(b->res[b->tup_rep[ids[at]]], q);
-        if (memcmp(k, q, sizeof k) == 0) break;
+    for (int j = 0; j < 8; j++) h = (h ^ k[j]) * 1099511628211ull, h ^= h >> 29;
+    return h ? h : 1;
+  };
+  struct Tab {
+    size_t cap = 4096;
+    std::vector<uint64_t> hs = std::vector<uint64_t>(4096, 0);
+    std::vector<uint32_t> ids = std::vector<uint32_t>(4096, 0);
+    std::vector<uint32_t> rep;  // first resource of each tuple, in first-occurrence order
+    void grow() {
+      std::vector<uint64_t> oh(cap * 2, 0);
+      std::vector<uint32_t> oi(cap * 2, 0);
+      oh.swap(hs);
+      oi.swap(ids);
+      cap *= 2;
+      for (size_t j = 0; j < oh.size(); j++)
+        if (oh[j]) {
+          size_t at = oh[j] & (cap - 1);
+          while (hs[at]) at = (at + 1) & (cap - 1);
+          hs[at] = oh[j];
+          ids[at] = oi[j];
+        }
+    }
+    // id of resource i's tuple (k, hash h), added when new
+    uint32_t id(const Batch* b, uint32_t i, const uint32_t* k, uint64_t h) {
+      size_t at = h & (cap - 1);
+      for (;; at = (at + 1) & (cap - 1)) {
+        if (hs[at] == 0) {
+          hs[at] = h;
+          ids[at] = (uint32_t)rep.size();
+          rep.push_back(i);
+          const uint32_t r = ids[at];
+          if (rep.size() * 2 > cap) grow();
+          return r;
+        }
+        if (hs[at] == h) {
+          uint32_t q[8];
+          tuple_key(b->res[rep[ids[at]]], q);
+          if (memcmp(k, q, 8 * sizeof(uint32_t)) == 0) return ids[at];
+        }
       }
     }
-    b->res[i].tup = ids[at];
-  }
+  };
+  // chunks numbered locally in parallel, then their tuple lists merged in chunk order (so
+  // ids stay in first-occurrence order over the whole batch) and the ids remapped
+  const size_t n = b->res.size();
+  const size_t C = std::max<size_t>(1, std::min<size_t>({(size_t)ingest_threads(), (size_t)16, n / 256}));
+  const size_t per = (n + C - 1) / std::max<size_t>(C, 1);
+  std::vector<Tab> tabs(C);
+  auto run = [&](auto&& f) {
+    std::vector<std::thread> th;
+    for (size_t c = 1; c < C; c++) th.emplace_back(f, c);
+    f((size_t)0);
+    for (auto& t : th) t.join();
+  };
+  run([&](size_t c) {
+    for (size_t i = c * per; i < std::min(n, (c + 1) * per); i++) {
+      uint32_t k[8];
+      key(b->res[i], k);
+      b->res[i].tup = tabs[c].id(b, (uint32_t)i, k, hash(k));
+    }
+  });
+  Tab g;
+  std::vector<std::vector<uint32_t>> remap(C);
+  for (size_t c = 0; c < C; c++)
+    for (uint32_t r : tabs[c].rep) {
+      uint32_t k[8];
+      key(b->res[r], k);
+      remap[c].push_back(g.id(b, r, k, hash(k)));
+    }
+  run([&](size_t c) {
+    for (size_t i = c * per; i < std::min(n, (c + 1) * per); i++) b->res[i].tup = remap[c][b->res[i].tup];
+  });
+  b->tup_rep = std::move(g.rep);
 }
 
 void ingest_resources(const PolicySet& ps, const char* json, size_t len, const char* ns_labels_json, Batch* b) {
@@ -1203,7 +1256,9 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
       if (selector_eval_host(ps.nsselectors[s], b->ns_labels[n]) == 1) b->ns_bits[n * b->ns_words + s / 32] |= 1u << (s % 32);
   // word-granular readers may touch up to 8 bytes past the last string
   b->strs.append(16, '\0');
+  if (verbose) fprintf(stderr, "[kvgpu] ingest: namespaces %.1f ms\n", ms());
   match_tuples(b);
+  if (verbose) fprintf(stderr, "[kvgpu] ingest: match tuples %.1f ms (%zu)\n", ms(), b->tup_rep.size());
   // interning keys are only needed while ingesting
   std::unordered_map<std::string, uint32_t>().swap(b->vout_id);
   std::vector<std::string>().swap(b->nsm_keys);
