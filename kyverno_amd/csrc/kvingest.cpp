@@ -989,7 +989,15 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
         r.ns_index = nmap[k][r.ns_index];
         b.res[resb[k] + i] = r;
       }
+      // the part's arrays are released here, in parallel (freed serially by the parts'
+      // destructors they cost ~70 ms per million Pods on the GPU box: page unmapping)
       StoreVec<Node>().swap(q.pcells);
+      decltype(q.vals)().swap(q.vals);
+      decltype(q.res)().swap(q.res);
+      decltype(q.rmask)().swap(q.rmask);
+      decltype(q.roff)().swap(q.roff);
+      decltype(q.kvs)().swap(q.kvs);
+      std::string().swap(q.strs);
     });
   for (auto& t : th) t.join();
 }
