@@ -141,6 +141,44 @@ def pmc_traffic(args) -> dict | None:
             "run_id": f"in-run PMC, pid {os.getpid()}, {time.strftime('%Y-%m-%dT%H:%M:%SZ', time.gmtime())}"}
 
 
+def ingest_parts(ps, args, kind_mix: int, mode: int):
+    """Parts session of --gpus N in one process: shard k (resources [k*N, (k+1)*N) of the stream)
+    synthesized and ingested by a worker thread (ctypes calls release the GIL; at most
+    KVGPU_BENCH_INFLIGHT shards in flight, default 2), attached to device k (device 0 for
+    --parts-per-gpu rehearsals) and dropped. Returns (session, per-shard info, t_start, t_end)."""
+    import concurrent.futures as cf
+
+    from kyverno_amd import batch, workloads
+
+    G = args.gpus
+    inflight = max(1, int(os.environ.get("KVGPU_BENCH_INFLIGHT", "2")))
+    sess = batch.Session.parts(ps, G, mode=mode)
+
+    def make(k):
+        data = batch.synth(workloads.SEED, args.n_res, kind_mix, first=k * args.n_res)
+        nb = len(data)
+        b = batch.Batch(ps, data)
+        return k, b, nb
+
+    info = [None] * G
+    t1 = time.time()
+    with cf.ThreadPoolExecutor(max_workers=inflight) as ex:
+        pending = set()
+        nxt = 0
+        while nxt < G or pending:
+            while nxt < G and len(pending) < inflight:
+                pending.add(ex.submit(make, nxt))
+                nxt += 1
+            done, pending = cf.wait(pending, return_when=cf.FIRST_COMPLETED)
+            for f in done:
+                k, b, nb = f.result()
+                sess.attach_part(k, b, 0 if args.parts_per_gpu > 1 else k)
+                info[k] = {"n_res": b.n_res, "store_bytes": b.store_bytes, "ndjson_bytes": nb}
+                b.close()  # the session holds the device copy
+    t2 = time.time()
+    return sess, info, t1, t2
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -155,7 +193,7 @@ def main():
                          "Default: full, scopes for c5")
     ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2: Pods x 100 pattern rules; c3: mixed kinds x 1000 policies with match/exclude; "
-                         "c4: anchor-heavy chart + test/policy/validate (138 rules) x Pods; "
+                         "c4: anchor-heavy chart + test/policy/validate + status forms (142 rules) x Pods; "
                          "c5: background scan, chart after autogen (105 rules) x mixed kinds, counts")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive kv_validate timing")
@@ -228,34 +266,35 @@ def main():
     if jit["kernels"]:
         log(f"[rank {rank}] specialized kernels: {jit['kernels']} ({jit['code_bytes'] / 1e3:.0f} KB code), "
             f"hiprtc {jit['compile_ms'] / 1e3:.1f}s")
-    # rank r evaluates the contiguous shard [r * N, (r + 1) * N) of one synthetic stream; the
-    # in-process path ingests [0, G * N) and the library cuts the same G shards of it
-    n_devs = args.gpus if inproc else 1
-    data = batch.synth(workloads.SEED, args.n_res * n_devs, kind_mix, first=rank * args.n_res)
-    ndjson_bytes = len(data)
-    t1 = time.time()
-    b = batch.Batch(ps, data)
-    del data
-    t2 = time.time()
-    log(f"[rank {rank}] compile+synth {t1 - t0:.2f}s ingest {t2 - t1:.2f}s store {b.store_bytes / 1e6:.1f} MB "
-        f"({b.store_bytes / b.n_res:.0f} B/resource), rules {ps.n_rules}")
     mode = {"full": batch.MODE_STATUS | batch.MODE_ERRORS, "counts": batch.MODE_COUNTS,
             "scopes": batch.MODE_COUNTS | batch.MODE_SCOPES}[args.mode]
-
-    # device-resident session: inputs uploaded and output buffers allocated once (untimed)
+    # rank r evaluates the contiguous shard [r * N, (r + 1) * N) of one synthetic stream
+    n_devs = args.gpus if inproc else 1
     if inproc:
-        mask = (1 << args.gpus) - 1
-        if args.parts_per_gpu > 1:  # rehearsal: the G parts as logical shards of device 0
-            if args.parts_per_gpu != args.gpus:
-                raise SystemExit("--parts-per-gpu must equal --gpus (all parts on device 0)")
-            os.environ["KVGPU_SHARDS_PER_DEVICE"] = str(args.parts_per_gpu)
-            mask = 1
-        sess = batch.Session(ps, b, mode=mode, device_mask=mask)
-        if sess.n_parts != args.gpus:
-            raise SystemExit(f"multi-device session has {sess.n_parts} parts, expected {args.gpus}")
-        log(f"in-process multi-device session: {sess.n_parts} parts (device mask {mask:#x})")
+        # one process drives the N devices (kv_session_create_parts): device k's shard
+        # [k * N, (k + 1) * N) is synthesized and ingested on its own (a few shards in flight),
+        # uploaded to its device and dropped, so the host never holds the node's whole batch
+        if args.parts_per_gpu > 1 and args.parts_per_gpu != args.gpus:
+            raise SystemExit("--parts-per-gpu must equal --gpus (all parts on device 0)")
+        sess, shard_info, t1, t2 = ingest_parts(ps, args, kind_mix, mode)
+        n_res_total = sum(x["n_res"] for x in shard_info)
+        store_bytes = sum(x["store_bytes"] for x in shard_info)
+        ndjson_bytes = sum(x["ndjson_bytes"] for x in shard_info)
+        namespaces = sess.scope_names() if args.mode == "scopes" else []
+        b = None
+        log(f"in-process multi-device session: {sess.n_parts} parts, RCCL ranks {sess.rccl_ranks()}")
     else:
+        data = batch.synth(workloads.SEED, args.n_res, kind_mix, first=rank * args.n_res)
+        ndjson_bytes = len(data)
+        t1 = time.time()
+        b = batch.Batch(ps, data)
+        del data
+        t2 = time.time()
+        n_res_total, store_bytes, namespaces = b.n_res, b.store_bytes, b.namespaces
+        # device-resident session: inputs uploaded and output buffers allocated once (untimed)
         sess = batch.Session(ps, b, device=local, mode=mode)
+    log(f"[rank {rank}] compile+synth {t1 - t0:.2f}s ingest {t2 - t1:.2f}s store {store_bytes / 1e6:.1f} MB "
+        f"({store_bytes / n_res_total:.0f} B/resource), rules {ps.n_rules}")
     sess.run(1)
     counts = sess.counts()
     n_fail = int(counts[:, 1].sum() + counts[:, 3].sum() + counts[:, 4].sum())
@@ -284,14 +323,14 @@ def main():
     counts = report.allreduce_counts(counts, dist)
     scopes = None
     if args.mode == "scopes":
-        names, sc = report.allreduce_scope_counts(b.namespaces, sess.scope_counts(len(b.namespaces)), dist)
+        names, sc = report.allreduce_scope_counts(namespaces, sess.scope_counts(len(namespaces)), dist)
         summ = report.scope_summaries(ps.rules, pols, names, sc)
         scopes = {"reports": len(summ), "fail": sum(v["fail"] for v in summ.values()),
                   "pass": sum(v["pass"] for v in summ.values())}
 
     n_gpus = n_devs * world
     rehearsal = inproc and args.parts_per_gpu > 1  # G logical parts on one physical device
-    n_pairs_rank = b.n_res * ps.n_rules // n_devs  # per GPU
+    n_pairs_rank = n_res_total * ps.n_rules // n_devs  # per GPU
     value = n_gpus * n_pairs_rank * args.steps / t_max
     # algorithmic bytes per launch: projected store read once + program tables + outputs
     prog_bytes = 0  # program/predicate tables are KB-scale (<0.01%)
@@ -299,8 +338,8 @@ def main():
     # the rare records that do not fit also write 32 B, not counted); scopes: status written and read back
     # by the scope-count kernel (2 B per pair) + the 4 B scope index of every resource
     out_bytes = {"full": n_pairs_rank + 8 * n_fail // n_devs, "counts": 0,
-                 "scopes": 2 * n_pairs_rank + 4 * b.n_res // n_devs}[args.mode]
-    b_alg = b.store_bytes // n_devs + prog_bytes + out_bytes  # per GPU (the slowest part's event time below)
+                 "scopes": 2 * n_pairs_rank + 4 * n_res_total // n_devs}[args.mode]
+    b_alg = store_bytes // n_devs + prog_bytes + out_bytes  # per GPU (the slowest part's event time below)
     achieved = b_alg / (kernel_ms / 1e3) / 1e9
     traffic, traffic_src = None, None  # filled below by the in-run PMC measurement (rank 0, N=1)
     out = {
@@ -317,10 +356,10 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": f"synthetic (kv_synth_range, seed 0x6B79766E, rank shard [r*N, (r+1)*N), N={args.n_res})",
-        "config": {"workload": workload, "resources_per_gpu": b.n_res // n_devs, "rules": ps.n_rules,
+        "config": {"workload": workload, "resources_per_gpu": n_res_total // n_devs, "rules": ps.n_rules,
                    "pairs_per_gpu": n_pairs_rank, "output": args.mode,
-                   "parallelism": (f"resource-shard x{n_gpus} (one process, kv_session_create_devices, "
-                                   f"RCCL count all-reduce in libkvgpu"
+                   "parallelism": (f"resource-shard x{n_gpus} (one process, kv_session_create_parts: per-device "
+                                   f"ingest, RCCL count all-reduce in libkvgpu"
                                    + (f", {args.parts_per_gpu} logical parts on device 0)" if args.parts_per_gpu > 1
                                       else ")")) if inproc else f"resource-shard x{world}",
                    "engine": args.engine},
@@ -332,8 +371,16 @@ def main():
     }
     if scopes is not None:
         out["policy_reports"] = scopes
+    # which RCCL reduces the PolicyReport counts: the communicator inside libkvgpu (in-process
+    # parts on distinct devices; 0 ranks = host sum of logical parts), or torch.distributed
+    if inproc:
+        out["rccl"] = {"ranks": sess.rccl_ranks(), "where": "libkvgpu ncclCommInitAll",
+                       "part_ms": [m / args.steps for m in sess.part_ms()]}
+    elif dist is not None:
+        out["rccl"] = {"ranks": world if dist.get_backend() == "nccl" else 0,
+                       "where": f"torch.distributed ({dist.get_backend()})"}
     # host ingest (NDJSON -> projected columnar store, kv_ingest; multi-threaded), outside `value`
-    out["ingest"] = {"seconds": t2 - t1, "resources_per_s": b.n_res / (t2 - t1),
+    out["ingest"] = {"seconds": t2 - t1, "resources_per_s": n_res_total / (t2 - t1),
                      "MB_per_s": ndjson_bytes / (t2 - t1) / 1e6,
                      "threads": int(os.environ.get("KVGPU_INGEST_THREADS", min(16, os.cpu_count() or 1)))}
     if rank == 0 and n_gpus == 1 and args.mode == "full" and not args.no_e2e:

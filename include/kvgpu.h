@@ -177,6 +177,26 @@ int kv_session_run(kv_session* s, int iters, double* event_ms, kv_error** err);
 int kv_session_counts(kv_session* s, int64_t* counts /* [n_rules][8], last pass */);
 int kv_session_scope_counts(kv_session* s, int64_t* counts /* [n_scopes][n_rules][8], last pass */);
 void kv_free_session(kv_session* s);
+/* Multi-device session assembled from per-device batches: each part's resources are
+ * ingested on their own (a background-scan worker per GPU, or one host feeding G devices
+ * without holding the whole node's batch; pkg/policy/policy_controller.go:453-454 ->
+ * pkg/policy/apply.go:72). kv_session_create_parts opens a session of n_parts parts;
+ * kv_session_attach_part uploads batch b to HIP device `device` as part `part` — the
+ * session keeps only the device copy, so the caller may free b right after. When the last
+ * part is attached the scopes become the sorted union of the parts' namespaces
+ * (kv_session_scopes / kv_session_scope_name) and the RCCL communicator is created (distinct
+ * devices); run / counts / scope_counts then work as for kv_session_create_devices
+ * (KV_E_DEVICE before that). kv_session_fetch is not available (no host batch). */
+int kv_session_create_parts(const kv_policyset* ps, const char* ctx_json, uint32_t mode, uint32_t n_parts,
+                            kv_session** out, kv_error** err);
+int kv_session_attach_part(kv_session* s, uint32_t part, const kv_batch* b, int device, kv_error** err);
+/* scope table of a session (batch namespaces; the union of the parts' for a parts session) */
+int kv_session_scopes(const kv_session* s, uint32_t* n_scopes);
+const char* kv_session_scope_name(const kv_session* s, uint32_t i);
+/* ranks of the session's RCCL communicator (0: counts summed on the host — one part, or
+ * logical parts of one device) and the HIP-event ms of each part's last kv_session_run */
+int kv_session_rccl_ranks(const kv_session* s, int* ranks);
+int kv_session_part_ms(const kv_session* s, double* ms /* [n_parts] */);
 
 /* Synthetic resource generator for the benchmark configs:
  * kind_mix 0 = Pods; 1 = Pods/Deployments/Services 60/25/15 (64 namespaces each);

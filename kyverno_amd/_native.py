@@ -97,6 +97,13 @@ def lib():
                                          ctypes.POINTER(vp)]
         L.kv_path_string.argtypes = [vp, u32]
         L.kv_path_string.restype = ctypes.c_char_p
+        L.kv_session_create_parts.argtypes = [vp, ctypes.c_char_p, u32, u32, ctypes.POINTER(vp), errpp]
+        L.kv_session_attach_part.argtypes = [vp, u32, vp, i32, errpp]
+        L.kv_session_scopes.argtypes = [vp, ctypes.POINTER(u32)]
+        L.kv_session_scope_name.argtypes = [vp, u32]
+        L.kv_session_scope_name.restype = ctypes.c_char_p
+        L.kv_session_rccl_ranks.argtypes = [vp, ctypes.POINTER(i32)]
+        L.kv_session_part_ms.argtypes = [vp, vp]
         for fn in ("kv_free_policyset", "kv_free_batch", "kv_free_result", "kv_free_buffer", "kv_free_session"):
             getattr(L, fn).argtypes = [vp]
             getattr(L, fn).restype = None
@@ -115,7 +122,8 @@ EXPORTED_SYMBOLS = [
     "kv_free_buffer", "kv_session_create", "kv_session_run", "kv_session_counts", "kv_free_session",
     "kv_session_scope_counts", "kv_result_scope_counts", "kv_batch_namespaces", "kv_batch_namespace",
     "kv_validate_devices", "kv_session_create_devices", "kv_session_parts", "kv_session_fetch", "kv_result_failures",
-    "kv_path_string",
+    "kv_path_string", "kv_session_create_parts", "kv_session_attach_part", "kv_session_scopes", "kv_session_scope_name",
+    "kv_session_rccl_ranks", "kv_session_part_ms",
 ]
 
 

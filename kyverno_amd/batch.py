@@ -122,7 +122,8 @@ class Batch:
         lib().kv_batch_namespaces(self._h, ctypes.byref(n))
         return [lib().kv_batch_namespace(self._h, i).decode("utf-8") for i in range(n.value)]
 
-    def __del__(self):
+    def close(self) -> None:
+        """Free the host batch now (e.g. once a parts session holds its device copy)."""
         h = getattr(self, "_h", None)
         if h is not None and h.value:
             try:
@@ -130,6 +131,9 @@ class Batch:
             except Exception:
                 pass
             self._h = None
+
+    def __del__(self):
+        self.close()
 
 
 class _ResultHandle:
@@ -287,11 +291,14 @@ def bench(policyset: PolicySet, batch: Batch, device: int = 0, mode: int = MODE_
 class Session:
     """Device-resident launch configuration: inputs and output buffers allocated once."""
 
-    def __init__(self, policyset: PolicySet, batch: Batch, device: int = 0, mode: int = MODE_COUNTS,
-                 ctx: dict | None = None, device_mask: int | None = None):
+    def __init__(self, policyset: PolicySet, batch: Batch | None, device: int = 0, mode: int = MODE_COUNTS,
+                 ctx: dict | None = None, device_mask: int | None = None, parts: int = 0):
         h = ctypes.c_void_p()
         err = new_err()
-        if device_mask is None:
+        if parts:  # parts session: attach_part() uploads each part's own batch
+            rc = lib().kv_session_create_parts(policyset._h, _dumps(ctx or {}), mode, parts, ctypes.byref(h),
+                                               ctypes.byref(err))
+        elif device_mask is None:
             rc = lib().kv_session_create(policyset._h, batch._h, _dumps(ctx or {}), device, mode, ctypes.byref(h),
                                          ctypes.byref(err))
         else:
@@ -304,6 +311,36 @@ class Session:
         n = ctypes.c_uint32()
         lib().kv_session_parts(h, ctypes.byref(n))
         self.n_parts = n.value
+
+    @classmethod
+    def parts(cls, policyset: PolicySet, n_parts: int, mode: int = MODE_COUNTS, ctx: dict | None = None) -> "Session":
+        """Multi-device session assembled from per-device batches (kv_session_create_parts): attach
+        each part's batch with attach_part(); the batch may be dropped right after."""
+        return cls(policyset, None, mode=mode, ctx=ctx, parts=n_parts)
+
+    def attach_part(self, part: int, batch: Batch, device: int) -> None:
+        err = new_err()
+        check(lib().kv_session_attach_part(self._h, part, batch._h, device, ctypes.byref(err)), err)
+
+    def scope_names(self) -> list[str]:
+        """Scope table: the batch's namespaces, or the sorted union of the parts' namespaces."""
+        n = ctypes.c_uint32()
+        if lib().kv_session_scopes(self._h, ctypes.byref(n)) != 0:
+            raise _native.KvError(-1, "kv_session_scopes failed (a part is not attached)")
+        return [lib().kv_session_scope_name(self._h, i).decode() for i in range(n.value)]
+
+    def rccl_ranks(self) -> int:
+        """Ranks of the session's RCCL communicator (0: counts summed on the host)."""
+        n = ctypes.c_int32()
+        if lib().kv_session_rccl_ranks(self._h, ctypes.byref(n)) != 0:
+            raise _native.KvError(-3, "kv_session_rccl_ranks failed")
+        return n.value
+
+    def part_ms(self) -> list[float]:
+        """HIP-event milliseconds of each part's last run()."""
+        out = np.zeros(self.n_parts, dtype=np.float64)
+        lib().kv_session_part_ms(self._h, out.ctypes.data)
+        return out.tolist()
 
     def fetch(self) -> "Result":
         """The last pass as a result (statuses, compacted error records, reduced counts)."""

@@ -105,7 +105,7 @@ struct Res {
   uint32_t ns_index;      // index into the batch namespace table (namespaceSelector bits, report scope)
   uint32_t flags;         // RF_*
   uint32_t tup;           // match tuple: resources with equal match inputs (every field above
-                          // but root and name) share one (Batch::tup_rep, kvj_mtup)
+                          // but root and name) share one (Batch::tup_rep, kv_mtup_kernel)
   uint32_t pad[4];
 };
 

@@ -47,21 +47,13 @@ struct DevBuf {
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
-  ~DevBuf() {
-    if (p) {
-      int cur;
-      if (hipGetDevice(&cur) == hipSuccess) {
-        (void)hipSetDevice(dev);
-        (void)hipFree(p);
-        (void)hipSetDevice(cur);
-      }
-    }
-  }
+  ~DevBuf() { release(); }
   template <class T, class A>
   void upload(const std::vector<T, A>& v, int device) {
     upload_raw(v.data(), v.size() * sizeof(T), device);
   }
   void upload_raw(const void* src, size_t bytes, int device) {
+    release();
     dev = device;
     n = bytes;
     HIPCHK(hipMalloc(&p, std::max<size_t>(bytes, 16)));
@@ -119,24 +111,36 @@ struct DevBuf {
     for (int i = 0; i < kRing; i++) (void)hipEventDestroy(ev[i]);
     (void)hipStreamDestroy(st);
   }
-  void alloc(size_t bytes, int device) {
+  void alloc(size_t bytes, int device) {  // (a buffer allocated before is freed first)
+    release();
     dev = device;
     n = bytes;
     HIPCHK(hipMalloc(&p, std::max<size_t>(bytes, 16)));
+  }
+  void release() {
+    if (!p) return;
+    int cur;
+    if (hipGetDevice(&cur) == hipSuccess) {
+      (void)hipSetDevice(dev);
+      (void)hipFree(p);
+      (void)hipSetDevice(cur);
+    }
+    p = nullptr;
+    n = 0;
   }
 };
 
 struct DevPolicySet {
   DevBuf prog, preds, alts, conjs, atoms, rules, filters, kinds, strrefs, strpairs, sels, sellabels, selexprs, kgs,
-      gsegs, gwords, pstr;
+      gsegs, gwords, pstr, fword, fbit, flist, frule;
   DevPS view{};
   // specialized kernels (KV_COMPILE_SPECIALIZE): one module per kernel program, one
   // function per rule chunk
   std::vector<hipModule_t> mods;
   std::vector<hipFunction_t> fns;
   hipFunction_t ptab_fn = nullptr;  // value-predicate table builder (kvj_ptab)
-  hipFunction_t mtup_fn = nullptr;  // match bits per tuple (kvj_mtup)
-  uint32_t mtup_words = 0;
+  uint32_t mtup_words = 0;          // match words per tuple (kv_mfac + kv_mtup, factored match)
+  uint32_t fac_slots = 0;
   uint32_t memo_words = 0, ptab_rows = 0;
   int dev = -1;
   bool specialized() const { return !mods.empty(); }
@@ -153,7 +157,7 @@ struct DevPolicySet {
 };
 
 struct DevBatchRes {
-  DevBuf nodes, vals, res, kvs, bstr, nsbits, koff, klen, kstr, nsms, lsets, asets, tuprep, view_dev;
+  DevBuf nodes, vals, res, kvs, bstr, nsbits, koff, klen, kstr, nsms, lsets, asets, tuprep, tupkent, kentrep, view_dev;
   // pattern variables (kvvars.cpp): the batch predicate table (a DevPS with its pred tables),
   // outcome ids per [dynamic leaf][res], statuses per [dynamic rule][res]
   DevBuf dpreds, dalts, dconjs, datoms, dgsegs, dgwords, dpstr, dps, dleaf, dynst;
@@ -532,9 +536,19 @@ DevPolicySet& dev_ps(kv_policyset* s, int device) {
                 local);
       }
     }
-    if (J.mtup_words) {
-      d->mtup_fn = byname.at("kvj_mtup");
+    if (J.mtup_words) {  // factored-match descriptors of the kernels' match bits
       d->mtup_words = J.mtup_words;
+      d->fac_slots = J.fac_slots;
+      d->fword.upload(J.fac_word, device);
+      d->fbit.upload(J.fac_bit, device);
+      d->flist.upload(J.fac_flist, device);
+      d->frule.upload(J.fac_rule, device);
+      v.fac_word = (const uint32_t*)d->fword.p;
+      v.fac_bit = (const uint32_t*)d->fbit.p;
+      v.fac_flist = (const uint32_t*)d->flist.p;
+      v.fac_rule = (const uint32_t*)d->frule.p;
+      v.fac_slots = J.fac_slots;
+      v.fac_words = J.mtup_words;
     }
     if (J.memo_words) {
       d->ptab_fn = byname.at("kvj_ptab");
@@ -583,6 +597,8 @@ DevBatchRes& dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
   d->lsets.upload(b.lsets, device);
   d->asets.upload(b.asets, device);
   d->tuprep.upload(b.tup_rep, device);
+  d->tupkent.upload(b.tup_kent, device);
+  d->kentrep.upload(b.kent_rep, device);
   DevBatch& v = d->view;
   v.nodes = (const Node*)d->nodes.p;
   v.vals = (const Val*)d->vals.p;
@@ -603,6 +619,10 @@ DevBatchRes& dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
   v.n_res = (uint32_t)b.res.size();
   v.tup_rep = (const uint32_t*)d->tuprep.p;
   v.n_tup = (uint32_t)b.tup_rep.size();
+  v.tup_kent = (const uint32_t*)d->tupkent.p;
+  v.kent_rep = (const uint32_t*)d->kentrep.p;
+  v.n_kent = (uint32_t)b.kent_rep.size();
+  v.n_ns = (uint32_t)b.namespaces.size();
   {  // pattern variables: every pointer valid (16-byte buffers when the policy set has none)
     const DynHost& h = bt->dyn_host(ps);
     d->dpreds.upload(h.tbl.preds, device);
@@ -821,7 +841,11 @@ struct DevSession {
   int device = 0;
   uint32_t mode = 0;
   uint64_t nrules = 0, nres = 0;
-  DevBuf fflags, pview, st, er8, er, cn, scope, scn, ptab, mtab, mtbf, mtup;
+  DevBuf fflags, pview, st, er8, er, cn, scope, scn, ptab, mtab, mtbf, mtup, ftab;
+  uint32_t fac_entities = 0, ntup = 0;
+  // a part of a parts session owns its batch's device copy (detach_batch): the caller's
+  // host batch may be freed once the part is attached
+  std::unique_ptr<DevBatchRes> own_batch;
   DevBuf r_offs, r_tot, r_base, r_out8, r_outw, r_wide;  // record compaction (fetch)
   uint32_t mt_words = 0, mt_entities = 0;
   uint32_t *mt_ns = nullptr, *mt_ann = nullptr, *mt_sel = nullptr;
@@ -874,14 +898,26 @@ struct DevSession {
       mt_words = P.mt_ns_words + P.mt_ann_words + P.mt_sel_words;
       mt_entities = (uint32_t)std::max({bb.nsms.size(), bb.asets.size(), bb.lsets.size()});
     }
-    if (dp.mtup_fn) {  // match bits of every rule per match tuple: mtup_words per tuple
+    if (dp.mtup_words) {  // match bits of every rule per match tuple: mtup_words per tuple
       mtup.alloc(std::max<size_t>((size_t)dp.mtup_words * bt->b.tup_rep.size(), 1) * sizeof(uint32_t), device);
       P.mtup = (const uint32_t*)mtup.p;
       P.mtup_words = dp.mtup_words;
+      // factor tables [slot][entity] of the five entity types, one allocation
+      const DevBatch& bv = *bhost;
+      const uint32_t ne[KV_FAC_TYPES] = {bv.n_kent, bv.n_nsm, bv.n_asets, bv.n_lsets, bv.n_ns};
+      uint64_t at = 0;
+      for (uint32_t t = 0; t < KV_FAC_TYPES; t++) {
+        P.fac_off[t] = at;
+        at += (uint64_t)dp.fac_slots * ne[t];
+        fac_entities = std::max(fac_entities, ne[t]);
+      }
+      ftab.alloc(std::max<uint64_t>(at, 1) * sizeof(uint32_t), device);
+      P.fac_tab = (uint32_t*)ftab.p;
     }
     pview.upload_raw(&P, sizeof(DevPS), device);  // read through a uniform pointer (scalar loads)
     nrules = ps->ps.rules.size();
     nres = bt->b.res.size();
+    ntup = (uint32_t)bt->b.tup_rep.size();
     O.full = 0;
     if (mode & (KV_MODE_STATUS | KV_MODE_ERRORS | KV_MODE_SCOPES)) {
       st.alloc(nrules * nres, device);
@@ -907,6 +943,29 @@ struct DevSession {
     HIPCHK(hipStreamCreate(&stream));
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
+  }
+  // take the batch's device copy out of the kv_batch (parts sessions: the host batch is the
+  // caller's, and may be freed after kv_session_attach_part)
+  void detach_batch() {
+    std::lock_guard<std::mutex> g(bt->mu);
+    auto it = bt->dev.find(device);
+    if (it != bt->dev.end()) {
+      own_batch = std::move(it->second);
+      bt->dev.erase(it);
+    }
+    bt = nullptr;
+  }
+  // renumber the scope of every resource through map (batch namespace -> session scope) and
+  // size the per-scope counts for n_total scopes
+  void remap_scopes(const std::vector<uint32_t>& map, uint32_t n_total) {
+    if (!(mode & KV_MODE_SCOPES)) return;
+    HIPCHK(hipSetDevice(device));
+    DevBuf m;
+    m.upload(map, device);
+    HIPCHK(launch_remap_u32((uint32_t*)scope.p, nres, (const uint32_t*)m.p, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    nscopes = n_total;
+    scn.alloc(std::max<uint64_t>((uint64_t)nscopes * nrules, 1) * KV_HIST * sizeof(unsigned long long), device);
   }
   ~DevSession() {
     (void)hipSetDevice(device);
@@ -955,12 +1014,8 @@ struct DevSession {
       HIPCHK(hipModuleLaunchKernel(dps->ptab_fn, (NV + KV_PTAB_PSEUDO + KV_WG - 1) / KV_WG, dps->ptab_rows, 1, KV_WG, 1, 1, 0,
                                    stream, targs, nullptr));
     }
-    if (dps->mtup_fn && bt->b.tup_rep.size()) {  // every rule's match bit per tuple (after kv_mtab)
-      uint32_t* MT = (uint32_t*)mtup.p;
-      void* margs[] = {(void*)&P, (void*)&bview, (void*)&MT};
-      HIPCHK(hipModuleLaunchKernel(dps->mtup_fn, (uint32_t)((bt->b.tup_rep.size() + KV_WG - 1) / KV_WG),
-                                   dps->mtup_words, 1, KV_WG, 1, 1, 0, stream, margs, nullptr));
-    }
+    if (dps->mtup_words && ntup)  // every rule's match bit per tuple (after kv_mtab)
+      HIPCHK(launch_mfac(P, bview, dps->fac_slots, fac_entities, dps->mtup_words, ntup, (uint32_t*)mtup.p, stream));
     DevOut Ov = O;
     uint32_t r0 = 0;
     void* args[] = {(void*)&P, (void*)&bview, (void*)&N, (void*)&V, (void*)&S, (void*)&Ov, (void*)&r0};
@@ -1059,6 +1114,79 @@ struct SessionSet {
   std::vector<ncclComm_t> comms;                           // one per part (distinct devices only)
   bool reduced = false;
   std::vector<int64_t> counts_, scope_counts_;
+  std::vector<double> part_ms;                             // HIP-event ms of each part's last run
+  // parts session (kv_session_create_parts): one caller batch per part, attached one by one;
+  // scopes = the sorted union of the parts' namespaces, set when the last part is attached
+  bool parts_mode = false, finalized = true;
+  std::string ctx;
+  std::vector<int> devs;
+  std::vector<std::vector<std::string>> part_ns;
+  std::vector<std::string> scope_names;
+
+  // parts session: n empty parts (kv_session_attach_part fills them)
+  SessionSet(kv_policyset* p, const char* ctx_json, uint32_t m, uint32_t n)
+      : ps(p), mode(m), parts_mode(true), finalized(false), ctx(ctx_json ? ctx_json : "") {
+    nrules = ps->ps.rules.size();
+    parts.resize(n);
+    ranges.assign(n, {0, 0});
+    devs.assign(n, -1);
+    part_ns.resize(n);
+  }
+  // part k = batch b on device d: uploaded, its device copy detached from the caller's batch
+  void attach(uint32_t k, kv_batch* b, int d) {
+    if (!parts_mode || finalized) throw std::runtime_error("not an open parts session");
+    if (k >= parts.size()) throw std::runtime_error("part index out of range");
+    if (parts[k]) throw std::runtime_error("part already attached");
+    auto ds = std::make_unique<DevSession>(ps, b, ctx.empty() ? nullptr : ctx.c_str(), d, mode);
+    part_ns[k] = b->b.namespaces;
+    ds->detach_batch();
+    parts[k] = std::move(ds);
+    devs[k] = d;
+    for (auto& q : parts)
+      if (!q) return;
+    finalize();
+  }
+  void finalize() {
+    uint64_t at = 0;
+    for (size_t k = 0; k < parts.size(); k++) {
+      ranges[k] = {at, at + parts[k]->nres};
+      at += parts[k]->nres;
+    }
+    nres = at;
+    std::vector<std::string> all;
+    for (auto& v : part_ns) all.insert(all.end(), v.begin(), v.end());
+    std::sort(all.begin(), all.end());
+    all.erase(std::unique(all.begin(), all.end()), all.end());
+    scope_names = all;
+    for (size_t k = 0; k < parts.size(); k++) {
+      std::vector<uint32_t> map(part_ns[k].size());
+      for (size_t i = 0; i < map.size(); i++)
+        map[i] = (uint32_t)(std::lower_bound(all.begin(), all.end(), part_ns[k][i]) - all.begin());
+      parts[k]->remap_scopes(map, (uint32_t)all.size());
+    }
+    init_comms(devs);
+    finalized = true;
+  }
+  void init_comms(const std::vector<int>& devices) {
+    std::vector<int> uniq(devices);
+    std::sort(uniq.begin(), uniq.end());
+    if (devices.size() > 1 && std::unique(uniq.begin(), uniq.end()) == uniq.end()) {  // one rank per device
+      comms.resize(devices.size());
+      if (ncclCommInitAll(comms.data(), (int)devices.size(), devices.data()) != ncclSuccess) {
+        comms.clear();
+        throw HipError("ncclCommInitAll failed");
+      }
+    }
+  }
+  void check_ready() const {
+    if (!finalized) throw std::runtime_error("parts session: not every part is attached");
+  }
+  int rccl_ranks() const {
+    if (comms.empty()) return 0;
+    int n = 0;
+    if (ncclCommCount(comms[0], &n) != ncclSuccess) return -1;
+    return n;
+  }
 
   SessionSet(kv_policyset* p, kv_batch* b, const char* ctx_json, const std::vector<int>& devices, uint32_t m)
       : ps(p), bt(b), mode(m) {
@@ -1108,15 +1236,7 @@ struct SessionSet {
     for (auto& t : th) t.join();
     for (auto& e : errs)
       if (!e.empty()) throw HipError(e);
-    std::vector<int> uniq(devices);
-    std::sort(uniq.begin(), uniq.end());
-    if (std::unique(uniq.begin(), uniq.end()) == uniq.end()) {  // RCCL needs one rank per device
-      comms.resize(devices.size());
-      if (ncclCommInitAll(comms.data(), (int)devices.size(), devices.data()) != ncclSuccess) {
-        comms.clear();
-        throw HipError("ncclCommInitAll failed");
-      }
-    }
+    init_comms(devices);  // RCCL needs one rank per device
   }
   ~SessionSet() {
     for (ncclComm_t c : comms) (void)ncclCommDestroy(c);
@@ -1143,20 +1263,32 @@ struct SessionSet {
   }
   // `iters` passes on every part concurrently; the slowest part's HIP-event time
   double run(int iters) {
+    check_ready();
     std::vector<double> ms(parts.size(), 0.0);
     each([&](size_t k) { ms[k] = parts[k]->run(iters); });
     reduced = false;
+    part_ms = ms;
     return *std::max_element(ms.begin(), ms.end());
   }
+  // a failed collective leaves ranks waiting: abort every communicator, never reuse them
+  [[noreturn]] void abort_comms(const std::string& what) {
+    for (ncclComm_t c : comms) (void)ncclCommAbort(c);
+    comms.clear();
+    comms_failed = true;
+    throw HipError(what);
+  }
+  bool comms_failed = false;
   // counts of the last pass summed over the parts: RCCL all-reduce (ncclUint64, sum)
   // of the device count arrays across distinct devices, else a host sum
   void reduce() {
+    check_ready();
+    if (comms_failed) throw HipError("RCCL communicators were aborted after a failed all-reduce");
     if (reduced) return;
     counts_.assign(nrules * KV_HIST, 0);
     scope_counts_.clear();
     const bool scopes = (mode & KV_MODE_SCOPES) != 0;
     if (!comms.empty()) {
-      if (ncclGroupStart() != ncclSuccess) throw HipError("ncclGroupStart failed");
+      if (ncclGroupStart() != ncclSuccess) abort_comms("ncclGroupStart failed");
       ncclResult_t enq = ncclSuccess;  // first failed enqueue; the group is still closed below
       for (size_t k = 0; k < parts.size() && enq == ncclSuccess; k++) {
         DevSession& d = *parts[k];
@@ -1167,12 +1299,11 @@ struct SessionSet {
                               d.stream);
       }
       const ncclResult_t end = ncclGroupEnd();
-      if (enq != ncclSuccess)
-        throw HipError(std::string("ncclAllReduce failed: ") + ncclGetErrorString(enq));
-      if (end != ncclSuccess) throw HipError(std::string("RCCL all-reduce failed: ") + ncclGetErrorString(end));
+      if (enq != ncclSuccess) abort_comms(std::string("ncclAllReduce failed: ") + ncclGetErrorString(enq));
+      if (end != ncclSuccess) abort_comms(std::string("RCCL all-reduce failed: ") + ncclGetErrorString(end));
       for (auto& d : parts) {
         HIPCHK(hipSetDevice(d->device));
-        HIPCHK(hipStreamSynchronize(d->stream));
+        if (hipStreamSynchronize(d->stream) != hipSuccess) abort_comms("RCCL all-reduce: stream synchronize failed");
       }
       counts_ = parts[0]->read_counts();
       if (scopes) scope_counts_ = parts[0]->read_scope_counts();
@@ -1190,6 +1321,7 @@ struct SessionSet {
     reduced = true;
   }
   void fetch(kv_result* out, double ms) {
+    if (parts_mode) throw std::runtime_error("kv_session_fetch: a parts session keeps no host batch");
     out->ps = ps;
     out->b = bt;
     out->n_rules = nrules;
@@ -1252,6 +1384,7 @@ struct kv_session {
   SessionSet set;
   kv_session(kv_policyset* p, kv_batch* b, const char* ctx_json, const std::vector<int>& devices, uint32_t m)
       : set(p, b, ctx_json, devices, m) {}
+  kv_session(kv_policyset* p, const char* ctx_json, uint32_t m, uint32_t n) : set(p, ctx_json, m, n) {}
 };
 
 extern "C" {
@@ -1278,12 +1411,18 @@ int kv_compile(const char* policies_json, size_t len, uint32_t flags, kv_policys
           if (!cached_plan) jit_refine_blocks(s->ps, chunk, s->jit.get());  // block sizes from probe compiles
           double ms = s->jit->compile_ms;
           jit_generate(s->ps, chunk, s->jit.get());
-          for (int round = 0; round < 40; round++) {  // register budget: re-plan kernels that spill
+          // register budget: re-plan kernels that spill until the compiled plan is the final one
+          // (the codes must belong to the last generated image: a plan still changing when the
+          // rounds run out is an error, never shipped nor cached)
+          bool settled = false;
+          for (int round = 0; round < 64 && !settled; round++) {
             jit_compile(s->jit.get());
             ms += s->jit->compile_ms;
-            if (!jit_plan_spills(s->jit.get())) break;
-            jit_generate(s->ps, chunk, s->jit.get());
+            settled = !jit_plan_spills(s->jit.get());
+            if (!settled) jit_generate(s->ps, chunk, s->jit.get());
           }
+          if (!settled)
+            throw std::runtime_error("kvjit: the register plan did not settle (kernels still spill after 64 re-plans)");
           s->jit->compile_ms = ms;
           jit_save_plan(pkey, *s->jit);
         }
@@ -1680,6 +1819,59 @@ int kv_session_create_devices(const kv_policyset* ps, const kv_batch* b, const c
   } catch (const std::exception& e) {
     return fail(err, KV_E_PARSE, e.what());
   }
+}
+
+int kv_session_create_parts(const kv_policyset* ps, const char* ctx_json, uint32_t mode, uint32_t n_parts,
+                            kv_session** out, kv_error** err) {
+  if (!ps || !out || n_parts == 0) return fail(err, KV_E_INVALID, "bad argument");
+  try {
+    *out = new kv_session(const_cast<kv_policyset*>(ps), ctx_json, mode, n_parts);
+    return 0;
+  } catch (const std::exception& e) {
+    return fail(err, KV_E_PARSE, e.what());
+  }
+}
+
+int kv_session_attach_part(kv_session* s, uint32_t part, const kv_batch* b, int device, kv_error** err) {
+  if (!s || !b) return fail(err, KV_E_INVALID, "null argument");
+  if (b->owner != s->set.ps) return fail(err, KV_E_INVALID, "batch was ingested for a different policy set");
+  try {
+    s->set.attach(part, const_cast<kv_batch*>(b), device);
+    return 0;
+  } catch (const HipError& e) {
+    return fail(err, KV_E_DEVICE, e.what());
+  } catch (const std::exception& e) {
+    return fail(err, KV_E_INVALID, e.what());
+  }
+}
+
+int kv_session_scopes(const kv_session* s, uint32_t* n_scopes) {
+  if (!s || !n_scopes) return KV_E_INVALID;
+  if (s->set.parts_mode) {
+    if (!s->set.finalized) return KV_E_INVALID;
+    *n_scopes = (uint32_t)s->set.scope_names.size();
+  } else {
+    *n_scopes = (uint32_t)s->set.bt->b.namespaces.size();
+  }
+  return 0;
+}
+
+const char* kv_session_scope_name(const kv_session* s, uint32_t i) {
+  if (!s) return nullptr;
+  const std::vector<std::string>& v = s->set.parts_mode ? s->set.scope_names : s->set.bt->b.namespaces;
+  return i < v.size() ? v[i].c_str() : nullptr;
+}
+
+int kv_session_rccl_ranks(const kv_session* s, int* ranks) {
+  if (!s || !ranks) return KV_E_INVALID;
+  *ranks = s->set.rccl_ranks();
+  return *ranks < 0 ? KV_E_DEVICE : 0;
+}
+
+int kv_session_part_ms(const kv_session* s, double* ms) {
+  if (!s || !ms) return KV_E_INVALID;
+  for (size_t k = 0; k < s->set.parts.size(); k++) ms[k] = k < s->set.part_ms.size() ? s->set.part_ms[k] : 0.0;
+  return 0;
 }
 
 int kv_session_parts(const kv_session* s, uint32_t* n_parts) {

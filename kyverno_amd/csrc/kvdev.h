@@ -19,6 +19,15 @@ hipError_t launch_validate(const DevPS* P, const DevBatch* B, uint32_t n_res, co
 hipError_t launch_mtab(const DevPS* P, const DevBatch* B, uint32_t words, uint32_t max_entities, uint32_t* ns,
                        uint32_t* an, uint32_t* sl, hipStream_t stream);
 
+// Factored match of a pass (after launch_mtab): the per-entity factor tables of every slot
+// (DevPS::fac_tab; max_entities = the largest entity count of the five types), then the match
+// words of every tuple into mtup[word][tuple].
+hipError_t launch_mfac(const DevPS* P, const DevBatch* B, uint32_t slots, uint32_t max_entities, uint32_t words,
+                       uint32_t n_tup, uint32_t* mtup, hipStream_t stream);
+
+// a[i] = map[a[i]] for i < n
+hipError_t launch_remap_u32(uint32_t* a, uint64_t n, const uint32_t* map, hipStream_t stream);
+
 // Error-record compaction in rule-major, resource order. phase 0: offs[rule][tile]
 // (exclusive, tiles of KV_WG resources), totals[rule], base[rule] (base[n_rules] =
 // all records); phase 1: scatter the dense records (and, with errw/outw, the full

@@ -65,13 +65,36 @@ struct DevPS {
   // match bits of the specialized kernels per match tuple (Res::tup): mtup[w * n_tup + tup]
   // bit b = rule at bit position 32*w+b (kernel order, kvjit.cpp) matches the tuple's
   // resources (1 for rules with name filters: evaluated per resource); built each pass by
-  // kvj_mtup after kv_mtab
+  // kv_mfac + kv_mtup after kv_mtab (factored match, below)
   const uint32_t* mtup;
   uint32_t mtup_words;
   // filter of each namespace-glob bit (mt_ns_words * 32 entries), then of each annotation bit
   // (mt_ann_words * 32); KV_SENT for unused bits (mtab_bit_filters, kvfold.cpp)
   const uint32_t* mt_bitf;
+  // Factored match (kv_mfac + kv_mtup, kvkernel.hip). MatchesResourceDescription of one
+  // filter is a conjunction of per-attribute criteria (pkg/engine/utils.go:265-336), so a
+  // rule's match is an OR of "planes" (one per `any` filter; `all` filters AND into one
+  // plane), each the AND of five per-entity words: kind entity, checkNameSpace string,
+  // annotation list, label list, namespace (namespaceSelector). A *slot* is one plane of one
+  // 32-rule word (bit b = rule at bit position 32*w+b); per slot and bit, fac_bit holds the
+  // plane's filter list (first, count | KV_FAC_PRESENT) in fac_flist.
+  //   fac_word[4w..4w+3] = first slot of word w, match planes | exclude planes << 8,
+  //                        bits evaluated per resource (name filters), bits evaluated per
+  //                        tuple by rule_matches (rules with more planes than KV_FAC_MAXP)
+  //   fac_rule[32w+b]    = rule at bit position 32w+b (KV_SENT: padding)
+  // Tables (built each pass by kv_mfac after kv_mtab): fac_tab + fac_off[t], [slot][entity]
+  // for entity type t (KV_FAC_KIND .. KV_FAC_NS).
+  const uint32_t* fac_word;
+  const uint32_t* fac_bit;
+  const uint32_t* fac_flist;
+  const uint32_t* fac_rule;
+  uint32_t fac_slots, fac_words;
+  uint32_t* fac_tab;
+  uint64_t fac_off[5];
 };
+constexpr uint32_t KV_FAC_PRESENT = 0x80000000u;
+constexpr uint32_t KV_FAC_MAXP = 8;  // match (and exclude) planes per word factored; beyond: rule_matches
+enum FacType : uint32_t { KV_FAC_KIND = 0, KV_FAC_NSM = 1, KV_FAC_ANN = 2, KV_FAC_SEL = 3, KV_FAC_NS = 4, KV_FAC_TYPES = 5 };
 
 struct DevBatch {
   const Node* nodes;
@@ -91,6 +114,10 @@ struct DevBatch {
   uint32_t n_res;
   const uint32_t* tup_rep;  // a resource of each match tuple (its Res is the tuple's inputs)
   uint32_t n_tup;
+  // kind entities: distinct (kind, group, version, kind flags) of the batch's tuples
+  const uint32_t* tup_kent;  // kind entity of each tuple
+  const uint32_t* kent_rep;  // a resource of each kind entity
+  uint32_t n_kent, n_ns;     // kind entities, namespaces (rows of ns_bits)
   // pattern variables (kvvars.cpp build_dyn): predicate table of the batch's distinct
   // substituted leaves, outcome (= predicate) id per [dynamic leaf][res], and the status
   // substitution decides per [dynamic rule][res] (0: evaluate, ST_ERROR, ST_CPU)

@@ -1134,6 +1134,27 @@ void match_tuples(Batch* b) {
     for (size_t i = c * per; i < std::min(n, (c + 1) * per); i++) b->res[i].tup = remap[c][b->res[i].tup];
   });
   b->tup_rep = std::move(g.rep);
+  // kind entities of the tuples (few: kinds x versions), found through the last hit first
+  // (tuples of one kind are numbered together in the kind-grouped store order)
+  b->tup_kent.resize(b->tup_rep.size());
+  b->kent_rep.clear();
+  auto kkey = [&](const Res& r) {
+    return std::array<uint32_t, 4>{r.kind, r.group, r.version, r.flags & (RF_KIND_NAMESPACE | RF_KIND_EMPTY)};
+  };
+  std::vector<std::array<uint32_t, 4>> kents;
+  uint32_t last = 0;
+  for (size_t t = 0; t < b->tup_rep.size(); t++) {
+    const auto k = kkey(b->res[b->tup_rep[t]]);
+    if (kents.empty() || kents[last] != k) {
+      last = 0;
+      while (last < kents.size() && kents[last] != k) last++;
+      if (last == kents.size()) {
+        kents.push_back(k);
+        b->kent_rep.push_back(b->tup_rep[t]);
+      }
+    }
+    b->tup_kent[t] = last;
+  }
 }
 
 void ingest_resources(const PolicySet& ps, const char* json, size_t len, const char* ns_labels_json, Batch* b) {

@@ -265,6 +265,9 @@ struct Batch {
   std::vector<uint32_t> order;
   // match tuples (Res::tup): a store index of each tuple's first resource
   std::vector<uint32_t> tup_rep;
+  // kind entities (factored match, DevBatch::tup_kent): distinct (kind, group, version, kind
+  // flags) of the tuples; the entity of each tuple and a resource of each entity
+  std::vector<uint32_t> tup_kent, kent_rep;
   // the arrays that cross PCIe in page-locked memory when g_hostmem provides it
   void pin_store() {
     vals = StoreVec<kv::Val>(StoreAlloc<kv::Val>(true));

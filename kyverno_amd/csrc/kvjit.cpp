@@ -35,6 +35,7 @@
 #include <unordered_map>
 
 #include "kvjit.hpp"
+#include "kvdevtypes.h"
 
 extern char** environ;
 
@@ -1284,7 +1285,7 @@ struct Gen {
     return f.str();
   }
 
-  // Match bits (kvj_mtup): the rule at LDS row q of the kernel being generated has bit
+  // Match bits (kv_mtup_kernel): the rule at LDS row q of the kernel being generated has bit
   // position 32 * mt_kbase + q; mt_bits[p] = the rule at bit position p (KV_SENT: padding).
   // A rule whose match reads the resource name is evaluated per resource behind its bit (which
   // the tuple kernel sets to 1).
@@ -1810,7 +1811,7 @@ struct Gen {
     if (hist_lds)  // every status row starts as NOMATCH (0xFF past the batch): only matched lanes store
       o << "  kv_prefill_rows(s_stw, " << nr << "u, r - threadIdx.x, n_res);\n";
     for (size_t bi = 0; bi < blocks.size(); bi++) {
-      // the block's match words (bits of its rules, kvj_mtup); a wave none of whose resources
+      // the block's match words (bits of its rules, kv_mtup_kernel); a wave none of whose resources
       // matches any rule of the block skips it whole (every rule NOMATCH on every lane)
       const uint32_t r0 = rows[bi].first, rn = rows[bi].second;
       const uint32_t p0 = mt_kbase * 32u + r0, p1 = p0 + rn;  // bit positions [p0, p1)
@@ -1857,31 +1858,75 @@ struct Gen {
     return rules;
   }
 
-  // kvj_mtup: the match bits of every rule for every match tuple (one thread per tuple and
-  // 32-rule word): g_match of the word's rules on the tuple's representative resource; a rule
-  // whose match reads the name gets bit 1 (its kernel evaluates it per resource)
-  void mtup_kernel() {
+  // Factored match descriptors (DevPS::fac_*, kv_mfac / kv_mtup in kvkernel.hip) for the
+  // match bits of every rule in kernel order. A rule's match is an OR of planes minus an OR
+  // of exclude planes (rule_matches, kvdevfn.h): `any` blocks give one plane per filter,
+  // `all` blocks one plane of all their filters, a legacy block one plane of its filter. A
+  // word takes as many match / exclude planes as its widest rule; rules with name filters
+  // keep their per-resource bit, rules with more than KV_FAC_MAXP planes run rule_matches per
+  // tuple.
+  void build_fac(JitImage* out) const {
     const uint32_t W = (uint32_t)(mt_bits.size() / 32u);
-    KernelText kt(*this, "kvj_mtup");
-    o << "extern \"C\" __global__ __launch_bounds__(KV_WG) void kvj_mtup(const DevPS* __restrict__ Pp, "
-         "const DevBatch* __restrict__ Bp, uint32_t* __restrict__ out) {\n"
-      << "  const DevPS& P = *Pp;\n  const DevBatch& B = *Bp;\n"
-      << "  const uint32_t t = blockIdx.x * KV_WG + threadIdx.x;\n"
-      << "  if (t >= B.n_tup) return;\n"
-      << "  const Res* __restrict__ R = B.res + B.tup_rep[t];\n"
-      << "  const uint32_t rkind = R->kind, rflags = R->flags;\n"
-      << "  uint32_t m = 0u;\n  switch (blockIdx.y) {\n";
+    out->fac_word.assign(4u * W, 0u);
+    out->fac_bit.clear();
+    out->fac_flist.clear();
+    out->fac_rule = mt_bits;
+    auto planes = [&](uint32_t mode, uint32_t first, uint32_t count) {
+      std::vector<std::vector<uint32_t>> p;
+      if (mode == 1) {
+        for (uint32_t f = first; f < first + count; f++) p.push_back({f});
+      } else if (mode == 2) {
+        std::vector<uint32_t> all;
+        for (uint32_t f = first; f < first + count; f++) all.push_back(f);
+        p.push_back(all);
+      } else {
+        p.push_back({first});
+      }
+      return p;
+    };
+    uint32_t slot = 0;
     for (uint32_t w = 0; w < W; w++) {
-      o << "    case " << w << "u:\n";
+      std::vector<std::vector<std::vector<uint32_t>>> mp(32), xp(32);
+      uint32_t nm = 0, nx = 0, named = 0, cx = 0;
       for (uint32_t b = 0; b < 32u; b++) {
         const uint32_t ri = mt_bits[w * 32u + b];
         if (ri == 0xFFFFFFFFu) continue;
-        if (name_dependent(ri)) o << "      m |= " << u32(1u << b) << ";\n";
-        else o << "      if (g_match_" << ri << "(P, B, R, rkind, rflags)) m |= " << u32(1u << b) << ";\n";
+        if (name_dependent(ri)) {
+          named |= 1u << b;
+          continue;
+        }
+        const RuleRec& rr = ps.rules[ri];
+        auto m = planes(rr.m_mode, rr.m_first, rr.m_count), x = planes(rr.x_mode, rr.x_first, rr.x_count);
+        if (m.size() > KV_FAC_MAXP || x.size() > KV_FAC_MAXP) {
+          cx |= 1u << b;
+          continue;
+        }
+        nm = std::max<uint32_t>(nm, (uint32_t)m.size());
+        nx = std::max<uint32_t>(nx, (uint32_t)x.size());
+        mp[b] = std::move(m);
+        xp[b] = std::move(x);
       }
-      o << "      break;\n";
+      out->fac_word[4u * w] = slot;
+      out->fac_word[4u * w + 1] = nm | nx << 8;
+      out->fac_word[4u * w + 2] = named;
+      out->fac_word[4u * w + 3] = cx;
+      for (uint32_t p = 0; p < nm + nx; p++, slot++)
+        for (uint32_t b = 0; b < 32u; b++) {
+          const auto& pl = p < nm ? mp[b] : xp[b];
+          const uint32_t k = p < nm ? p : p - nm;
+          if (k < pl.size()) {
+            out->fac_bit.push_back((uint32_t)out->fac_flist.size());
+            out->fac_bit.push_back((uint32_t)pl[k].size() | KV_FAC_PRESENT);
+            out->fac_flist.insert(out->fac_flist.end(), pl[k].begin(), pl[k].end());
+          } else {
+            out->fac_bit.push_back(0u);
+            out->fac_bit.push_back(0u);
+          }
+        }
     }
-    o << "  }\n  out[(size_t)blockIdx.y * B.n_tup + t] = m;\n}\n\n";
+    out->fac_slots = slot;
+    if (out->fac_flist.empty()) out->fac_flist.push_back(0u);
+    if (out->fac_bit.empty()) out->fac_bit.assign(2, 0u);
   }
 
   // Register weight of rule ri in a fused block: the state it keeps across the block (status
@@ -2067,7 +2112,7 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
     }
   }
   out->mtup_words = (uint32_t)(g.mt_bits.size() / 32u);
-  if (out->mtup_words && !out->probe) g.mtup_kernel();
+  if (out->mtup_words && !out->probe) g.build_fac(out);
   out->memo_preds.clear();
   out->memo_words = 0;
   if (!g.mpreds.empty() && !out->probe) {

@@ -42,8 +42,11 @@ struct JitImage {
   std::vector<uint32_t> memo_preds;
   uint32_t memo_words = 0;
   uint32_t ptab_row = 1;    // predicates per kvj_ptab grid row (one row: every predicate of a value)
-  // match bits per tuple (kvj_mtup, DevPS::mtup): words of 32 rules in kernel order
+  // match bits per tuple (kv_mtup_kernel, DevPS::mtup): words of 32 rules in kernel order,
+  // from the factored-match descriptors (DevPS::fac_*, kvjit.cpp build_fac)
   uint32_t mtup_words = 0;
+  std::vector<uint32_t> fac_word, fac_bit, fac_flist, fac_rule;
+  uint32_t fac_slots = 0;
   bool probe = false;       // a block-probe image (jit_refine_blocks): rule kernels only
   double gen_ms = 0, compile_ms = 0;
 };

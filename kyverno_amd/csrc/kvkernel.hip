@@ -381,6 +381,51 @@ hipError_t launch_mtab(const DevPS* P, const DevBatch* B, uint32_t words, uint32
   return hipGetLastError();
 }
 
+// Factored match tables (DevPS::fac_*): grid.z = entity type, grid.y = slot (uniform per
+// workgroup: the slot's filter lists are scalar loads), grid.x = entities of the type.
+__global__ __launch_bounds__(KV_WG) void kv_mfac_kernel(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp) {
+  const DevPS& P = *Pp;
+  const DevBatch& B = *Bp;
+  const uint32_t t = blockIdx.z, s = blockIdx.y, e = blockIdx.x * KV_WG + threadIdx.x;
+  const uint32_t ne = fac_entities(B, t);
+  if (e >= ne) return;
+  P.fac_tab[P.fac_off[t] + (size_t)s * ne + e] = fac_cell(P, B, t, e, s);
+}
+
+// Match words per tuple: grid.y = word (uniform plane counts and masks), grid.x = tuples;
+// mtup[w * n_tup + t] (word-major: a wave writes 256 contiguous bytes)
+__global__ __launch_bounds__(KV_WG) void kv_mtup_kernel(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp,
+                                                         uint32_t* __restrict__ out) {
+  const DevPS& P = *Pp;
+  const DevBatch& B = *Bp;
+  const uint32_t t = blockIdx.x * KV_WG + threadIdx.x, w = blockIdx.y;
+  if (t >= B.n_tup) return;
+  out[(size_t)w * B.n_tup + t] = mtup_word(P, B, t, w);
+}
+
+// a[i] = map[a[i]] (scope renumbering of a parts session, kv_session_attach_part)
+__global__ __launch_bounds__(KV_WG) void kv_remap_kernel(uint32_t* __restrict__ a, uint64_t n,
+                                                          const uint32_t* __restrict__ map) {
+  const uint64_t i = (uint64_t)blockIdx.x * KV_WG + threadIdx.x;
+  if (i < n) a[i] = map[a[i]];
+}
+
+hipError_t launch_remap_u32(uint32_t* a, uint64_t n, const uint32_t* map, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(kv_remap_kernel, dim3((uint32_t)((n + KV_WG - 1) / KV_WG)), dim3(KV_WG), 0, stream, a, n, map);
+  return hipGetLastError();
+}
+
+hipError_t launch_mfac(const DevPS* P, const DevBatch* B, uint32_t slots, uint32_t max_entities, uint32_t words,
+                       uint32_t n_tup, uint32_t* mtup, hipStream_t stream) {
+  if (slots && max_entities)
+    hipLaunchKernelGGL(kv_mfac_kernel, dim3((max_entities + KV_WG - 1) / KV_WG, slots, KV_FAC_TYPES), dim3(KV_WG), 0,
+                       stream, P, B);
+  if (words && n_tup)
+    hipLaunchKernelGGL(kv_mtup_kernel, dim3((n_tup + KV_WG - 1) / KV_WG, words), dim3(KV_WG), 0, stream, P, B, mtup);
+  return hipGetLastError();
+}
+
 }  // namespace kv
 
 // ---------------------------------------------------------------------------

@@ -158,6 +158,25 @@ def c3_policies(n_policies: int = 1000, seed: int = SEED) -> list[dict]:
     return pols
 
 
+def name_filter_policy() -> dict:
+    """Rules whose match / exclude reads the resource name (`name`, `names` globs; evaluated per
+    resource behind the match-tuple bit), mixed with namespace / selector / any blocks, for the
+    C3 stream (pkg/engine/utils.go:129-229)."""
+    pat = {"metadata": {"name": "?*"}}
+    rules = [
+        _rule("name-pod", pat, match={"resources": {"kinds": ["Pod"], "name": "pod-1*"}}),
+        _rule("names-any", pat, match={"any": [{"resources": {"kinds": ["Deployment"], "names": ["*-2?", "dep-3*"]}},
+                                                {"resources": {"kinds": ["Service"], "namespaces": ["ns-1*"]}}]}),
+        _rule("exclude-name", pat, match={"resources": {"kinds": ["*"]}}, exclude={"resources": {"name": "*-7*"}}),
+        _rule("exclude-names-ns", pat, match={"resources": {"kinds": ["Pod", "Service"],
+                                                             "selector": {"matchLabels": {"app": "*"}}}},
+              exclude={"any": [{"resources": {"names": ["pod-9*", "svc-8*"]}},
+                               {"resources": {"namespaces": ["ns-5*"]}}]}),
+        _rule("plain", pat, match={"resources": {"kinds": ["Pod"], "namespaces": ["ns-2*"]}}),
+    ]
+    return _policy("names", rules)
+
+
 _GOLDEN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
 
 
@@ -177,12 +196,33 @@ def validate_corpus_policies() -> list[dict]:
     return [p["policy"] for p in pols if p["src"].startswith("test/policy/validate/")]
 
 
+# Rules whose outcome on the synthetic Pods spreads over PASS / FAIL / ERROR / SKIP, so the
+# benchmark streams exercise every status at scale (validation.go:421-444 status mapping,
+# validate.go:29-50 MatchPattern skip / missing-anchor forms, anchorKey.go:11-145):
+#   a conditional anchor that mismatches on most Pods (SKIP; ERROR where the label is absent),
+#   a negation anchor under a condition (SKIP / FAIL / ERROR), a condition anchor next to a plain
+#   key (missing anchor key -> ERROR), a global anchor inside containers[] (SKIP).
+STATUS_FORM_RULES = {
+    "cond-tier-image": {"metadata": {"labels": {"(tier)": "frontend"}}, "spec": {"containers": [{"image": "*:v1.*"}]}},
+    "cond-app-no-hostnet": {"metadata": {"labels": {"(app)": "web"}}, "spec": {"X(hostNetwork)": "null"}},
+    "cond-owner-app": {"metadata": {"labels": {"(owner)": "team-*", "app": "api"}}},
+    "global-latest-always": {"spec": {"containers": [{"<(image)": "*:latest", "imagePullPolicy": "Always"}]}},
+}
+
+
+def status_form_policy() -> dict:
+    """One policy of the STATUS_FORM_RULES (no autogen: pod-policies.kyverno.io/autogen-controllers none)."""
+    return _policy("status-forms", [_rule(k, v) for k, v in STATUS_FORM_RULES.items()],
+                   annotations={"pod-policies.kyverno.io/autogen-controllers": "none"})
+
+
 def c4_policies() -> list[dict]:
     """C4: anchor-heavy set = chart + test/policy/validate, after the CLI's defaults + autogen
-    (pkg/kyverno/common/common.go:177-216): 138 rules, every one device-routed."""
+    (pkg/kyverno/common/common.go:177-216): 138 rules, every one device-routed, plus the 4
+    STATUS_FORM_RULES (SKIP / ERROR at scale): 142 rules."""
     from . import autogen
 
-    return autogen.mutate_policies(chart_policies() + validate_corpus_policies())
+    return autogen.mutate_policies(chart_policies() + validate_corpus_policies() + [status_form_policy()])
 
 
 def c5_policies() -> list[dict]:

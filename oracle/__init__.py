@@ -56,6 +56,8 @@ class Oracle:
         L.orc_match_pattern.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         L.orc_match_pattern.restype = ctypes.c_void_p
         L.orc_substitute.argtypes = [ctypes.c_char_p]
+        L.orc_expand_in_metadata.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.orc_expand_in_metadata.restype = ctypes.c_void_p
         L.orc_substitute.restype = ctypes.c_void_p
         L.orc_validate.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
         L.orc_substitute_message.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
@@ -125,6 +127,14 @@ class Oracle:
                       subst: bool = False) -> dict:
         return json.loads(self._take(self.lib.orc_match_pattern(entry, resource_json.encode(), res_mode,
                                                                   pattern_json.encode(), int(subst))))
+
+    def expand_in_metadata(self, pattern: dict, resource: dict) -> dict:
+        """The pattern after ExpandInMetadata (wildcard label / annotation keys replaced by the
+        resource keys they match, wildcards.go:69-161)."""
+        p = self.lib.orc_expand_in_metadata(json.dumps(pattern).encode(), json.dumps(resource).encode())
+        if not p:
+            raise RuntimeError(self.lib.orc_last_error().decode())
+        return json.loads(self._take(p))
 
     def substitute(self, pattern_json: str) -> dict:
         return json.loads(self._take(self.lib.orc_substitute(pattern_json.encode())))

@@ -113,6 +113,24 @@ int orc_compare(int kind, const char* value_json, int value_mode, const char* pa
   return -1;
 }
 
+// ExpandInMetadata (pkg/engine/wildcards/wildcards.go:69-161) of a pattern / resource pair:
+// the pattern after replaceWildcardsInMapKeys, as JSON ({"panic": msg} when the reference panics)
+char* orc_expand_in_metadata(const char* pattern_json, const char* resource_json) {
+  try {
+    Value p = parse_json(pattern_json, NumMode::Float);
+    Value r = parse_json(resource_json, NumMode::Unstructured);
+    try {
+      ExpandInMetadata(p, r);
+    } catch (const GoPanic& e) {
+      return dup("{\"panic\":" + jstr(e.what) + "}");
+    }
+    return dup(to_json(p));
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return nullptr;
+  }
+}
+
 // MatchPattern(resource, pattern) -> {"set":b,"msg":s,"path":s,"skip":b}
 // entry: 0 MatchPattern, 1 validateResourceElement("/"), 2 validateMap("/")
 char* orc_match_pattern(int entry, const char* resource_json, int res_mode, const char* pattern_json, int do_subst) {

@@ -114,13 +114,43 @@ def _bench(*args):
 
 @pytest.mark.parametrize("cfg", ["c2", "c5"])
 def test_bench_in_process_parts_match_one_gpu(cfg):
-    """`bench.py --gpus N` without a launcher runs one kv_session_create_devices session over N
-    parts (here: N logical parts of device 0); its reduced counts equal one part over the same
-    [0, N * n) stream."""
+    """`bench.py --gpus N` without a launcher runs one kv_session_create_parts session over N
+    parts, each ingested on its own (here: N logical parts of device 0); its reduced counts equal
+    one part over the same [0, N * n) stream."""
     n = 8192
     one = _bench("--config", cfg, "--gpus", "1", "--n-res", str(4 * n))
     four = _bench("--config", cfg, "--gpus", "4", "--parts-per-gpu", "4", "--n-res", str(n))
-    assert four["parts"] == 4 and four["n_gpus"] == 1 and "kv_session_create_devices" in four["config"]["parallelism"]
+    assert four["parts"] == 4 and four["n_gpus"] == 1 and "kv_session_create_parts" in four["config"]["parallelism"]
+    assert four["rccl"]["ranks"] == 0 and len(four["rccl"]["part_ms"]) == 4  # logical parts: host sum
     assert four["status_counts"] == one["status_counts"]
     if "policy_reports" in one:
         assert four["policy_reports"] == one["policy_reports"]
+
+
+@pytest.mark.parametrize("parts", [2, 3])
+def test_parts_session_matches_one_batch(parts):
+    """kv_session_create_parts + kv_session_attach_part: each part's shard of the stream ingested
+    on its own (own namespace table, tuples, kind entities), its host batch freed after attach;
+    counts and per-scope counts (on the sorted union of the parts' namespaces) equal one batch."""
+    from kyverno_amd import batch, workloads
+
+    ps = batch.PolicySet(workloads.c5_policies(), specialize=True)
+    n = 6000
+    whole = batch.Batch(ps, batch.synth(workloads.SEED + 5, parts * n, 1))
+    mode = batch.MODE_COUNTS | batch.MODE_SCOPES
+    ref = batch.validate(ps, whole, mode=mode)
+    s = batch.Session.parts(ps, parts, mode=mode)
+    for k in reversed(range(parts)):  # attach order does not matter
+        b = batch.Batch(ps, batch.synth(workloads.SEED + 5, n, 1, first=k * n))
+        s.attach_part(k, b, 0)
+        b.close()
+    s.run(2)
+    assert s.rccl_ranks() == 0
+    assert np.array_equal(s.counts(), ref.counts)
+    names = s.scope_names()
+    assert names == sorted(whole.namespaces)
+    sc = s.scope_counts(len(names))
+    order = [whole.namespaces.index(x) for x in names]
+    assert np.array_equal(sc, ref.scope_counts[order])
+    with pytest.raises(Exception):
+        s.fetch()  # a parts session keeps no host batch

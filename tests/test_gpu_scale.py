@@ -6,7 +6,7 @@ error messages:
 * C3: the whole 1 000-policy / 1 973-rule set on mixed Pods/Deployments/Services,
   at the shipped kernel plan and at 40 rules per kernel;
 * C2: 1 M Pods x 100 rules (the headline workload);
-* C4: 1 M Pods x 138 anchor-heavy rules.
+* C4: 1 M Pods x 142 anchor-heavy rules (incl. the SKIP / ERROR status forms).
 Reference semantics: pkg/engine/validation.go:26-106 (oracle/src/engine.cpp).
 """
 import json
@@ -89,11 +89,25 @@ def test_c2_full_scale(orc):
 
 
 def test_c4_full_scale(orc):
-    """C4 at its benchmark size: 1 M synthetic Pods x 138 anchor-heavy chart + test/policy/validate rules."""
+    """C4 at its benchmark size: 1 M synthetic Pods x 142 anchor-heavy rules (chart +
+    test/policy/validate + the status-form rules): every status incl. SKIP and ERROR at scale, their
+    messages sampled against the per-pair oracle."""
     from kyverno_amd import batch, workloads
 
     data = batch.synth(workloads.SEED + 4, 1_000_000).strip()
-    _check(orc, workloads.c4_policies(), data)
+    r = _check(orc, workloads.c4_policies(), data, n_msgs=300)
+    assert (r.status == 3).sum() > 100_000 and (r.status == 4).sum() > 100_000
+
+
+def test_name_filters_mixed_kinds(orc):
+    """match / exclude `name` and `names` globs (per-resource match behind the tuple bit) on the
+    mixed-kind C3 stream, next to rules the factored match decides (pkg/engine/utils.go:129-229)."""
+    from kyverno_amd import batch, workloads
+    pols = [workloads.name_filter_policy()] + workloads.c3_policies(40)
+    data = batch.synth(workloads.SEED + 21, 4000, workloads.C3_KIND_MIX).strip()
+    r = _check(orc, pols, data, min_fail=0)
+    for q in range(5):
+        assert 0 < (r.status[q] != 5).sum() < r.n_res  # each name rule matches some resources, not all
 
 
 def test_c3_scope_counts_full_policy_set(orc):

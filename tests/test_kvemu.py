@@ -48,6 +48,21 @@ def test_generated_kernels_match_oracle(orc, cfg):
     assert (st == 0).sum() > 0 and (st == 1).sum() > 0
 
 
+def test_generated_kernels_name_filters(orc):
+    """Rules whose match / exclude reads the name (evaluated per resource behind the tuple bit)
+    next to factored-match rules, on the mixed-kind C3 stream."""
+    from kyverno_amd import workloads
+
+    pols = [workloads.name_filter_policy()] + workloads.c3_policies(30)
+    ress = _synth(workloads.SEED + 21, 1200, workloads.C3_KIND_MIX)
+    st, _ = _emulate(pols, ress, "names")
+    ost = oracle_status(orc, pols, ress)
+    bad = np.argwhere(st != ost)
+    assert not len(bad), [(int(a), int(b), int(st[a, b]), int(ost[a, b])) for a, b in bad[:20]]
+    for q in range(5):
+        assert 0 < (st[q] != 5).sum() < st.shape[1]
+
+
 def test_generated_kernels_reference_corpus(orc):
     c = load_gold("corpus.json")[0]
     pols = [p["policy"] for p in c["policies"]]

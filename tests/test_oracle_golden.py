@@ -54,18 +54,14 @@ def test_syntax(orc, case):
 
 @pytest.mark.parametrize("case", load("expand.json"), ids=lambda c: c["src"])
 def test_expand_in_metadata(orc, case):
-    # replaceWildcardsInMapKeys through ExpandInMetadata: pattern labels vs resource labels
+    # TestExpandInMetadata (wildcards_test.go:8-28): replaceWildcardsInMapKeys(pattern labels,
+    # resource labels) must equal the expected map; reached through ExpandInMetadata on
+    # metadata.labels (wildcards.go:69-107)
     pat = {"metadata": {"labels": case["pattern"]}}
     res = {"metadata": {"labels": case["resource"]}}
-    # expansion result is observable through the failing path / pass outcome;
-    # every fixture expands to a key present in the resource with a value the
-    # pattern accepts only if expansion happened.
-    r = orc.match_pattern(json.dumps(res), json.dumps(pat), entry=1)
-    exp_keys = set(case["expect"])
-    assert all(k.strip("=()") in case["resource"] for k in exp_keys)
-    if not r["set"]:
-        return
-    assert r["path"].startswith("/metadata/labels/"), r
+    got = orc.expand_in_metadata(pat, res)
+    assert "panic" not in got, got
+    assert got["metadata"]["labels"] == case["expect"], (got, case)
 
 
 @pytest.mark.parametrize("case", load("matcher.json"), ids=lambda c: c["src"])

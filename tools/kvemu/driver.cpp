@@ -40,7 +40,7 @@ extern "C" void kvemu_mtab(const DevPS* P, const DevBatch* B, uint32_t words, ui
                            uint32_t* an, uint32_t* sl);
 
 typedef void (*ptab_fn)(const DevPS*, const Val*, const uint8_t*, uint32_t, uint32_t*);
-typedef void (*mtup_fn)(const DevPS*, const DevBatch*, uint32_t*);
+extern "C" void kvemu_mfac(const DevPS* P, const DevBatch* B, uint32_t* mtup);
 typedef void (*chunk_fn)(const DevPS*, const DevBatch*, const Node*, const Val*, const uint8_t*, DevOut, uint32_t);
 
 static std::string slurp(const char* p) {
@@ -178,6 +178,28 @@ int main(int argc, char** argv) {
     B.n_res = (uint32_t)b.res.size();
     B.tup_rep = b.tup_rep.data();
     B.n_tup = (uint32_t)b.tup_rep.size();
+    B.tup_kent = b.tup_kent.data();
+    B.kent_rep = b.kent_rep.data();
+    B.n_kent = (uint32_t)b.kent_rep.size();
+    B.n_ns = (uint32_t)b.namespaces.size();
+    // factored match (as kv_session: descriptors of the image, [slot][entity] tables per type)
+    P.fac_word = img.fac_word.data();
+    P.fac_bit = img.fac_bit.data();
+    P.fac_flist = img.fac_flist.data();
+    P.fac_rule = img.fac_rule.data();
+    P.fac_slots = img.fac_slots;
+    P.fac_words = img.mtup_words;
+    std::vector<uint32_t> ftab;
+    {
+      const uint32_t ne[KV_FAC_TYPES] = {B.n_kent, B.n_nsm, B.n_asets, B.n_lsets, B.n_ns};
+      uint64_t at = 0;
+      for (uint32_t t = 0; t < KV_FAC_TYPES; t++) {
+        P.fac_off[t] = at;
+        at += (uint64_t)img.fac_slots * ne[t];
+      }
+      ftab.assign(std::max<uint64_t>(at, 1), 0xA5A5A5A5u);
+      P.fac_tab = ftab.data();
+    }
     std::vector<uint32_t> mtup(std::max<size_t>((size_t)img.mtup_words * b.tup_rep.size(), 1), 0xA5A5A5A5u);
     P.mtup = mtup.data();
     P.mtup_words = img.mtup_words;
@@ -217,11 +239,7 @@ int main(int argc, char** argv) {
       const uint32_t rows = (uint32_t)((img.memo_preds.size() + img.ptab_row - 1) / img.ptab_row);
       grid((NV + KV_PTAB_PSEUDO + KV_WG - 1) / KV_WG, rows, [&]() { f(&P, B.vals, B.bstr, NV, ptab.data()); });
     }
-    if (img.mtup_words && B.n_tup) {  // match bits per tuple (as kv_session, after the match tables)
-      auto f = (mtup_fn)dlsym(RTLD_DEFAULT, "kvj_mtup");
-      if (!f) throw std::runtime_error("kvj_mtup not linked in");
-      grid((B.n_tup + KV_WG - 1) / KV_WG, img.mtup_words, [&]() { f(&P, &B, mtup.data()); });
-    }
+    if (img.mtup_words && B.n_tup) kvemu_mfac(&P, &B, mtup.data());  // (as kv_session, after the match tables)
     std::vector<uint8_t> status(nr * nres, 0xEE);
     std::vector<ErrRec8> err8(nr * nres);
     std::vector<ErrRec> errw;
