@@ -335,10 +335,11 @@ def main():
     # algorithmic bytes per launch: projected store read once + program tables + outputs
     prog_bytes = 0  # program/predicate tables are KB-scale (<0.01%)
     # full: 1 B status + 8 B compact error record per FAIL/ERROR/SKIP pair (kvdevtypes.h ErrRec8;
-    # the rare records that do not fit also write 32 B, not counted); scopes: status written and read back
-    # by the scope-count kernel (2 B per pair) + the 4 B scope index of every resource
+    # the rare records that do not fit also write 32 B, not counted); scopes: the 4 B scope index of
+    # every resource (the rule kernels count per scope inside the pass; the per-scope counts
+    # themselves are KB-scale)
     out_bytes = {"full": n_pairs_rank + 8 * n_fail // n_devs, "counts": 0,
-                 "scopes": 2 * n_pairs_rank + 4 * n_res_total // n_devs}[args.mode]
+                 "scopes": 4 * n_res_total // n_devs}[args.mode]
     b_alg = store_bytes // n_devs + prog_bytes + out_bytes  # per GPU (the slowest part's event time below)
     achieved = b_alg / (kernel_ms / 1e3) / 1e9
     traffic, traffic_src = None, None  # filled below by the in-run PMC measurement (rank 0, N=1)

@@ -369,6 +369,7 @@ struct kv_result {
   HostArray<uint8_t> status;
   std::once_flag sc_once;
   HostArray<uint8_t> status_c;
+  bool status_c_ready = false;      // status_c written by the fetch (device-side permutation)
   std::vector<ResultPart> parts;    // by resource range
   bool errors = false;              // KV_MODE_ERRORS: records fetched
   std::vector<int64_t> counts;
@@ -393,6 +394,7 @@ struct kv_result {
   // order, rules split over host threads (a permuted batch only)
   const uint8_t* status_caller() {
     if (b->b.order.empty() || status.empty()) return status.empty() ? nullptr : status.data();
+    if (status_c_ready) return status_c.data();
     std::call_once(sc_once, [this]() {
       status_c.alloc(status.size());
       const uint32_t* ord = b->b.order.data();
@@ -847,6 +849,7 @@ struct DevSession {
   // host batch may be freed once the part is attached
   std::unique_ptr<DevBatchRes> own_batch;
   DevBuf r_offs, r_tot, r_base, r_out8, r_outw, r_wide;  // record compaction (fetch)
+  DevBuf inv_d, stc;                                     // caller-order statuses (fetch)
   uint32_t mt_words = 0, mt_entities = 0;
   uint32_t *mt_ns = nullptr, *mt_ann = nullptr, *mt_sel = nullptr;
   uint32_t nscopes = 0, nvals = 0;
@@ -919,7 +922,9 @@ struct DevSession {
     nres = bt->b.res.size();
     ntup = (uint32_t)bt->b.tup_rep.size();
     O.full = 0;
-    if (mode & (KV_MODE_STATUS | KV_MODE_ERRORS | KV_MODE_SCOPES)) {
+    // the status matrix: asked for, or the bytecode engine's per-scope counts read it back
+    // (the specialized kernels count scopes inside the pass, O.full bit 3)
+    if ((mode & (KV_MODE_STATUS | KV_MODE_ERRORS)) || ((mode & KV_MODE_SCOPES) && !dp.specialized())) {
       st.alloc(nrules * nres, device);
       O.status = (uint8_t*)st.p;
       O.full |= 1;
@@ -939,6 +944,9 @@ struct DevSession {
       nscopes = (uint32_t)bt->b.namespaces.size();
       scope.upload(sc, device);
       scn.alloc(std::max<uint64_t>((uint64_t)nscopes * nrules, 1) * KV_HIST * sizeof(unsigned long long), device);
+      O.scope = (const uint32_t*)scope.p;
+      O.scounts = (unsigned long long*)scn.p;
+      if (dp.specialized()) O.full |= 8;
     }
     HIPCHK(hipStreamCreate(&stream));
     HIPCHK(hipEventCreate(&e0));
@@ -966,6 +974,7 @@ struct DevSession {
     HIPCHK(hipStreamSynchronize(stream));
     nscopes = n_total;
     scn.alloc(std::max<uint64_t>((uint64_t)nscopes * nrules, 1) * KV_HIST * sizeof(unsigned long long), device);
+    O.scounts = (unsigned long long*)scn.p;
   }
   ~DevSession() {
     (void)hipSetDevice(device);
@@ -981,16 +990,17 @@ struct DevSession {
     HIPCHK(hipEventRecord(e0, stream));
     for (int i = 0; i < iters; i++) {
       HIPCHK(hipMemsetAsync(cn.p, 0, cn.n, stream));
+      if (mode & KV_MODE_SCOPES) HIPCHK(hipMemsetAsync(scn.p, 0, scn.n, stream));
       HIPCHK(launch_mtab((const DevPS*)pview.p, bview, mt_words, mt_entities, mt_ns, mt_ann, mt_sel, stream));
       if (dps->specialized() && !vm) {
-        launch_specialized();
+        launch_specialized();  // (per-scope counts inside the rule kernels)
       } else {
-        HIPCHK(launch_validate((const DevPS*)pview.p, bview, (uint32_t)nres, O, 0, (uint32_t)nrules, stream));
-      }
-      if (mode & KV_MODE_SCOPES) {
-        HIPCHK(hipMemsetAsync(scn.p, 0, scn.n, stream));
-        HIPCHK(launch_scope_counts(O.status, (const uint32_t*)scope.p, (uint32_t)nres, (uint32_t)nrules, nscopes,
-                                   (unsigned long long*)scn.p, stream));
+        DevOut Ov = O;
+        Ov.full &= ~8u;
+        HIPCHK(launch_validate((const DevPS*)pview.p, bview, (uint32_t)nres, Ov, 0, (uint32_t)nrules, stream));
+        if (mode & KV_MODE_SCOPES)
+          HIPCHK(launch_scope_counts(O.status, (const uint32_t*)scope.p, (uint32_t)nres, (uint32_t)nrules, nscopes,
+                                     (unsigned long long*)scn.p, stream));
       }
     }
     HIPCHK(hipEventRecord(e1, stream));
@@ -1048,6 +1058,17 @@ struct DevSession {
     if (O.status && (mode & (KV_MODE_STATUS | KV_MODE_ERRORS)) && nres && nrules)
       HIPCHK(hipMemcpy2DAsync(out->status.data() + lo, n_total, st.p, nres, nres, nrules, hipMemcpyDeviceToHost,
                               stream));
+    // a permuted batch fetched whole: the caller-order matrix is gathered on the device
+    // (out[rule][j] = st[rule][store index of j]) and copied too, instead of a host scatter
+    if (O.status && (mode & (KV_MODE_STATUS | KV_MODE_ERRORS)) && nres && nrules && bt && lo == 0 &&
+        nres == n_total && !bt->b.order.empty()) {
+      if (!inv_d.p) inv_d.upload_raw(bt->inverse(), nres * sizeof(uint32_t), device);
+      if (!stc.p) stc.alloc(nrules * nres, device);
+      HIPCHK(launch_gather_rows((const uint8_t*)st.p, (const uint32_t*)inv_d.p, nrules, nres, (uint8_t*)stc.p, stream));
+      out->status_c.alloc(nrules * nres);
+      HIPCHK(hipMemcpyAsync(out->status_c.data(), stc.p, nrules * nres, hipMemcpyDeviceToHost, stream));
+      out->status_c_ready = true;
+    }
     lap("status D2H");
     if (O.err8 && nres && nrules) {
       const uint32_t tiles = (uint32_t)((nres + KV_WG - 1) / KV_WG);

@@ -25,6 +25,10 @@ hipError_t launch_mtab(const DevPS* P, const DevBatch* B, uint32_t words, uint32
 hipError_t launch_mfac(const DevPS* P, const DevBatch* B, uint32_t slots, uint32_t max_entities, uint32_t words,
                        uint32_t n_tup, uint32_t* mtup, hipStream_t stream);
 
+// out[rule][j] = in[rule][inv[j]] (caller-order status matrix)
+hipError_t launch_gather_rows(const uint8_t* in, const uint32_t* inv, uint64_t n_rules, uint64_t n_res, uint8_t* out,
+                              hipStream_t stream);
+
 // a[i] = map[a[i]] for i < n
 hipError_t launch_remap_u32(uint32_t* a, uint64_t n, const uint32_t* map, hipStream_t stream);
 

@@ -632,86 +632,6 @@ KV_FN bool rule_matches(const DevPS& P, const DevBatch& B, const Res* __restrict
   return true;
 }
 
-// ------------------------------------------------------------------ factored match
-// doesResourceMatchConditionBlock (pkg/engine/utils.go:265-336) of one filter is a conjunction
-// of per-attribute criteria; fac_crit is the factor of entity type t (DevPS::fac_*): the
-// filter's criteria on that attribute, every other criterion taken as true. The kind factor
-// carries the launch-folded flags (MF_EMPTY, user info); the namespaceSelector factor is
-// exempt for kind Namespace / empty kinds (utils.go:323), applied per tuple (mtup_word).
-KV_FN uint32_t fac_entities(const DevBatch& B, uint32_t t) {
-  switch (t) {
-    case KV_FAC_KIND: return B.n_kent;
-    case KV_FAC_NSM: return B.n_nsm;
-    case KV_FAC_ANN: return B.n_asets;
-    case KV_FAC_SEL: return B.n_lsets;
-    default: return B.n_ns;
-  }
-}
-KV_FN bool fac_crit(const DevPS& P, const DevBatch& B, uint32_t t, uint32_t e, uint32_t f) {
-  const uint32_t fl = sld(P.fflags + f);
-  const MFilter& F = P.filters[f];
-  switch (t) {
-    case KV_FAC_KIND: {
-      if (fl & (MF_EMPTY | MF_UI_FAIL)) return false;
-      if (!(fl & MF_KINDS)) return true;
-      const Res* __restrict__ R = B.res + B.kent_rep[e];
-      return block_errs_masked(P, B, R, R->kind, R->flags, f, MF_KINDS) == 0;
-    }
-    case KV_FAC_NSM: return !(fl & MF_NSS) || mt_bit(P.mt_ns, sld(&F.nss_bit), B.n_nsm, e);
-    case KV_FAC_ANN: return !(fl & MF_ANN) || mt_bit(P.mt_ann, sld(&F.ann_bit), B.n_asets, e);
-    case KV_FAC_SEL: return !(fl & MF_SEL) || mt_bit(P.mt_sel, sld(&F.sel), B.n_lsets, e);
-    default: {
-      if (!(fl & MF_NSSEL)) return true;
-      const uint32_t bit = sld(&F.nssel_bit);
-      return (B.ns_bits[(size_t)e * B.ns_words + bit / 32u] >> (bit % 32u)) & 1u;
-    }
-  }
-}
-// Word of slot s for entity e of type t (bit b: every filter of the plane at bit b passes the
-// type-t factor; an absent plane is 0). Table layout [slot][entity] per type.
-KV_FN uint32_t fac_cell(const DevPS& P, const DevBatch& B, uint32_t t, uint32_t e, uint32_t s) {
-  uint32_t w = 0;
-  for (uint32_t b = 0; b < 32u; b++) {
-    const uint32_t first = sld(P.fac_bit + 2u * (s * 32u + b)), cnt = sld(P.fac_bit + 2u * (s * 32u + b) + 1u);
-    if (!(cnt & KV_FAC_PRESENT)) continue;
-    bool ok = true;
-    for (uint32_t k = first; k < first + (cnt & ~KV_FAC_PRESENT) && ok; k++) ok = fac_crit(P, B, t, e, sld(P.fac_flist + k));
-    w |= (ok ? 1u : 0u) << b;
-  }
-  return w;
-}
-KV_FN const uint32_t* fac_table(const DevPS& P, uint32_t t) { return P.fac_tab + P.fac_off[t]; }
-// Match word w of tuple t: OR over the match planes of the AND of the five factors, minus the
-// OR of the exclude planes; rules with name filters keep bit 1 (their rule kernel evaluates
-// the match per resource), rules with more planes than KV_FAC_MAXP run rule_matches here.
-KV_FN uint32_t mtup_word(const DevPS& P, const DevBatch& B, uint32_t t, uint32_t w) {
-  const Res* __restrict__ R = B.res + B.tup_rep[t];
-  const uint32_t s0 = sld(P.fac_word + 4u * w), np = sld(P.fac_word + 4u * w + 1u);
-  const uint32_t named = sld(P.fac_word + 4u * w + 2u), cx = sld(P.fac_word + 4u * w + 3u);
-  const uint32_t nm = np & 0xFFu, nx = (np >> 8) & 0xFFu;
-  const uint32_t eK = B.tup_kent[t], eN = R->nsm, eA = R->aset, eL = R->lset, eS = R->ns_index, rflags = R->flags;
-  const uint32_t nK = B.n_kent, nN = B.n_nsm, nA = B.n_asets, nL = B.n_lsets, nS = B.n_ns;
-  const uint32_t* __restrict__ tK = fac_table(P, KV_FAC_KIND);
-  const uint32_t* __restrict__ tN = fac_table(P, KV_FAC_NSM);
-  const uint32_t* __restrict__ tA = fac_table(P, KV_FAC_ANN);
-  const uint32_t* __restrict__ tL = fac_table(P, KV_FAC_SEL);
-  const uint32_t* __restrict__ tS = fac_table(P, KV_FAC_NS);
-  const uint32_t kex = (rflags & (RF_KIND_NAMESPACE | RF_KIND_EMPTY)) ? 0xFFFFFFFFu : 0u;
-  uint32_t m = 0u, x = 0u;
-  for (uint32_t p = 0; p < nm + nx; p++) {
-    const size_t s = s0 + p;
-    const uint32_t v = tK[s * nK + eK] & tN[s * nN + eN] & tA[s * nA + eA] & tL[s * nL + eL] & (tS[s * nS + eS] | kex);
-    if (p < nm) m |= v;
-    else x |= v;
-  }
-  m = (m & ~x) | named;
-  for (uint32_t c = cx; c; c &= c - 1u) {
-    const uint32_t b = (uint32_t)__builtin_ctz(c);
-    if (rule_matches(P, B, R, R->kind, rflags, P.rules[sld(P.fac_rule + 32u * w + b)])) m |= 1u << b;
-  }
-  return m;
-}
-
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
@@ -785,9 +705,9 @@ __device__ __forceinline__ uint32_t kv_leaf_word(const DevPS& P, const Node* __r
   return x;
 }
 
-// final status of one rule on this lane: its byte in the workgroup's LDS row of the rule
-// (0xFF: no resource; copied to the status matrix and counted by kv_count_status_lds at
-// the end of the kernel) and, for FAIL / ERROR / SKIP, the error record
+// final status of one rule on this lane: its byte in the wave's LDS row of the rule (KV_ROW
+// bytes per wave; 0xFF: no resource; copied to the status matrix and counted when the block
+// ends, kv_wflush) and, for FAIL / ERROR / SKIP, the error record
 // The record address is computed where the record is written: `r` and `ri` (uniform: every
 // caller passes a constant or a wave-uniform member index) pass through empty asm statements
 // so the compiler cannot hoist one address per rule out of the element loops (a wide fused
@@ -804,13 +724,13 @@ __device__ __forceinline__ void kv_final(const DevOut& O, uint32_t ri, uint32_t 
 #endif
     store_err(O, ri, n_res, r, e.kind + z, e.flags, e.pn + z, e.key + z, e.res + z, e.i0, e.i1, e.i2, e.i3);
   }
-  s_row[threadIdx.x] = valid ? (uint8_t)st : (uint8_t)0xFFu;
+  s_row[threadIdx.x & (KV_ROW - 1u)] = valid ? (uint8_t)st : (uint8_t)0xFFu;
 }
 
 // final status `st` of the members `m` of a rule group (kvjit.cpp: rules whose programs differ
 // only in their leaf predicates and pattern-node ids, evaluated once with one bit per member):
 // member j is rule tab[j] (or ri0 + j * sri), its pattern nodes are the group's shifted by
-// tab[n + j] (or j * spn), its status row is s_row0 + j * KV_WG; `ekx` is the error of the
+// tab[n + j] (or j * spn), its status row is s_row0 + j * KV_ROW; `ekx` is the error of the
 // group's representative (kind | flags << 4 | node << 8; 0: none)
 __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_t r, bool valid, uint32_t m, uint32_t st,
                                         uint32_t ekx, uint32_t i0, uint32_t i1, uint32_t i2, uint32_t i3,
@@ -818,31 +738,128 @@ __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_
                                         uint32_t sri, uint32_t spn) {
   for (uint32_t j = 0; j < n; j++) {  // uniform over the members (scalar rule ids and rows)
     if (!((m >> j) & 1u)) continue;
-    const uint32_t ri = tab ? tab[j] : ri0 + j * sri;
+    // (j is uniform, so is the member's rule id: named so, the compiler keeps it scalar)
+    const uint32_t ri = __builtin_amdgcn_readfirstlane(tab ? tab[j] : ri0 + j * sri);
     const uint32_t ek = ekx ? ekx + ((tab ? tab[n + j] : j * spn) << 8) : 0u;
     const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
-    kv_final(O, ri, n_res, r, valid, st, e, s_row0 + j * (uint32_t)KV_WG);
+    kv_final(O, ri, n_res, r, valid, st, e, s_row0 + j * KV_ROW);
   }
 }
 
-// the workgroup's LDS status rows (nr rules x KV_WG lanes, one byte each) set to NOMATCH for
-// the lanes holding a resource (0xFF past the batch), with 32-bit stores spread over the
-// workgroup; the rule code then stores only the statuses of matched lanes
-__device__ __forceinline__ void kv_prefill_rows(uint32_t* s_stw, uint32_t nr, uint32_t base, uint32_t n_res) {
-  const uint32_t nv = n_res > base ? n_res - base : 0u;
+// ------------------------------------------------------------------ wave status rows
+// The rule kernels stage one status byte per (rule, lane) in LDS rows private to the wave
+// (KV_ROW bytes per rule and wave, the current fused block's rules only): a row is prefilled
+// with NOMATCH (kv_wprefill), matched lanes store their status (kv_final), and when the block
+// ends the wave copies its rows to the status matrix and counts them (kv_wflush) - no
+// workgroup barrier, and the rows are reused by the next block.
+// Ordering inside a wave: LDS operations of one wave execute in program order; the fence
+// keeps the compiler from moving the lanes' row accesses across it.
+__device__ __forceinline__ void kv_wsync() {
+#ifndef KVEMU
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
+}
+
+// the wave's rows [0, nr) set to NOMATCH for lanes holding a resource, 0xFF past the batch
+// (first = the wave's first resource)
+__device__ __forceinline__ void kv_wprefill(uint8_t* s_w, uint32_t nr, uint32_t first, uint32_t n_res) {
+  const uint32_t nv = n_res > first ? n_res - first : 0u;
 #ifdef KVEMU
   // host emulation runs the lanes one after another: each lane fills its own bytes
-  for (uint32_t q = 0; q < nr; q++)
-    ((uint8_t*)s_stw)[q * (uint32_t)KV_WG + threadIdx.x] = threadIdx.x < nv ? (uint8_t)ST_NOMATCH : (uint8_t)0xFFu;
+  const uint32_t l = threadIdx.x & (KV_ROW - 1u);
+  for (uint32_t q = 0; q < nr; q++) s_w[q * KV_ROW + l] = l < nv ? (uint8_t)ST_NOMATCH : (uint8_t)0xFFu;
 #else
-  for (uint32_t i = threadIdx.x; i < nr * ((uint32_t)KV_WG / 4u); i += (uint32_t)KV_WG) {
-    const uint32_t l = (i % ((uint32_t)KV_WG / 4u)) * 4u;
-    uint32_t w = 0u;
-    for (uint32_t k = 0u; k < 4u; k++) w |= (l + k < nv ? (uint32_t)ST_NOMATCH : 0xFFu) << (8u * k);
-    s_stw[i] = w;
+  uint32_t* w = (uint32_t*)s_w;
+  for (uint32_t i = threadIdx.x & 63u; i < nr * (KV_ROW / 4u); i += 64u) {
+    const uint32_t l = (i % (KV_ROW / 4u)) * 4u;
+    uint32_t x = 0u;
+    for (uint32_t k = 0u; k < 4u; k++) x |= (l + k < nv ? (uint32_t)ST_NOMATCH : 0xFFu) << (8u * k);
+    w[i] = x;
   }
-  __syncthreads();
+  kv_wsync();
 #endif
+}
+
+// histogram of one status row (KV_ROW bytes) restricted to the lanes of mask m (other bytes
+// read as 0xFE, no status), into c[KV_HIST]
+__device__ __forceinline__ void kv_count_row(const uint32_t* w, uint64_t m, uint32_t* c) {
+  uint32_t c0 = 0u, c1 = 0u, c5 = 0u, cx = 0u, n = 0u;
+#pragma unroll 4
+  for (uint32_t i = 0; i < KV_ROW / 4u; i++) {
+    const uint32_t b = (uint32_t)(m >> (4u * i)) & 15u;
+    const uint32_t keep = (((b * 0x00204081u) & 0x01010101u) * 0xFFu);  // byte k = 0xFF if bit k
+    const uint32_t x = (w[i] & keep) | (0xFEFEFEFEu & ~keep);
+    c0 += kv_count_bytes(x, 0x00000000u);
+    c1 += kv_count_bytes(x, 0x01010101u);
+    c5 += kv_count_bytes(x, 0x05050505u);
+    cx += kv_count_bytes(x, 0xFFFFFFFFu);
+    n += (uint32_t)__popc(b);
+  }
+  for (uint32_t k = 0; k < (uint32_t)KV_HIST; k++) c[k] = 0u;
+  c[ST_PASS] = c0;
+  c[ST_FAIL] = c1;
+  c[ST_NOMATCH] = c5;
+  if (c0 + c1 + c5 + cx < n) {
+    const uint32_t rest[4] = {ST_WARN, ST_ERROR, ST_SKIP, ST_CPU};
+    for (uint32_t k = 0; k < 4u; k++) {
+      uint32_t q = 0u;
+      for (uint32_t i = 0; i < KV_ROW / 4u; i++) {
+        const uint32_t b = (uint32_t)(m >> (4u * i)) & 15u;
+        const uint32_t keep = (((b * 0x00204081u) & 0x01010101u) * 0xFFu);
+        q += kv_count_bytes((w[i] & keep) | (0xFEFEFEFEu & ~keep), rest[k] * 0x01010101u);
+      }
+      c[rest[k]] = q;
+    }
+  }
+}
+
+// End of a fused block for this wave: the rows of the block's nr rules (kernel rules
+// rules[0..nr)) go to the status matrix (O.full & 1), lane q counts row q into the
+// workgroup's LDS histogram s_cnt[q][KV_HIST] (flushed with global atomics when the kernel
+// ends), and with per-scope counts (O.full & 8) into s_scnt for the lanes of the workgroup's
+// scope wsc (the store is ordered by kind and namespace, so a workgroup mostly holds one
+// scope) or straight into O.scounts for lanes of other scopes. `sc` is this lane's scope.
+__device__ __forceinline__ void kv_wflush(const DevOut& O, uint8_t* s_w, uint32_t nr, const uint32_t* rules,
+                                          uint32_t* s_cnt, uint32_t* s_scnt, uint32_t n_res, uint32_t r, bool valid,
+                                          uint32_t sc, uint32_t wsc, uint32_t n_rules) {
+  kv_wsync();
+  const uint32_t l = threadIdx.x & (KV_ROW - 1u);
+  if ((O.full & 1u) && valid) {
+#pragma unroll 4
+    for (uint32_t q = 0; q < nr; q++) O.status[(size_t)rules[q] * n_res + r] = s_w[q * KV_ROW + l];
+  }
+#ifndef KVEMU
+  const uint64_t all = __ballot(true);
+  for (uint32_t q = l; q < nr; q += 64u) {
+    uint32_t c[KV_HIST];
+    kv_count_row((const uint32_t*)(s_w + q * KV_ROW), ~0ull, c);
+    for (uint32_t k = 0; k < (uint32_t)KV_HIST; k++)
+      if (c[k] && k != 7u) atomicAdd(&s_cnt[q * KV_HIST + k], c[k]);
+  }
+  if (O.full & 8u) {
+    // one pass per distinct scope among the wave's resources (one, inside a namespace run)
+    uint64_t rem = __ballot(valid) & all;
+    while (rem) {
+      const uint32_t s = __builtin_amdgcn_readlane(sc, (uint32_t)__builtin_ctzll(rem));
+      const uint64_t m = __ballot(valid && sc == s) & rem;
+      rem &= ~m;
+      for (uint32_t q = l; q < nr; q += 64u) {
+        uint32_t c[KV_HIST];
+        kv_count_row((const uint32_t*)(s_w + q * KV_ROW), m, c);
+        for (uint32_t k = 0; k < (uint32_t)KV_HIST; k++) {
+          if (!c[k] || k == 7u) continue;
+          if (s == wsc) atomicAdd(&s_scnt[q * KV_HIST + k], c[k]);
+          else atomicAdd(&O.scounts[((size_t)s * n_rules + rules[q]) * KV_HIST + k], (unsigned long long)c[k]);
+        }
+      }
+    }
+  }
+#else
+  (void)s_cnt; (void)s_scnt; (void)sc; (void)wsc; (void)n_rules; (void)rules;  // (counts are not emulated)
+#endif
+  kv_wsync();
 }
 
 // histogram of one rule's KV_WG status bytes (64 words in LDS) added to counts[KV_HIST]

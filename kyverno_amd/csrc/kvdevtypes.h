@@ -131,10 +131,14 @@ struct DevOut {
   ErrRec8* err8;               // [rule][res] (written for fail/error/skip)
   ErrRec* err;                 // [rule][res] (only records flagged ERR8_WIDE)
   unsigned long long* counts;  // [rule][8]
-  uint32_t full;               // bit0 status, bit1 error records, bit2 full 32 B records (not 8 B)
+  uint32_t full;               // bit0 status, bit1 error records, bit2 full 32 B records (not 8 B),
+                               // bit3 per-scope counts (specialized kernels: counted in the pass)
+  unsigned long long* scounts; // [scope][rule][8] (bit3)
+  const uint32_t* scope;       // scope of every resource (bit3)
 };
 
 constexpr int KV_WG = 256;
+constexpr uint32_t KV_ROW = 64;  // bytes of one wave status row (one per lane)
 constexpr uint32_t KV_PTAB_PSEUDO = 3;  // ptab columns of a null, a map and an array node
 constexpr int KV_HIST = 8;
 

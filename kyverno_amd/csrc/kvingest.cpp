@@ -1026,26 +1026,86 @@ std::string_view raw_string_of(const char* p, size_t n, const char* key, size_t 
   return {};
 }
 
-// Store order from per-resource kind keys: the kinds in order of first appearance, the
-// resources of each kind in input order (stable counting sort); empty when every resource
-// has the same kind. Resources of one kind then share wave groups, so a rule that matches
-// other kinds only is skipped by whole waves (its match fails uniformly) instead of running
-// its pattern walk for the few lanes of a mixed wave (C5: 6.1 -> 4.3 ms per pass).
-std::vector<uint32_t> kind_order(const std::vector<std::string_view>& kinds) {
-  std::unordered_map<std::string_view, uint32_t> id;
-  std::vector<uint32_t> kid(kinds.size()), cnt;
-  for (size_t i = 0; i < kinds.size(); i++) {
-    auto it = id.emplace(kinds[i], (uint32_t)id.size()).first;
-    kid[i] = it->second;
-    if (kid[i] >= cnt.size()) cnt.push_back(0);
-    cnt[kid[i]]++;
-  }
-  if (id.size() < 2) return {};
-  if (const char* e = getenv("KVGPU_INGEST_ORDER"); e && e[0] == '0') return {};  // input order (A/B)
-  std::vector<uint32_t> at(cnt.size(), 0);
-  for (size_t k = 1; k < cnt.size(); k++) at[k] = at[k - 1] + cnt[k - 1];
-  std::vector<uint32_t> order(kinds.size());
-  for (size_t i = 0; i < kinds.size(); i++) order[at[kid[i]]++] = (uint32_t)i;
+// Store order from per-resource (kind, namespace) keys: kinds in order of first appearance,
+// inside a kind its namespaces in order of first appearance, input order inside a (kind,
+// namespace) run (stable counting sort, per-thread key tables merged in thread order); empty
+// when every resource has the same key. Resources of one kind share wave groups, so a rule that
+// matches other kinds only is skipped by whole waves (its match fails uniformly) instead of
+// running its pattern walk for the few lanes of a mixed wave (C5: 6.1 -> 4.3 ms per pass); and
+// resources of one namespace share waves and workgroups, so the rule kernels count per-scope
+// PolicyReport results for a whole wave at once (kv_wflush) and neighbouring resources share
+// match tuples.
+std::vector<uint32_t> store_order(const std::vector<std::string_view>& kinds, const std::vector<std::string_view>& nss,
+                                  unsigned T) {
+  struct KeyHash {
+    size_t operator()(const std::pair<std::string_view, std::string_view>& k) const {
+      return std::hash<std::string_view>()(k.first) * 1000003u ^ std::hash<std::string_view>()(k.second);
+    }
+  };
+  using Map = std::unordered_map<std::pair<std::string_view, std::string_view>, uint32_t, KeyHash>;
+  const size_t n = kinds.size();
+  const size_t C = std::max<size_t>(1, std::min<size_t>(T, n / 4096 + 1));
+  const size_t per = (n + C - 1) / C;
+  std::vector<Map> local(C);
+  std::vector<std::vector<std::pair<std::string_view, std::string_view>>> lkeys(C);
+  std::vector<uint32_t> key(n);
+  auto run = [&](auto&& f) {
+    std::vector<std::thread> th;
+    for (size_t c = 1; c < C; c++) th.emplace_back(f, c);
+    f((size_t)0);
+    for (auto& t : th) t.join();
+  };
+  run([&](size_t c) {
+    for (size_t i = c * per; i < std::min(n, (c + 1) * per); i++) {
+      const auto k = std::make_pair(kinds[i], nss[i]);
+      auto it = local[c].find(k);
+      if (it == local[c].end()) {
+        it = local[c].emplace(k, (uint32_t)lkeys[c].size()).first;
+        lkeys[c].push_back(k);
+      }
+      key[i] = it->second;
+    }
+  });
+  // global key ids in first-appearance order; kinds and namespaces ranked by first appearance
+  Map gid;
+  std::unordered_map<std::string_view, uint32_t> kid, nid;
+  std::vector<std::pair<uint64_t, uint32_t>> rank;  // (kind rank << 32 | namespace rank, key id)
+  std::vector<std::vector<uint32_t>> remap(C);
+  for (size_t c = 0; c < C; c++)
+    for (const auto& k : lkeys[c]) {
+      auto it = gid.find(k);
+      if (it == gid.end()) {
+        it = gid.emplace(k, (uint32_t)gid.size()).first;
+        const uint64_t kr = kid.emplace(k.first, (uint32_t)kid.size()).first->second;
+        const uint64_t nr = nid.emplace(k.second, (uint32_t)nid.size()).first->second;
+        rank.push_back({kr << 32 | nr, it->second});
+      }
+      remap[c].push_back(it->second);
+    }
+  if (gid.size() < 2) return {};
+  std::sort(rank.begin(), rank.end());
+  std::vector<uint32_t> slot(gid.size());  // key id -> position of its run
+  for (size_t q = 0; q < rank.size(); q++) slot[rank[q].second] = (uint32_t)q;
+  // counting sort: per-thread run sizes, run offsets per thread, parallel scatter
+  const size_t K = gid.size();
+  std::vector<std::vector<uint32_t>> cnt(C, std::vector<uint32_t>(K, 0));
+  run([&](size_t c) {
+    for (size_t i = c * per; i < std::min(n, (c + 1) * per); i++) {
+      key[i] = slot[remap[c][key[i]]];
+      cnt[c][key[i]]++;
+    }
+  });
+  uint32_t at = 0;
+  for (size_t k = 0; k < K; k++)
+    for (size_t c = 0; c < C; c++) {
+      const uint32_t x = cnt[c][k];
+      cnt[c][k] = at;
+      at += x;
+    }
+  std::vector<uint32_t> order(n);
+  run([&](size_t c) {
+    for (size_t i = c * per; i < std::min(n, (c + 1) * per); i++) order[cnt[c][key[i]]++] = (uint32_t)i;
+  });
   return order;
 }
 
@@ -1182,18 +1242,19 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
     const size_t nres = starts.size(), groups = (nres + KV_LANES - 1) / KV_LANES;
     const size_t per = (groups + T - 1) / T * KV_LANES;
     const size_t P = (nres + per - 1) / per;
-    {  // store order: resources grouped by kind
-      std::vector<std::string_view> kinds(nres);
+    {  // store order: resources grouped by kind, then namespace
+      std::vector<std::string_view> kinds(nres), nss(nres);
       std::vector<std::thread> kt;
       for (size_t k = 0; k < P; k++)
         kt.emplace_back([&, k]() {
           for (size_t i = k * per; i < std::min(nres, (k + 1) * per); i++) {
             const size_t end = i + 1 < nres ? starts[i + 1] : len;
             kinds[i] = raw_string_of(json + starts[i], end - starts[i], "\"kind\"", 6);
+            nss[i] = raw_string_of(json + starts[i], end - starts[i], "\"namespace\"", 11);
           }
         });
       for (auto& t : kt) t.join();
-      b->order = kind_order(kinds);
+      b->order = store_order(kinds, nss, T);
     }
     const std::vector<uint32_t>& order = b->order;
     std::vector<Batch> parts(P);
@@ -1243,13 +1304,16 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
     if (len <= (64u << 20)) {  // small inputs: documents held, taken in store order
       std::vector<JDoc> docs;
       parse_json_stream(json, len, NUM_UNSTRUCTURED, [&](JDoc& d) { docs.push_back(std::move(d)); });
-      std::vector<std::string_view> kinds(docs.size());
+      std::vector<std::string_view> kinds(docs.size()), nss(docs.size());
       for (size_t i = 0; i < docs.size(); i++) {
         const JDoc& d = docs[i];
         const int64_t c = d.at(d.root).t == J_MAP ? d.get(d.root, "kind") : -1;
         if (c >= 0 && d.at((uint32_t)c).t == J_STR) kinds[i] = d.sval(d.at((uint32_t)c));
+        const int64_t m = d.at(d.root).t == J_MAP ? d.get(d.root, "metadata") : -1;
+        const int64_t ns = m >= 0 && d.at((uint32_t)m).t == J_MAP ? d.get((uint32_t)m, "namespace") : -1;
+        if (ns >= 0 && d.at((uint32_t)ns).t == J_STR) nss[i] = d.sval(d.at((uint32_t)ns));
       }
-      b->order = kind_order(kinds);
+      b->order = store_order(kinds, nss, 1);
       for (size_t q = 0; q < docs.size(); q++) in.take(docs[b->order.empty() ? q : b->order[q]]);
     } else {
       parse_json_stream(json, len, NUM_UNSTRUCTURED, [&](JDoc& d) { in.take(d); });

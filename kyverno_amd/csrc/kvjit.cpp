@@ -929,7 +929,7 @@ struct Gen {
       std::ostringstream r;
       r << "kv_gfin(O, n_res, r, valid, " << m << ", " << st << ", " << u32(kind | (pcn.flags << 4) | (pn << 8));
       for (uint32_t lv = 0; lv < 4; lv++) r << ", " << (lv <= g.max_level ? li(lv) : std::string("0u"));
-      r << ", (uint8_t*)s_stw + " << u32(g.grow) << ", " << (g.gtab.empty() ? std::string("nullptr") : g.gtab) << ", "
+      r << ", s_w + " << u32(g.grow) << ", " << (g.gtab.empty() ? std::string("nullptr") : g.gtab) << ", "
         << u32(g.gn) << ", " << u32(g.gri[0]) << ", " << u32(g.gsri) << ", " << u32(g.gspn) << ");";
       return r.str();
     };
@@ -1310,7 +1310,8 @@ struct Gen {
   std::string block_decls;      // declarations the current kernel's blocks need (member tables)
 
   // Code block of one fused chunk inside a kernel body (its own C++ scope); the
-  // chunk's status rows are s_stw rows [hbase, hbase + rules).
+  // chunk's status rows are the wave rows s_w + q * KV_ROW, q = position in the block
+  // (hbase = the block's first position in the kernel: match bits, names).
   //
   // Lean rules (hist_lds kernels): at the end of stage segment k a rule that enters stage
   // loop k keeps only one bit (am<k>_<w>, bit q of its block position), one that jumps past
@@ -1393,7 +1394,7 @@ struct Gen {
         g.gn = (uint32_t)G.members.size();
         g.gri = G.members;
         g.gdpn = G.dpn;
-        g.grow = (hbase + q) * 256u;
+        g.grow = q * KV_ROW;  // the block's wave rows (reused by every block)
         for (const auto& m : G.preds)
           for (uint32_t pi : m) pred_fn(pi);
         for (size_t i = 0; i < G.leafpcs.size(); i++) {
@@ -1430,7 +1431,7 @@ struct Gen {
       return std::string(m) + std::to_string(k) + "_" + std::to_string(q / 32);
     };
     auto mbit = [&](uint32_t q) { return u32(1u << (q % 32)); };
-    auto row = [&](uint32_t q) { return "(uint8_t*)s_stw + " + u32((hbase + q) * 256u); };
+    auto row = [&](uint32_t q) { return "s_w + " + u32(q * KV_ROW); };
     // EState of rule g from its registers (error kind / flags / pattern node in `ekx`)
     auto estate = [&](const RGen* g, const std::string& ekx) {
       std::ostringstream k;
@@ -1463,7 +1464,7 @@ struct Gen {
       if (!g) return store_st(q, g, st, "0u");
       if (g->grp)  // the members alive here end with the group's status (no error record)
         return "  if ((rs" + s + " & 0xFFu) != ST_STORED_)\n    kv_gfin(O, n_res, r, valid, al" + s + ", rs" + s +
-               " & 0xFFu, 0u, 0u, 0u, 0u, 0u, (uint8_t*)s_stw + " + u32(g->grow) + ", " +
+               " & 0xFFu, 0u, 0u, 0u, 0u, 0u, s_w + " + u32(g->grow) + ", " +
                (g->gtab.empty() ? std::string("nullptr") : g->gtab) + ", " + u32(g->gn) + ", " + u32(g->gri[0]) + ", " +
                u32(g->gsri) + ", " + u32(g->gspn) + ");\n";
       return "  if ((rs" + s + " & 0xFFu) != ST_STORED_" + (hist_lds ? std::string(" && (rs" + s + " & 0xFFu) != ST_NOMATCH") : "") +
@@ -1481,7 +1482,7 @@ struct Gen {
         for (uint32_t j = 0; j < g.gn; j++) {
           const uint32_t ri = g.gri[j];
           const RuleRec& rr = ps.rules[ri];
-          const std::string rw = "(uint8_t*)s_stw + " + u32(g.grow + j * 256u);
+          const std::string rw = "s_w + " + u32(g.grow + j * KV_ROW);
           auto st = [&](const std::string& x) {
             return "{ const EState e_{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u}; kv_final(O, " + u32(ri) +
                    ", n_res, r, valid, " + x + ", e_, " + rw + "); }";
@@ -1755,15 +1756,25 @@ struct Gen {
   // One kernel running the fused chunks `chs` one after the other for each
   // resource: a workgroup re-reads its resources' node rows per chunk while they
   // are still cache-resident, instead of one grid-wide pass per chunk.
+  // Statuses: each wave stages the current block's statuses in its own LDS rows (KV_ROW
+  // bytes per rule) and flushes them when the block ends (kv_wprefill / kv_wflush): status
+  // matrix, per-rule histogram in LDS, per-scope counts; the histograms leave the workgroup
+  // with global atomics when the kernel ends. LDS per workgroup: 4 waves x the largest
+  // block's rows + 2 x 32 B per rule of the kernel (kernel_lds).
+  static uint32_t kernel_lds(uint32_t nr, uint32_t max_block) {
+    return (uint32_t)(KV_WG / 64) * max_block * KV_ROW + 2u * nr * KV_HIST * 4u;
+  }
   std::vector<uint32_t> group_kernel(const std::string& name, const std::vector<const JitChunk*>& chs, int waves) {
     std::vector<std::string> blocks;
-    std::vector<std::pair<uint32_t, uint32_t>> rows;  // LDS rows [first, first + count) of each block
+    std::vector<std::pair<uint32_t, uint32_t>> rows;  // kernel rule positions [first, first + count) of each block
     std::vector<uint32_t> rules;
-    uint32_t nr_all = 0;
-    for (const JitChunk* c : chs) nr_all += (uint32_t)c->rules.size();
-    hist_lds = nr_all * 256u <= 48u * 1024u;  // <= 48 KB of status bytes
-    if (!hist_lds)  // (the NOMATCH prefill and the histogram use the LDS status rows)
-      throw std::runtime_error("kvjit: at most 192 rules per kernel (KVGPU_JIT_CHUNK)");
+    uint32_t nr_all = 0, maxb = 1;
+    for (const JitChunk* c : chs) {
+      nr_all += (uint32_t)c->rules.size();
+      maxb = std::max<uint32_t>(maxb, (uint32_t)c->rules.size());
+    }
+    hist_lds = true;
+    if (nr_all > 192u) throw std::runtime_error("kvjit: at most 192 rules per kernel (KVGPU_JIT_CHUNK)");
     block_decls.clear();
     mt_kbase = (uint32_t)(mt_bits.size() / 32u);
     for (const JitChunk* c : chs) {
@@ -1788,12 +1799,9 @@ struct Gen {
       << "(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp, const Node* __restrict__ N, "
          "const Val* __restrict__ V, const uint8_t* __restrict__ S, DevOut O, uint32_t r0) {\n"
       << "  constexpr uint32_t FIN_ = " << u32(FIN) << ", ACT_ = " << u32(ACT) << ", ST_STORED_ = 0x7Eu;\n"
-      << (hist_lds ? "  __shared__ uint32_t s_stw[" + std::to_string(nr * 256u / 4) + "];\n"
-                   : "  __shared__ uint32_t s_hist[" + std::to_string(nr) + "][KV_HIST];\n")
+      << "  __shared__ uint32_t s_stw[" << (KV_WG / 64) * maxb * (KV_ROW / 4) << "];\n"
+      << "  __shared__ uint32_t s_cnt[" << nr * KV_HIST << "], s_scnt[" << nr * KV_HIST << "];\n"
       << "  const DevPS& P = *Pp;\n  const DevBatch& B = *Bp;\n  const uint8_t* __restrict__ pstr = P.pstr;\n";
-    if (!hist_lds)
-      o << "  for (uint32_t q = threadIdx.x; q < " << nr << "u * KV_HIST; q += KV_WG) (&s_hist[0][0])[q] = 0u;\n"
-        << "  __syncthreads();\n";
     // Workgroup b runs tile (b % 8) * n/8 + b / 8, so each XCD (blocks b, b+8, ... share one)
     // walks a contiguous resource range and its L2 sees the values those resources share
     // (the value table and ptab lines are numbered by first occurrence): C2 -0.6 %, C3 -1 %
@@ -1807,15 +1815,21 @@ struct Gen {
       << "  uint32_t root = ABSENT, rkind = KEY_NONE, rflags = 0u, rtup = 0u;\n"
       << "  if (valid) { root = ni(R->root); rkind = R->kind; rflags = R->flags; rtup = R->tup; }\n"
       << "  Node rootn{0u, 0u, 0u, 0u};\n  if (valid) rootn = N[root];\n"
-      << "  const uint32_t* __restrict__ mtr_ = P.mtup + rtup;\n  const uint32_t ntup_ = B.n_tup;\n";
-    if (hist_lds)  // every status row starts as NOMATCH (0xFF past the batch): only matched lanes store
-      o << "  kv_prefill_rows(s_stw, " << nr << "u, r - threadIdx.x, n_res);\n";
+      << "  const uint32_t* __restrict__ mtr_ = P.mtup + rtup;\n  const uint32_t ntup_ = B.n_tup;\n"
+      // the wave's status rows, its first resource; scope of this lane and of the workgroup
+      << "  uint8_t* s_w = (uint8_t*)s_stw + (threadIdx.x >> 6) * " << maxb * KV_ROW << "u;\n"
+      << "  const uint32_t wfirst_ = r - (threadIdx.x & 63u);\n"
+      << "  const uint32_t wg0_ = r - threadIdx.x;\n"
+      << "  const uint32_t sc_ = (O.full & 8u) && valid ? O.scope[r] : 0xFFFFFFFFu;\n"
+      << "  const uint32_t wsc_ = (O.full & 8u) && wg0_ < n_res ? O.scope[wg0_] : 0xFFFFFFFFu;\n"
+      << "  for (uint32_t q = threadIdx.x; q < " << nr * KV_HIST << "u; q += KV_WG) { s_cnt[q] = 0u; s_scnt[q] = 0u; }\n"
+      << "  __syncthreads();\n";
     for (size_t bi = 0; bi < blocks.size(); bi++) {
       // the block's match words (bits of its rules, kv_mtup_kernel); a wave none of whose resources
       // matches any rule of the block skips it whole (every rule NOMATCH on every lane)
       const uint32_t r0 = rows[bi].first, rn = rows[bi].second;
       const uint32_t p0 = mt_kbase * 32u + r0, p1 = p0 + rn;  // bit positions [p0, p1)
-      o << "  {\n";
+      o << "  kv_wprefill(s_w, " << rn << "u, wfirst_, n_res);\n  {\n";
       std::string any = "0u";
       for (uint32_t w = p0 / 32u; w * 32u < p1; w++) {
         const uint32_t lo = std::max(p0, w * 32u) - w * 32u, hi = std::min(p1, w * 32u + 32u) - w * 32u;
@@ -1823,38 +1837,21 @@ struct Gen {
         o << "  const uint32_t mw" << w << " = valid ? mtr_[(size_t)" << w << "u * ntup_] : 0u;\n";
         any += " | (mw" + std::to_string(w) + " & " + u32(m) + ")";
       }
-      if (hist_lds) {
-        // (the rows of a skipped block keep their NOMATCH prefill)
-        o << "  if (__ballot((" << any << ") != 0u) != 0ull) {\n" << blocks[bi] << "  }\n";
-      } else {
-        o << blocks[bi];
-      }
+      // (the rows of a skipped block keep their NOMATCH prefill)
+      o << "  if (__ballot((" << any << ") != 0u) != 0ull) {\n" << blocks[bi] << "  }\n";
       o << "  }\n";
+      o << "  kv_wflush(O, s_w, " << rn << "u, " << name << "_rules + " << r0 << "u, s_cnt + " << r0 * KV_HIST
+        << "u, s_scnt + " << r0 * KV_HIST << "u, n_res, r, valid, sc_, wsc_, P.n_rules);\n";
     }
-    if (hist_lds) {
-      // the status rows staged in LDS go to the status matrix (one byte per rule and lane,
-      // 64 B per wave and rule); one thread per rule counts its 256 status bytes and adds the
-      // non-zero counts
-      o << "  __syncthreads();\n"
-        << "  if ((O.full & 1u) && valid) {\n"
-        << "    const uint8_t* s_b = (const uint8_t*)s_stw + threadIdx.x;\n"
-        << "#pragma unroll 4\n"
-        << "    for (uint32_t q = 0; q < " << nr << "u; q++) O.status[(size_t)" << name
-        << "_rules[q] * n_res + r] = s_b[q * KV_WG];\n"
-        << "  }\n"
-        << "  if (threadIdx.x < " << nr << "u) {\n"
-        << "    const uint32_t* w_ = s_stw + threadIdx.x * (KV_WG / 4u);\n"
-        << "    kv_count_status_lds(w_, O.counts + (size_t)" << name << "_rules[threadIdx.x] * KV_HIST);\n"
-        << "  }\n}\n\n";
-      hist_lds = false;
-      return rules;
-    }
+    // the workgroup's histograms leave with one global atomic per non-zero counter
     o << "  __syncthreads();\n"
-      << "  for (uint32_t q = threadIdx.x; q < " << nr << "u * KV_HIST; q += KV_WG) {\n"
-      << "    const uint32_t v = (&s_hist[0][0])[q];\n"
-      << "    if (v) atomicAdd(&O.counts[(size_t)" << name << "_rules[q / KV_HIST] * KV_HIST + q % KV_HIST], "
-         "(unsigned long long)v);\n"
+      << "  for (uint32_t q = threadIdx.x; q < " << nr * KV_HIST << "u; q += KV_WG) {\n"
+      << "    const uint32_t ri_ = " << name << "_rules[q / KV_HIST], k_ = q % KV_HIST;\n"
+      << "    if (s_cnt[q]) atomicAdd(&O.counts[(size_t)ri_ * KV_HIST + k_], (unsigned long long)s_cnt[q]);\n"
+      << "    if (s_scnt[q]) atomicAdd(&O.scounts[((size_t)wsc_ * P.n_rules + ri_) * KV_HIST + k_], "
+         "(unsigned long long)s_scnt[q]);\n"
       << "  }\n}\n\n";
+    hist_lds = false;
     return rules;
   }
 
@@ -2076,17 +2073,25 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
     // it). Default: ceil(n / chunk_rules) ranges of near-equal size.
     // KVGPU_JIT_WAVES: launch bound in waves per SIMD (default 8, 0: none)
     if (out->plan.empty() && n) {
-      // first bound: 8 waves, or what the kernel's LDS status rows (256 B per rule) leave of a
-      // CU's 160 KB (one workgroup = one wave per SIMD); the spill plan splits blocks (or
-      // lowers the bound) until the compiler meets it
+      // first bound: about 160 KB / (256 B x rules) waves, at most 8 and at most what the
+      // kernel's LDS (kernel_lds) leaves of a CU's 160 KB (one workgroup = one wave per SIMD);
+      // the spill plan splits blocks (or lowers the bound) until the compiler meets it. A kernel
+      // of many rules keeps more state live across its fused blocks, and trading occupancy for
+      // fewer, larger blocks (fewer walks of the resource tree) wins there: C2 (100 rules, one
+      // kernel) 6 waves 4 blocks 0.697 ms, 7 waves 16 blocks 0.902 ms, 8 waves 35 blocks
+      // 1.224 ms per pass (round 4, gpurun_out/r4b/ab); C4's ~70-rule kernels run at 8.
       const char* wz = getenv("KVGPU_JIT_WAVES");
       const uint32_t parts = (n + chunk_rules - 1) / chunk_rules;
       std::vector<uint32_t> sorted;
       for (auto& o : order) sorted.push_back(o.second);
       for (uint32_t k = 0; k < parts; k++) {
         const uint32_t a = (uint32_t)((uint64_t)n * k / parts), e = (uint32_t)((uint64_t)n * (k + 1) / parts);
-        const int lds_waves = (int)std::max<uint32_t>(1u, (160u * 1024u) / std::max<uint32_t>(1u, (e - a) * 256u));
-        out->plan.push_back({a, e - a, wz ? atoi(wz) : std::min(8, lds_waves), g.initial_blocks(sorted, a, e)});
+        std::vector<uint32_t> bl = g.initial_blocks(sorted, a, e);
+        const uint32_t maxb = bl.empty() ? 1u : *std::max_element(bl.begin(), bl.end());
+        // workgroups of 4 waves: waves per SIMD = workgroups per CU the LDS admits
+        const int lds_waves = (int)std::max<uint32_t>(1u, (160u * 1024u) / Gen::kernel_lds(e - a, maxb));
+        const int rule_waves = (int)std::max<uint32_t>(1u, (160u * 1024u) / std::max<uint32_t>(1u, (e - a) * 256u));
+        out->plan.push_back({a, e - a, wz ? atoi(wz) : std::min({8, lds_waves, rule_waves}), bl});
       }
     }
     for (const JitKernelPlan& kp : out->plan) {

@@ -29,6 +29,7 @@ using namespace kv;
 #define KV_RCHUNK 64
 
 #include "kvdevfn.h"
+#include "kvfac.h"
 
 // ------------------------------------------------------------------ kernel
 extern "C" __global__ __launch_bounds__(KV_WG) __attribute__((amdgpu_waves_per_eu(4))) void kv_validate_kernel(const DevPS* __restrict__ Pp,
@@ -381,15 +382,20 @@ hipError_t launch_mtab(const DevPS* P, const DevBatch* B, uint32_t words, uint32
   return hipGetLastError();
 }
 
-// Factored match tables (DevPS::fac_*): grid.z = entity type, grid.y = slot (uniform per
-// workgroup: the slot's filter lists are scalar loads), grid.x = entities of the type.
+// Factored match tables (DevPS::fac_*): grid.z = entity type, grid.y = slot, grid.x = groups
+// of 8 entities; 32 lanes per (entity, slot) evaluate the word's 32 bits at once (lane k: bit
+// k) and a ballot assembles the word (one lane per word walked the 32 filter lists one after
+// the other: 33 us per pass on C2, a chain of dependent loads)
 __global__ __launch_bounds__(KV_WG) void kv_mfac_kernel(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp) {
   const DevPS& P = *Pp;
   const DevBatch& B = *Bp;
-  const uint32_t t = blockIdx.z, s = blockIdx.y, e = blockIdx.x * KV_WG + threadIdx.x;
+  const uint32_t t = blockIdx.z, s = blockIdx.y, k = threadIdx.x & 31u;
+  const uint32_t e = blockIdx.x * (KV_WG / 32) + threadIdx.x / 32u;
   const uint32_t ne = fac_entities(B, t);
-  if (e >= ne) return;
-  P.fac_tab[P.fac_off[t] + (size_t)s * ne + e] = fac_cell(P, B, t, e, s);
+  const bool v = e < ne && fac_bit_of(P, B, t, e, s, k);
+  const uint64_t m = __ballot(v);
+  if (k != 0 || e >= ne) return;
+  P.fac_tab[P.fac_off[t] + (size_t)s * ne + e] = (threadIdx.x & 32u) ? (uint32_t)(m >> 32) : (uint32_t)m;
 }
 
 // Match words per tuple: grid.y = word (uniform plane counts and masks), grid.x = tuples;
@@ -401,6 +407,24 @@ __global__ __launch_bounds__(KV_WG) void kv_mtup_kernel(const DevPS* __restrict_
   const uint32_t t = blockIdx.x * KV_WG + threadIdx.x, w = blockIdx.y;
   if (t >= B.n_tup) return;
   out[(size_t)w * B.n_tup + t] = mtup_word(P, B, t, w);
+}
+
+// out[rule][j] = in[rule][inv[j]]: a status matrix in store order gathered into the caller's
+// resource order (writes coalesced; reads follow the permutation, which keeps runs of a kind
+// and namespace together)
+__global__ __launch_bounds__(KV_WG) void kv_gather_rows_kernel(const uint8_t* __restrict__ in,
+                                                                const uint32_t* __restrict__ inv, uint64_t n_res,
+                                                                uint8_t* __restrict__ out) {
+  const uint64_t j = (uint64_t)blockIdx.x * KV_WG + threadIdx.x, rule = blockIdx.y;
+  if (j < n_res) out[rule * n_res + j] = in[rule * n_res + inv[j]];
+}
+
+hipError_t launch_gather_rows(const uint8_t* in, const uint32_t* inv, uint64_t n_rules, uint64_t n_res, uint8_t* out,
+                              hipStream_t stream) {
+  if (!n_rules || !n_res) return hipSuccess;
+  hipLaunchKernelGGL(kv_gather_rows_kernel, dim3((uint32_t)((n_res + KV_WG - 1) / KV_WG), (uint32_t)n_rules), dim3(KV_WG),
+                     0, stream, in, inv, n_res, out);
+  return hipGetLastError();
 }
 
 // a[i] = map[a[i]] (scope renumbering of a parts session, kv_session_attach_part)
@@ -419,8 +443,8 @@ hipError_t launch_remap_u32(uint32_t* a, uint64_t n, const uint32_t* map, hipStr
 hipError_t launch_mfac(const DevPS* P, const DevBatch* B, uint32_t slots, uint32_t max_entities, uint32_t words,
                        uint32_t n_tup, uint32_t* mtup, hipStream_t stream) {
   if (slots && max_entities)
-    hipLaunchKernelGGL(kv_mfac_kernel, dim3((max_entities + KV_WG - 1) / KV_WG, slots, KV_FAC_TYPES), dim3(KV_WG), 0,
-                       stream, P, B);
+    hipLaunchKernelGGL(kv_mfac_kernel, dim3((max_entities + KV_WG / 32 - 1) / (KV_WG / 32), slots, KV_FAC_TYPES),
+                       dim3(KV_WG), 0, stream, P, B);
   if (words && n_tup)
     hipLaunchKernelGGL(kv_mtup_kernel, dim3((n_tup + KV_WG - 1) / KV_WG, words), dim3(KV_WG), 0, stream, P, B, mtup);
   return hipGetLastError();

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One parameterised GPU call (kernels from the in-tree code-object cache, tools/jit_warm.sh).
 # Steps run in this order, each under its own time limit, stopping at the first failure:
-#   TESTS=1        pytest -m gpu (TESTS_ARGS: extra pytest args, e.g. a -k filter)
+#   TESTS=1        pytest -m gpu (TESTS_K: a -k expression; TESTS_ARGS: extra pytest args)
 #   SMOKE=1        __graft_entry__.smoke()
 #   BENCH=1        the default bench line (C2: e2e leg, CPU baseline, in-run PMC traffic)
 #   PROF=1         rocprofv3 kernel stats of the default bench
@@ -12,8 +12,8 @@ set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"; O="gpurun_out/${OUT:-r4}"; mkdir -p "$O"
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp KVGPU_PROGRESS=1 KVGPU_JIT_CACHE="$R/kyverno_amd/jitcache"
 if [ -n "$TESTS" ]; then
-  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread --durations=20 \
-    $TESTS_ARGS > "$O/gpu_tests.log" 2>&1 || { echo "tests failed"; tail -40 "$O/gpu_tests.log"; exit 1; }
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread --durations=20 \
+    ${TESTS_K:+-k "$TESTS_K"} $TESTS_ARGS > "$O/gpu_tests.log" 2>&1 || { echo "tests failed"; tail -40 "$O/gpu_tests.log"; exit 1; }
   tail -3 "$O/gpu_tests.log"
 fi
 if [ -n "$SMOKE" ]; then

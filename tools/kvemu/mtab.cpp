@@ -3,6 +3,7 @@
 // kv_mfac_kernel / kv_mtup_kernel), with the same prelude the specialized kernels see.
 #include "shim.h"
 #include "../../build/kvgpu/kvjit_prelude.h"
+#include "../../kyverno_amd/csrc/kvfac.h"
 
 extern "C" void kvemu_mtab(const DevPS* P, const DevBatch* B, uint32_t words, uint32_t max_entities, uint32_t* ns,
                            uint32_t* an, uint32_t* sl) {
