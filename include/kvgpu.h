@@ -48,7 +48,8 @@ enum {
 /* kv_validate modes (bit set). KV_MODE_SCOPES adds per-scope counts
  * (scope = namespace; "" = cluster scope), the PolicyReport / ClusterPolicyReport
  * summaries of pkg/kyverno/apply/report.go:76-179 and the background controller's
- * pkg/policyreport/builder.go:245-308; it keeps the status matrix on the device. */
+ * pkg/policyreport/builder.go:245-308; the specialized kernels count them inside the
+ * pass (no status matrix unless KV_MODE_STATUS / KV_MODE_ERRORS is asked for too). */
 enum { KV_MODE_STATUS = 1, KV_MODE_ERRORS = 2, KV_MODE_COUNTS = 4, KV_MODE_SCOPES = 8 };
 
 enum { KV_E_INVALID = -1, KV_E_PARSE = -2, KV_E_DEVICE = -3, KV_E_RANGE = -4, KV_E_NOMEM = -5 };
@@ -146,7 +147,8 @@ double kv_result_kernel_ms(const kv_result* r);
 /* Bulk export of the failing pairs (KV_MODE_ERRORS): every FAIL / ERROR / SKIP pair,
  * rule-major and in resource order: pair i = (rule[i], res[i]); path_id[i] names the
  * failing path of a FAIL pair (KV_PATH_NONE for ERROR / SKIP), rendered once per
- * distinct path by kv_path_string (e.g. "/spec/containers/0/image/"). The arrays and
+ * distinct path by kv_path_string (e.g. "/spec/containers/0/image/"; ids numbered by first
+ * appearance in the returned order). The arrays and
  * strings live as long as the result. This is what a Go caller builds
  * RuleResponse.Message from without one call per pair (validation.go:510-547). */
 enum { KV_PATH_NONE = 0xFFFFFFFFu };

@@ -424,9 +424,9 @@ struct kv_result {
     e.pnode = c.w0 >> 7;
     e.keynode = ABSENT;
     e.resnode = ABSENT;
-    e.idx[0] = c.w1 & 4095u;
-    e.idx[1] = (c.w1 >> 12) & 1023u;
-    e.idx[2] = c.w1 >> 22;
+    e.idx[0] = c.w1 & 1023u;
+    e.idx[1] = (c.w1 >> 10) & 255u;
+    e.idx[2] = (c.w1 >> 18) & 255u;
     e.idx[3] = 0;
     return e;
   }
@@ -845,6 +845,7 @@ struct DevSession {
   uint64_t nrules = 0, nres = 0;
   DevBuf fflags, pview, st, er8, er, cn, scope, scn, ptab, mtab, mtbf, mtup, ftab;
   uint32_t fac_entities = 0, ntup = 0;
+  bool rec_compact = false;  // the last pass wrote records per wave segment (specialized kernels)
   // a part of a parts session owns its batch's device copy (detach_batch): the caller's
   // host batch may be freed once the part is attached
   std::unique_ptr<DevBatchRes> own_batch;
@@ -992,7 +993,8 @@ struct DevSession {
       HIPCHK(hipMemsetAsync(cn.p, 0, cn.n, stream));
       if (mode & KV_MODE_SCOPES) HIPCHK(hipMemsetAsync(scn.p, 0, scn.n, stream));
       HIPCHK(launch_mtab((const DevPS*)pview.p, bview, mt_words, mt_entities, mt_ns, mt_ann, mt_sel, stream));
-      if (dps->specialized() && !vm) {
+      rec_compact = dps->specialized() && !vm;
+      if (rec_compact) {
         launch_specialized();  // (per-scope counts inside the rule kernels)
       } else {
         DevOut Ov = O;
@@ -1081,7 +1083,7 @@ struct DevSession {
       }
       HIPCHK(launch_rec_compact(O.status, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                 (unsigned long long*)r_tot.p, (unsigned long long*)r_base.p, nullptr, nullptr, nullptr,
-                                0, stream));
+                                0, rec_compact, stream));
       part->base.resize(nrules + 1);
       part->offs.resize((size_t)nrules * tiles);
       HIPCHK(hipMemcpyAsync(part->base.data(), r_base.p, part->base.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
@@ -1095,7 +1097,7 @@ struct DevSession {
       HIPCHK(hipMemsetAsync(r_wide.p, 0, sizeof(uint32_t), stream));
       HIPCHK(launch_rec_compact(O.status, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                 nullptr, (unsigned long long*)r_base.p, (ErrRec8*)r_out8.p, nullptr,
-                                (uint32_t*)r_wide.p, 1, stream));
+                                (uint32_t*)r_wide.p, 1, rec_compact, stream));
       part->rec.alloc(total);
       if (total)
         HIPCHK(hipMemcpyAsync(part->rec.data(), r_out8.p, total * sizeof(ErrRec8), hipMemcpyDeviceToHost, stream));
@@ -1112,7 +1114,7 @@ struct DevSession {
         if (r_outw.n < total * sizeof(ErrRec)) r_outw.alloc(std::max<uint64_t>(total, 1) * sizeof(ErrRec), device);
         HIPCHK(launch_rec_compact(O.status, O.err8, O.err, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                   nullptr, (unsigned long long*)r_base.p, (ErrRec8*)r_out8.p, (ErrRec*)r_outw.p,
-                                  (uint32_t*)r_wide.p, 1, stream));
+                                  (uint32_t*)r_wide.p, 1, false, stream));
         part->recw.alloc(total);
         HIPCHK(hipMemcpyAsync(part->recw.data(), r_outw.p, total * sizeof(ErrRec), hipMemcpyDeviceToHost, stream));
       }
@@ -1758,7 +1760,7 @@ int kv_result_failures(const kv_result* cr, uint64_t* n, const uint32_t** rule, 
                 id = it->second;
               } else {
                 const ErrRec e = kv_result::decode(c);
-                const uint64_t key = (uint64_t)path_pnode(ps, e) << 32 | c.w1;
+                const uint64_t key = (uint64_t)path_pnode(ps, e) << 32 | (c.w1 & ERR8_IDX_MASK);
                 auto it = compact.find(key);
                 if (it == compact.end()) {
                   const std::string path = render_path(ps, r->batch_of(p), e);
@@ -1779,22 +1781,48 @@ int kv_result_failures(const kv_result* cr, uint64_t* n, const uint32_t** rule, 
           }
         }
       }
-      if (!r->b->b.order.empty()) {  // caller order: by rule, then caller resource index
-        std::vector<size_t> ix(r->f_rule.size());
-        for (size_t i = 0; i < ix.size(); i++) ix[i] = i;
-        std::sort(ix.begin(), ix.end(), [r](size_t x, size_t y) {
-          return r->f_rule[x] != r->f_rule[y] ? r->f_rule[x] < r->f_rule[y] : r->f_res[x] < r->f_res[y];
-        });
-        std::vector<uint32_t> fr(ix.size()), fp(ix.size());
-        std::vector<uint64_t> fs(ix.size());
-        for (size_t i = 0; i < ix.size(); i++) {
-          fr[i] = r->f_rule[ix[i]];
-          fs[i] = r->f_res[ix[i]];
-          fp[i] = r->f_path[ix[i]];
-        }
-        r->f_rule.swap(fr);
+      if (!r->b->b.order.empty()) {
+        // caller order: by rule, then caller resource index. Each rule's pairs are a subset of
+        // [0, n_res) with distinct caller indices: scattered into a per-thread slot array and
+        // swept in order (rules split over host threads; no comparison sort)
+        std::vector<size_t> rb(r->n_rules + 1, 0);
+        for (size_t i = 0; i < r->f_rule.size(); i++) rb[r->f_rule[i] + 1]++;
+        for (uint32_t rl = 0; rl < r->n_rules; rl++) rb[rl + 1] += rb[rl];
+        std::vector<uint64_t> fs(r->f_res.size());
+        std::vector<uint32_t> fp(r->f_path.size());
+        const unsigned T = std::max(1u, std::min<unsigned>(16u, std::thread::hardware_concurrency()));
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < T; t++)
+          th.emplace_back([&, t]() {
+            std::vector<uint32_t> slot;  // caller index -> path id + 1 (0: no pair)
+            for (uint32_t rl = t; rl < r->n_rules; rl += T) {
+              if (rb[rl] == rb[rl + 1]) continue;
+              if (slot.empty()) slot.assign(r->n_res, 0u);
+              for (size_t i = rb[rl]; i < rb[rl + 1]; i++) slot[r->f_res[i]] = r->f_path[i] + 1u;
+              size_t o = rb[rl];
+              for (uint64_t j = 0; j < r->n_res && o < rb[rl + 1]; j++)
+                if (slot[j]) {
+                  fs[o] = j;
+                  fp[o++] = slot[j] - 1u;
+                  slot[j] = 0u;
+                }
+            }
+          });
+        for (auto& x : th) x.join();
         r->f_res.swap(fs);
         r->f_path.swap(fp);
+        // path ids numbered by first appearance in the returned order
+        std::vector<uint32_t> renum(r->f_paths.size(), KV_PATH_NONE);
+        std::vector<std::string> paths;
+        for (uint32_t& id : r->f_path) {
+          if (id == KV_PATH_NONE) continue;
+          if (renum[id] == KV_PATH_NONE) {
+            renum[id] = (uint32_t)paths.size();
+            paths.push_back(std::move(r->f_paths[id]));
+          }
+          id = renum[id];
+        }
+        r->f_paths.swap(paths);
       }
     });
   } catch (const std::exception&) {

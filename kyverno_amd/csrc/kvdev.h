@@ -34,12 +34,14 @@ hipError_t launch_remap_u32(uint32_t* a, uint64_t n, const uint32_t* map, hipStr
 
 // Error-record compaction in rule-major, resource order. phase 0: offs[rule][tile]
 // (exclusive, tiles of KV_WG resources), totals[rule], base[rule] (base[n_rules] =
-// all records); phase 1: scatter the dense records (and, with errw/outw, the full
-// ones) to out8[base[rule] + offs[rule][tile] + rank]; *wide |= 1 if a compact
-// record is flagged ERR8_WIDE.
+// all records); phase 1: scatter the records (compact: appended per wave segment by the
+// specialized kernels, else at their pair's slot; with errw/outw also the full ones) to
+// out8[base[rule] + offs[rule][tile] + rank]; *wide |= 1 if a compact record is flagged
+// ERR8_WIDE.
 hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const ErrRec* errw, uint32_t n_res,
                               uint32_t n_rules, uint32_t* offs, unsigned long long* totals, unsigned long long* base,
-                              ErrRec8* out8, ErrRec* outw, uint32_t* wide, int phase, hipStream_t stream);
+                              ErrRec8* out8, ErrRec* outw, uint32_t* wide, int phase, bool compact,
+                              hipStream_t stream);
 
 constexpr uint32_t KV_SCOPE_CHUNK = 65536;  // resources per workgroup of the scope-count kernel
 constexpr uint32_t KV_SCOPE_LDS = 2048;     // scopes held in LDS (2048 x 8 x 4 B = 64 KB)

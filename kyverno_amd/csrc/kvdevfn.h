@@ -652,6 +652,17 @@ struct EState {
 // compact form, flagged `wide` when the indices / key do not fit. Passes with
 // O.full bit 2 (re-run by the host only when some record was wide) write the
 // full 32 B form instead; the flag is uniform, so this is a scalar branch.
+// compact record words (kvdevtypes.h ErrRec8) of an error at loop indices i0..i3 on the
+// resource of lane r % 64; `wide` when they do not fit
+__device__ __forceinline__ uint2 err8_pack(uint32_t kind, uint32_t flags, uint32_t pn, uint32_t key, uint32_t i0,
+                                           uint32_t i1, uint32_t i2, uint32_t i3, uint32_t r) {
+  const uint32_t fits = (i0 < 1024u) & (i1 < 256u) & (i2 < 256u) & (i3 == 0u) & (key == ABSENT) & (pn < (1u << 25));
+  uint2 w;
+  w.x = kind | (flags << 4) | ((fits ^ 1u) << 6) | (pn << 7);
+  w.y = (i0 & 1023u) | ((i1 & 255u) << 10) | ((i2 & 255u) << 18) | ((r & 63u) << 26);
+  return w;
+}
+
 // Record of rule ri on resource r: the rule's row base is uniform and r the only per-lane
 // part of the address (a scalar base + 32-bit vector offset store).
 __device__ __forceinline__ void store_err(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, uint32_t kind,
@@ -670,11 +681,7 @@ __device__ __forceinline__ void store_err(const DevOut& O, uint32_t ri, uint32_t
     return;
   }
 #endif
-  const uint32_t fits = (i0 < 4096u) & (i1 < 1024u) & (i2 < 1024u) & (i3 == 0u) & (key == ABSENT) & (pn < (1u << 25));
-  uint2 w;
-  w.x = kind | (flags << 4) | ((fits ^ 1u) << 6) | (pn << 7);
-  w.y = i0 | (i1 << 12) | (i2 << 22);
-  ((uint2*)(O.err8 + (size_t)ri * n_res))[r] = w;
+  ((uint2*)(O.err8 + (size_t)ri * n_res))[r] = err8_pack(kind, flags, pn, key, i0, i1, i2, i3, r);
 }
 
 // number of bytes of w equal to the byte replicated in b4 (exact SWAR zero-byte count)
@@ -707,7 +714,8 @@ __device__ __forceinline__ uint32_t kv_leaf_word(const DevPS& P, const Node* __r
 
 // final status of one rule on this lane: its byte in the wave's LDS row of the rule (KV_ROW
 // bytes per wave; 0xFF: no resource; copied to the status matrix and counted when the block
-// ends, kv_wflush) and, for FAIL / ERROR / SKIP, the error record
+// ends, kv_wflush) and, for FAIL / ERROR / SKIP, the error record, appended to the wave's
+// segment of the rule's record row through the row's LDS counter (ErrRec8 layout)
 // The record address is computed where the record is written: `r` and `ri` (uniform: every
 // caller passes a constant or a wave-uniform member index) pass through empty asm statements
 // so the compiler cannot hoist one address per rule out of the element loops (a wide fused
@@ -722,7 +730,16 @@ __device__ __forceinline__ void kv_final(const DevOut& O, uint32_t ri, uint32_t 
     asm volatile("" : "+v"(r), "+v"(z));
     asm volatile("" : "+s"(ri));
 #endif
+#if defined(KV_JIT_PRELUDE) && !defined(KVEMU)
+    if (!(O.full & 4)) {  // (full records come from a bytecode-engine re-run)
+      const uint32_t slot = atomicAdd((uint32_t*)(s_row + KV_ROW), 1u);  // (one record per lane and rule)
+      if (slot < 64u)
+        ((uint2*)(O.err8 + (size_t)ri * n_res))[(r & ~63u) + slot] =
+            err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, r);
+    }
+#else
     store_err(O, ri, n_res, r, e.kind + z, e.flags, e.pn + z, e.key + z, e.res + z, e.i0, e.i1, e.i2, e.i3);
+#endif
   }
   s_row[threadIdx.x & (KV_ROW - 1u)] = valid ? (uint8_t)st : (uint8_t)0xFFu;
 }
@@ -730,7 +747,7 @@ __device__ __forceinline__ void kv_final(const DevOut& O, uint32_t ri, uint32_t 
 // final status `st` of the members `m` of a rule group (kvjit.cpp: rules whose programs differ
 // only in their leaf predicates and pattern-node ids, evaluated once with one bit per member):
 // member j is rule tab[j] (or ri0 + j * sri), its pattern nodes are the group's shifted by
-// tab[n + j] (or j * spn), its status row is s_row0 + j * KV_ROW; `ekx` is the error of the
+// tab[n + j] (or j * spn), its status row is s_row0 + j * KV_RSTRIDE; `ekx` is the error of the
 // group's representative (kind | flags << 4 | node << 8; 0: none)
 __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_t r, bool valid, uint32_t m, uint32_t st,
                                         uint32_t ekx, uint32_t i0, uint32_t i1, uint32_t i2, uint32_t i3,
@@ -742,7 +759,7 @@ __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_
     const uint32_t ri = __builtin_amdgcn_readfirstlane(tab ? tab[j] : ri0 + j * sri);
     const uint32_t ek = ekx ? ekx + ((tab ? tab[n + j] : j * spn) << 8) : 0u;
     const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
-    kv_final(O, ri, n_res, r, valid, st, e, s_row0 + j * KV_ROW);
+    kv_final(O, ri, n_res, r, valid, st, e, s_row0 + j * KV_RSTRIDE);
   }
 }
 
@@ -769,14 +786,15 @@ __device__ __forceinline__ void kv_wprefill(uint8_t* s_w, uint32_t nr, uint32_t 
 #ifdef KVEMU
   // host emulation runs the lanes one after another: each lane fills its own bytes
   const uint32_t l = threadIdx.x & (KV_ROW - 1u);
-  for (uint32_t q = 0; q < nr; q++) s_w[q * KV_ROW + l] = l < nv ? (uint8_t)ST_NOMATCH : (uint8_t)0xFFu;
+  for (uint32_t q = 0; q < nr; q++) s_w[q * KV_RSTRIDE + l] = l < nv ? (uint8_t)ST_NOMATCH : (uint8_t)0xFFu;
 #else
+  // word k of a row: the status bytes of lanes 4k..4k+3; the last word: the record counter
   uint32_t* w = (uint32_t*)s_w;
-  for (uint32_t i = threadIdx.x & 63u; i < nr * (KV_ROW / 4u); i += 64u) {
-    const uint32_t l = (i % (KV_ROW / 4u)) * 4u;
+  for (uint32_t i = threadIdx.x & 63u; i < nr * (KV_RSTRIDE / 4u); i += 64u) {
+    const uint32_t k4 = i % (KV_RSTRIDE / 4u), l = k4 * 4u;
     uint32_t x = 0u;
     for (uint32_t k = 0u; k < 4u; k++) x |= (l + k < nv ? (uint32_t)ST_NOMATCH : 0xFFu) << (8u * k);
-    w[i] = x;
+    w[i] = k4 == KV_ROW / 4u ? 0u : x;
   }
   kv_wsync();
 #endif
@@ -828,13 +846,13 @@ __device__ __forceinline__ void kv_wflush(const DevOut& O, uint8_t* s_w, uint32_
   const uint32_t l = threadIdx.x & (KV_ROW - 1u);
   if ((O.full & 1u) && valid) {
 #pragma unroll 4
-    for (uint32_t q = 0; q < nr; q++) O.status[(size_t)rules[q] * n_res + r] = s_w[q * KV_ROW + l];
+    for (uint32_t q = 0; q < nr; q++) O.status[(size_t)rules[q] * n_res + r] = s_w[q * KV_RSTRIDE + l];
   }
 #ifndef KVEMU
   const uint64_t all = __ballot(true);
   for (uint32_t q = l; q < nr; q += 64u) {
     uint32_t c[KV_HIST];
-    kv_count_row((const uint32_t*)(s_w + q * KV_ROW), ~0ull, c);
+    kv_count_row((const uint32_t*)(s_w + q * KV_RSTRIDE), ~0ull, c);
     for (uint32_t k = 0; k < (uint32_t)KV_HIST; k++)
       if (c[k] && k != 7u) atomicAdd(&s_cnt[q * KV_HIST + k], c[k]);
   }
@@ -847,7 +865,7 @@ __device__ __forceinline__ void kv_wflush(const DevOut& O, uint8_t* s_w, uint32_
       rem &= ~m;
       for (uint32_t q = l; q < nr; q += 64u) {
         uint32_t c[KV_HIST];
-        kv_count_row((const uint32_t*)(s_w + q * KV_ROW), m, c);
+        kv_count_row((const uint32_t*)(s_w + q * KV_RSTRIDE), m, c);
         for (uint32_t k = 0; k < (uint32_t)KV_HIST; k++) {
           if (!c[k] || k == 7u) continue;
           if (s == wsc) atomicAdd(&s_scnt[q * KV_HIST + k], c[k]);

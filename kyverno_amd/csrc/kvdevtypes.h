@@ -15,14 +15,21 @@ struct ErrRec {
 
 // Compact error record (8 B per FAIL / ERROR / SKIP pair, the one written per pass):
 //   w0 = kind | flags << 4 | wide << 6 | pnode << 7          (pnode < 2^25)
-//   w1 = idx0 | idx1 << 12 | idx2 << 22    (idx0 < 4096, idx1 / idx2 < 1024, idx3 == 0)
+//   w1 = idx0 | idx1 << 10 | idx2 << 18 | lane << 26  (idx0 < 1024, idx1 / idx2 < 256, idx3 == 0;
+//        lane = the resource's lane in its wave)
 // A record that does not fit (larger loop indices, a fourth loop level, a resolved
 // wildcard key) sets `wide`; the host then re-runs the pass with full records
 // (DevOut::full bit 2) into the 32 B ErrRec array.
+// Layout in err8[rule][res]: the bytecode engine writes a record at its pair's slot; the
+// specialized kernels append the records of a wave to the front of the wave's 64-slot segment
+// (err8[rule][wave first resource + k], k in order of writing), so a wave writes whole lines
+// instead of 8 B into 32 B sectors; the fetch restores resource order from the lane field
+// (kv_rec_scatter_kernel).
 struct ErrRec8 {
   uint32_t w0, w1;
 };
 constexpr uint32_t ERR8_WIDE = 1u << 6;
+constexpr uint32_t ERR8_IDX_MASK = (1u << 26) - 1u;  // w1 without the lane
 
 struct DevPS {
   const Inst* prog;
@@ -138,7 +145,8 @@ struct DevOut {
 };
 
 constexpr int KV_WG = 256;
-constexpr uint32_t KV_ROW = 64;  // bytes of one wave status row (one per lane)
+constexpr uint32_t KV_ROW = 64;  // lanes of one wave status row (one status byte each)
+constexpr uint32_t KV_RSTRIDE = KV_ROW + 4u;  // LDS bytes per row: the statuses + the row's record counter
 constexpr uint32_t KV_PTAB_PSEUDO = 3;  // ptab columns of a null, a map and an array node
 constexpr int KV_HIST = 8;
 

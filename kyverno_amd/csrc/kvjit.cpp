@@ -1310,7 +1310,7 @@ struct Gen {
   std::string block_decls;      // declarations the current kernel's blocks need (member tables)
 
   // Code block of one fused chunk inside a kernel body (its own C++ scope); the
-  // chunk's status rows are the wave rows s_w + q * KV_ROW, q = position in the block
+  // chunk's status rows are the wave rows s_w + q * KV_RSTRIDE, q = position in the block
   // (hbase = the block's first position in the kernel: match bits, names).
   //
   // Lean rules (hist_lds kernels): at the end of stage segment k a rule that enters stage
@@ -1394,7 +1394,7 @@ struct Gen {
         g.gn = (uint32_t)G.members.size();
         g.gri = G.members;
         g.gdpn = G.dpn;
-        g.grow = q * KV_ROW;  // the block's wave rows (reused by every block)
+        g.grow = q * KV_RSTRIDE;  // the block's wave rows (reused by every block)
         for (const auto& m : G.preds)
           for (uint32_t pi : m) pred_fn(pi);
         for (size_t i = 0; i < G.leafpcs.size(); i++) {
@@ -1431,7 +1431,7 @@ struct Gen {
       return std::string(m) + std::to_string(k) + "_" + std::to_string(q / 32);
     };
     auto mbit = [&](uint32_t q) { return u32(1u << (q % 32)); };
-    auto row = [&](uint32_t q) { return "s_w + " + u32(q * KV_ROW); };
+    auto row = [&](uint32_t q) { return "s_w + " + u32(q * KV_RSTRIDE); };
     // EState of rule g from its registers (error kind / flags / pattern node in `ekx`)
     auto estate = [&](const RGen* g, const std::string& ekx) {
       std::ostringstream k;
@@ -1482,7 +1482,7 @@ struct Gen {
         for (uint32_t j = 0; j < g.gn; j++) {
           const uint32_t ri = g.gri[j];
           const RuleRec& rr = ps.rules[ri];
-          const std::string rw = "s_w + " + u32(g.grow + j * KV_ROW);
+          const std::string rw = "s_w + " + u32(g.grow + j * KV_RSTRIDE);
           auto st = [&](const std::string& x) {
             return "{ const EState e_{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u}; kv_final(O, " + u32(ri) +
                    ", n_res, r, valid, " + x + ", e_, " + rw + "); }";
@@ -1756,13 +1756,13 @@ struct Gen {
   // One kernel running the fused chunks `chs` one after the other for each
   // resource: a workgroup re-reads its resources' node rows per chunk while they
   // are still cache-resident, instead of one grid-wide pass per chunk.
-  // Statuses: each wave stages the current block's statuses in its own LDS rows (KV_ROW
+  // Statuses: each wave stages the current block's statuses in its own LDS rows (KV_RSTRIDE
   // bytes per rule) and flushes them when the block ends (kv_wprefill / kv_wflush): status
   // matrix, per-rule histogram in LDS, per-scope counts; the histograms leave the workgroup
   // with global atomics when the kernel ends. LDS per workgroup: 4 waves x the largest
   // block's rows + 2 x 32 B per rule of the kernel (kernel_lds).
   static uint32_t kernel_lds(uint32_t nr, uint32_t max_block) {
-    return (uint32_t)(KV_WG / 64) * max_block * KV_ROW + 2u * nr * KV_HIST * 4u;
+    return (uint32_t)(KV_WG / 64) * max_block * KV_RSTRIDE + 2u * nr * KV_HIST * 4u;
   }
   std::vector<uint32_t> group_kernel(const std::string& name, const std::vector<const JitChunk*>& chs, int waves) {
     std::vector<std::string> blocks;
@@ -1791,6 +1791,7 @@ struct Gen {
     o << "__device__ const uint32_t " << name << "_rules[" << nr << "] = {";
     for (uint32_t q = 0; q < nr; q++) o << (q ? ", " : "") << u32(rules[q]);
     o << "};\n";
+
     // Occupancy over registers: the rule kernels are latency-bound on dependent
     // tree loads, so they ask for 8 waves per SIMD (<= 64 VGPRs) unless the plan
     // relaxes it for a kernel that would spill (jit_plan_spills).
@@ -1799,7 +1800,7 @@ struct Gen {
       << "(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp, const Node* __restrict__ N, "
          "const Val* __restrict__ V, const uint8_t* __restrict__ S, DevOut O, uint32_t r0) {\n"
       << "  constexpr uint32_t FIN_ = " << u32(FIN) << ", ACT_ = " << u32(ACT) << ", ST_STORED_ = 0x7Eu;\n"
-      << "  __shared__ uint32_t s_stw[" << (KV_WG / 64) * maxb * (KV_ROW / 4) << "];\n"
+      << "  __shared__ uint32_t s_stw[" << (KV_WG / 64) * maxb * (KV_RSTRIDE / 4) << "];\n"
       << "  __shared__ uint32_t s_cnt[" << nr * KV_HIST << "], s_scnt[" << nr * KV_HIST << "];\n"
       << "  const DevPS& P = *Pp;\n  const DevBatch& B = *Bp;\n  const uint8_t* __restrict__ pstr = P.pstr;\n";
     // Workgroup b runs tile (b % 8) * n/8 + b / 8, so each XCD (blocks b, b+8, ... share one)
@@ -1817,13 +1818,15 @@ struct Gen {
       << "  Node rootn{0u, 0u, 0u, 0u};\n  if (valid) rootn = N[root];\n"
       << "  const uint32_t* __restrict__ mtr_ = P.mtup + rtup;\n  const uint32_t ntup_ = B.n_tup;\n"
       // the wave's status rows, its first resource; scope of this lane and of the workgroup
-      << "  uint8_t* s_w = (uint8_t*)s_stw + (threadIdx.x >> 6) * " << maxb * KV_ROW << "u;\n"
+      << "  uint8_t* s_w = (uint8_t*)s_stw + (threadIdx.x >> 6) * " << maxb * KV_RSTRIDE << "u;\n"
       << "  const uint32_t wfirst_ = r - (threadIdx.x & 63u);\n"
       << "  const uint32_t wg0_ = r - threadIdx.x;\n"
       << "  const uint32_t sc_ = (O.full & 8u) && valid ? O.scope[r] : 0xFFFFFFFFu;\n"
       << "  const uint32_t wsc_ = (O.full & 8u) && wg0_ < n_res ? O.scope[wg0_] : 0xFFFFFFFFu;\n"
       << "  for (uint32_t q = threadIdx.x; q < " << nr * KV_HIST << "u; q += KV_WG) { s_cnt[q] = 0u; s_scnt[q] = 0u; }\n"
       << "  __syncthreads();\n";
+    // one copy of the row prefill / flush per block (a loop over the blocks with a uniform switch
+    // measured 80 VGPRs + 60 spilled on C2's first plan, against 80 + 1 unrolled)
     for (size_t bi = 0; bi < blocks.size(); bi++) {
       // the block's match words (bits of its rules, kv_mtup_kernel); a wave none of whose resources
       // matches any rule of the block skips it whole (every rule NOMATCH on every lane)

@@ -282,9 +282,9 @@ int main(int argc, char** argv) {
       e.pnode = c.w0 >> 7;
       e.keynode = ABSENT;
       e.resnode = ABSENT;
-      e.idx[0] = c.w1 & 4095u;
-      e.idx[1] = (c.w1 >> 12) & 1023u;
-      e.idx[2] = c.w1 >> 22;
+      e.idx[0] = c.w1 & 1023u;
+      e.idx[1] = (c.w1 >> 10) & 255u;
+      e.idx[2] = (c.w1 >> 18) & 255u;
       errw[o] = e;
     }
     wide_any |= wide;
