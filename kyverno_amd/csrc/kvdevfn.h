@@ -880,6 +880,39 @@ __device__ __forceinline__ void kv_wflush(const DevOut& O, uint8_t* s_w, uint32_
   kv_wsync();
 }
 
+// End of a fused block that the whole wave skipped (no lane matches any of its rules): every
+// status is NOMATCH, written and counted without the LDS rows (as kv_wflush would)
+__device__ __forceinline__ void kv_wflush_nomatch(const DevOut& O, uint32_t nr, const uint32_t* rules, uint32_t* s_cnt,
+                                                  uint32_t* s_scnt, uint32_t n_res, uint32_t r, bool valid,
+                                                  uint32_t sc, uint32_t wsc, uint32_t n_rules) {
+  if ((O.full & 1u) && valid) {
+#pragma unroll 4
+    for (uint32_t q = 0; q < nr; q++) O.status[(size_t)rules[q] * n_res + r] = (uint8_t)ST_NOMATCH;
+  }
+#ifndef KVEMU
+  const uint32_t l = threadIdx.x & 63u;
+  const uint64_t vm = __ballot(valid);
+  const uint32_t nv = (uint32_t)__popcll(vm);
+  if (nv)
+    for (uint32_t q = l; q < nr; q += 64u) atomicAdd(&s_cnt[q * KV_HIST + ST_NOMATCH], nv);
+  if (O.full & 8u) {
+    uint64_t rem = vm;
+    while (rem) {
+      const uint32_t s = __builtin_amdgcn_readlane(sc, (uint32_t)__builtin_ctzll(rem));
+      const uint64_t m = __ballot(valid && sc == s) & rem;
+      rem &= ~m;
+      const uint32_t n = (uint32_t)__popcll(m);
+      for (uint32_t q = l; q < nr; q += 64u) {
+        if (s == wsc) atomicAdd(&s_scnt[q * KV_HIST + ST_NOMATCH], n);
+        else atomicAdd(&O.scounts[((size_t)s * n_rules + rules[q]) * KV_HIST + ST_NOMATCH], (unsigned long long)n);
+      }
+    }
+  }
+#else
+  (void)s_cnt; (void)s_scnt; (void)sc; (void)wsc; (void)n_rules;
+#endif
+}
+
 // histogram of one rule's KV_WG status bytes (64 words in LDS) added to counts[KV_HIST]
 __device__ __forceinline__ void kv_count_status_lds(const uint32_t* w, unsigned long long* counts) {
   uint32_t c0 = 0u, c1 = 0u, c5 = 0u, cx = 0u;

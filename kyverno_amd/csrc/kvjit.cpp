@@ -1832,7 +1832,7 @@ struct Gen {
       // matches any rule of the block skips it whole (every rule NOMATCH on every lane)
       const uint32_t r0 = rows[bi].first, rn = rows[bi].second;
       const uint32_t p0 = mt_kbase * 32u + r0, p1 = p0 + rn;  // bit positions [p0, p1)
-      o << "  kv_wprefill(s_w, " << rn << "u, wfirst_, n_res);\n  {\n";
+      o << "  {\n";
       std::string any = "0u";
       for (uint32_t w = p0 / 32u; w * 32u < p1; w++) {
         const uint32_t lo = std::max(p0, w * 32u) - w * 32u, hi = std::min(p1, w * 32u + 32u) - w * 32u;
@@ -1840,11 +1840,18 @@ struct Gen {
         o << "  const uint32_t mw" << w << " = valid ? mtr_[(size_t)" << w << "u * ntup_] : 0u;\n";
         any += " | (mw" + std::to_string(w) + " & " + u32(m) + ")";
       }
-      // (the rows of a skipped block keep their NOMATCH prefill)
-      o << "  if (__ballot((" << any << ") != 0u) != 0ull) {\n" << blocks[bi] << "  }\n";
+      const std::string fargs = std::to_string(rn) + "u, " + name + "_rules + " + std::to_string(r0) + "u, s_cnt + " +
+                                std::to_string(r0 * KV_HIST) + "u, s_scnt + " + std::to_string(r0 * KV_HIST) +
+                                "u, n_res, r, valid, sc_, wsc_, P.n_rules);\n";
+      // a skipped block's statuses are all NOMATCH: written and counted without the rows
+      o << "  if (__ballot((" << any << ") != 0u) != 0ull) {\n"
+        << "  kv_wprefill(s_w, " << rn << "u, wfirst_, n_res);\n"
+        << "  {\n" << blocks[bi] << "  }\n"
+        << "  kv_wflush(O, s_w, " << fargs
+        << "  } else {\n"
+        << "  kv_wflush_nomatch(O, " << fargs
+        << "  }\n";
       o << "  }\n";
-      o << "  kv_wflush(O, s_w, " << rn << "u, " << name << "_rules + " << r0 << "u, s_cnt + " << r0 * KV_HIST
-        << "u, s_scnt + " << r0 * KV_HIST << "u, n_res, r, valid, sc_, wsc_, P.n_rules);\n";
     }
     // the workgroup's histograms leave with one global atomic per non-zero counter
     o << "  __syncthreads();\n"
@@ -2437,7 +2444,12 @@ bool jit_plan_spills(JitImage* img) {
     size_t big = 0;
     for (size_t b = 1; b < np.blocks.size(); b++)
       if (np.blocks[b] > np.blocks[big]) big = b;
-    if (!np.blocks.empty() && np.blocks[big] > 1) {  // the largest block in two halves
+    if (kp.waves > 6 && np.blocks.size() > 1) {
+      // the blocks met the bound alone (jit_refine_blocks) and the kernel still does not: the
+      // pressure crosses blocks, which splitting one block at a time fixes only slowly (C4:
+      // 20+ recompiles); a kernel of multi-block form gives up a wave first (down to 6)
+      np.waves = kp.waves - 1;
+    } else if (!np.blocks.empty() && np.blocks[big] > 1) {  // the largest block in two halves
       const uint32_t c = np.blocks[big], h = c / 2;
       np.blocks[big] = h;
       np.blocks.insert(np.blocks.begin() + big + 1, c - h);

@@ -64,10 +64,10 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out);
 void jit_compile(JitImage* img);
 uint64_t code_bytes(const JitImage& img);
 // Register budget of the plan: no kernel ships with a private (scratch) segment, and a wave
-// bound is kept only when the compiler met it. A kernel that spills (or exceeds the registers)
-// under its bound of w waves per SIMD has its largest block split in two; a kernel of
-// one-rule blocks is compiled at w - 1, then without a bound (a one-rule kernel that still
-// spills: std::runtime_error).
+// bound is kept only when the compiler met it. A multi-block kernel that spills (or exceeds the
+// registers) under a bound of w > 6 waves per SIMD is recompiled at w - 1; otherwise its
+// largest block is split in two; a kernel of one-rule blocks is compiled at w - 1, then
+// without a bound (a one-rule kernel that still spills: std::runtime_error).
 // Returns true when the plan changed (regenerate + compile again; the kernels that did not
 // change come from the code-object cache).
 bool jit_plan_spills(JitImage* img);

@@ -214,9 +214,10 @@ def test_parallel_ingest_matches_serial():
 
 @engines
 def test_wide_error_records(orc, spec):
-    """Failing paths whose loop indices overflow the compact 8 B error record (index >= 4096 at
-    level 0, >= 1024 at levels 1-2, a fourth loop level) or name a resolved wildcard label key:
-    the device writes the full record beside the compact one (kvdevtypes.h ErrRec8)."""
+    """Failing paths whose loop indices overflow the compact 8 B error record (index >= 1024 at
+    level 0, >= 256 at levels 1-2, a fourth loop level) or name a resolved wildcard label key:
+    the pass is re-run writing full records (kvdevtypes.h ErrRec8); indices just below the limits
+    stay compact."""
     def pod(n0, n1, bad0, bad1, labels):
         cs = [{"name": f"c{i}", "image": "nginx:1.0", "ports": [{"containerPort": 80}] * (n1 if i == bad0 else 1)}
               for i in range(n0)]
@@ -231,7 +232,8 @@ def test_wide_error_records(orc, spec):
         return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "d"}, "spec": x}
 
     ress = [pod(5000, 1, 4500, 0, {"app-x": "no"}), pod(3, 2000, 1, 1500, {"app-y": "web"}),
-            pod(10, 3, 2, 1, {"tier": "x"}), deep(1), deep(0)]
+            pod(10, 3, 2, 1, {"tier": "x"}), deep(1), deep(0), pod(1100, 1, 1023, 0, {}), pod(1100, 1, 1024, 0, {}),
+            pod(2, 300, 1, 255, {}), pod(2, 300, 1, 256, {})]
     pol = {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "wide"},
            "spec": {"rules": [
                {"name": "port", "match": {"resources": {"kinds": ["Pod"]}},
@@ -246,6 +248,10 @@ def test_wide_error_records(orc, spec):
     assert r.path(0, 1) == "/spec/containers/1/ports/1500/containerPort/"
     assert r.path(1, 0) == "/metadata/labels/app-x/"
     assert r.path(2, 3) == "/spec/l/1/l/1/l/1/l/1/v/"
+    assert r.path(0, 5) == "/spec/containers/1023/ports/0/containerPort/"
+    assert r.path(0, 6) == "/spec/containers/1024/ports/0/containerPort/"
+    assert r.path(0, 7) == "/spec/containers/1/ports/255/containerPort/"
+    assert r.path(0, 8) == "/spec/containers/1/ports/256/containerPort/"
 
 
 @pytest.mark.gpu
