@@ -132,7 +132,7 @@ struct DevBuf {
 
 struct DevPolicySet {
   DevBuf prog, preds, alts, conjs, atoms, rules, filters, kinds, strrefs, strpairs, sels, sellabels, selexprs, kgs,
-      gsegs, gwords, pstr, fword, fbit, flist, frule;
+      gsegs, gwords, pstr, fword, fbit, flist, frule, rcompact;
   DevPS view{};
   // specialized kernels (KV_COMPILE_SPECIALIZE): one module per kernel program, one
   // function per rule chunk
@@ -538,6 +538,7 @@ DevPolicySet& dev_ps(kv_policyset* s, int device) {
                 local);
       }
     }
+    d->rcompact.upload(J.rec_compact, device);  // record layout per rule (JitImage::rec_compact)
     if (J.mtup_words) {  // factored-match descriptors of the kernels' match bits
       d->mtup_words = J.mtup_words;
       d->fac_slots = J.fac_slots;
@@ -1083,7 +1084,7 @@ struct DevSession {
       }
       HIPCHK(launch_rec_compact(O.status, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                 (unsigned long long*)r_tot.p, (unsigned long long*)r_base.p, nullptr, nullptr, nullptr,
-                                0, rec_compact, stream));
+                                0, rec_compact ? (const uint8_t*)dps->rcompact.p : nullptr, stream));
       part->base.resize(nrules + 1);
       part->offs.resize((size_t)nrules * tiles);
       HIPCHK(hipMemcpyAsync(part->base.data(), r_base.p, part->base.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
@@ -1097,7 +1098,7 @@ struct DevSession {
       HIPCHK(hipMemsetAsync(r_wide.p, 0, sizeof(uint32_t), stream));
       HIPCHK(launch_rec_compact(O.status, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                 nullptr, (unsigned long long*)r_base.p, (ErrRec8*)r_out8.p, nullptr,
-                                (uint32_t*)r_wide.p, 1, rec_compact, stream));
+                                (uint32_t*)r_wide.p, 1, rec_compact ? (const uint8_t*)dps->rcompact.p : nullptr, stream));
       part->rec.alloc(total);
       if (total)
         HIPCHK(hipMemcpyAsync(part->rec.data(), r_out8.p, total * sizeof(ErrRec8), hipMemcpyDeviceToHost, stream));
@@ -1114,7 +1115,7 @@ struct DevSession {
         if (r_outw.n < total * sizeof(ErrRec)) r_outw.alloc(std::max<uint64_t>(total, 1) * sizeof(ErrRec), device);
         HIPCHK(launch_rec_compact(O.status, O.err8, O.err, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                   nullptr, (unsigned long long*)r_base.p, (ErrRec8*)r_out8.p, (ErrRec*)r_outw.p,
-                                  (uint32_t*)r_wide.p, 1, false, stream));
+                                  (uint32_t*)r_wide.p, 1, nullptr, stream));
         part->recw.alloc(total);
         HIPCHK(hipMemcpyAsync(part->recw.data(), r_outw.p, total * sizeof(ErrRec), hipMemcpyDeviceToHost, stream));
       }

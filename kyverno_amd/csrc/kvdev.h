@@ -40,7 +40,7 @@ hipError_t launch_remap_u32(uint32_t* a, uint64_t n, const uint32_t* map, hipStr
 // ERR8_WIDE.
 hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const ErrRec* errw, uint32_t n_res,
                               uint32_t n_rules, uint32_t* offs, unsigned long long* totals, unsigned long long* base,
-                              ErrRec8* out8, ErrRec* outw, uint32_t* wide, int phase, bool compact,
+                              ErrRec8* out8, ErrRec* outw, uint32_t* wide, int phase, const uint8_t* compact,
                               hipStream_t stream);
 
 constexpr uint32_t KV_SCOPE_CHUNK = 65536;  // resources per workgroup of the scope-count kernel

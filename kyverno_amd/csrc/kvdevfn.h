@@ -712,17 +712,20 @@ __device__ __forceinline__ uint32_t kv_leaf_word(const DevPS& P, const Node* __r
   return x;
 }
 
-// final status of one rule on this lane: its byte in the wave's LDS row of the rule (KV_ROW
-// bytes per wave; 0xFF: no resource; copied to the status matrix and counted when the block
-// ends, kv_wflush) and, for FAIL / ERROR / SKIP, the error record, appended to the wave's
-// segment of the rule's record row through the row's LDS counter (ErrRec8 layout)
-// The record address is computed where the record is written: `r` and `ri` (uniform: every
-// caller passes a constant or a wave-uniform member index) pass through empty asm statements
-// so the compiler cannot hoist one address per rule out of the element loops (a wide fused
-// block finalizes dozens of rules inside one loop; hoisted, their addresses alone took 2-4
-// VGPRs or an SGPR pair per rule).
+// record `e` of rule ri on resource r at `slot` of its wave's segment of the rule's record row
+// (slot < 64: a rule ends once per lane)
+__device__ __forceinline__ void kv_rec_put(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, uint32_t slot,
+                                           const EState& e, uint32_t z) {
+  ((uint2*)(O.err8 + (size_t)ri * n_res))[(r & ~63u) + (slot & 63u)] =
+      err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, r);
+}
+
+// final status of one rule on this lane: its byte in status row `row` of the workgroup (s_row;
+// 0xFF: no resource; copied to the status matrix and counted when the kernel ends, kv_end_flush)
+// and, for FAIL / ERROR / SKIP, the error record, appended to the wave's segment of the rule's
+// record row through the wave's counter byte of the row (ErrRec8 layout)
 __device__ __forceinline__ void kv_final(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, bool valid,
-                                         uint32_t st, const EState& e, uint8_t* s_row) {
+                                         uint32_t st, const EState& e, uint8_t* s_row, uint32_t row) {
   if (valid && (O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP)) {
     uint32_t z = 0u;  // an opaque zero: the site's constant record words are built here, not
                       // hoisted out of the loops as one constant register tuple per site
@@ -732,43 +735,85 @@ __device__ __forceinline__ void kv_final(const DevOut& O, uint32_t ri, uint32_t 
 #endif
 #if defined(KV_JIT_PRELUDE) && !defined(KVEMU)
     if (!(O.full & 4)) {  // (full records come from a bytecode-engine re-run)
-      const uint32_t slot = atomicAdd((uint32_t*)(s_row + KV_ROW), 1u);  // (one record per lane and rule)
-      if (slot < 64u)
-        ((uint2*)(O.err8 + (size_t)ri * n_res))[(r & ~63u) + slot] =
-            err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, r);
+      // the row's byte of the wave's counter word; the increment is wave-uniform, so the atomic
+      // optimizer issues one LDS add of popcount(exec) << sh per wave
+      uint8_t* s_c = s_row - KV_ROW0 - row * KV_RSTRIDE + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * KV_KROWS;
+      const uint32_t sh = 8u * (row & 3u);
+      kv_rec_put(O, ri, n_res, r, atomicAdd((uint32_t*)(s_c + (row & ~3u)), 1u << sh) >> sh, e, z);
     }
 #else
     store_err(O, ri, n_res, r, e.kind + z, e.flags, e.pn + z, e.key + z, e.res + z, e.i0, e.i1, e.i2, e.i3);
 #endif
   }
-  s_row[threadIdx.x & (KV_ROW - 1u)] = valid ? (uint8_t)st : (uint8_t)0xFFu;
+  s_row[threadIdx.x] = valid ? (uint8_t)st : (uint8_t)0xFFu;
 }
 
 // final status `st` of the members `m` of a rule group (kvjit.cpp: rules whose programs differ
 // only in their leaf predicates and pattern-node ids, evaluated once with one bit per member):
 // member j is rule tab[j] (or ri0 + j * sri), its pattern nodes are the group's shifted by
-// tab[n + j] (or j * spn), its status row is s_row0 + j * KV_RSTRIDE; `ekx` is the error of the
-// group's representative (kind | flags << 4 | node << 8; 0: none)
+// tab[n + j] (or j * spn), its status row is row0 + j (s_row0 + j * KV_RSTRIDE); `ekx` is the
+// error of the group's representative (kind | flags << 4 | node << 8; 0: none).
+// Records (round 4 A/B, C3 / C2 ms per pass, gpurun_out/ab2): a counter round trip per member
+// 9.38 / 0.71; one wave-level add per 8 members (ballot counts) 10.73 / 0.74 (the ballots
+// doubled the code); a lane-level 64-bit add per 8 members, below, 9.15 / 0.70; groups of
+// n >= KV_GSLOT members write each record at its resource slot instead (no counter; partial
+// lines, C3 writes 7.55 -> 9.74 GB) 8.22 ms.
 __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_t r, bool valid, uint32_t m, uint32_t st,
                                         uint32_t ekx, uint32_t i0, uint32_t i1, uint32_t i2, uint32_t i3,
-                                        uint8_t* s_row0, const uint32_t* tab, uint32_t n, uint32_t ri0,
+                                        uint8_t* s_row0, uint32_t row0, const uint32_t* tab, uint32_t n, uint32_t ri0,
                                         uint32_t sri, uint32_t spn) {
+#if defined(KV_JIT_PRELUDE) && !defined(KVEMU)
+  const bool rec = valid && (O.full & 2) && !(O.full & 4) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP);
+  constexpr uint32_t NW = 5u;  // 64-bit counter words a group of < 32 rows touches
+  const uint32_t w0 = row0 >> 3;
+  unsigned long long old[NW] = {0ull, 0ull, 0ull, 0ull, 0ull};
+  if (n < KV_GSLOT && rec) {
+    // this lane's members as counter bytes: one lane-level add per word returns the slots of
+    // all its members of the word (slots in the order the lanes' adds land; the record carries
+    // its lane). The address is named lane-varying so the atomic optimizer leaves the adds alone.
+    unsigned long long inc[NW] = {0ull, 0ull, 0ull, 0ull, 0ull};
+    for (uint32_t j = 0; j < n; j++)
+      inc[((row0 + j) >> 3) - w0] |= (unsigned long long)((m >> j) & 1u) << (8u * ((row0 + j) & 7u));
+    uint32_t oz = 0u;
+    asm volatile("" : "+v"(oz));
+    unsigned long long* s_c = (unsigned long long*)(s_row0 - KV_ROW0 - row0 * KV_RSTRIDE +
+                                                    __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * KV_KROWS) + w0 + oz;
+    for (uint32_t k = 0; k < NW; k++)
+      if (inc[k]) old[k] = atomicAdd(s_c + k, inc[k]);
+  }
   for (uint32_t j = 0; j < n; j++) {  // uniform over the members (scalar rule ids and rows)
     if (!((m >> j) & 1u)) continue;
     // (j is uniform, so is the member's rule id: named so, the compiler keeps it scalar)
     const uint32_t ri = __builtin_amdgcn_readfirstlane(tab ? tab[j] : ri0 + j * sri);
+    if (rec) {
+      uint32_t z = 0u, rr = r;
+      asm volatile("" : "+v"(rr), "+v"(z));
+      const uint32_t ek = ekx ? ekx + ((tab ? tab[n + j] : j * spn) << 8) : 0u;
+      const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
+      if (n >= KV_GSLOT)
+        ((uint2*)(O.err8 + (size_t)ri * n_res))[rr] = err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, rr);
+      else
+        kv_rec_put(O, ri, n_res, rr, (uint32_t)(old[((row0 + j) >> 3) - w0] >> (8u * ((row0 + j) & 7u))) & 0xFFu, e, z);
+    }
+    s_row0[j * KV_RSTRIDE + threadIdx.x] = valid ? (uint8_t)st : (uint8_t)0xFFu;
+  }
+#else
+  for (uint32_t j = 0; j < n; j++) {
+    if (!((m >> j) & 1u)) continue;
+    const uint32_t ri = __builtin_amdgcn_readfirstlane(tab ? tab[j] : ri0 + j * sri);
     const uint32_t ek = ekx ? ekx + ((tab ? tab[n + j] : j * spn) << 8) : 0u;
     const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
-    kv_final(O, ri, n_res, r, valid, st, e, s_row0 + j * KV_RSTRIDE);
+    kv_final(O, ri, n_res, r, valid, st, e, s_row0 + j * KV_RSTRIDE, row0 + j);
   }
+#endif
 }
 
-// ------------------------------------------------------------------ wave status rows
-// The rule kernels stage one status byte per (rule, lane) in LDS rows private to the wave
-// (KV_ROW bytes per rule and wave, the current fused block's rules only): a row is prefilled
-// with NOMATCH (kv_wprefill), matched lanes store their status (kv_final), and when the block
-// ends the wave copies its rows to the status matrix and counts them (kv_wflush) - no
-// workgroup barrier, and the rows are reused by the next block.
+// ------------------------------------------------------------------ status rows
+// The rule kernels stage one status byte per (rule, lane) in LDS rows of the workgroup
+// (KV_RSTRIDE bytes per rule: KV_WG status bytes + a record counter byte per wave), prefilled
+// with NOMATCH (kv_prefill_rows); matched lanes store their status (kv_final); a fused block
+// that no lane of a wave matches costs that wave nothing. When the kernel ends each wave copies
+// its statuses to the status matrix and counts its segment of every row (kv_end_flush).
 // Ordering inside a wave: LDS operations of one wave execute in program order; the fence
 // keeps the compiler from moving the lanes' row accesses across it.
 __device__ __forceinline__ void kv_wsync() {
@@ -779,33 +824,33 @@ __device__ __forceinline__ void kv_wsync() {
 #endif
 }
 
-// the wave's rows [0, nr) set to NOMATCH for lanes holding a resource, 0xFF past the batch
-// (first = the wave's first resource)
-__device__ __forceinline__ void kv_wprefill(uint8_t* s_w, uint32_t nr, uint32_t first, uint32_t n_res) {
-  const uint32_t nv = n_res > first ? n_res - first : 0u;
+// record counters zeroed and rows [0, nr) set to NOMATCH for the lanes holding a resource (0xFF
+// past the batch); s_stw = the kernel's LDS (KV_ROW0 counter bytes, then the rows), base = the
+// workgroup's first resource
+__device__ __forceinline__ void kv_prefill_rows(uint32_t* s_stw, uint32_t nr, uint32_t base, uint32_t n_res) {
+  const uint32_t nv = n_res > base ? n_res - base : 0u;
 #ifdef KVEMU
   // host emulation runs the lanes one after another: each lane fills its own bytes
-  const uint32_t l = threadIdx.x & (KV_ROW - 1u);
-  for (uint32_t q = 0; q < nr; q++) s_w[q * KV_RSTRIDE + l] = l < nv ? (uint8_t)ST_NOMATCH : (uint8_t)0xFFu;
+  for (uint32_t q = 0; q < nr; q++)
+    ((uint8_t*)s_stw)[KV_ROW0 + q * KV_RSTRIDE + threadIdx.x] = threadIdx.x < nv ? (uint8_t)ST_NOMATCH : (uint8_t)0xFFu;
 #else
-  // word k of a row: the status bytes of lanes 4k..4k+3; the last word: the record counter
-  uint32_t* w = (uint32_t*)s_w;
-  for (uint32_t i = threadIdx.x & 63u; i < nr * (KV_RSTRIDE / 4u); i += 64u) {
-    const uint32_t k4 = i % (KV_RSTRIDE / 4u), l = k4 * 4u;
-    uint32_t x = 0u;
-    for (uint32_t k = 0u; k < 4u; k++) x |= (l + k < nv ? (uint32_t)ST_NOMATCH : 0xFFu) << (8u * k);
-    w[i] = k4 == KV_ROW / 4u ? 0u : x;
-  }
-  kv_wsync();
+  if (threadIdx.x < KV_ROW0 / 4u) s_stw[threadIdx.x] = 0u;
+  // thread t writes status word t % 64 of rows t / 64, t / 64 + 4, ... (one pattern per thread)
+  uint32_t* rows = s_stw + KV_ROW0 / 4u;
+  const uint32_t k = threadIdx.x & 63u, l = k * 4u;
+  uint32_t x = 0u;
+  for (uint32_t j = 0u; j < 4u; j++) x |= (l + j < nv ? (uint32_t)ST_NOMATCH : 0xFFu) << (8u * j);
+  for (uint32_t q = threadIdx.x >> 6; q < nr; q += (uint32_t)KV_WG / 64u) rows[q * (KV_RSTRIDE / 4u) + k] = x;
+  __syncthreads();
 #endif
 }
 
-// histogram of one status row (KV_ROW bytes) restricted to the lanes of mask m (other bytes
-// read as 0xFE, no status), into c[KV_HIST]
-__device__ __forceinline__ void kv_count_row(const uint32_t* w, uint64_t m, uint32_t* c) {
+// histogram of one 64-lane status segment (16 words) restricted to the lanes of mask m (other
+// bytes read as 0xFE, no status), into c[KV_HIST]
+__device__ __forceinline__ void kv_count_seg(const uint32_t* w, uint64_t m, uint32_t* c) {
   uint32_t c0 = 0u, c1 = 0u, c5 = 0u, cx = 0u, n = 0u;
 #pragma unroll 4
-  for (uint32_t i = 0; i < KV_ROW / 4u; i++) {
+  for (uint32_t i = 0; i < 16u; i++) {
     const uint32_t b = (uint32_t)(m >> (4u * i)) & 15u;
     const uint32_t keep = (((b * 0x00204081u) & 0x01010101u) * 0xFFu);  // byte k = 0xFF if bit k
     const uint32_t x = (w[i] & keep) | (0xFEFEFEFEu & ~keep);
@@ -823,7 +868,7 @@ __device__ __forceinline__ void kv_count_row(const uint32_t* w, uint64_t m, uint
     const uint32_t rest[4] = {ST_WARN, ST_ERROR, ST_SKIP, ST_CPU};
     for (uint32_t k = 0; k < 4u; k++) {
       uint32_t q = 0u;
-      for (uint32_t i = 0; i < KV_ROW / 4u; i++) {
+      for (uint32_t i = 0; i < 16u; i++) {
         const uint32_t b = (uint32_t)(m >> (4u * i)) & 15u;
         const uint32_t keep = (((b * 0x00204081u) & 0x01010101u) * 0xFFu);
         q += kv_count_bytes((w[i] & keep) | (0xFEFEFEFEu & ~keep), rest[k] * 0x01010101u);
@@ -833,83 +878,81 @@ __device__ __forceinline__ void kv_count_row(const uint32_t* w, uint64_t m, uint
   }
 }
 
-// End of a fused block for this wave: the rows of the block's nr rules (kernel rules
-// rules[0..nr)) go to the status matrix (O.full & 1), lane q counts row q into the
-// workgroup's LDS histogram s_cnt[q][KV_HIST] (flushed with global atomics when the kernel
-// ends), and with per-scope counts (O.full & 8) into s_scnt for the lanes of the workgroup's
-// scope wsc (the store is ordered by kind and namespace, so a workgroup mostly holds one
-// scope) or straight into O.scounts for lanes of other scopes. `sc` is this lane's scope.
-__device__ __forceinline__ void kv_wflush(const DevOut& O, uint8_t* s_w, uint32_t nr, const uint32_t* rules,
-                                          uint32_t* s_cnt, uint32_t* s_scnt, uint32_t n_res, uint32_t r, bool valid,
-                                          uint32_t sc, uint32_t wsc, uint32_t n_rules) {
-  kv_wsync();
-  const uint32_t l = threadIdx.x & (KV_ROW - 1u);
-  if ((O.full & 1u) && valid) {
-#pragma unroll 4
-    for (uint32_t q = 0; q < nr; q++) O.status[(size_t)rules[q] * n_res + r] = s_w[q * KV_RSTRIDE + l];
-  }
+// End of the rule kernel for this wave: its statuses of the nr rules (kernel rules
+// rules[0..nr)) go to the status matrix (O.full & 1); lane q counts the wave's segment of row q
+// (every lane, and with per-scope counts, O.full & 8, the lanes of the workgroup's scope wsc;
+// lanes of other scopes go straight to O.scounts) and leaves the 16 counts in that segment
+// (counts[KV_HIST], scope counts[KV_HIST]); after a workgroup barrier one thread per (rule,
+// count) sums the four waves' segments into O.counts / O.scounts with a global atomic. The
+// store is ordered by kind and namespace, so a workgroup mostly holds one scope. `sc` is this
+// lane's scope.
+__device__ __forceinline__ void kv_end_flush(const DevOut& O, uint32_t* s_stw, uint32_t nr, const uint32_t* rules,
+                                             uint32_t n_res, uint32_t r, bool valid, uint32_t sc, uint32_t wsc,
+                                             uint32_t n_rules) {
+  const uint8_t* s_b = (const uint8_t*)s_stw + KV_ROW0;
+  __syncthreads();  // (the waves read each other's rows)
 #ifndef KVEMU
-  const uint64_t all = __ballot(true);
-  for (uint32_t q = l; q < nr; q += 64u) {
-    uint32_t c[KV_HIST];
-    kv_count_row((const uint32_t*)(s_w + q * KV_RSTRIDE), ~0ull, c);
-    for (uint32_t k = 0; k < (uint32_t)KV_HIST; k++)
-      if (c[k] && k != 7u) atomicAdd(&s_cnt[q * KV_HIST + k], c[k]);
-  }
-  if (O.full & 8u) {
-    // one pass per distinct scope among the wave's resources (one, inside a namespace run)
-    uint64_t rem = __ballot(valid) & all;
-    while (rem) {
-      const uint32_t s = __builtin_amdgcn_readlane(sc, (uint32_t)__builtin_ctzll(rem));
-      const uint64_t m = __ballot(valid && sc == s) & rem;
-      rem &= ~m;
-      for (uint32_t q = l; q < nr; q += 64u) {
-        uint32_t c[KV_HIST];
-        kv_count_row((const uint32_t*)(s_w + q * KV_RSTRIDE), m, c);
-        for (uint32_t k = 0; k < (uint32_t)KV_HIST; k++) {
-          if (!c[k] || k == 7u) continue;
-          if (s == wsc) atomicAdd(&s_scnt[q * KV_HIST + k], c[k]);
-          else atomicAdd(&O.scounts[((size_t)s * n_rules + rules[q]) * KV_HIST + k], (unsigned long long)c[k]);
-        }
-      }
+  const uint32_t wg0 = r - threadIdx.x;
+  if ((O.full & 1u) && wg0 + (uint32_t)KV_WG <= n_res && (n_res & 15u) == 0u) {
+    // 16 B per lane, 16 lanes per row: each wave store writes 4 rows of the workgroup (C3 9.10
+    // -> 8.96 ms per pass against a byte per lane and row); a partial workgroup, or rows not
+    // 16 B aligned: a byte per lane
+    const uint32_t l = threadIdx.x & 63u, c16 = (l & 15u) * 16u;
+    for (uint32_t q = (threadIdx.x >> 4); q < nr; q += (uint32_t)KV_WG / 16u) {
+      *(uint4*)(O.status + (size_t)rules[q] * n_res + wg0 + c16) = *(const uint4*)(s_b + q * KV_RSTRIDE + c16);
     }
-  }
-#else
-  (void)s_cnt; (void)s_scnt; (void)sc; (void)wsc; (void)n_rules; (void)rules;  // (counts are not emulated)
+  } else
 #endif
-  kv_wsync();
-}
-
-// End of a fused block that the whole wave skipped (no lane matches any of its rules): every
-// status is NOMATCH, written and counted without the LDS rows (as kv_wflush would)
-__device__ __forceinline__ void kv_wflush_nomatch(const DevOut& O, uint32_t nr, const uint32_t* rules, uint32_t* s_cnt,
-                                                  uint32_t* s_scnt, uint32_t n_res, uint32_t r, bool valid,
-                                                  uint32_t sc, uint32_t wsc, uint32_t n_rules) {
   if ((O.full & 1u) && valid) {
 #pragma unroll 4
-    for (uint32_t q = 0; q < nr; q++) O.status[(size_t)rules[q] * n_res + r] = (uint8_t)ST_NOMATCH;
+    for (uint32_t q = 0; q < nr; q++) O.status[(size_t)rules[q] * n_res + r] = s_b[q * KV_RSTRIDE + threadIdx.x];
   }
 #ifndef KVEMU
-  const uint32_t l = threadIdx.x & 63u;
+  const uint32_t l = threadIdx.x & 63u, w = threadIdx.x >> 6;
   const uint64_t vm = __ballot(valid);
-  const uint32_t nv = (uint32_t)__popcll(vm);
-  if (nv)
-    for (uint32_t q = l; q < nr; q += 64u) atomicAdd(&s_cnt[q * KV_HIST + ST_NOMATCH], nv);
+  uint64_t mw = 0ull;  // the wave's lanes of the workgroup's scope
   if (O.full & 8u) {
     uint64_t rem = vm;
-    while (rem) {
+    while (rem) {  // one pass per distinct scope among the wave's resources
       const uint32_t s = __builtin_amdgcn_readlane(sc, (uint32_t)__builtin_ctzll(rem));
       const uint64_t m = __ballot(valid && sc == s) & rem;
       rem &= ~m;
-      const uint32_t n = (uint32_t)__popcll(m);
+      if (s == wsc) {
+        mw = m;
+        continue;
+      }
       for (uint32_t q = l; q < nr; q += 64u) {
-        if (s == wsc) atomicAdd(&s_scnt[q * KV_HIST + ST_NOMATCH], n);
-        else atomicAdd(&O.scounts[((size_t)s * n_rules + rules[q]) * KV_HIST + ST_NOMATCH], (unsigned long long)n);
+        uint32_t c[KV_HIST];
+        kv_count_seg((const uint32_t*)(s_b + q * KV_RSTRIDE + w * 64u), m, c);
+        for (uint32_t k = 0; k < (uint32_t)KV_HIST; k++)
+          if (c[k] && k != 7u) atomicAdd(&O.scounts[((size_t)s * n_rules + rules[q]) * KV_HIST + k], (unsigned long long)c[k]);
       }
     }
   }
+  kv_wsync();
+  for (uint32_t q = l; q < nr; q += 64u) {
+    uint32_t* seg = (uint32_t*)(s_b + q * KV_RSTRIDE + w * 64u);
+    uint32_t c[KV_HIST], cs[KV_HIST];
+    kv_count_seg(seg, ~0ull, c);
+    if (mw) kv_count_seg(seg, mw, cs);
+    else for (uint32_t k = 0; k < (uint32_t)KV_HIST; k++) cs[k] = 0u;
+    for (uint32_t k = 0; k < (uint32_t)KV_HIST; k++) {
+      seg[k] = k == 7u ? 0u : c[k];
+      seg[KV_HIST + k] = k == 7u ? 0u : cs[k];
+    }
+  }
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < nr * 2u * KV_HIST; t += (uint32_t)KV_WG) {
+    const uint32_t q = t / (2u * KV_HIST), k = t % (2u * KV_HIST);
+    uint32_t v = 0u;
+    for (uint32_t x = 0; x < (uint32_t)KV_WG / 64u; x++) v += ((const uint32_t*)(s_b + q * KV_RSTRIDE + x * 64u))[k];
+    if (!v) continue;
+    if (k < (uint32_t)KV_HIST) atomicAdd(&O.counts[(size_t)rules[q] * KV_HIST + k], (unsigned long long)v);
+    else if ((O.full & 8u) && wsc != 0xFFFFFFFFu)
+      atomicAdd(&O.scounts[((size_t)wsc * n_rules + rules[q]) * KV_HIST + (k - KV_HIST)], (unsigned long long)v);
+  }
 #else
-  (void)s_cnt; (void)s_scnt; (void)sc; (void)wsc; (void)n_rules;
+  (void)sc; (void)wsc; (void)n_rules;  // (counts are not emulated)
 #endif
 }
 

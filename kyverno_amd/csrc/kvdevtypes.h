@@ -145,8 +145,14 @@ struct DevOut {
 };
 
 constexpr int KV_WG = 256;
-constexpr uint32_t KV_ROW = 64;  // lanes of one wave status row (one status byte each)
-constexpr uint32_t KV_RSTRIDE = KV_ROW + 4u;  // LDS bytes per row: the statuses + the row's record counter
+// LDS of a specialized rule kernel: the waves' record counters (a byte per (wave, row), wave
+// stride KV_KROWS), then one status row per rule of the kernel (KV_RSTRIDE bytes: a byte per lane)
+constexpr uint32_t KV_RSTRIDE = KV_WG;
+constexpr uint32_t KV_KROWS = 128u;             // most rules (rows) per specialized kernel
+constexpr uint32_t KV_ROW0 = 4u * KV_KROWS;     // byte offset of row 0
+// rule groups of at least this many members write their records at the resource's slot of
+// the record row, the other rules append them to the wave's segment (kvdevfn.h kv_gfin)
+constexpr uint32_t KV_GSLOT = 16u;
 constexpr uint32_t KV_PTAB_PSEUDO = 3;  // ptab columns of a null, a map and an array node
 constexpr int KV_HIST = 8;
 

@@ -1259,6 +1259,7 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
     const std::vector<uint32_t>& order = b->order;
     std::vector<Batch> parts(P);
     std::vector<std::string> errs(P);
+    std::vector<double> tparse(P, 0.0), ttake(P, 0.0);
     std::vector<std::thread> th;
     for (size_t k = 0; k < P; k++)
       th.emplace_back([&, k]() {
@@ -1272,13 +1273,19 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
             const size_t end = i + 1 < nres ? starts[i + 1] : len;
             doc.nodes.clear();
             doc.strs.clear();
+            const auto tp0 = std::chrono::steady_clock::now();
             const size_t used = parse_one(json + starts[i], end - starts[i], NUM_UNSTRUCTURED, &doc);
+            const auto tp1 = std::chrono::steady_clock::now();
+            tparse[k] += std::chrono::duration<double, std::milli>(tp1 - tp0).count();
             if (lines)  // the document must end its line
               for (size_t x = starts[i] + used; x < end; x++)
                 if (json[x] != ' ' && json[x] != '\t' && json[x] != '\r' && json[x] != '\n') throw NotLines();
             in.take(doc);
+            ttake[k] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp1).count();
           }
+          const auto tf0 = std::chrono::steady_clock::now();
           in.flush_group();
+          ttake[k] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count();
         } catch (const NotLines&) {
           errs[k] = "\x01";
         } catch (const std::exception& ex) {
@@ -1291,7 +1298,11 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
     if (relines) continue;  // not one document per line: scan
     for (auto& e : errs)
       if (!e.empty()) throw std::runtime_error(e);
-    if (verbose) fprintf(stderr, "[kvgpu] ingest: %zu threads %.1f ms\n", P, ms());
+    if (verbose) {
+      double tp = 0, tt = 0;
+      for (size_t k = 0; k < P; k++) tp += tparse[k], tt += ttake[k];
+      fprintf(stderr, "[kvgpu] ingest: %zu threads %.1f ms (per thread: parse %.1f ms, take %.1f ms)\n", P, ms(), tp / P, tt / P);
+    }
     merge_batches(parts, *b, (uint32_t)ps.keys.size());
     if (verbose)
       fprintf(stderr, "[kvgpu] ingest: merge %.1f ms (%zu vals, %llu rows, %zu string bytes)\n", ms(), b->vals.size(),

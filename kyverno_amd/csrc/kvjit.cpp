@@ -80,7 +80,7 @@ struct Gen {
   // per rule). Hoisted lookups are branch-free (a failed guard reads cell 0 and discards
   // it) and are placed at the top of their chunk / fused-loop body, so the loads of one
   // tree level issue together instead of one dependent wait per lookup.
-  explicit Gen(const PolicySet& p) : ps(p) {}
+  explicit Gen(const PolicySet& p) : ps(p), rec_slot(p.rules.size(), 0) {}
 
   // leaf predicate `pi` on node expression `n` (arrays: every element): one bit of the
   // value-predicate table
@@ -835,7 +835,7 @@ struct Gen {
     // rule group: the representative's program run once for all members (bit j of `al` = member
     // j alive on this lane); every error is decided where it is raised (kv_gfin)
     bool grp = false;
-    uint32_t gn = 1, grow = 0, gsri = 0, gspn = 0;      // members, LDS row offset of member 0, steps
+    uint32_t gn = 1, grow = 0, gsri = 0, gspn = 0;      // members, LDS row of member 0, steps
     std::vector<uint32_t> gri, gdpn;                    // member rule ids, pattern-node shifts
     std::map<uint32_t, uint32_t> gslot;                 // representative LEAF pc -> slot of member 0
     std::string gtab;                                   // member table (empty: arithmetic)
@@ -929,7 +929,7 @@ struct Gen {
       std::ostringstream r;
       r << "kv_gfin(O, n_res, r, valid, " << m << ", " << st << ", " << u32(kind | (pcn.flags << 4) | (pn << 8));
       for (uint32_t lv = 0; lv < 4; lv++) r << ", " << (lv <= g.max_level ? li(lv) : std::string("0u"));
-      r << ", s_w + " << u32(g.grow) << ", " << (g.gtab.empty() ? std::string("nullptr") : g.gtab) << ", "
+      r << ", s_w + " << u32(KV_ROW0 + g.grow * KV_RSTRIDE) << ", " << u32(g.grow) << ", " << (g.gtab.empty() ? std::string("nullptr") : g.gtab) << ", "
         << u32(g.gn) << ", " << u32(g.gri[0]) << ", " << u32(g.gsri) << ", " << u32(g.gspn) << ");";
       return r.str();
     };
@@ -1291,6 +1291,7 @@ struct Gen {
   // the tuple kernel sets to 1).
   uint32_t mt_kbase = 0;
   std::vector<uint32_t> mt_bits;
+  std::vector<uint8_t> rec_slot;  // rules whose records go to their resource slot (KV_GSLOT)
   bool name_dependent(uint32_t ri) const {
     const RuleRec& rr = ps.rules[ri];
     for (uint32_t f = rr.m_first; f < rr.m_first + rr.m_count; f++)
@@ -1310,8 +1311,7 @@ struct Gen {
   std::string block_decls;      // declarations the current kernel's blocks need (member tables)
 
   // Code block of one fused chunk inside a kernel body (its own C++ scope); the
-  // chunk's status rows are the wave rows s_w + q * KV_RSTRIDE, q = position in the block
-  // (hbase = the block's first position in the kernel: match bits, names).
+  // chunk's status rows are s_stw rows [hbase, hbase + rules) (KV_RSTRIDE bytes each).
   //
   // Lean rules (hist_lds kernels): at the end of stage segment k a rule that enters stage
   // loop k keeps only one bit (am<k>_<w>, bit q of its block position), one that jumps past
@@ -1394,7 +1394,9 @@ struct Gen {
         g.gn = (uint32_t)G.members.size();
         g.gri = G.members;
         g.gdpn = G.dpn;
-        g.grow = q * KV_RSTRIDE;  // the block's wave rows (reused by every block)
+        if (g.gn >= KV_GSLOT)
+          for (uint32_t m : G.members) rec_slot.at(m) = 1;
+        g.grow = hbase + q;
         for (const auto& m : G.preds)
           for (uint32_t pi : m) pred_fn(pi);
         for (size_t i = 0; i < G.leafpcs.size(); i++) {
@@ -1431,7 +1433,8 @@ struct Gen {
       return std::string(m) + std::to_string(k) + "_" + std::to_string(q / 32);
     };
     auto mbit = [&](uint32_t q) { return u32(1u << (q % 32)); };
-    auto row = [&](uint32_t q) { return "s_w + " + u32(q * KV_RSTRIDE); };
+    // status row of block position q: its LDS address and row index
+    auto row = [&](uint32_t q) { return "s_w + " + u32(KV_ROW0 + (hbase + q) * KV_RSTRIDE) + ", " + u32(hbase + q); };
     // EState of rule g from its registers (error kind / flags / pattern node in `ekx`)
     auto estate = [&](const RGen* g, const std::string& ekx) {
       std::ostringstream k;
@@ -1464,7 +1467,7 @@ struct Gen {
       if (!g) return store_st(q, g, st, "0u");
       if (g->grp)  // the members alive here end with the group's status (no error record)
         return "  if ((rs" + s + " & 0xFFu) != ST_STORED_)\n    kv_gfin(O, n_res, r, valid, al" + s + ", rs" + s +
-               " & 0xFFu, 0u, 0u, 0u, 0u, 0u, s_w + " + u32(g->grow) + ", " +
+               " & 0xFFu, 0u, 0u, 0u, 0u, 0u, s_w + " + u32(KV_ROW0 + g->grow * KV_RSTRIDE) + ", " + u32(g->grow) + ", " +
                (g->gtab.empty() ? std::string("nullptr") : g->gtab) + ", " + u32(g->gn) + ", " + u32(g->gri[0]) + ", " +
                u32(g->gsri) + ", " + u32(g->gspn) + ");\n";
       return "  if ((rs" + s + " & 0xFFu) != ST_STORED_" + (hist_lds ? std::string(" && (rs" + s + " & 0xFFu) != ST_NOMATCH") : "") +
@@ -1482,7 +1485,7 @@ struct Gen {
         for (uint32_t j = 0; j < g.gn; j++) {
           const uint32_t ri = g.gri[j];
           const RuleRec& rr = ps.rules[ri];
-          const std::string rw = "s_w + " + u32(g.grow + j * KV_RSTRIDE);
+          const std::string rw = "s_w + " + u32(KV_ROW0 + (g.grow + j) * KV_RSTRIDE) + ", " + u32(g.grow + j);
           auto st = [&](const std::string& x) {
             return "{ const EState e_{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u}; kv_final(O, " + u32(ri) +
                    ", n_res, r, valid, " + x + ", e_, " + rw + "); }";
@@ -1756,23 +1759,25 @@ struct Gen {
   // One kernel running the fused chunks `chs` one after the other for each
   // resource: a workgroup re-reads its resources' node rows per chunk while they
   // are still cache-resident, instead of one grid-wide pass per chunk.
-  // Statuses: each wave stages the current block's statuses in its own LDS rows (KV_RSTRIDE
-  // bytes per rule) and flushes them when the block ends (kv_wprefill / kv_wflush): status
-  // matrix, per-rule histogram in LDS, per-scope counts; the histograms leave the workgroup
-  // with global atomics when the kernel ends. LDS per workgroup: 4 waves x the largest
-  // block's rows + 2 x 32 B per rule of the kernel (kernel_lds).
-  static uint32_t kernel_lds(uint32_t nr, uint32_t max_block) {
-    return (uint32_t)(KV_WG / 64) * max_block * KV_RSTRIDE + 2u * nr * KV_HIST * 4u;
+  // Statuses: one LDS row per rule of the kernel (KV_RSTRIDE bytes: a status byte per lane)
+  // after the waves' record counters (KV_ROW0 bytes: a byte per (wave, rule)), prefilled with NOMATCH, flushed once when the kernel ends
+  // (kv_end_flush: status matrix, per-rule and per-scope histograms). A per-block flush of
+  // wave-private rows (round 4, first build) freed the LDS but cost C5 25 flushes per wave:
+  // 3.91 against 3.25 ms per pass.
+  static uint32_t kernel_lds(uint32_t nr) { return KV_ROW0 + nr * KV_RSTRIDE; }
+  // workgroups of 4 waves a CU's 160 KB LDS admits (= waves per SIMD): allocations are made in
+  // 1280 B granules (C3's 124-rule kernels, 32 240 B, ran at 4 workgroups per CU and 1.3x the
+  // time of the 123-rule ones at 31 980 B; round 4, gpurun_out/r4h)
+  static int lds_waves(uint32_t nr) {
+    const uint32_t g = 1280u, b = (kernel_lds(nr) + g - 1u) / g * g;
+    return (int)std::max<uint32_t>(1u, (160u * 1024u) / std::max(b, g));
   }
   std::vector<uint32_t> group_kernel(const std::string& name, const std::vector<const JitChunk*>& chs, int waves) {
     std::vector<std::string> blocks;
-    std::vector<std::pair<uint32_t, uint32_t>> rows;  // kernel rule positions [first, first + count) of each block
+    std::vector<std::pair<uint32_t, uint32_t>> rows;  // LDS rows [first, first + count) of each block
     std::vector<uint32_t> rules;
-    uint32_t nr_all = 0, maxb = 1;
-    for (const JitChunk* c : chs) {
-      nr_all += (uint32_t)c->rules.size();
-      maxb = std::max<uint32_t>(maxb, (uint32_t)c->rules.size());
-    }
+    uint32_t nr_all = 0;
+    for (const JitChunk* c : chs) nr_all += (uint32_t)c->rules.size();
     hist_lds = true;
     if (nr_all > 192u) throw std::runtime_error("kvjit: at most 192 rules per kernel (KVGPU_JIT_CHUNK)");
     block_decls.clear();
@@ -1791,7 +1796,6 @@ struct Gen {
     o << "__device__ const uint32_t " << name << "_rules[" << nr << "] = {";
     for (uint32_t q = 0; q < nr; q++) o << (q ? ", " : "") << u32(rules[q]);
     o << "};\n";
-
     // Occupancy over registers: the rule kernels are latency-bound on dependent
     // tree loads, so they ask for 8 waves per SIMD (<= 64 VGPRs) unless the plan
     // relaxes it for a kernel that would spill (jit_plan_spills).
@@ -1800,8 +1804,7 @@ struct Gen {
       << "(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp, const Node* __restrict__ N, "
          "const Val* __restrict__ V, const uint8_t* __restrict__ S, DevOut O, uint32_t r0) {\n"
       << "  constexpr uint32_t FIN_ = " << u32(FIN) << ", ACT_ = " << u32(ACT) << ", ST_STORED_ = 0x7Eu;\n"
-      << "  __shared__ uint32_t s_stw[" << (KV_WG / 64) * maxb * (KV_RSTRIDE / 4) << "];\n"
-      << "  __shared__ uint32_t s_cnt[" << nr * KV_HIST << "], s_scnt[" << nr * KV_HIST << "];\n"
+      << "  __shared__ unsigned long long s_stq[" << kernel_lds(nr) / 8 << "];\n  uint32_t* s_stw = (uint32_t*)s_stq;\n"
       << "  const DevPS& P = *Pp;\n  const DevBatch& B = *Bp;\n  const uint8_t* __restrict__ pstr = P.pstr;\n";
     // Workgroup b runs tile (b % 8) * n/8 + b / 8, so each XCD (blocks b, b+8, ... share one)
     // walks a contiguous resource range and its L2 sees the values those resources share
@@ -1817,16 +1820,9 @@ struct Gen {
       << "  if (valid) { root = ni(R->root); rkind = R->kind; rflags = R->flags; rtup = R->tup; }\n"
       << "  Node rootn{0u, 0u, 0u, 0u};\n  if (valid) rootn = N[root];\n"
       << "  const uint32_t* __restrict__ mtr_ = P.mtup + rtup;\n  const uint32_t ntup_ = B.n_tup;\n"
-      // the wave's status rows, its first resource; scope of this lane and of the workgroup
-      << "  uint8_t* s_w = (uint8_t*)s_stw + (threadIdx.x >> 6) * " << maxb * KV_RSTRIDE << "u;\n"
-      << "  const uint32_t wfirst_ = r - (threadIdx.x & 63u);\n"
-      << "  const uint32_t wg0_ = r - threadIdx.x;\n"
-      << "  const uint32_t sc_ = (O.full & 8u) && valid ? O.scope[r] : 0xFFFFFFFFu;\n"
-      << "  const uint32_t wsc_ = (O.full & 8u) && wg0_ < n_res ? O.scope[wg0_] : 0xFFFFFFFFu;\n"
-      << "  for (uint32_t q = threadIdx.x; q < " << nr * KV_HIST << "u; q += KV_WG) { s_cnt[q] = 0u; s_scnt[q] = 0u; }\n"
-      << "  __syncthreads();\n";
-    // one copy of the row prefill / flush per block (a loop over the blocks with a uniform switch
-    // measured 80 VGPRs + 60 spilled on C2's first plan, against 80 + 1 unrolled)
+      << "  uint8_t* s_w = (uint8_t*)s_stw;\n"
+      // every status row starts as NOMATCH (0xFF past the batch): only matched lanes store
+      << "  kv_prefill_rows(s_stw, " << nr << "u, r - threadIdx.x, n_res);\n";
     for (size_t bi = 0; bi < blocks.size(); bi++) {
       // the block's match words (bits of its rules, kv_mtup_kernel); a wave none of whose resources
       // matches any rule of the block skips it whole (every rule NOMATCH on every lane)
@@ -1840,27 +1836,15 @@ struct Gen {
         o << "  const uint32_t mw" << w << " = valid ? mtr_[(size_t)" << w << "u * ntup_] : 0u;\n";
         any += " | (mw" + std::to_string(w) + " & " + u32(m) + ")";
       }
-      const std::string fargs = std::to_string(rn) + "u, " + name + "_rules + " + std::to_string(r0) + "u, s_cnt + " +
-                                std::to_string(r0 * KV_HIST) + "u, s_scnt + " + std::to_string(r0 * KV_HIST) +
-                                "u, n_res, r, valid, sc_, wsc_, P.n_rules);\n";
-      // a skipped block's statuses are all NOMATCH: written and counted without the rows
-      o << "  if (__ballot((" << any << ") != 0u) != 0ull) {\n"
-        << "  kv_wprefill(s_w, " << rn << "u, wfirst_, n_res);\n"
-        << "  {\n" << blocks[bi] << "  }\n"
-        << "  kv_wflush(O, s_w, " << fargs
-        << "  } else {\n"
-        << "  kv_wflush_nomatch(O, " << fargs
-        << "  }\n";
+      // (the rows of a skipped block keep their NOMATCH prefill)
+      o << "  if (__ballot((" << any << ") != 0u) != 0ull) {\n" << blocks[bi] << "  }\n";
       o << "  }\n";
     }
-    // the workgroup's histograms leave with one global atomic per non-zero counter
-    o << "  __syncthreads();\n"
-      << "  for (uint32_t q = threadIdx.x; q < " << nr * KV_HIST << "u; q += KV_WG) {\n"
-      << "    const uint32_t ri_ = " << name << "_rules[q / KV_HIST], k_ = q % KV_HIST;\n"
-      << "    if (s_cnt[q]) atomicAdd(&O.counts[(size_t)ri_ * KV_HIST + k_], (unsigned long long)s_cnt[q]);\n"
-      << "    if (s_scnt[q]) atomicAdd(&O.scounts[((size_t)wsc_ * P.n_rules + ri_) * KV_HIST + k_], "
-         "(unsigned long long)s_scnt[q]);\n"
-      << "  }\n}\n\n";
+    // statuses to the status matrix, per-rule (and per-scope) histograms
+    o << "  const uint32_t wg0_ = r - threadIdx.x;\n"
+      << "  kv_end_flush(O, s_stw, " << nr << "u, " << name << "_rules, n_res, r, valid, "
+         "(O.full & 8u) && valid ? O.scope[r] : 0xFFFFFFFFu, (O.full & 8u) && wg0_ < n_res ? O.scope[wg0_] : 0xFFFFFFFFu, "
+         "P.n_rules);\n}\n\n";
     hist_lds = false;
     return rules;
   }
@@ -2051,7 +2035,8 @@ std::string rule_kind_key(const PolicySet& ps, uint32_t ri) {
 
 uint32_t jit_chunk_rules() {
   const char* ch = getenv("KVGPU_JIT_CHUNK");
-  return ch && atoi(ch) > 0 ? (uint32_t)atoi(ch) : 128u;
+  // (at most KV_KROWS: the kernels' record counters have a byte per (wave, rule))
+  return ch && atoi(ch) > 0 ? std::min<uint32_t>((uint32_t)atoi(ch), KV_KROWS) : KV_KROWS;
 }
 
 void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
@@ -2065,18 +2050,14 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   for (uint32_t ri = 0; ri < ps.rules.size(); ri++) g.match_fn(ri);
   out->chunks.clear();
   const uint32_t n = (uint32_t)ps.rules.size();
-  if (chunk_rules == 0) chunk_rules = 128;
+  if (chunk_rules == 0 || chunk_rules > KV_KROWS) chunk_rules = KV_KROWS;
   {
     // rules that walk the same arrays and leaves share a kernel (and its hoisted lookups)
     std::vector<std::pair<std::string, uint32_t>> order;
-    // rules grouped by the kinds they match first, walk signature second (C5 4.07 -> 3.72 ms,
-    // C3 10.19 -> 10.32; KVGPU_JIT_KINDSORT=0: signature only, for A/B)
-    const bool kind_first = !(getenv("KVGPU_JIT_KINDSORT") && getenv("KVGPU_JIT_KINDSORT")[0] == '0');
+    // rules grouped by the kinds they match first, walk signature second (round 3: C5 4.07 ->
+    // 3.72 ms against signature only, C3 10.19 -> 10.32)
     for (uint32_t ri = 0; ri < n; ri++)
-      order.push_back({ps.rules[ri].route == 0 ? "0" + (kind_first ? rule_kind_key(ps, ri) + "#" : std::string()) +
-                                                     rule_signature(ps, ri)
-                                               : "1",
-                       ri});
+      order.push_back({ps.rules[ri].route == 0 ? "0" + rule_kind_key(ps, ri) + "#" + rule_signature(ps, ri) : "1", ri});
     std::stable_sort(order.begin(), order.end());
     // One kernel per range of the signature order: its rules run as one fused block (every
     // array they walk is walked once per resource, all rules of the range in one loop over
@@ -2091,15 +2072,17 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
       // kernel) 6 waves 4 blocks 0.697 ms, 7 waves 16 blocks 0.902 ms, 8 waves 35 blocks
       // 1.224 ms per pass (round 4, gpurun_out/r4b/ab); C4's ~70-rule kernels run at 8.
       const char* wz = getenv("KVGPU_JIT_WAVES");
-      const uint32_t parts = (n + chunk_rules - 1) / chunk_rules;
+      uint32_t parts = (n + chunk_rules - 1) / chunk_rules;
+      // one more range while the longest ranges would get fewer workgroups per CU than the
+      // shortest (C3: 1 973 rules in 16 ranges of 123/124 -> 17 of 116/117)
+      while (parts < n && Gen::lds_waves((n + parts - 1) / parts) < Gen::lds_waves(n / parts)) parts++;
       std::vector<uint32_t> sorted;
       for (auto& o : order) sorted.push_back(o.second);
       for (uint32_t k = 0; k < parts; k++) {
         const uint32_t a = (uint32_t)((uint64_t)n * k / parts), e = (uint32_t)((uint64_t)n * (k + 1) / parts);
         std::vector<uint32_t> bl = g.initial_blocks(sorted, a, e);
-        const uint32_t maxb = bl.empty() ? 1u : *std::max_element(bl.begin(), bl.end());
         // workgroups of 4 waves: waves per SIMD = workgroups per CU the LDS admits
-        const int lds_waves = (int)std::max<uint32_t>(1u, (160u * 1024u) / Gen::kernel_lds(e - a, maxb));
+        const int lds_waves = Gen::lds_waves(e - a);
         const int rule_waves = (int)std::max<uint32_t>(1u, (160u * 1024u) / std::max<uint32_t>(1u, (e - a) * 256u));
         out->plan.push_back({a, e - a, wz ? atoi(wz) : std::min({8, lds_waves, rule_waves}), bl});
       }
@@ -2128,6 +2111,8 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   }
   out->mtup_words = (uint32_t)(g.mt_bits.size() / 32u);
   if (out->mtup_words && !out->probe) g.build_fac(out);
+  out->rec_compact.assign(n, 1);
+  for (uint32_t ri = 0; ri < n; ri++) out->rec_compact[ri] = g.rec_slot[ri] ? 0 : 1;
   out->memo_preds.clear();
   out->memo_words = 0;
   if (!g.mpreds.empty() && !out->probe) {

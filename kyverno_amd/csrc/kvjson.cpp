@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <emmintrin.h>
 
 namespace kvh {
 
@@ -98,14 +99,25 @@ struct P {
     if (i >= n || s[i] != '"') fail("expected string");
     i++;
     const size_t start = o;
-    // fast path: plain ASCII run
+    // fast path: plain ASCII run (16 bytes per step: quote, backslash, control or non-ASCII)
     while (true) {
       size_t j = i;
+      const __m128i q = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\'), lim = _mm_set1_epi8(0x20);
+      while (j + 16 <= n) {
+        const __m128i x = _mm_loadu_si128((const __m128i*)(s + j));
+        // c < 0x20 or c >= 0x80: one signed compare, c < 0x20 as signed bytes, covers both
+        const __m128i stop = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(x, q), _mm_cmpeq_epi8(x, bs)),
+                                          _mm_cmpgt_epi8(lim, x));
+        const int m = _mm_movemask_epi8(stop);
+        if (m) { j += (size_t)__builtin_ctz((unsigned)m); goto found; }
+        j += 16;
+      }
       while (j < n) {
         unsigned char c = (unsigned char)s[j];
         if (c == '"' || c == '\\' || c < 0x20 || c >= 0x80) break;
         j++;
       }
+    found:
       putn(s + i, j - i);
       i = j;
       if (i >= n) fail("unterminated string");

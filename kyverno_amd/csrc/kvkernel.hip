@@ -455,10 +455,10 @@ hipError_t launch_mfac(const DevPS* P, const DevBatch* B, uint32_t slots, uint32
 // ---------------------------------------------------------------------------
 // Error-record compaction (fetch time, outside the timed passes): the rule
 // kernels write an 8 B record per FAIL / ERROR / SKIP pair, at its [rule][res] slot
-// (bytecode engine) or appended to its wave's 64-slot segment of the rule's row
-// (specialized kernels, `compact`; the record carries its lane); these kernels gather
-// them, rule-major and in resource order, into a compact array, so only the records cross
-// PCIe. Tiles of KV_WG resources: count -> per-rule exclusive scan over tiles -> rule
+// (bytecode engine; specialized rule-group members) or appended to its wave's 64-slot
+// segment of the rule's row (the other specialized rules, compact[rule] = 1; the record
+// carries its lane); these kernels gather them, rule-major and in resource order, into a
+// compact array, so only the records cross PCIe. Tiles of KV_WG resources: count -> per-rule exclusive scan over tiles -> rule
 // bases -> scatter.
 namespace kv {
 
@@ -532,7 +532,8 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_scatter_kernel(const uint8_t* __
                                                                 uint32_t tiles, const uint32_t* __restrict__ offs,
                                                                 const unsigned long long* __restrict__ base,
                                                                 ErrRec8* __restrict__ out8, ErrRec* __restrict__ outw,
-                                                                uint32_t* __restrict__ wide, uint32_t compact) {
+                                                                uint32_t* __restrict__ wide,
+                                                                const uint8_t* __restrict__ compact) {
   __shared__ uint32_t s_w[KV_WG / 64];
   const uint32_t rule = blockIdx.y, r = blockIdx.x * KV_WG + threadIdx.x, lane = threadIdx.x & 63;
   const size_t o = (size_t)rule * n_res + r;
@@ -543,7 +544,7 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_scatter_kernel(const uint8_t* __
   uint32_t before = 0;  // records of the tile's earlier waves
   for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) before += s_w[w];
   const unsigned long long tile0 = base[rule] + offs[(size_t)rule * tiles + blockIdx.x] + before;
-  if (compact) {
+  if (compact && compact[rule]) {  // (rule is uniform: a scalar branch)
     // slot `lane` of the wave's segment holds the wave's lane-th record written; its lane field
     // gives its rank among the wave's record lanes
     if (lane >= (uint32_t)__popcll(m)) return;
@@ -563,7 +564,8 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_scatter_kernel(const uint8_t* __
 
 hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const ErrRec* errw, uint32_t n_res,
                               uint32_t n_rules, uint32_t* offs, unsigned long long* totals, unsigned long long* base,
-                              ErrRec8* out8, ErrRec* outw, uint32_t* wide, int phase, bool compact, hipStream_t stream) {
+                              ErrRec8* out8, ErrRec* outw, uint32_t* wide, int phase, const uint8_t* compact,
+                              hipStream_t stream) {
   if (n_res == 0 || n_rules == 0) return hipSuccess;
   const uint32_t tiles = (n_res + KV_WG - 1) / KV_WG;
   if (phase == 0) {  // offsets and bases
@@ -572,7 +574,7 @@ hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const 
     hipLaunchKernelGGL(kv_rec_base_kernel, dim3(1), dim3(KV_WG), 0, stream, totals, n_rules, base);
   } else {
     hipLaunchKernelGGL(kv_rec_scatter_kernel, dim3(tiles, n_rules), dim3(KV_WG), 0, stream, status, err8, errw, n_res,
-                       tiles, offs, base, out8, outw, wide, compact ? 1u : 0u);
+                       tiles, offs, base, out8, outw, wide, compact);
   }
   return hipGetLastError();
 }
