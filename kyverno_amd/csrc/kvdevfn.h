@@ -755,19 +755,30 @@ __device__ __forceinline__ void kv_final(const DevOut& O, uint32_t ri, uint32_t 
 // error of the group's representative (kind | flags << 4 | node << 8; 0: none).
 // Records (round 4 A/B, C3 / C2 ms per pass, gpurun_out/ab2): a counter round trip per member
 // 9.38 / 0.71; one wave-level add per 8 members (ballot counts) 10.73 / 0.74 (the ballots
-// doubled the code); a lane-level 64-bit add per 8 members, below, 9.15 / 0.70; groups of
-// n >= KV_GSLOT members write each record at its resource slot instead (no counter; partial
-// lines, C3 writes 7.55 -> 9.74 GB) 8.22 ms.
+// doubled the code); a lane-level 64-bit add per 8 members, below, 9.15 / 0.70; `slot` (the
+// generator's choice per group, JitImage::rec_compact): each record at its resource slot
+// instead (no counter; partial lines: C3 writes 7.55 -> 9.74 GB) 8.22 ms. A one-member group
+// (C4's and C5's rules) takes the wave-level add of a single rule: 64 lanes adding to one LDS
+// word serialise.
 __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_t r, bool valid, uint32_t m, uint32_t st,
                                         uint32_t ekx, uint32_t i0, uint32_t i1, uint32_t i2, uint32_t i3,
                                         uint8_t* s_row0, uint32_t row0, const uint32_t* tab, uint32_t n, uint32_t ri0,
-                                        uint32_t sri, uint32_t spn) {
+                                        uint32_t sri, uint32_t spn, bool slot) {
 #if defined(KV_JIT_PRELUDE) && !defined(KVEMU)
+  if (n == 1u && !slot) {  // a one-member group ends like a single rule (one wave-level add)
+    if (m & 1u) {
+      const uint32_t ri = __builtin_amdgcn_readfirstlane(tab ? tab[0] : ri0);
+      const uint32_t ek = ekx ? ekx + ((tab ? tab[1] : 0u) << 8) : 0u;
+      const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
+      kv_final(O, ri, n_res, r, valid, st, e, s_row0, row0);
+    }
+    return;
+  }
   const bool rec = valid && (O.full & 2) && !(O.full & 4) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP);
   constexpr uint32_t NW = 5u;  // 64-bit counter words a group of < 32 rows touches
   const uint32_t w0 = row0 >> 3;
   unsigned long long old[NW] = {0ull, 0ull, 0ull, 0ull, 0ull};
-  if (n < KV_GSLOT && rec) {
+  if (!slot && rec) {
     // this lane's members as counter bytes: one lane-level add per word returns the slots of
     // all its members of the word (slots in the order the lanes' adds land; the record carries
     // its lane). The address is named lane-varying so the atomic optimizer leaves the adds alone.
@@ -790,7 +801,7 @@ __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_
       asm volatile("" : "+v"(rr), "+v"(z));
       const uint32_t ek = ekx ? ekx + ((tab ? tab[n + j] : j * spn) << 8) : 0u;
       const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
-      if (n >= KV_GSLOT)
+      if (slot)
         ((uint2*)(O.err8 + (size_t)ri * n_res))[rr] = err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, rr);
       else
         kv_rec_put(O, ri, n_res, rr, (uint32_t)(old[((row0 + j) >> 3) - w0] >> (8u * ((row0 + j) & 7u))) & 0xFFu, e, z);

@@ -150,9 +150,6 @@ constexpr int KV_WG = 256;
 constexpr uint32_t KV_RSTRIDE = KV_WG;
 constexpr uint32_t KV_KROWS = 128u;             // most rules (rows) per specialized kernel
 constexpr uint32_t KV_ROW0 = 4u * KV_KROWS;     // byte offset of row 0
-// rule groups of at least this many members write their records at the resource's slot of
-// the record row, the other rules append them to the wave's segment (kvdevfn.h kv_gfin)
-constexpr uint32_t KV_GSLOT = 16u;
 constexpr uint32_t KV_PTAB_PSEUDO = 3;  // ptab columns of a null, a map and an array node
 constexpr int KV_HIST = 8;
 

@@ -66,6 +66,14 @@ std::string f64(double v) {
   return "__longlong_as_double(" + i64((int64_t)b) + ")";
 }
 
+// rule groups of at least this many members write their records at the resource's slot of the
+// record row; the other rules append theirs to the wave's segment (kvdevfn.h kv_gfin). Round 4
+// (gpurun_out/ab3, ms per pass / GB written): from 16 members C2 0.720 / 0.47 (its 20- and
+// 21-member image-glob groups go to slots), C3 8.22 / 9.7; from 22 C2 0.701 / 0.40, C3 8.24 /
+// 9.4; never C2 0.699 / 0.40, C3 9.13 / 7.5.
+constexpr uint32_t kGslotMembers = 22u;
+uint32_t gslot_members() { return kGslotMembers; }
+
 struct Gen {
   const PolicySet& ps;
   std::ostringstream o;
@@ -930,7 +938,8 @@ struct Gen {
       r << "kv_gfin(O, n_res, r, valid, " << m << ", " << st << ", " << u32(kind | (pcn.flags << 4) | (pn << 8));
       for (uint32_t lv = 0; lv < 4; lv++) r << ", " << (lv <= g.max_level ? li(lv) : std::string("0u"));
       r << ", s_w + " << u32(KV_ROW0 + g.grow * KV_RSTRIDE) << ", " << u32(g.grow) << ", " << (g.gtab.empty() ? std::string("nullptr") : g.gtab) << ", "
-        << u32(g.gn) << ", " << u32(g.gri[0]) << ", " << u32(g.gsri) << ", " << u32(g.gspn) << ");";
+        << u32(g.gn) << ", " << u32(g.gri[0]) << ", " << u32(g.gsri) << ", " << u32(g.gspn) << ", "
+        << (g.gn >= gslot_members() ? "true" : "false") << ");";
       return r.str();
     };
     auto raise = [&](uint32_t kind, uint32_t pn, uint32_t catch_pc) {
@@ -1291,7 +1300,7 @@ struct Gen {
   // the tuple kernel sets to 1).
   uint32_t mt_kbase = 0;
   std::vector<uint32_t> mt_bits;
-  std::vector<uint8_t> rec_slot;  // rules whose records go to their resource slot (KV_GSLOT)
+  std::vector<uint8_t> rec_slot;  // rules whose records go to their resource slot (gslot_members)
   bool name_dependent(uint32_t ri) const {
     const RuleRec& rr = ps.rules[ri];
     for (uint32_t f = rr.m_first; f < rr.m_first + rr.m_count; f++)
@@ -1394,7 +1403,7 @@ struct Gen {
         g.gn = (uint32_t)G.members.size();
         g.gri = G.members;
         g.gdpn = G.dpn;
-        if (g.gn >= KV_GSLOT)
+        if (g.gn >= gslot_members())
           for (uint32_t m : G.members) rec_slot.at(m) = 1;
         g.grow = hbase + q;
         for (const auto& m : G.preds)
@@ -1469,7 +1478,7 @@ struct Gen {
         return "  if ((rs" + s + " & 0xFFu) != ST_STORED_)\n    kv_gfin(O, n_res, r, valid, al" + s + ", rs" + s +
                " & 0xFFu, 0u, 0u, 0u, 0u, 0u, s_w + " + u32(KV_ROW0 + g->grow * KV_RSTRIDE) + ", " + u32(g->grow) + ", " +
                (g->gtab.empty() ? std::string("nullptr") : g->gtab) + ", " + u32(g->gn) + ", " + u32(g->gri[0]) + ", " +
-               u32(g->gsri) + ", " + u32(g->gspn) + ");\n";
+               u32(g->gsri) + ", " + u32(g->gspn) + ", " + (g->gn >= gslot_members() ? "true" : "false") + ");\n";
       return "  if ((rs" + s + " & 0xFFu) != ST_STORED_" + (hist_lds ? std::string(" && (rs" + s + " & 0xFFu) != ST_NOMATCH") : "") +
              ") {\n" + store_st(q, g, st, "ek" + s) + "  }\n";
     };

@@ -48,7 +48,7 @@ struct JitImage {
   std::vector<uint32_t> fac_word, fac_bit, fac_flist, fac_rule;
   uint32_t fac_slots = 0;
   // per rule: 1 = its records are appended to its wave's 64-slot segment (lane in the record),
-  // 0 = at the resource's slot (members of rule groups of >= KV_GSLOT rules; kvdevfn.h kv_gfin)
+  // 0 = at the resource's slot (members of large rule groups; kvjit.cpp gslot_members)
   std::vector<uint8_t> rec_compact;
   bool probe = false;       // a block-probe image (jit_refine_blocks): rule kernels only
   double gen_ms = 0, compile_ms = 0;
