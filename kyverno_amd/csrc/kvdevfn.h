@@ -912,6 +912,9 @@ __device__ __forceinline__ void kv_end_flush(const DevOut& O, uint32_t* s_stw, u
     for (uint32_t q = (threadIdx.x >> 4); q < nr; q += (uint32_t)KV_WG / 16u) {
       *(uint4*)(O.status + (size_t)rules[q] * n_res + wg0 + c16) = *(const uint4*)(s_b + q * KV_RSTRIDE + c16);
     }
+    // (a wave copies the other waves' segments, which they overwrite with counts below; the
+    // condition is uniform over the workgroup)
+    __syncthreads();
   } else
 #endif
   if ((O.full & 1u) && valid) {
