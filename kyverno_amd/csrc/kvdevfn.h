@@ -970,30 +970,6 @@ __device__ __forceinline__ void kv_end_flush(const DevOut& O, uint32_t* s_stw, u
 #endif
 }
 
-// histogram of one rule's KV_WG status bytes (64 words in LDS) added to counts[KV_HIST]
-__device__ __forceinline__ void kv_count_status_lds(const uint32_t* w, unsigned long long* counts) {
-  uint32_t c0 = 0u, c1 = 0u, c5 = 0u, cx = 0u;
-#pragma unroll 8
-  for (uint32_t i = 0; i < KV_WG / 4u; i++) {
-    const uint32_t x = w[i];
-    c0 += kv_count_bytes(x, 0x00000000u);
-    c1 += kv_count_bytes(x, 0x01010101u);
-    c5 += kv_count_bytes(x, 0x05050505u);
-    cx += kv_count_bytes(x, 0xFFFFFFFFu);
-  }
-  if (c0) atomicAdd(&counts[ST_PASS], (unsigned long long)c0);
-  if (c1) atomicAdd(&counts[ST_FAIL], (unsigned long long)c1);
-  if (c5) atomicAdd(&counts[ST_NOMATCH], (unsigned long long)c5);
-  if (c0 + c1 + c5 + cx < (uint32_t)KV_WG) {
-    const uint32_t rest[4] = {ST_WARN, ST_ERROR, ST_SKIP, ST_CPU};
-    for (uint32_t k = 0; k < 4u; k++) {
-      uint32_t c = 0u;
-      for (uint32_t i = 0; i < KV_WG / 4u; i++) c += kv_count_bytes(w[i], rest[k] * 0x01010101u);
-      if (c) atomicAdd(&counts[rest[k]], (unsigned long long)c);
-    }
-  }
-}
-
 // status + error record (FAIL/ERROR/SKIP) + per-rule histogram with the
 // common statuses counted by one ballot each (fused specialized kernels)
 __device__ __forceinline__ void store_result2(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, bool valid,

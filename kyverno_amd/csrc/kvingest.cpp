@@ -1033,7 +1033,7 @@ std::string_view raw_string_of(const char* p, size_t n, const char* key, size_t 
 // matches other kinds only is skipped by whole waves (its match fails uniformly) instead of
 // running its pattern walk for the few lanes of a mixed wave (C5: 6.1 -> 4.3 ms per pass); and
 // resources of one namespace share waves and workgroups, so the rule kernels count per-scope
-// PolicyReport results for a whole wave at once (kv_wflush) and neighbouring resources share
+// PolicyReport results for a whole wave at once (kv_end_flush) and neighbouring resources share
 // match tuples.
 std::vector<uint32_t> store_order(const std::vector<std::string_view>& kinds, const std::vector<std::string_view>& nss,
                                   unsigned T) {
@@ -1109,6 +1109,11 @@ std::vector<uint32_t> store_order(const std::vector<std::string_view>& kinds, co
   return order;
 }
 
+// The match inputs of a resource: every Res field the match code reads (kvfac.h, the generated
+// g_blk_* filters: kind, group, version, nsm, lset, aset, ns_index, flags; name-dependent rules
+// are evaluated per resource behind bit 1). A new match input in Res must join the key; the
+// assert trips when Res changes shape.
+static_assert(sizeof(Res) == 64, "Res changed: check that tuple_key still covers every match input");
 static void tuple_key(const Res& r, uint32_t* k) {
   k[0] = r.kind; k[1] = r.group; k[2] = r.version; k[3] = r.nsm;
   k[4] = r.lset; k[5] = r.aset; k[6] = r.ns_index; k[7] = r.flags;

@@ -891,9 +891,9 @@ struct Gen {
   };
 
   HoistTable* gT = nullptr;  // global (root-derived) hoist table of the current chunk
-  // per-rule histogram of a group kernel from its statuses staged in LDS (one byte per rule and
-  // lane, counted once at the end: kv_count_status_lds); kernels of more than 192 rules (48 KB of
-  // status bytes) count with ballots + LDS atomics per rule and wave instead
+  // per-rule histogram of a rule kernel from its statuses staged in LDS (one byte per rule and
+  // lane, counted once when the kernel ends: kv_end_flush); otherwise (store_result2) with ballots
+  // + LDS atomics per rule and wave
   bool hist_lds = false;
 
   void emit_region(RGen& g, const Region& R, std::ostringstream& w) {
