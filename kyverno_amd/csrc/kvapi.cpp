@@ -997,6 +997,9 @@ struct DevSession {
       rec_compact = dps->specialized() && !vm;
       if (rec_compact) {
         launch_specialized();  // (per-scope counts inside the rule kernels)
+        if (O.full & 8u)  // per-rule totals from the per-scope counts (the kernels add only those)
+          HIPCHK(launch_scope_totals((const unsigned long long*)scn.p, nscopes, (uint32_t)nrules,
+                                     (unsigned long long*)cn.p, stream));
       } else {
         DevOut Ov = O;
         Ov.full &= ~8u;

@@ -47,6 +47,8 @@ constexpr uint32_t KV_SCOPE_CHUNK = 65536;  // resources per workgroup of the sc
 constexpr uint32_t KV_SCOPE_LDS = 2048;     // scopes held in LDS (2048 x 8 x 4 B = 64 KB)
 
 // counts[scope][rule][KV_HIST] += histogram of status[rule][res] by scope[res]
+hipError_t launch_scope_totals(const unsigned long long* scounts, uint32_t n_scopes, uint32_t n_rules,
+                               unsigned long long* counts, hipStream_t stream);
 hipError_t launch_scope_counts(const uint8_t* status, const uint32_t* scope, uint32_t n_res, uint32_t n_rules,
                                uint32_t n_scopes, unsigned long long* out, hipStream_t stream);
 

@@ -948,7 +948,8 @@ __device__ __forceinline__ void kv_end_flush(const DevOut& O, uint32_t* s_stw, u
     uint32_t* seg = (uint32_t*)(s_b + q * KV_RSTRIDE + w * 64u);
     uint32_t c[KV_HIST], cs[KV_HIST];
     kv_count_seg(seg, ~0ull, c);
-    if (mw) kv_count_seg(seg, mw, cs);
+    if (mw == vm) for (uint32_t k = 0; k < (uint32_t)KV_HIST; k++) cs[k] = c[k];  // (one scope: the common case)
+    else if (mw) kv_count_seg(seg, mw, cs);
     else for (uint32_t k = 0; k < (uint32_t)KV_HIST; k++) cs[k] = 0u;
     for (uint32_t k = 0; k < (uint32_t)KV_HIST; k++) {
       seg[k] = k == 7u ? 0u : c[k];
@@ -961,8 +962,10 @@ __device__ __forceinline__ void kv_end_flush(const DevOut& O, uint32_t* s_stw, u
     uint32_t v = 0u;
     for (uint32_t x = 0; x < (uint32_t)KV_WG / 64u; x++) v += ((const uint32_t*)(s_b + q * KV_RSTRIDE + x * 64u))[k];
     if (!v) continue;
-    if (k < (uint32_t)KV_HIST) atomicAdd(&O.counts[(size_t)rules[q] * KV_HIST + k], (unsigned long long)v);
-    else if ((O.full & 8u) && wsc != 0xFFFFFFFFu)
+    if (k < (uint32_t)KV_HIST) {
+      // (with per-scope counts the per-rule totals are their sum, kv_scope_totals_kernel)
+      if (!(O.full & 8u)) atomicAdd(&O.counts[(size_t)rules[q] * KV_HIST + k], (unsigned long long)v);
+    } else if ((O.full & 8u) && wsc != 0xFFFFFFFFu)
       atomicAdd(&O.scounts[((size_t)wsc * n_rules + rules[q]) * KV_HIST + (k - KV_HIST)], (unsigned long long)v);
   }
 #else

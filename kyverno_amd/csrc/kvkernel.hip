@@ -646,6 +646,28 @@ hipError_t launch_scope_counts(const uint8_t* status, const uint32_t* scope, uin
   return hipGetLastError();
 }
 
+// counts[rule][k] = sum over scopes of scounts[scope][rule][k]: the per-rule histogram of a
+// SCOPES pass of the specialized kernels, which add to the per-scope counts only
+// (kvdevfn.h kv_end_flush); one thread per (rule, status), coalesced over the scopes' rows
+__global__ __launch_bounds__(KV_WG) void kv_scope_totals_kernel(const unsigned long long* __restrict__ sc,
+                                                                uint32_t n_scopes, uint32_t n,
+                                                                unsigned long long* __restrict__ counts) {
+  const uint32_t i = blockIdx.x * KV_WG + threadIdx.x;
+  if (i >= n) return;
+  unsigned long long t = 0ull;
+  for (uint32_t s = 0; s < n_scopes; s++) t += sc[(size_t)s * n + i];
+  counts[i] = t;
+}
+
+hipError_t launch_scope_totals(const unsigned long long* scounts, uint32_t n_scopes, uint32_t n_rules,
+                               unsigned long long* counts, hipStream_t stream) {
+  const uint32_t n = n_rules * (uint32_t)KV_HIST;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(kv_scope_totals_kernel, dim3((n + KV_WG - 1) / KV_WG), dim3(KV_WG), 0, stream, scounts, n_scopes,
+                     n, counts);
+  return hipGetLastError();
+}
+
 // One wave per row of the wave-group layout: lane l takes its packed cell (the number of
 // set mask bits below l is its rank in the row) or the zero cell. Reads the packed cells
 // and masks once, writes every cell once (coalesced 1 KB per row).
