@@ -70,31 +70,43 @@ KV_FN const uint32_t* fac_table(const DevPS& P, uint32_t t) { return P.fac_tab +
 // Match word w of tuple t: OR over the match planes of the AND of the five factors, minus the
 // OR of the exclude planes; rules with name filters keep bit 1 (their rule kernel evaluates
 // the match per resource), rules with more planes than KV_FAC_MAXP run rule_matches here.
-KV_FN uint32_t mtup_word(const DevPS& P, const DevBatch& B, uint32_t t, uint32_t w) {
+// a tuple's entities (read once per tuple, for all the words a thread computes)
+struct MtupIn {
+  const Res* R;
+  uint32_t eK, eN, eA, eL, eS, rflags, kex;
+};
+KV_FN MtupIn mtup_in(const DevBatch& B, uint32_t t) {
   const Res* __restrict__ R = B.res + B.tup_rep[t];
+  MtupIn in{R, B.tup_kent[t], R->nsm, R->aset, R->lset, R->ns_index, R->flags, 0u};
+  in.kex = (in.rflags & (RF_KIND_NAMESPACE | RF_KIND_EMPTY)) ? 0xFFFFFFFFu : 0u;
+  return in;
+}
+KV_FN uint32_t mtup_word_in(const DevPS& P, const DevBatch& B, const MtupIn& in, uint32_t w) {
   const uint32_t s0 = sld(P.fac_word + 4u * w), np = sld(P.fac_word + 4u * w + 1u);
   const uint32_t named = sld(P.fac_word + 4u * w + 2u), cx = sld(P.fac_word + 4u * w + 3u);
   const uint32_t nm = np & 0xFFu, nx = (np >> 8) & 0xFFu;
-  const uint32_t eK = B.tup_kent[t], eN = R->nsm, eA = R->aset, eL = R->lset, eS = R->ns_index, rflags = R->flags;
   const uint32_t nK = B.n_kent, nN = B.n_nsm, nA = B.n_asets, nL = B.n_lsets, nS = B.n_ns;
   const uint32_t* __restrict__ tK = fac_table(P, KV_FAC_KIND);
   const uint32_t* __restrict__ tN = fac_table(P, KV_FAC_NSM);
   const uint32_t* __restrict__ tA = fac_table(P, KV_FAC_ANN);
   const uint32_t* __restrict__ tL = fac_table(P, KV_FAC_SEL);
   const uint32_t* __restrict__ tS = fac_table(P, KV_FAC_NS);
-  const uint32_t kex = (rflags & (RF_KIND_NAMESPACE | RF_KIND_EMPTY)) ? 0xFFFFFFFFu : 0u;
   uint32_t m = 0u, x = 0u;
   for (uint32_t p = 0; p < nm + nx; p++) {
     const size_t s = s0 + p;
-    const uint32_t v = tK[s * nK + eK] & tN[s * nN + eN] & tA[s * nA + eA] & tL[s * nL + eL] & (tS[s * nS + eS] | kex);
+    const uint32_t v =
+        tK[s * nK + in.eK] & tN[s * nN + in.eN] & tA[s * nA + in.eA] & tL[s * nL + in.eL] & (tS[s * nS + in.eS] | in.kex);
     if (p < nm) m |= v;
     else x |= v;
   }
   m = (m & ~x) | named;
   for (uint32_t c = cx; c; c &= c - 1u) {
     const uint32_t b = (uint32_t)__builtin_ctz(c);
-    if (rule_matches(P, B, R, R->kind, rflags, P.rules[sld(P.fac_rule + 32u * w + b)])) m |= 1u << b;
+    if (rule_matches(P, B, in.R, in.R->kind, in.rflags, P.rules[sld(P.fac_rule + 32u * w + b)])) m |= 1u << b;
   }
   return m;
+}
+KV_FN uint32_t mtup_word(const DevPS& P, const DevBatch& B, uint32_t t, uint32_t w) {
+  return mtup_word_in(P, B, mtup_in(B, t), w);
 }
 

@@ -398,15 +398,20 @@ __global__ __launch_bounds__(KV_WG) void kv_mfac_kernel(const DevPS* __restrict_
   P.fac_tab[P.fac_off[t] + (size_t)s * ne + e] = (threadIdx.x & 32u) ? (uint32_t)(m >> 32) : (uint32_t)m;
 }
 
-// Match words per tuple: grid.y = word (uniform plane counts and masks), grid.x = tuples;
-// mtup[w * n_tup + t] (word-major: a wave writes 256 contiguous bytes)
+// Match words per tuple: grid.x = tuples, grid.y = runs of KV_MTUP_WORDS words (uniform plane
+// counts and masks); a thread reads its tuple's entities once for its run of words (one word
+// per thread re-read the tuple's Res for every word: C3, 62 words, 2.9 GB per pass);
+// mtup[w * n_tup + t] (word-major: a wave writes 256 contiguous bytes per word)
+constexpr uint32_t KV_MTUP_WORDS = 8u;
 __global__ __launch_bounds__(KV_WG) void kv_mtup_kernel(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp,
                                                          uint32_t* __restrict__ out) {
   const DevPS& P = *Pp;
   const DevBatch& B = *Bp;
-  const uint32_t t = blockIdx.x * KV_WG + threadIdx.x, w = blockIdx.y;
+  const uint32_t t = blockIdx.x * KV_WG + threadIdx.x, w0 = blockIdx.y * KV_MTUP_WORDS;
   if (t >= B.n_tup) return;
-  out[(size_t)w * B.n_tup + t] = mtup_word(P, B, t, w);
+  const MtupIn in = mtup_in(B, t);
+  const uint32_t w1 = min(w0 + KV_MTUP_WORDS, P.fac_words);
+  for (uint32_t w = w0; w < w1; w++) out[(size_t)w * B.n_tup + t] = mtup_word_in(P, B, in, w);
 }
 
 // out[rule][j] = in[rule][inv[j]]: a status matrix in store order gathered into the caller's
@@ -446,7 +451,8 @@ hipError_t launch_mfac(const DevPS* P, const DevBatch* B, uint32_t slots, uint32
     hipLaunchKernelGGL(kv_mfac_kernel, dim3((max_entities + KV_WG / 32 - 1) / (KV_WG / 32), slots, KV_FAC_TYPES),
                        dim3(KV_WG), 0, stream, P, B);
   if (words && n_tup)
-    hipLaunchKernelGGL(kv_mtup_kernel, dim3((n_tup + KV_WG - 1) / KV_WG, words), dim3(KV_WG), 0, stream, P, B, mtup);
+    hipLaunchKernelGGL(kv_mtup_kernel, dim3((n_tup + KV_WG - 1) / KV_WG, (words + KV_MTUP_WORDS - 1) / KV_MTUP_WORDS),
+                       dim3(KV_WG), 0, stream, P, B, mtup);
   return hipGetLastError();
 }
 
