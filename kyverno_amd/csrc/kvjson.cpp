@@ -211,6 +211,7 @@ struct P {
       size_t base = scratch.size();
       ws();
       if (i < n && s[i] == '}') { i++; v.first = (uint32_t)d->nodes.size(); v.count = 0; return; }
+      uint64_t seen = 0;  // keys of this map so far by (length, first byte, last byte) signature bit
       while (true) {
         ws();
         JNode ch;
@@ -219,12 +220,17 @@ struct P {
         if (i >= n || s[i] != ':') fail("expected :");
         i++;
         value(ch, depth + 1);
-        // duplicate key: last one wins (replace in place)
-        bool dup = false;
+        // duplicate key: last one wins (replace in place); the earlier keys are compared only
+        // when one of them has the same signature
         const std::string_view k(sb + ch.key_off, ch.key_len);
-        for (size_t q = base; q < scratch.size(); q++) {
-          if (std::string_view(sb + scratch[q].key_off, scratch[q].key_len) == k) { scratch[q] = ch; dup = true; break; }
-        }
+        const uint64_t sig = 1ull << ((k.size() * 7u + (k.empty() ? 0u : (unsigned char)k[0] * 3u +
+                                                                        (unsigned char)k.back())) & 63u);
+        bool dup = false;
+        if (seen & sig)
+          for (size_t q = base; q < scratch.size(); q++) {
+            if (std::string_view(sb + scratch[q].key_off, scratch[q].key_len) == k) { scratch[q] = ch; dup = true; break; }
+          }
+        seen |= sig;
         if (!dup) scratch.push_back(ch);
         ws();
         if (i < n && s[i] == ',') { i++; continue; }

@@ -129,3 +129,20 @@ def test_parallel_ingest_host_tables():
             os.environ.pop("KVGPU_INGEST_THREADS", None)
         got.append((b.n_res, b.namespaces))
     assert got[0] == got[1] and got[0][0] == 6000
+
+
+def test_duplicate_json_keys_last_wins():
+    """encoding/json (unstructured.UnmarshalJSON) keeps the last of duplicate object keys; the
+    decoder's signature filter must still find every duplicate (same length, first and last
+    byte) and ignore keys that only share a signature bit."""
+    from kyverno_amd import batch
+
+    ps = batch.PolicySet([{"metadata": {"name": "p"}, "spec": {"rules": []}}])
+    docs = [
+        b'{"kind": "Pod", "metadata": {"namespace": "a", "name": "x", "namespace": "b"}}',
+        b'{"kind": "Pod", "metadata": {"namespace": "c", "labels": {"k1": "v", "k2": "w", "k1": "z"}}}',
+        b'{"kind": "Pod", "metadata": {"namespace": "a", "ab": 1, "ba": 2, "aab": 3}}',
+    ]
+    b = batch.Batch(ps, b"\n".join(docs))
+    assert b.n_res == 3
+    assert sorted(b.namespaces) == ["a", "b", "c"]  # doc 0's namespace is "b", not "a"
