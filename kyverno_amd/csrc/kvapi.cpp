@@ -861,6 +861,10 @@ struct DevSession {
   DevPolicySet* dps = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
+  // specialized passes: the match tables (kv_mtab, kv_mfac, kv_mtup) run on `side` while
+  // `stream` builds the value-predicate table (kvj_ptab); the rule kernels wait for both
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 
   DevSession(kv_policyset* p, kv_batch* b, const char* ctx_json, int dev, uint32_t m)
       : ps(p), bt(b), device(dev), mode(m) {
@@ -953,6 +957,9 @@ struct DevSession {
     HIPCHK(hipStreamCreate(&stream));
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
   }
   // take the batch's device copy out of the kv_batch (parts sessions: the host batch is the
   // caller's, and may be freed after kv_session_attach_part)
@@ -982,6 +989,9 @@ struct DevSession {
     (void)hipSetDevice(device);
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (side) (void)hipStreamDestroy(side);
     if (stream) (void)hipStreamDestroy(stream);
   }
   // enqueue `iters` passes, wait, return HIP-event milliseconds of all passes
@@ -991,10 +1001,17 @@ struct DevSession {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipEventRecord(e0, stream));
     for (int i = 0; i < iters; i++) {
-      HIPCHK(hipMemsetAsync(cn.p, 0, cn.n, stream));
-      if (mode & KV_MODE_SCOPES) HIPCHK(hipMemsetAsync(scn.p, 0, scn.n, stream));
-      HIPCHK(launch_mtab((const DevPS*)pview.p, bview, mt_words, mt_entities, mt_ns, mt_ann, mt_sel, stream));
       rec_compact = dps->specialized() && !vm;
+      // the match tables on the side stream, forked from and joined back into `stream`
+      // (specialized passes; the bytecode engine runs everything in order on `stream`)
+      hipStream_t ms = rec_compact ? side : stream;
+      if (rec_compact) {
+        HIPCHK(hipEventRecord(ev_fork, stream));
+        HIPCHK(hipStreamWaitEvent(side, ev_fork, 0));
+      }
+      HIPCHK(hipMemsetAsync(cn.p, 0, cn.n, ms));
+      if (mode & KV_MODE_SCOPES) HIPCHK(hipMemsetAsync(scn.p, 0, scn.n, ms));
+      HIPCHK(launch_mtab((const DevPS*)pview.p, bview, mt_words, mt_entities, mt_ns, mt_ann, mt_sel, ms));
       if (rec_compact) {
         launch_specialized();  // (per-scope counts inside the rule kernels)
         if (O.full & 8u)  // per-rule totals from the per-scope counts (the kernels add only those)
@@ -1017,7 +1034,11 @@ struct DevSession {
   }
   // one launch per rule kernel of the specialized kernels, 256 resources per workgroup
   void launch_specialized() {
-    if (nres == 0) return;
+    if (nres == 0) {  // (join the side stream's table work all the same)
+      HIPCHK(hipEventRecord(ev_join, side));
+      HIPCHK(hipStreamWaitEvent(stream, ev_join, 0));
+      return;
+    }
     const uint32_t blocks = (uint32_t)((nres + KV_WG - 1) / KV_WG);
     const DevPS* P = (const DevPS*)pview.p;
     const Node* N = bhost->nodes;
@@ -1030,8 +1051,10 @@ struct DevSession {
       HIPCHK(hipModuleLaunchKernel(dps->ptab_fn, (NV + KV_PTAB_PSEUDO + KV_WG - 1) / KV_WG, dps->ptab_rows, 1, KV_WG, 1, 1, 0,
                                    stream, targs, nullptr));
     }
-    if (dps->mtup_words && ntup)  // every rule's match bit per tuple (after kv_mtab)
-      HIPCHK(launch_mfac(P, bview, dps->fac_slots, fac_entities, dps->mtup_words, ntup, (uint32_t*)mtup.p, stream));
+    if (dps->mtup_words && ntup)  // every rule's match bit per tuple (after kv_mtab, on the side stream)
+      HIPCHK(launch_mfac(P, bview, dps->fac_slots, fac_entities, dps->mtup_words, ntup, (uint32_t*)mtup.p, side));
+    HIPCHK(hipEventRecord(ev_join, side));
+    HIPCHK(hipStreamWaitEvent(stream, ev_join, 0));
     DevOut Ov = O;
     uint32_t r0 = 0;
     void* args[] = {(void*)&P, (void*)&bview, (void*)&N, (void*)&V, (void*)&S, (void*)&Ov, (void*)&r0};
