@@ -1310,11 +1310,13 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
     }
     merge_batches(parts, *b, (uint32_t)ps.keys.size());
     if (verbose)
-      fprintf(stderr, "[kvgpu] ingest: merge %.1f ms (%zu vals, %llu rows, %zu string bytes)\n", ms(), b->vals.size(),
-              (unsigned long long)b->n_rows, b->strs.size());
+      fprintf(stderr, "[kvgpu] ingest: merge %.1f ms (%zu vals, %llu rows, %zu string bytes, %zu/%zu/%zu nsm/label/annotation sets)\n",
+              ms(), b->vals.size(), (unsigned long long)b->n_rows, b->strs.size(), b->nsms.size(), b->lsets.size(),
+              b->asets.size());
     for (size_t i = 0; i < b->namespaces.size(); i++) ns_index.emplace(b->namespaces[i], (uint32_t)i);
     parallel = true;
   }
+  if (verbose) fprintf(stderr, "[kvgpu] ingest: parts released %.1f ms\n", ms());
   if (!parallel) {
     Ingest in(ps, *b);
     if (len <= (64u << 20)) {  // small inputs: documents held, taken in store order
@@ -1363,6 +1365,7 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
   for (size_t n = 0; n < b->namespaces.size(); n++)
     for (uint32_t s = 0; s < nsel; s++)
       if (selector_eval_host(ps.nsselectors[s], b->ns_labels[n]) == 1) b->ns_bits[n * b->ns_words + s / 32] |= 1u << (s % 32);
+  if (verbose) fprintf(stderr, "[kvgpu] ingest: namespace selectors %.1f ms\n", ms());
   // word-granular readers may touch up to 8 bytes past the last string
   b->strs.append(16, '\0');
   if (verbose) fprintf(stderr, "[kvgpu] ingest: namespaces %.1f ms\n", ms());
