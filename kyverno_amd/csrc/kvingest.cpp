@@ -294,6 +294,26 @@ struct Ingest {
                              [&](const Probe::Slot& x) { return tn.slot_keys[x.id] == k; });
   }
 
+  // slot of the key at child position `pos` of a slot-addressed map at trie node t, remembered
+  // per (node, position): documents of one kind list their keys in the same order, so most
+  // lookups are one compare against the previous document's key instead of a hash and probe
+  struct PosSlot {
+    std::string key;
+    int32_t slot = -2;  // -2: empty
+  };
+  std::vector<std::vector<PosSlot>> pos_cache;
+  int32_t slot_at(int32_t t, uint32_t pos, std::string_view k) {
+    if (pos >= 64u) return slot_of(t, k);
+    if (pos_cache.size() <= (size_t)t) pos_cache.resize(ps.trie.nodes.size());
+    std::vector<PosSlot>& pc = pos_cache[t];
+    if (pc.size() <= pos) pc.resize(pos + 1);
+    PosSlot& e = pc[pos];
+    if (e.slot != -2 && e.key == k) return e.slot;
+    e.key.assign(k.data(), k.size());
+    e.slot = slot_of(t, k);
+    return e.slot;
+  }
+
   // sorted-children buffers of the keep-all maps being walked, one per nesting depth (a
   // deque: growing it keeps the outer frames' references valid)
   std::deque<std::vector<uint32_t>> ch_pool;
@@ -336,7 +356,7 @@ struct Ingest {
         ch_depth--;
       } else {
         for (uint32_t c = n.first; c < n.first + n.count; c++) {
-          const int32_t si = slot_of(s.t, d.key(d.at(c)));
+          const int32_t si = slot_at(s.t, c - n.first, d.key(d.at(c)));
           js[c] = si;
           if (si >= 0) unite(s.kids[si], d, c, js);
         }
