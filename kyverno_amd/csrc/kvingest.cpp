@@ -1255,6 +1255,25 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
   // NDJSON first (documents = lines); when a document does not end its line, the values are
   // found again by the full scan
   bool lines = T > 1 && len >= (1u << 20) && first < len && json[first] == '{' && split_lines(json, len, T, &starts);
+  // The merged store's page-locked blocks are taken from the pool while the documents are parsed:
+  // a thread takes blocks of the estimated sizes (resource headers: exact; packed node cells: about
+  // the input's bytes; values: an eighth of them) and hands them back, so the merge finds them in
+  // the pool instead of page-locking fresh memory then (the first batch of a process: ~200 ms
+  // per million Pods on the GPU box). A block is used when it is 1-2x the size asked for.
+  struct Join {
+    std::thread t;
+    ~Join() {
+      if (t.joinable()) t.join();
+    }
+  } prewarm;
+  if (g_hostmem.take && g_hostmem.give && starts.size() >= 65536) {
+    const size_t est[3] = {starts.size() * sizeof(Res), len, len / 8};
+    prewarm.t = std::thread([est]() {
+      for (size_t e : est)
+        if (e >= (16u << 20))
+          if (void* p = g_hostmem.take(e)) g_hostmem.give(p);
+    });
+  }
   for (int attempt = 0; attempt < 2 && !parallel; attempt++) {
     if (attempt == 1 || !lines) {
       starts.clear();
@@ -1328,7 +1347,14 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
       for (size_t k = 0; k < P; k++) tp += tparse[k], tt += ttake[k];
       fprintf(stderr, "[kvgpu] ingest: %zu threads %.1f ms (per thread: parse %.1f ms, take %.1f ms)\n", P, ms(), tp / P, tt / P);
     }
+    if (prewarm.t.joinable()) prewarm.t.join();
     merge_batches(parts, *b, (uint32_t)ps.keys.size());
+    {  // what the parts still hold is freed in parallel too (serially ~70-80 ms per million
+       // Pods on the GPU box, after the merge threads have released the store arrays)
+      std::vector<std::thread> ft;
+      for (size_t k = 0; k < P; k++) ft.emplace_back([&parts, k]() { Batch dead(std::move(parts[k])); });
+      for (auto& t : ft) t.join();
+    }
     if (verbose)
       fprintf(stderr, "[kvgpu] ingest: merge %.1f ms (%zu vals, %llu rows, %zu string bytes, %zu/%zu/%zu nsm/label/annotation sets)\n",
               ms(), b->vals.size(), (unsigned long long)b->n_rows, b->strs.size(), b->nsms.size(), b->lsets.size(),
