@@ -1300,6 +1300,7 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
       for (auto& t : kt) t.join();
       b->order = store_order(kinds, nss, T);
     }
+    if (verbose) fprintf(stderr, "[kvgpu] ingest: store order %.1f ms\n", ms());
     const std::vector<uint32_t>& order = b->order;
     std::vector<Batch> parts(P);
     std::vector<std::string> errs(P);
