@@ -1943,11 +1943,20 @@ struct Gen {
   }
 
   // First block sizes of the kernel of sorted rules [a, e): greedy runs whose weight stays
-  // within KVGPU_JIT_BLOCK_W (default 160); a rule of the same structural form as an
-  // earlier rule of the run joins it for free (rule groups run its program once).
+  // within a budget (KVGPU_JIT_BLOCK_W, default 160, see below); a rule of the same structural
+  // form as an earlier rule of the run joins it for free (rule groups run its program once).
+  // A kernel the default budget cuts into many blocks is cut again with 1.5x the budget: it
+  // re-walks its resources once per block, and the block probes still split whatever does not
+  // fit its registers (round 4, gpurun_out/ab9 / ab8, ms per pass: C5 3.45 -> 3.25, C4 1.00 ->
+  // 0.99; C2, three blocks, keeps the default: with 1.5x 0.694 -> 0.712).
   std::vector<uint32_t> initial_blocks(const std::vector<uint32_t>& sorted, uint32_t a, uint32_t e) {
     const char* bw = getenv("KVGPU_JIT_BLOCK_W");
-    const uint32_t budget = bw && atoi(bw) > 0 ? (uint32_t)atoi(bw) : 160u;
+    if (bw && atoi(bw) > 0) return initial_blocks_w(sorted, a, e, (uint32_t)atoi(bw));
+    std::vector<uint32_t> out = initial_blocks_w(sorted, a, e, 160u);
+    if (out.size() >= 6) out = initial_blocks_w(sorted, a, e, 240u);
+    return out;
+  }
+  std::vector<uint32_t> initial_blocks_w(const std::vector<uint32_t>& sorted, uint32_t a, uint32_t e, uint32_t budget) {
     std::vector<uint32_t> out;
     std::set<std::string> forms;
     uint32_t cur = 0, w = 0;
