@@ -158,8 +158,9 @@ def ingest_parts(ps, args, kind_mix: int, mode: int):
     def make(k):
         data = batch.synth(workloads.SEED, args.n_res, kind_mix, first=k * args.n_res)
         nb = len(data)
+        t = time.time()
         b = batch.Batch(ps, data)
-        return k, b, nb
+        return k, b, nb, time.time() - t
 
     info = [None] * G
     t1 = time.time()
@@ -172,12 +173,25 @@ def ingest_parts(ps, args, kind_mix: int, mode: int):
                 nxt += 1
             done, pending = cf.wait(pending, return_when=cf.FIRST_COMPLETED)
             for f in done:
-                k, b, nb = f.result()
-                sess.attach_part(k, b, 0 if args.parts_per_gpu > 1 else k)
-                info[k] = {"n_res": b.n_res, "store_bytes": b.store_bytes, "ndjson_bytes": nb}
+                k, b, nb, secs = f.result()
+                dev = 0 if args.parts_per_gpu > 1 else k
+                sess.attach_part(k, b, dev)
+                info[k] = {"n_res": b.n_res, "store_bytes": b.store_bytes, "ndjson_bytes": nb, "ingest_s": secs,
+                           "device": dev}
                 b.close()  # the session holds the device copy
     t2 = time.time()
     return sess, info, t1, t2
+
+
+def check_rccl(ranks: int, devices) -> None:
+    """The in-process parts session must reduce its counts over one RCCL rank per distinct device
+    (kv_session_rccl_ranks = ncclCommCount); parts that all share one device sum on the host
+    (0 ranks). Anything else means the multi-device path is not the one being measured."""
+    distinct = len(set(devices))
+    want = distinct if distinct > 1 else 0
+    if ranks != want:
+        raise SystemExit(f"bench: RCCL communicator has {ranks} ranks, expected {want} "
+                         f"({distinct} distinct devices among {len(devices)} parts)")
 
 
 def e2e_stream(ps, n_res: int, kind_mix: int, device: int, seed: int, chunk: int) -> dict:
@@ -324,6 +338,7 @@ def main():
         namespaces = sess.scope_names() if args.mode == "scopes" else []
         b = None
         log(f"in-process multi-device session: {sess.n_parts} parts, RCCL ranks {sess.rccl_ranks()}")
+        check_rccl(sess.rccl_ranks(), [x["device"] for x in shard_info])
     else:
         data = batch.synth(workloads.SEED, args.n_res, kind_mix, first=rank * args.n_res)
         ndjson_bytes = len(data)
@@ -417,7 +432,9 @@ def main():
     # parts on distinct devices; 0 ranks = host sum of logical parts), or torch.distributed
     if inproc:
         out["rccl"] = {"ranks": sess.rccl_ranks(), "where": "libkvgpu ncclCommInitAll",
-                       "part_ms": [m / args.steps for m in sess.part_ms()]}
+                       "devices": sorted(set(x["device"] for x in shard_info)),
+                       "part_ms": [m / args.steps for m in sess.part_ms()],
+                       "part_ingest_s": [x["ingest_s"] for x in shard_info]}
     elif dist is not None:
         out["rccl"] = {"ranks": world if dist.get_backend() == "nccl" else 0,
                        "where": f"torch.distributed ({dist.get_backend()})"}
@@ -441,6 +458,7 @@ def main():
         te1 = time.perf_counter()
         out["e2e_kv_validate"] = {"seconds": te1 - te0, "evals_per_s": n_pairs_rank / (te1 - te0),
                                   "kernel_ms": r2.kernel_ms,
+                                  "phases_ms": {k: round(v, 3) for k, v in r2.phases.items()},
                                   "includes": "H2D store upload + 1 pass + D2H status/error records "
                                               "(steady state: after one untimed kv_validate of another batch)"}
         del r2, b2

@@ -119,6 +119,10 @@ int kv_validate_devices(const kv_policyset* ps, const kv_batch* b, const char* c
 int kv_result_status(const kv_result* r, const uint8_t** status, uint64_t* n_rules, uint64_t* n_res);
 /* counts[rule * 8 + status] */
 int kv_result_counts(const kv_result* r, const int64_t** counts);
+/* phase i of the kv_validate that produced r: its name ("upload", "setup", "pass", "host_alloc",
+ * "status_d2h", "records_count", "records_scatter_d2h", ...) and wall-clock milliseconds;
+ * KV_E_RANGE past the last phase. Diagnostics of the host boundary (no reference counterpart). */
+int kv_result_phase(const kv_result* r, uint32_t i, const char** name, double* ms);
 /* counts[(scope * n_rules + rule) * 8 + status] (KV_MODE_SCOPES) */
 int kv_result_scope_counts(const kv_result* r, const int64_t** counts, uint32_t* n_scopes);
 /* failing path of a FAIL pair, e.g. "/spec/containers/0/image/" (needs KV_MODE_ERRORS);

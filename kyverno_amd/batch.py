@@ -184,6 +184,13 @@ class Result:
         self.counts = np.frombuffer(cb, dtype=np.int64).reshape(self.n_rules, 8).copy() if self.n_rules else \
             np.zeros((0, 8), np.int64)
         self.kernel_ms = L.kv_result_kernel_ms(h)
+        # wall-clock phases of the kv_validate behind this result (upload, setup, pass, fetch steps)
+        self.phases = {}
+        nm, ms, i = ctypes.c_char_p(), ctypes.c_double(), 0
+        while L.kv_result_phase(h, i, ctypes.byref(nm), ctypes.byref(ms)) == 0:
+            key = nm.value.decode()
+            self.phases[key] = self.phases.get(key, 0.0) + ms.value
+            i += 1
         sc, ns = ctypes.c_void_p(), ctypes.c_uint32()
         self.scope_counts = None  # [scope][rule][8] with MODE_SCOPES
         if L.kv_result_scope_counts(h, ctypes.byref(sc), ctypes.byref(ns)) == 0 and self.n_rules and ns.value:

@@ -161,6 +161,10 @@ struct DevBatchRes {
   // pattern variables (kvvars.cpp): the batch predicate table (a DevPS with its pred tables),
   // outcome ids per [dynamic leaf][res], statuses per [dynamic rule][res]
   DevBuf dpreds, dalts, dconjs, datoms, dgsegs, dgwords, dpstr, dps, dleaf, dynst;
+  // path columns of the specialized kernels (kvcol.h): the pool, the column descriptors, the
+  // families and their per-group element-row prefixes; build time and pool size
+  DevBuf pcol, pcold, pfam, perow;
+  double pcol_ms = 0;
   DevBatch view{};
 };
 
@@ -364,18 +368,24 @@ struct kv_result {
   const kv_policyset* ps = nullptr;
   const kv_batch* b = nullptr;
   uint64_t n_rules = 0, n_res = 0;
-  // [rule][res] in the batch's store order (Batch::order); `res` below is a store index unless
-  // named a caller index. kv_result_status returns status_c, the caller order, when they differ.
+  // [rule][res] in the batch's store order (Batch::order), or in the caller's order with
+  // caller_order; `res` below is an index into it unless named a caller index.
+  // kv_result_status returns the caller order (status_c, a host permutation, when they differ).
   HostArray<uint8_t> status;
   std::once_flag sc_once;
   HostArray<uint8_t> status_c;
-  bool status_c_ready = false;      // status_c written by the fetch (device-side permutation)
+  // statuses and records were fetched in the caller's order (a permuted batch fetched whole:
+  // DevSession::fetch); `status` is then the caller order and `res` below a caller index
+  bool caller_order = false;
   std::vector<ResultPart> parts;    // by resource range
   bool errors = false;              // KV_MODE_ERRORS: records fetched
   std::vector<int64_t> counts;
   std::vector<int64_t> scope_counts;  // [scope][rule][KV_HIST] (KV_MODE_SCOPES)
   double kernel_ms = 0;
   uint32_t mode = 0;
+  // wall-clock phases of the kv_validate that made this result (kv_result_phase): upload, setup,
+  // pass, then the fetch's device work and copies, each ended by a stream synchronize
+  std::vector<std::pair<std::string, double>> phases;
   // bulk failure export (kv_result_failures), built on first use
   std::once_flag fail_once;
   std::vector<uint32_t> f_rule, f_path;
@@ -384,17 +394,18 @@ struct kv_result {
 
   bool has_err() const { return errors; }
   // store index of caller index `res`
-  uint64_t sidx(uint64_t res) const {
+  uint64_t sidx(uint64_t res) const { return caller_order ? res : store_of(res); }
+  // the batch's store slot of caller index `res` (indexes the batch-side tables: dynamic leaves)
+  uint64_t store_of(uint64_t res) const {
     const uint32_t* iv = const_cast<kv_batch*>(b)->inverse();
     return iv ? iv[res] : res;
   }
-  // caller index of store index `s`
-  uint64_t cidx(uint64_t s) const { return b->b.order.empty() ? s : b->b.order[s]; }
+  // caller index of status / record index `s`
+  uint64_t cidx(uint64_t s) const { return caller_order || b->b.order.empty() ? s : b->b.order[s]; }
   // the statuses in caller order: rows of the store-order matrix scattered through the batch
   // order, rules split over host threads (a permuted batch only)
   const uint8_t* status_caller() {
-    if (b->b.order.empty() || status.empty()) return status.empty() ? nullptr : status.data();
-    if (status_c_ready) return status_c.data();
+    if (b->b.order.empty() || status.empty() || caller_order) return status.empty() ? nullptr : status.data();
     std::call_once(sc_once, [this]() {
       status_c.alloc(status.size());
       const uint32_t* ord = b->b.order.data();
@@ -564,6 +575,58 @@ DevPolicySet& dev_ps(kv_policyset* s, int device) {
   return ref;
 }
 
+// Path columns of the batch for the policy set's specialized kernels (kvcol.h, kvdevtypes.h):
+// family 0 at [wave group][column][lane] (wave groups padded to whole workgroups, so every lane
+// of the rule kernels' grid has its cells), then each family's element rows; built once per
+// batch and device from the node rows (d->view_dev must hold the batch view).
+void build_pcol(const JitImage& J, const Batch& b, DevBatchRes* d, int device) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const uint32_t nf = (uint32_t)J.fam_ncols.size(), j0 = J.fam_ncols.at(0);
+  const uint64_t groups64 = (b.res.size() + KV_WG - 1) / KV_WG * (KV_WG / KV_LANES);
+  if (groups64 > 0x3FFFFFFull) throw std::runtime_error("path columns: too many resources");
+  const uint32_t groups = (uint32_t)groups64;
+  d->pcold.upload(J.cols, device);
+  d->perow.alloc((size_t)std::max<uint32_t>(1u, nf - 1) * (groups + 1) * sizeof(uint32_t), device);
+  HIPCHK(hipMemset(d->perow.p, 0, d->perow.n));
+  std::vector<ColFam> fams(nf);
+  for (uint32_t f = 0; f < nf; f++) {
+    fams[f].arr_col = J.fam_arr[f];
+    fams[f].ncols = J.fam_ncols[f];
+    fams[f].erow = f ? (uint32_t*)d->perow.p + (size_t)(f - 1) * (groups + 1) : nullptr;
+  }
+  d->pfam.upload(fams, device);
+  const DevBatch* Bd = (const DevBatch*)d->view_dev.p;
+  const ColDesc* cd = (const ColDesc*)d->pcold.p;
+  std::vector<uint32_t> erow;
+  if (nf > 1) {
+    HIPCHK(launch_pcol_rows(Bd, cd, (const ColFam*)d->pfam.p, nf, groups, nullptr));
+    erow.resize((size_t)(nf - 1) * (groups + 1));
+    HIPCHK(hipMemcpy(erow.data(), d->perow.p, erow.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  }
+  const uint64_t root_cells = (uint64_t)groups * j0 * KV_LANES;
+  uint64_t cells = root_cells;
+  for (uint32_t f = 1; f < nf; f++) {
+    fams[f].off_lo = (uint32_t)cells;
+    fams[f].off_hi = (uint32_t)(cells >> 32);
+    cells += (uint64_t)erow[(size_t)(f - 1) * (groups + 1) + groups] * fams[f].ncols * KV_LANES;
+  }
+  // (the kernels index cells with 32 bits)
+  if (cells >= (1ull << 32)) throw std::runtime_error("path columns: more than 2^32 cells");
+  HIPCHK(hipMemcpy(d->pfam.p, fams.data(), fams.size() * sizeof(ColFam), hipMemcpyHostToDevice));
+  d->pcol.alloc(cells * sizeof(Node), device);
+  if (cells > root_cells)  // element rows past a lane's own elements stay zero
+    HIPCHK(hipMemset((Node*)d->pcol.p + root_cells, 0, (cells - root_cells) * sizeof(Node)));
+  HIPCHK(launch_pcol_build(Bd, cd, (const ColFam*)d->pfam.p, j0, 0, j0, groups, false, (Node*)d->pcol.p, nullptr));
+  HIPCHK(launch_pcol_build(Bd, cd, (const ColFam*)d->pfam.p, j0, j0, (uint32_t)J.cols.size() - j0, groups, true,
+                           (Node*)d->pcol.p, nullptr));
+  HIPCHK(hipStreamSynchronize(nullptr));
+  d->view.pcol = (const Node*)d->pcol.p;
+  d->pcol_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (getenv("KVGPU_VERBOSE"))
+    fprintf(stderr, "[kvgpu] path columns: %zu columns in %u families, %.1f MB, built in %.2f ms\n", J.cols.size(), nf,
+            cells * sizeof(Node) / 1e6, d->pcol_ms);
+}
+
 DevBatchRes& dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
   std::lock_guard<std::mutex> g(bt->mu);
   auto it = bt->dev.find(device);
@@ -651,6 +714,10 @@ DevBatchRes& dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
     v.dyn_st = (const uint8_t*)d->dynst.p;
   }
   d->view_dev.upload_raw(&d->view, sizeof(DevBatch), device);
+  if (bt->owner && bt->owner->jit && !bt->owner->jit->cols.empty() && !b.res.empty()) {
+    build_pcol(*bt->owner->jit, b, d.get(), device);
+    d->view_dev.upload_raw(&d->view, sizeof(DevBatch), device);
+  }
   auto& ref = *d;
   bt->dev[device] = std::move(d);
   return ref;
@@ -852,6 +919,7 @@ struct DevSession {
   std::unique_ptr<DevBatchRes> own_batch;
   DevBuf r_offs, r_tot, r_base, r_out8, r_outw, r_wide;  // record compaction (fetch)
   DevBuf inv_d, stc;                                     // caller-order statuses (fetch)
+  DevBuf ord_d, r_mask;                                  // caller-order records: batch order, record lanes
   uint32_t mt_words = 0, mt_entities = 0;
   uint32_t *mt_ns = nullptr, *mt_ann = nullptr, *mt_sel = nullptr;
   uint32_t nscopes = 0, nvals = 0;
@@ -866,15 +934,15 @@ struct DevSession {
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 
+  double upload_ms = 0;  // policy set + batch upload of the constructor (path columns included)
   DevSession(kv_policyset* p, kv_batch* b, const char* ctx_json, int dev, uint32_t m)
       : ps(p), bt(b), device(dev), mode(m) {
     HIPCHK(hipSetDevice(device));
     const auto tc0 = std::chrono::steady_clock::now();
     DevPolicySet& dp = dev_ps(ps, device);
     DevBatchRes& db = dev_batch(bt, ps->ps, device);
-    if (getenv("KVGPU_VERBOSE"))
-      fprintf(stderr, "[kvgpu] session: policy set + batch upload %.1f ms\n",
-              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc0).count());
+    upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc0).count();
+    if (getenv("KVGPU_VERBOSE")) fprintf(stderr, "[kvgpu] session: policy set + batch upload %.1f ms\n", upload_ms);
     bview = (const DevBatch*)db.view_dev.p;
     bhost = &db.view;
     dps = &dp;
@@ -1077,28 +1145,39 @@ struct DevSession {
   void fetch(kv_result* out, ResultPart* part, uint64_t lo, uint64_t n_total) {
     HIPCHK(hipSetDevice(device));
     const bool verbose = getenv("KVGPU_VERBOSE") != nullptr;
-    const auto tf0 = std::chrono::steady_clock::now();
+    auto tl = std::chrono::steady_clock::now();
+    // phase boundary: the stream drained, the time since the last one into the result's phases
+    // (the first part's, so parts on several devices do not add up)
     auto lap = [&](const char* what) {
-      if (!verbose) return;
       HIPCHK(hipStreamSynchronize(stream));
-      fprintf(stderr, "[kvgpu] fetch: %s at %.1f ms\n", what,
-              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count());
+      const auto now = std::chrono::steady_clock::now();
+      const double ms = std::chrono::duration<double, std::milli>(now - tl).count();
+      tl = now;
+      if (part == &out->parts[0]) out->phases.push_back({what, ms});
+      if (verbose) fprintf(stderr, "[kvgpu] fetch: %s %.1f ms\n", what, ms);
     };
-    if (O.status && (mode & (KV_MODE_STATUS | KV_MODE_ERRORS)) && nres && nrules)
-      HIPCHK(hipMemcpy2DAsync(out->status.data() + lo, n_total, st.p, nres, nres, nrules, hipMemcpyDeviceToHost,
-                              stream));
-    // a permuted batch fetched whole: the caller-order matrix is gathered on the device
-    // (out[rule][j] = st[rule][store index of j]) and copied too, instead of a host scatter
-    if (O.status && (mode & (KV_MODE_STATUS | KV_MODE_ERRORS)) && nres && nrules && bt && lo == 0 &&
-        nres == n_total && !bt->b.order.empty()) {
+    const bool want_st = O.status && (mode & (KV_MODE_STATUS | KV_MODE_ERRORS)) && nres && nrules;
+    // A permuted batch fetched whole comes back in the caller's order: the statuses are gathered on
+    // the device (stc[rule][j] = st[rule][store index of j]) and the records scattered to the
+    // caller's (rule, resource) order, so one status matrix crosses PCIe and the host permutes
+    // nothing. Its copy runs on the side stream, beside the record kernels.
+    const bool caller = want_st && bt && lo == 0 && nres == n_total && !bt->b.order.empty();
+    bool side_copy = false;
+    if (caller) {
       if (!inv_d.p) inv_d.upload_raw(bt->inverse(), nres * sizeof(uint32_t), device);
       if (!stc.p) stc.alloc(nrules * nres, device);
       HIPCHK(launch_gather_rows((const uint8_t*)st.p, (const uint32_t*)inv_d.p, nrules, nres, (uint8_t*)stc.p, stream));
-      out->status_c.alloc(nrules * nres);
-      HIPCHK(hipMemcpyAsync(out->status_c.data(), stc.p, nrules * nres, hipMemcpyDeviceToHost, stream));
-      out->status_c_ready = true;
+      HIPCHK(hipEventRecord(ev_fork, stream));
+      HIPCHK(hipStreamWaitEvent(side, ev_fork, 0));
+      HIPCHK(hipMemcpyAsync(out->status.data(), stc.p, nrules * nres, hipMemcpyDeviceToHost, side));
+      side_copy = true;
+      out->caller_order = true;
+      lap("status_gather");
+    } else if (want_st) {
+      HIPCHK(hipMemcpy2DAsync(out->status.data() + lo, n_total, st.p, nres, nres, nrules, hipMemcpyDeviceToHost,
+                              stream));
+      lap("status_d2h");
     }
-    lap("status D2H");
     if (O.err8 && nres && nrules) {
       const uint32_t tiles = (uint32_t)((nres + KV_WG - 1) / KV_WG);
       part->tiles = tiles;
@@ -1108,30 +1187,44 @@ struct DevSession {
         r_base.alloc((nrules + 1) * sizeof(unsigned long long), device);
         r_wide.alloc(sizeof(uint32_t), device);
       }
-      HIPCHK(launch_rec_compact(O.status, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
+      const uint32_t* ord = nullptr;
+      unsigned long long* masks = nullptr;
+      if (caller) {  // record ranks over the caller-order statuses
+        if (!ord_d.p) ord_d.upload_raw(bt->b.order.data(), nres * sizeof(uint32_t), device);
+        if (!r_mask.p) r_mask.alloc((size_t)nrules * tiles * (KV_WG / 64) * sizeof(unsigned long long), device);
+        ord = (const uint32_t*)ord_d.p;
+        masks = (unsigned long long*)r_mask.p;
+      }
+      const uint8_t* rank_st = caller ? (const uint8_t*)stc.p : O.status;
+      HIPCHK(launch_rec_compact(rank_st, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                 (unsigned long long*)r_tot.p, (unsigned long long*)r_base.p, nullptr, nullptr, nullptr,
-                                0, rec_compact ? (const uint8_t*)dps->rcompact.p : nullptr, stream));
+                                0, rec_compact ? (const uint8_t*)dps->rcompact.p : nullptr, nullptr, masks, stream));
       part->base.resize(nrules + 1);
       part->offs.resize((size_t)nrules * tiles);
       HIPCHK(hipMemcpyAsync(part->base.data(), r_base.p, part->base.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
                             stream));
       HIPCHK(hipMemcpyAsync(part->offs.data(), r_offs.p, part->offs.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
                             stream));
-      HIPCHK(hipStreamSynchronize(stream));
-      lap("record counts");
+      lap("records_count");
       const uint64_t total = part->base[nrules];
       if (r_out8.n < total * sizeof(ErrRec8)) r_out8.alloc(std::max<uint64_t>(total, 1) * sizeof(ErrRec8), device);
       HIPCHK(hipMemsetAsync(r_wide.p, 0, sizeof(uint32_t), stream));
       HIPCHK(launch_rec_compact(O.status, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                 nullptr, (unsigned long long*)r_base.p, (ErrRec8*)r_out8.p, nullptr,
-                                (uint32_t*)r_wide.p, 1, rec_compact ? (const uint8_t*)dps->rcompact.p : nullptr, stream));
+                                (uint32_t*)r_wide.p, 1, rec_compact ? (const uint8_t*)dps->rcompact.p : nullptr, ord,
+                                masks, stream));
+      lap("records_scatter");
+      const auto th0 = std::chrono::steady_clock::now();
       part->rec.alloc(total);
+      if (part == &out->parts[0])
+        out->phases.push_back(
+            {"host_alloc", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count()});
+      tl = std::chrono::steady_clock::now();
       if (total)
         HIPCHK(hipMemcpyAsync(part->rec.data(), r_out8.p, total * sizeof(ErrRec8), hipMemcpyDeviceToHost, stream));
       uint32_t wide = 0;
       HIPCHK(hipMemcpyAsync(&wide, r_wide.p, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipStreamSynchronize(stream));
-      lap("records scatter + D2H");
+      lap("records_d2h");
       if (wide) {  // re-run the pass once writing full records (same statuses), compact those too
         if (!er.p) er.alloc(nrules * nres * sizeof(ErrRec), device);
         O.err = (ErrRec*)er.p;
@@ -1141,12 +1234,17 @@ struct DevSession {
         if (r_outw.n < total * sizeof(ErrRec)) r_outw.alloc(std::max<uint64_t>(total, 1) * sizeof(ErrRec), device);
         HIPCHK(launch_rec_compact(O.status, O.err8, O.err, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                   nullptr, (unsigned long long*)r_base.p, (ErrRec8*)r_out8.p, (ErrRec*)r_outw.p,
-                                  (uint32_t*)r_wide.p, 1, nullptr, stream));
+                                  (uint32_t*)r_wide.p, 1, nullptr, ord, masks, stream));
         part->recw.alloc(total);
         HIPCHK(hipMemcpyAsync(part->recw.data(), r_outw.p, total * sizeof(ErrRec), hipMemcpyDeviceToHost, stream));
+        lap("records_wide_rerun");
       }
     }
     HIPCHK(hipStreamSynchronize(stream));
+    if (side_copy) {
+      HIPCHK(hipStreamSynchronize(side));
+      lap("status_d2h_wait");
+    }
   }
 };
 
@@ -1383,7 +1481,10 @@ struct SessionSet {
     if (mode & KV_MODE_SCOPES) out->scope_counts = scope_counts_;
     if (parts[0]->O.status && (mode & (KV_MODE_STATUS | KV_MODE_ERRORS))) {
       HIPCHK(hipSetDevice(parts[0]->device));
+      const auto ta = std::chrono::steady_clock::now();
       out->status.alloc(nrules * nres);
+      out->phases.push_back(
+          {"host_alloc", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count()});
     }
     out->errors = (mode & KV_MODE_ERRORS) != 0;
     out->parts.resize(parts.size());
@@ -1419,7 +1520,12 @@ void run(kv_policyset* ps, kv_batch* bt, const char* ctx_json, const std::vector
   double t = s.run(n) / n;
   const auto t2 = std::chrono::steady_clock::now();
   if (ms) *ms = t;
-  if (out) s.fetch(out, t);
+  if (out) {
+    auto d = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    const double up = s.parts.empty() ? 0.0 : s.parts[0]->upload_ms;
+    out->phases = {{"upload", up}, {"setup", d(t0, t1) - up}, {"pass", d(t1, t2)}};
+    s.fetch(out, t);
+  }
   if (getenv("KVGPU_VERBOSE")) {  // host-boundary breakdown
     const auto t3 = std::chrono::steady_clock::now();
     auto d = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -1631,6 +1737,14 @@ int kv_result_status(const kv_result* r, const uint8_t** status, uint64_t* n_rul
   return 0;
 }
 
+int kv_result_phase(const kv_result* r, uint32_t i, const char** name, double* ms) {
+  if (!r) return KV_E_INVALID;
+  if (i >= r->phases.size()) return KV_E_RANGE;
+  if (name) *name = r->phases[i].first.c_str();
+  if (ms) *ms = r->phases[i].second;
+  return 0;
+}
+
 int kv_result_counts(const kv_result* r, const int64_t** counts) {
   if (!r || !counts) return KV_E_INVALID;
   *counts = r->counts.data();
@@ -1692,7 +1806,8 @@ int kv_result_error_message(const kv_result* r, uint32_t rule, uint64_t res, con
                             char* buf, size_t cap) {
   if (!r || !r->has_err() || !resource_json) return KV_E_INVALID;
   if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
-  res = r->sidx(res);  // the caller's document of its resource `res`, the record of its store slot
+  const uint64_t s = r->store_of(res);  // the batch's tables are in store order
+  res = r->sidx(res);  // the caller's document of its resource `res`, the record of its status slot
   size_t o = (size_t)rule * r->n_res + res;
   const uint8_t st = r->status[o];
   if (st != ST_FAIL && st != ST_ERROR && st != ST_SKIP) return KV_E_INVALID;
@@ -1706,10 +1821,10 @@ int kv_result_error_message(const kv_result* r, uint32_t rule, uint64_t res, con
     std::string pv;
     const std::string* dyn_pv = nullptr;
     if (e.pnode < r->ps->ps.pnodes.size() && r->ps->ps.pnodes[e.pnode].dleaf >= 0) {
-      const ResultPart* p = r->part_of(res);
+      const ResultPart* p = r->part_of(s);
       kv_batch* kb = p->shard ? p->shard.get() : const_cast<kv_batch*>(r->b);
       const DynHost& h = kb->dyn_host(r->ps->ps);
-      const uint64_t nl = kb->b.res.size(), local = res - p->lo;
+      const uint64_t nl = kb->b.res.size(), local = s - p->lo;
       const uint32_t o = h.dleaf[(size_t)r->ps->ps.pnodes[e.pnode].dleaf * nl + local];
       pv = pattern_go_v(outcome_value(kb->b.vout_tab[o]));
       dyn_pv = &pv;
@@ -1731,15 +1846,16 @@ int kv_result_subst_error(const kv_result* r, uint32_t rule, uint64_t res, char*
   if (!r) return KV_E_INVALID;
   if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
   if (r->status.empty()) return KV_E_INVALID;  // counts-only result: no statuses were fetched
+  const uint64_t s = r->store_of(res);          // (the batch's tables are in store order)
   res = r->sidx(res);
   try {
     const RuleRec& rr = r->ps->ps.rules[rule];
     if (!rr.dyn || r->status[(size_t)rule * r->n_res + res] != ST_ERROR) return 0;
-    const ResultPart* p = r->part_of(res);
+    const ResultPart* p = r->part_of(s);
     if (!p) return 0;
     kv_batch* kb = p->shard ? p->shard.get() : const_cast<kv_batch*>(r->b);
     const DynHost& h = kb->dyn_host(r->ps->ps);
-    const uint64_t nl = kb->b.res.size(), local = res - p->lo;
+    const uint64_t nl = kb->b.res.size(), local = s - p->lo;
     const size_t q = (size_t)(rr.dyn - 1) * nl + local;
     if (h.dyn_st[q] != ST_ERROR) return 0;
     // ruleError(rule, Validation, "variable substitution failed", err) (validation.go:186-188)
@@ -1808,7 +1924,7 @@ int kv_result_failures(const kv_result* cr, uint64_t* n, const uint32_t** rule, 
           }
         }
       }
-      if (!r->b->b.order.empty()) {
+      if (!r->b->b.order.empty() && !r->caller_order) {
         // caller order: by rule, then caller resource index. Each rule's pairs are a subset of
         // [0, n_res) with distinct caller indices: scattered into a per-thread slot array and
         // swept in order (rules split over host threads; no comparison sort)

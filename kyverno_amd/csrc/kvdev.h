@@ -34,14 +34,16 @@ hipError_t launch_remap_u32(uint32_t* a, uint64_t n, const uint32_t* map, hipStr
 
 // Error-record compaction in rule-major, resource order. phase 0: offs[rule][tile]
 // (exclusive, tiles of KV_WG resources), totals[rule], base[rule] (base[n_rules] =
-// all records); phase 1: scatter the records (compact: appended per wave segment by the
-// specialized kernels, else at their pair's slot; with errw/outw also the full ones) to
-// out8[base[rule] + offs[rule][tile] + rank]; *wide |= 1 if a compact record is flagged
-// ERR8_WIDE.
+// all records) over `status`, and with `masks` every wave's record lanes
+// (masks[rule][res / 64]); phase 1: scatter the records (compact: appended per wave segment by
+// the specialized kernels, else at their pair's slot; with errw/outw also the full ones) of the
+// store-order `status` to out8[base[rule] + offs[rule][tile] + rank]; *wide |= 1 if a compact
+// record is flagged ERR8_WIDE. With `order` (store index -> caller index) phase 0 ran over the
+// caller-order statuses and phase 1 puts each record at its caller index's place.
 hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const ErrRec* errw, uint32_t n_res,
                               uint32_t n_rules, uint32_t* offs, unsigned long long* totals, unsigned long long* base,
                               ErrRec8* out8, ErrRec* outw, uint32_t* wide, int phase, const uint8_t* compact,
-                              hipStream_t stream);
+                              const uint32_t* order, unsigned long long* masks, hipStream_t stream);
 
 constexpr uint32_t KV_SCOPE_CHUNK = 65536;  // resources per workgroup of the scope-count kernel
 constexpr uint32_t KV_SCOPE_LDS = 2048;     // scopes held in LDS (2048 x 8 x 4 B = 64 KB)
@@ -56,5 +58,15 @@ hipError_t launch_scope_counts(const uint8_t* status, const uint32_t* scope, uin
 // (rank among the row's set bits, from roff[row]), else the zero cell (row padding)
 hipError_t launch_expand_rows(const Node* pcells, const uint64_t* rmask, const uint32_t* roff, uint64_t n_rows,
                               Node* nodes, hipStream_t stream);
+
+// Path columns of a batch (kvcol.h, kvdevtypes.h ColDesc / ColFam; n_groups: 64-lane wave
+// groups, a multiple of 4). rows: for every family f > 0 the element rows of each wave group
+// (the most any of its lanes needs) into fams[f].erow, then their exclusive prefix (the
+// family's total at erow[n_groups]). build: the cells of columns [c0, c0 + n) of every lane
+// into the pool (family-0 columns first; element columns read their family arrays' cells).
+hipError_t launch_pcol_rows(const DevBatch* B, const ColDesc* cols, const ColFam* fams, uint32_t n_fam,
+                            uint32_t n_groups, hipStream_t stream);
+hipError_t launch_pcol_build(const DevBatch* B, const ColDesc* cols, const ColFam* fams, uint32_t j0, uint32_t c0,
+                             uint32_t n, uint32_t n_groups, bool elem, Node* pool, hipStream_t stream);
 
 }  // namespace kv

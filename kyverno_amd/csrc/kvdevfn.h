@@ -5,6 +5,7 @@
 
 #define KV_SENT 0xFFFFFFFFu
 
+
 // Linkage of the shared helpers: the bytecode VM (kvkernel.hip) keeps the
 // generic ones out of line; the specialized kernels' prelude (kvjit.cpp)
 // defines KV_JIT_PRELUDE so everything is inlined and the rule kernels make no
@@ -760,6 +761,8 @@ __device__ __forceinline__ void kv_final(const DevOut& O, uint32_t ri, uint32_t 
 // instead (no counter; partial lines: C3 writes 7.55 -> 9.74 GB) 8.22 ms. A one-member group
 // (C4's and C5's rules) takes the wave-level add of a single rule: 64 lanes adding to one LDS
 // word serialise.
+// V: the finalization variant of the generated kernels (kvjit.cpp, KVGPU_JIT_GFIN)
+template <int V = 0>
 __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_t r, bool valid, uint32_t m, uint32_t st,
                                         uint32_t ekx, uint32_t i0, uint32_t i1, uint32_t i2, uint32_t i3,
                                         uint8_t* s_row0, uint32_t row0, const uint32_t* tab, uint32_t n, uint32_t ri0,
@@ -774,6 +777,56 @@ __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_
     }
     return;
   }
+  if constexpr (V == 1) {
+  // this lane's members one after the other (a member's record slot: one lane-level LDS add on
+  // its row's counter byte); rule ids and rows per lane
+  const bool rec = valid && (O.full & 2) && !(O.full & 4) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP);
+  const uint8_t st8 = valid ? (uint8_t)st : (uint8_t)0xFFu;
+  uint8_t* s_c = s_row0 - KV_ROW0 - row0 * KV_RSTRIDE + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * KV_KROWS;
+  for (uint32_t mm = m; mm; mm &= mm - 1u) {
+    const uint32_t j = (uint32_t)__builtin_ctz(mm), row = row0 + j;
+    if (rec) {
+      const uint32_t ri = tab ? tab[j] : ri0 + j * sri;
+      uint32_t z = 0u, rr = r;
+      asm volatile("" : "+v"(rr), "+v"(z));
+      const uint32_t ek = ekx ? ekx + ((tab ? tab[n + j] : j * spn) << 8) : 0u;
+      const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
+      if (slot) {
+        ((uint2*)(O.err8 + (size_t)ri * n_res))[rr] = err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, rr);
+      } else {
+        const uint32_t sh = 8u * (row & 3u);
+        kv_rec_put(O, ri, n_res, rr, (atomicAdd((uint32_t*)(s_c + (row & ~3u)), 1u << sh) >> sh) & 0xFFu, e, z);
+      }
+    }
+    s_row0[j * KV_RSTRIDE + threadIdx.x] = st8;
+  }
+  } else if constexpr (V == 2) {
+  // the members some lane of the wave ends here, one after the other: a uniform loop (scalar rule
+  // ids and rows, the wave-level counter add of a single rule), as many rounds as distinct members
+  for (uint32_t mm = m;;) {
+    const unsigned long long act = __ballot(mm != 0u);
+    if (act == 0ull) break;
+    const uint32_t j = __builtin_amdgcn_readlane((uint32_t)__builtin_ctz(mm | 0x80000000u), (uint32_t)__builtin_ctzll(act));
+    if ((mm >> j) & 1u) {
+      const uint32_t ri = __builtin_amdgcn_readfirstlane(tab ? tab[j] : ri0 + j * sri);
+      if (slot) {
+        const bool rec = valid && (O.full & 2) && !(O.full & 4) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP);
+        if (rec) {
+          uint32_t z = 0u, rr = r;
+          asm volatile("" : "+v"(rr), "+v"(z));
+          const uint32_t ek = ekx ? ekx + ((tab ? tab[n + j] : j * spn) << 8) : 0u;
+          ((uint2*)(O.err8 + (size_t)ri * n_res))[rr] = err8_pack((ek & 15u) + z, (ek >> 4) & 15u, (ek >> 8) + z, ABSENT, i0, i1, i2, i3, rr);
+        }
+        s_row0[j * KV_RSTRIDE + threadIdx.x] = valid ? (uint8_t)st : (uint8_t)0xFFu;
+      } else {
+        const uint32_t ek = ekx ? ekx + ((tab ? tab[n + j] : j * spn) << 8) : 0u;
+        const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
+        kv_final(O, ri, n_res, r, valid, st, e, s_row0 + j * KV_RSTRIDE, row0 + j);
+      }
+    }
+    mm &= ~(1u << j);
+  }
+  } else {
   const bool rec = valid && (O.full & 2) && !(O.full & 4) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP);
   constexpr uint32_t NW = 5u;  // 64-bit counter words a group of < 32 rows touches
   const uint32_t w0 = row0 >> 3;
@@ -807,6 +860,7 @@ __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_
         kv_rec_put(O, ri, n_res, rr, (uint32_t)(old[((row0 + j) >> 3) - w0] >> (8u * ((row0 + j) & 7u))) & 0xFFu, e, z);
     }
     s_row0[j * KV_RSTRIDE + threadIdx.x] = valid ? (uint8_t)st : (uint8_t)0xFFu;
+  }
   }
 #else
   for (uint32_t j = 0; j < n; j++) {

@@ -131,6 +131,39 @@ struct DevBatch {
   const DevPS* dps;
   const uint32_t* dleaf;
   const uint8_t* dyn_st;
+  // path columns of the specialized kernels (kvcol.h; null without them)
+  const Node* pcol;
+};
+
+// ------------------------------------------------------------------ path columns
+// The specialized kernels read every lookup whose path from the resource root (or from the
+// element of a fused array loop) is static from a column of the batch's nodes at that path,
+// one coalesced 16 B load, instead of chasing the path through the node rows (kvjit.cpp
+// hoist). Columns come in families: family 0 has one column per root path, laid out
+// [wave group][column][lane]; family f > 0 belongs to one array path (its "family array", a
+// column of family 0) and holds one column per path relative to that array's elements, laid
+// out [element row][column][lane] with the element rows of each wave group together
+// (element i of a lane's array: row E + i, E = the family array cell's `c`). Cell of a present
+// node: {type | KV_COL_PRESENT, a, b, c'} with c' = the node's own index for a map, the cell
+// offset of its element rows for a family array, the node's c otherwise; absent: all zero.
+// Built once per batch and device (kvcol.h, kv_pcol_* in kvkernel.hip).
+constexpr uint32_t KV_COL_MAXD = 12;            // steps of a column path
+constexpr uint32_t KV_COL_SCAN = 0x80000000u;   // step: key id of a keep-all map (else a slot)
+constexpr uint32_t KV_COL_PRESENT = 16u;        // kt of a present cell: type | KV_COL_PRESENT
+struct ColDesc {
+  uint32_t fam;      // 0: a root path, f > 0: a path relative to the elements of family f
+  uint32_t j;        // column within its family
+  uint32_t nsteps;   // path length
+  uint32_t arr_fam;  // family columns 0: the family whose array this column holds (0: none)
+  uint32_t steps[KV_COL_MAXD];
+};
+// per family: its array's column in family 0 (family 0: unused), its columns; set per batch:
+// the first cell of its element rows in the pool, and (device pointer) the exclusive prefix of
+// element rows per wave group (n_groups + 1 entries: the last one is the family's row count)
+struct ColFam {
+  uint32_t arr_col, ncols;
+  uint32_t off_lo, off_hi;
+  uint32_t* erow;
 };
 
 struct DevOut {

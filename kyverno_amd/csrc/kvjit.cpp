@@ -88,7 +88,92 @@ struct Gen {
   // per rule). Hoisted lookups are branch-free (a failed guard reads cell 0 and discards
   // it) and are placed at the top of their chunk / fused-loop body, so the loads of one
   // tree level issue together instead of one dependent wait per lookup.
-  explicit Gen(const PolicySet& p) : ps(p), rec_slot(p.rules.size(), 0) {}
+  explicit Gen(const PolicySet& p) : ps(p), rec_slot(p.rules.size(), 0) {
+    const char* c = getenv("KVGPU_JIT_COLS");
+    cols_on = !(c && !strcmp(c, "0"));
+    fams.emplace_back();
+    col_of(0, "R");  // column 0 of family 0: the root
+  }
+
+  // ---------------------------------------------------------------- path columns
+  // Hoisted lookups (below) read the node at their static path from a column of the batch
+  // (kvdevtypes.h, built per batch by kvcol.h) instead of walking the node rows from the root
+  // or the loop element: one independent coalesced load per lookup instead of a chain of
+  // dependent ones. Family 0 holds root paths; family f > 0 the paths relative to the elements
+  // of one array path (a column of family 0). Columns are numbered in order of first use; the
+  // column count of each family is a macro (KVC_J<f>) defined at the head of every kernel
+  // program once the whole image is generated.
+  bool cols_on = true;
+  struct Fam {
+    std::string arr;                          // family array expr (family 0: "")
+    std::map<std::string, uint32_t> idx;      // relative expr -> column
+    std::vector<std::vector<uint32_t>> steps; // per column: its path steps
+  };
+  std::vector<Fam> fams;
+  std::map<std::string, uint32_t> fam_of;  // family array expr -> family
+  static constexpr uint32_t kNoCol = 0xFFFFFFFFu;
+  // steps of a symbolic path: "/s<slot>" (slot-addressed map) or "/k<key>" (keep-all map
+  // scan) after the root token ("R", or "E<tag>" of a loop element, or nothing)
+  static bool expr_steps(const std::string& ex, std::vector<uint32_t>* out) {
+    out->clear();
+    size_t at = ex.find('/');
+    while (at != std::string::npos) {
+      const size_t nx = ex.find('/', at + 1);
+      const std::string tok = ex.substr(at + 1, nx == std::string::npos ? std::string::npos : nx - at - 1);
+      if (tok.size() < 2 || (tok[0] != 's' && tok[0] != 'k')) return false;
+      const unsigned long v = strtoul(tok.c_str() + 1, nullptr, 10);
+      if (v >= KV_COL_SCAN) return false;
+      out->push_back((uint32_t)v | (tok[0] == 'k' ? KV_COL_SCAN : 0u));
+      at = nx;
+    }
+    return out->size() <= KV_COL_MAXD;
+  }
+  uint32_t col_of(uint32_t f, const std::string& rel) {
+    Fam& F = fams.at(f);
+    auto it = F.idx.find(rel);
+    if (it != F.idx.end()) return it->second;
+    std::vector<uint32_t> st;
+    if (!expr_steps(rel, &st)) return kNoCol;
+    const uint32_t j = (uint32_t)F.steps.size();
+    F.idx.emplace(rel, j);
+    F.steps.push_back(st);
+    return j;
+  }
+  // family of the elements of array expr `arr` (a root path); its column 0 is the element itself
+  uint32_t family(const std::string& arr) {
+    auto it = fam_of.find(arr);
+    if (it != fam_of.end()) return it->second;
+    if (col_of(0, arr) == kNoCol) return kNoCol;
+    const uint32_t f = (uint32_t)fams.size();
+    fams.emplace_back();
+    fams.back().arr = arr;
+    col_of(f, "");
+    fam_of.emplace(arr, f);
+    return f;
+  }
+  // the plan (JitImage::cols / fam_*) and the macro block of the kernel programs
+  void col_plan(JitImage* out, std::string* defs) const {
+    out->cols.clear();
+    out->fam_arr.clear();
+    out->fam_ncols.clear();
+    std::ostringstream d;
+    for (uint32_t f = 0; f < fams.size(); f++) {
+      const Fam& F = fams[f];
+      out->fam_arr.push_back(f ? fams[0].idx.at(F.arr) : 0u);  // (family 0 columns come first)
+      out->fam_ncols.push_back((uint32_t)F.steps.size());
+      d << "#define KVC_J" << f << " " << F.steps.size() << "u\n";
+      for (uint32_t j = 0; j < F.steps.size(); j++) {
+        ColDesc c{};
+        c.fam = f;
+        c.j = j;
+        c.nsteps = (uint32_t)F.steps[j].size();
+        for (uint32_t s = 0; s < c.nsteps; s++) c.steps[s] = F.steps[j][s];
+        out->cols.push_back(c);
+      }
+    }
+    for (uint32_t f = 1; f < fams.size(); f++) out->cols.at(out->fam_arr[f]).arr_fam = f;
+    *defs = d.str();
+  }
 
   // leaf predicate `pi` on node expression `n` (arrays: every element): one bit of the
   // value-predicate table
@@ -814,6 +899,10 @@ struct Gen {
     std::set<std::string> words;    // hoisted table-word loads (Gen::pw)
     size_t flushed = 0;
     uint32_t n = 0;
+    // path columns: the family its lookups read (-1: none, walk the node rows), the root token
+    // of its exprs (an element family) and the cell-offset expression of its lane's column 0
+    int fam = -1;
+    std::string troot, cell0;
     std::string flush() {
       std::string s;
       for (; flushed < code.size(); flushed++) s += code[flushed];
@@ -859,6 +948,17 @@ struct Gen {
     HVar h{T.prefix + "h" + std::to_string(T.n), T.prefix + "hn" + std::to_string(T.n)};
     T.n++;
     std::ostringstream c;
+    const uint32_t j = T.fam >= 0 ? col_of((uint32_t)T.fam, T.fam == 0 ? ex : ex.substr(T.troot.size())) : kNoCol;
+    if (j != kNoCol) {
+      // the node from its path column (absent: the zero cell); the index only where the
+      // lookup's presence (or a map's own index: wildcard keys) is asked for
+      c << "  const Node " << h.node << " = PC[" << T.cell0 << " + " << u32(j * KV_LANES) << "];\n"
+        << "  const uint32_t " << h.idx << " = " << h.node << ".kt == 0u ? ABSENT : node_type(" << h.node
+        << ".kt) == NT_MAP ? " << h.node << ".c : 0u;\n";
+      T.code.push_back(c.str());
+      T.vars.emplace(ex, h);
+      return h;
+    }
     c << "  uint32_t " << h.idx << " = ABSENT; Node " << h.node << "{0u, 0u, 0u, 0u};\n";
     if (scan) {
       c << "  if (node_type(" << p.node << ".kt) == NT_MAP) for (uint32_t q_ = 0u; q_ < " << p.node << ".b; q_++) { "
@@ -935,7 +1035,7 @@ struct Gen {
         if (g.uses_anchor) st = "((areg" + s + " & ~apres" + s + ") ? ST_ERROR : " + st + ")";
       }
       std::ostringstream r;
-      r << "kv_gfin(O, n_res, r, valid, " << m << ", " << st << ", " << u32(kind | (pcn.flags << 4) | (pn << 8));
+      r << "kv_gfin<KVJ_GFIN>(O, n_res, r, valid, " << m << ", " << st << ", " << u32(kind | (pcn.flags << 4) | (pn << 8));
       for (uint32_t lv = 0; lv < 4; lv++) r << ", " << (lv <= g.max_level ? li(lv) : std::string("0u"));
       r << ", s_w + " << u32(KV_ROW0 + g.grow * KV_RSTRIDE) << ", " << u32(g.grow) << ", " << (g.gtab.empty() ? std::string("nullptr") : g.gtab) << ", "
         << u32(g.gn) << ", " << u32(g.gri[0]) << ", " << u32(g.gsri) << ", " << u32(g.gspn) << ", "
@@ -1253,7 +1353,9 @@ struct Gen {
   std::string group_form(uint32_t ri, std::vector<uint32_t>* preds, std::vector<uint32_t>* pns,
                          std::vector<uint32_t>* leafpcs) const {
     const RuleRec& rr = ps.rules[ri];
-    if (rr.route != 0) return "";
+    // (pattern-variable rules stay out of groups: their substitution status is decided per
+    // member before the walk, and a group's record layout may be per resource slot)
+    if (rr.route != 0 || rr.dyn) return "";
     const uint32_t b = rr.prog, e = prog_end(ps, b);
     std::ostringstream f;
     auto rel = [&](uint32_t t) { return (int64_t)t - (int64_t)b; };
@@ -1385,6 +1487,10 @@ struct Gen {
     std::vector<RGen> gs;
     HoistTable global;
     global.prefix = "g";
+    if (cols_on) {
+      global.fam = 0;
+      global.cell0 = "gc_";
+    }
     gT = &global;
     size_t K = 0;
     for (uint32_t q = 0; q < nr; q++) {
@@ -1474,11 +1580,9 @@ struct Gen {
       const std::string s = g ? g->s : "_" + std::to_string(ch.rules[q]);
       const std::string st = "rs" + s + " & 0xFFu";
       if (!g) return store_st(q, g, st, "0u");
-      if (g->grp)  // the members alive here end with the group's status (no error record)
-        return "  if ((rs" + s + " & 0xFFu) != ST_STORED_)\n    kv_gfin(O, n_res, r, valid, al" + s + ", rs" + s +
-               " & 0xFFu, 0u, 0u, 0u, 0u, 0u, s_w + " + u32(KV_ROW0 + g->grow * KV_RSTRIDE) + ", " + u32(g->grow) + ", " +
-               (g->gtab.empty() ? std::string("nullptr") : g->gtab) + ", " + u32(g->gn) + ", " + u32(g->gri[0]) + ", " +
-               u32(g->gsri) + ", " + u32(g->gspn) + ", " + (g->gn >= gslot_members() ? "true" : "false") + ");\n";
+      // the members alive at a group's end passed: their PASS was staged by the match code
+      // (a group ends only at DONE, ST_PASS, or with every member decided, ST_STORED_)
+      if (g->grp) return std::string();
       return "  if ((rs" + s + " & 0xFFu) != ST_STORED_" + (hist_lds ? std::string(" && (rs" + s + " & 0xFFu) != ST_NOMATCH") : "") +
              ") {\n" + store_st(q, g, st, "ek" + s) + "  }\n";
     };
@@ -1489,26 +1593,33 @@ struct Gen {
       for (const RGen& x : gs)
         if (x.q == q && x.grp) gp = &x;
       if (gp) {
+        // a group's members are consecutive rows, so their match bits are consecutive bits of the
+        // block's match words: one extract instead of a branch per member. Statuses are staged
+        // here, branch-free: PASS for every member that runs (a failure overwrites its byte where
+        // it is raised, so the group's end stores nothing), CPU for the members an anchor-error
+        // phrase or a panicking labels / annotations shape routes (rows start as NOMATCH; 0xFF
+        // past the batch)
         const RGen& g = *gp;
         std::ostringstream k;
+        const uint32_t p0 = mt_kbase * 32u + g.grow, w0 = p0 / 32u, s0 = p0 % 32u;
+        const uint32_t mask = g.gn >= 32 ? 0xFFFFFFFFu : (1u << g.gn) - 1u;
+        k << "  { uint32_t mt_ = ((mw" << w0 << " >> " << s0 << "u)";
+        if (s0 + g.gn > 32u) k << " | (mw" << (w0 + 1) << " << " << (32u - s0) << "u)";
+        k << ") & " << hex32(mask) << ";\n";
+        for (uint32_t j = 0; j < g.gn; j++)
+          if (name_dependent(g.gri[j]))
+            k << "    if (((mt_ >> " << j << "u) & 1u) && !g_match_" << g.gri[j] << "(P, B, R, rkind, rflags)) mt_ &= "
+              << hex32(~(1u << j)) << ";\n";
+        k << "    uint32_t cpu_ = (rflags & RF_MAGIC) ? mt_ : 0u;\n";
         for (uint32_t j = 0; j < g.gn; j++) {
-          const uint32_t ri = g.gri[j];
-          const RuleRec& rr = ps.rules[ri];
-          const std::string rw = "s_w + " + u32(KV_ROW0 + (g.grow + j) * KV_RSTRIDE) + ", " + u32(g.grow + j);
-          auto st = [&](const std::string& x) {
-            return "{ const EState e_{0u, 0u, 0u, ABSENT, ABSENT, 0u, 0u, 0u, 0u}; kv_final(O, " + u32(ri) +
-                   ", n_res, r, valid, " + x + ", e_, " + rw + "); }";
-          };
-          k << "  if (" << mt_cond(ri, hbase + g.q + j) << ") {\n"
-            << "    if (rflags & RF_MAGIC) " << st("ST_CPU") << "\n";
-          if (rr.flags & RR_META_EXPAND) k << "    else if (rflags & " << u32(meta_bad_flags(rr.flags)) << ") " << st("ST_CPU") << "\n";
-          if (rr.dyn)
-            k << "    else if (B.dyn_st[(size_t)" << (rr.dyn - 1) << "u * n_res + r]) " << st("B.dyn_st[(size_t)" + std::to_string(rr.dyn - 1) + "u * n_res + r]") << "\n";
-          // (hist_lds: the row was prefilled with NOMATCH)
-          k << "    else al" << g.s << " |= " << u32(1u << j) << ";\n  }";
-          if (hist_lds) k << "\n";
-          else k << " else " << st("ST_NOMATCH") << "\n";
+          const RuleRec& rr = ps.rules[g.gri[j]];
+          if (rr.flags & RR_META_EXPAND)
+            k << "    cpu_ |= (rflags & " << u32(meta_bad_flags(rr.flags)) << ") ? (mt_ & " << u32(1u << j) << ") : 0u;\n";
         }
+        for (uint32_t j = 0; j < g.gn; j++)
+          k << "    s_w[" << u32(KV_ROW0 + (g.grow + j) * KV_RSTRIDE) << " + threadIdx.x] = valid ? (uint8_t)(((mt_ >> " << j
+            << "u) & 1u) ? (((cpu_ >> " << j << "u) & 1u) ? ST_CPU : ST_PASS) : ST_NOMATCH) : (uint8_t)0xFFu;\n";
+        k << "    al" << g.s << " = mt_ & ~cpu_; }\n";
         k << "  rs" << g.s << " = al" << g.s << " ? " << u32(g.b) << " : FIN_ | ST_STORED_;\n";
         return k.str();
       }
@@ -1657,6 +1768,14 @@ struct Gen {
         HoistTable T;
         T.prefix = "l" + tag + "_";
         const std::string troot = "E" + tag;
+        // the elements' lookups from the columns of the array's family (the array must be a
+        // column itself: its cell carries the offset of its element rows)
+        const uint32_t fam = cols_on && key[0] == 'R' && fams[0].idx.count(key) ? family(key) : kNoCol;
+        if (fam != kNoCol) {
+          T.fam = (int)fam;
+          T.troot = troot;
+          T.cell0 = "ec" + tag;
+        }
         std::ostringstream bodies;
         std::vector<uint32_t> gmask(nw, 0);  // lean rules of the group, per mask word
         for (RGen* gp : grp) {
@@ -1708,17 +1827,22 @@ struct Gen {
           for (uint32_t x = d + 1; x < g.expr.size(); x++) g.expr[x].clear();  // loop-local exprs end here
         }
         body << "  { // fused loop " << tag << " over " << key << " (" << grp.size() << " rules)\n"
-             << "    uint32_t fn" << tag << " = 0u, ff" << tag << " = 0u;\n    if (((0u";
+             << "    uint32_t fn" << tag << " = 0u, ff" << tag << " = 0u, fe" << tag << " = 0u;\n    if (((0u";
         for (RGen* gp : grp)
           if (!gp->lean[k]) body << " | rs" << gp->s;
         body << ") & ACT_)";
         for (uint32_t w = 0; w < nw; w++)
           if (gmask[w]) body << " | (am" << k << "_" << w << " & " << u32(gmask[w]) << ")";
-        body << ") { const Node an_ = " << arr_node << "; ff" << tag << " = an_.a; fn" << tag << " = an_.b; }\n";
+        body << ") { const Node an_ = " << arr_node << "; ff" << tag << " = an_.a; fn" << tag << " = an_.b; fe" << tag
+             << " = an_.c; }\n";
         body << "    for (uint32_t fli" << tag << " = 0u; fli" << tag << " < fn" << tag << "; fli" << tag << "++) {\n"
-             << "      const uint32_t el" << tag << " = ni(ff" << tag << " + fli" << tag << ");\n"
-             << "      const Node eln" << tag << " = N[el" << tag << "];\n"
-             << T.flush() << bodies.str() << "    }\n";
+             << "      const uint32_t el" << tag << " = ni(ff" << tag << " + fli" << tag << ");\n";
+        if (fam != kNoCol)  // the element's column-0 cell: element row fe + i of its family
+          body << "      const uint32_t ec" << tag << " = fe" << tag << " + fli" << tag << " * (KVC_J" << fam
+               << " * " << u32(KV_LANES) << ") + ln_;\n      const Node eln" << tag << " = PC[ec" << tag << "];\n";
+        else
+          body << "      const Node eln" << tag << " = N[el" << tag << "];\n";
+        body << T.flush() << bodies.str() << "    }\n";
         for (RGen* gp : grp)
           if (!gp->lean[k]) body << "    rs" << gp->s << " &= ~ACT_;\n";
         body << "  }\n";
@@ -1788,7 +1912,8 @@ struct Gen {
     uint32_t nr_all = 0;
     for (const JitChunk* c : chs) nr_all += (uint32_t)c->rules.size();
     hist_lds = true;
-    if (nr_all > 192u) throw std::runtime_error("kvjit: at most 192 rules per kernel (KVGPU_JIT_CHUNK)");
+    // (the waves' record counters hold a byte per (wave, row): KV_KROWS rows)
+    if (nr_all > KV_KROWS) throw std::runtime_error("kvjit: at most KV_KROWS rules per kernel (KVGPU_JIT_CHUNK)");
     block_decls.clear();
     mt_kbase = (uint32_t)(mt_bits.size() / 32u);
     for (const JitChunk* c : chs) {
@@ -1827,7 +1952,14 @@ struct Gen {
       << "  const Res* __restrict__ R = B.res + (valid ? r : 0u);\n"
       << "  uint32_t root = ABSENT, rkind = KEY_NONE, rflags = 0u, rtup = 0u;\n"
       << "  if (valid) { root = ni(R->root); rkind = R->kind; rflags = R->flags; rtup = R->tup; }\n"
-      << "  Node rootn{0u, 0u, 0u, 0u};\n  if (valid) rootn = N[root];\n"
+      << "  Node rootn{0u, 0u, 0u, 0u};\n";
+    if (cols_on)  // path columns (kvdevtypes.h): cell offset of this lane's family-0 columns; column 0 = the root
+      o << "  const Node* __restrict__ PC = B.pcol;\n"
+        << "  const uint32_t ln_ = threadIdx.x & " << u32(KV_LANES - 1) << ", gc_ = (r >> 6) * (KVC_J0 * " << u32(KV_LANES)
+        << ") + ln_;\n  if (valid) rootn = PC[gc_];\n";
+    else
+      o << "  if (valid) rootn = N[root];\n";
+    o
       << "  const uint32_t* __restrict__ mtr_ = P.mtup + rtup;\n  const uint32_t ntup_ = B.n_tup;\n"
       << "  uint8_t* s_w = (uint8_t*)s_stw;\n"
       // every status row starts as NOMATCH (0xFF past the batch): only matched lanes store
@@ -2131,6 +2263,19 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   if (out->mtup_words && !out->probe) g.build_fac(out);
   out->rec_compact.assign(n, 1);
   for (uint32_t ri = 0; ri < n; ri++) out->rec_compact[ri] = g.rec_slot[ri] ? 0 : 1;
+  std::string cdefs;  // the column count of every path-column family (KVC_J<f>)
+  g.col_plan(out, &cdefs);
+  // group finalization (kvdevfn.h kv_gfin): 0 members unrolled, 1 per-lane member loop, 2 uniform
+  // loop over the members some lane ends (KVGPU_JIT_GFIN, A/B)
+  {
+    const char* gf = getenv("KVGPU_JIT_GFIN");
+    cdefs = "#define KVJ_GFIN " + std::to_string(gf ? atoi(gf) : 0) + "\n" + cdefs;
+  }
+  if (!g.cols_on) {
+    out->cols.clear();
+    out->fam_arr.clear();
+    out->fam_ncols.clear();
+  }
   out->memo_preds.clear();
   out->memo_words = 0;
   if (!g.mpreds.empty() && !out->probe) {
@@ -2176,7 +2321,7 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   out->common = prelude;
   out->kernel_name.clear();
   out->kernel_src.clear();
-  out->source = prelude + helpers;
+  out->source = prelude + cdefs + helpers;
   for (auto& k : g.kernels) {
     std::vector<char> used(defs.size(), 0);
     std::vector<size_t> stack;
@@ -2192,7 +2337,7 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
     for (size_t d = 0; d < defs.size(); d++)
       if (used[d]) prog += defs[d].second;
     out->kernel_name.push_back(k.first);
-    out->kernel_src.push_back(prog + k.second);
+    out->kernel_src.push_back(cdefs + prog + k.second);
     out->source += k.second;
   }
   out->gen_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -2407,6 +2552,28 @@ bool co_kernel_info(const std::vector<char>& co, const std::string& name, uint32
     }
   }
   return kd && fn;
+}
+
+// SGPR spill count of a code object's kernel from its AMDGPU metadata note (msgpack:
+// ".sgpr_spill_count" then a positive fixint / uint8 / uint16 / uint32; one kernel per object).
+// SGPRs spill into VGPR lanes (v_writelane / v_readlane), not into the private segment.
+uint32_t co_sgpr_spills(const std::vector<char>& co) {
+  static const char key[] = "\xb1.sgpr_spill_count";
+  const auto it = std::search(co.begin(), co.end(), key, key + sizeof key - 1);
+  if (it == co.end()) return 0;
+  const size_t at = (size_t)(it - co.begin()) + sizeof key - 1;
+  if (at >= co.size()) return 0;
+  const uint8_t t = (uint8_t)co[at];
+  auto be = [&](size_t n) {
+    uint32_t v = 0;
+    for (size_t i = 0; i < n && at + 1 + i < co.size(); i++) v = v << 8 | (uint8_t)co[at + 1 + i];
+    return v;
+  };
+  if (t < 0x80) return t;
+  if (t == 0xcc) return be(1);
+  if (t == 0xcd) return be(2);
+  if (t == 0xce) return be(4);
+  return 0;
 }
 
 bool jit_plan_spills(JitImage* img) {

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "kvinternal.hpp"
+#include "kvdevtypes.h"
 
 namespace kvh {
 
@@ -50,7 +51,11 @@ struct JitImage {
   // per rule: 1 = its records are appended to its wave's 64-slot segment (lane in the record),
   // 0 = at the resource's slot (members of large rule groups; kvjit.cpp gslot_members)
   std::vector<uint8_t> rec_compact;
-  bool probe = false;       // a block-probe image (jit_refine_blocks): rule kernels only
+  // path columns the kernels read (kvdevtypes.h ColDesc, built per batch by kvcol.h): every
+  // column; per family its array's column in family 0 and its column count
+  std::vector<kv::ColDesc> cols;
+  std::vector<uint32_t> fam_arr, fam_ncols;
+  bool probe = false;      // a block-probe image (jit_refine_blocks): rule kernels only
   double gen_ms = 0, compile_ms = 0;
 };
 
@@ -87,5 +92,7 @@ bool jit_load_plan(const std::string& key, JitImage* img);
 void jit_save_plan(const std::string& key, const JitImage& img);
 bool co_kernel_info(const std::vector<char>& co, const std::string& name, uint32_t* private_seg, uint64_t* code,
                     uint32_t* vgprs = nullptr);
+// SGPRs the compiler spilled into VGPR lanes (AMDGPU metadata .sgpr_spill_count)
+uint32_t co_sgpr_spills(const std::vector<char>& co);
 
 }  // namespace kvh

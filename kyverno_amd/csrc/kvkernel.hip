@@ -30,6 +30,7 @@ using namespace kv;
 
 #include "kvdevfn.h"
 #include "kvfac.h"
+#include "kvcol.h"
 
 // ------------------------------------------------------------------ kernel
 extern "C" __global__ __launch_bounds__(KV_WG) __attribute__((amdgpu_waves_per_eu(4))) void kv_validate_kernel(const DevPS* __restrict__ Pp,
@@ -471,12 +472,15 @@ namespace kv {
 __device__ __forceinline__ bool has_record(uint8_t s) { return s == ST_FAIL || s == ST_ERROR || s == ST_SKIP; }
 
 __global__ __launch_bounds__(KV_WG) void kv_rec_count_kernel(const uint8_t* __restrict__ status, uint32_t n_res,
-                                                              uint32_t tiles, uint32_t* __restrict__ counts) {
+                                                              uint32_t tiles, uint32_t* __restrict__ counts,
+                                                              unsigned long long* __restrict__ masks) {
   __shared__ uint32_t s_w[KV_WG / 64];
   const uint32_t rule = blockIdx.y, r = blockIdx.x * KV_WG + threadIdx.x;
   const bool f = r < n_res && has_record(status[(size_t)rule * n_res + r]);
   const uint64_t m = __ballot(f);
   if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+  // (caller-order fetch: every wave's record lanes, the ranks of the scatter below)
+  if (masks && (threadIdx.x & 63) == 0) masks[(size_t)rule * tiles * (KV_WG / 64) + (r >> 6)] = m;
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t t = 0;
@@ -539,7 +543,9 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_scatter_kernel(const uint8_t* __
                                                                 const unsigned long long* __restrict__ base,
                                                                 ErrRec8* __restrict__ out8, ErrRec* __restrict__ outw,
                                                                 uint32_t* __restrict__ wide,
-                                                                const uint8_t* __restrict__ compact) {
+                                                                const uint8_t* __restrict__ compact,
+                                                                const uint32_t* __restrict__ order,
+                                                                const unsigned long long* __restrict__ masks) {
   __shared__ uint32_t s_w[KV_WG / 64];
   const uint32_t rule = blockIdx.y, r = blockIdx.x * KV_WG + threadIdx.x, lane = threadIdx.x & 63;
   const size_t o = (size_t)rule * n_res + r;
@@ -550,18 +556,29 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_scatter_kernel(const uint8_t* __
   uint32_t before = 0;  // records of the tile's earlier waves
   for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) before += s_w[w];
   const unsigned long long tile0 = base[rule] + offs[(size_t)rule * tiles + blockIdx.x] + before;
+  // destination of the record of store slot s (rank `rk` among the wave's record lanes): the store
+  // order, or with `order` the caller's (offs / base over the caller-order statuses, `masks` their
+  // record lanes per wave: the rank of caller index j in its tile)
+  auto dest = [&](uint32_t s, uint32_t rk) -> unsigned long long {
+    if (!order) return tile0 + rk;
+    const uint32_t j = order[s];
+    const unsigned long long* mr = masks + (size_t)rule * tiles * (KV_WG / 64);
+    uint32_t q = (uint32_t)__popcll(mr[j >> 6] & ((1ull << (j & 63u)) - 1ull));
+    for (uint32_t w = (j >> 6) & ~3u; w < (j >> 6); w++) q += (uint32_t)__popcll(mr[w]);
+    return base[rule] + offs[(size_t)rule * tiles + (j >> 8)] + q;
+  };
   if (compact && compact[rule]) {  // (rule is uniform: a scalar branch)
     // slot `lane` of the wave's segment holds the wave's lane-th record written; its lane field
     // gives its rank among the wave's record lanes
     if (lane >= (uint32_t)__popcll(m)) return;
     const ErrRec8 e = err8[o];
     const uint32_t l = e.w1 >> 26;
-    out8[tile0 + (uint32_t)__popcll(m & ((1ull << l) - 1ull))] = e;
+    out8[dest((r & ~63u) + l, (uint32_t)__popcll(m & ((1ull << l) - 1ull)))] = e;
     if (e.w0 & ERR8_WIDE) atomicOr(wide, 1u);
     return;
   }
   if (!f) return;
-  const unsigned long long idx = tile0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+  const unsigned long long idx = dest(r, (uint32_t)__popcll(m & ((1ull << lane) - 1ull)));
   const ErrRec8 e = err8[o];
   out8[idx] = e;
   if (outw) outw[idx] = errw[o];
@@ -571,16 +588,17 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_scatter_kernel(const uint8_t* __
 hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const ErrRec* errw, uint32_t n_res,
                               uint32_t n_rules, uint32_t* offs, unsigned long long* totals, unsigned long long* base,
                               ErrRec8* out8, ErrRec* outw, uint32_t* wide, int phase, const uint8_t* compact,
-                              hipStream_t stream) {
+                              const uint32_t* order, unsigned long long* masks, hipStream_t stream) {
   if (n_res == 0 || n_rules == 0) return hipSuccess;
   const uint32_t tiles = (n_res + KV_WG - 1) / KV_WG;
   if (phase == 0) {  // offsets and bases
-    hipLaunchKernelGGL(kv_rec_count_kernel, dim3(tiles, n_rules), dim3(KV_WG), 0, stream, status, n_res, tiles, offs);
+    hipLaunchKernelGGL(kv_rec_count_kernel, dim3(tiles, n_rules), dim3(KV_WG), 0, stream, status, n_res, tiles, offs,
+                       masks);
     hipLaunchKernelGGL(kv_rec_scan_kernel, dim3(n_rules), dim3(KV_WG), 0, stream, offs, tiles, totals);
     hipLaunchKernelGGL(kv_rec_base_kernel, dim3(1), dim3(KV_WG), 0, stream, totals, n_rules, base);
   } else {
     hipLaunchKernelGGL(kv_rec_scatter_kernel, dim3(tiles, n_rules), dim3(KV_WG), 0, stream, status, err8, errw, n_res,
-                       tiles, offs, base, out8, outw, wide, compact);
+                       tiles, offs, base, out8, outw, wide, compact, order, masks);
   }
   return hipGetLastError();
 }
@@ -697,6 +715,73 @@ hipError_t launch_expand_rows(const Node* pcells, const uint64_t* rmask, const u
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(kv_expand_rows_kernel, dim3((uint32_t)blocks), dim3(KV_WG), 0, stream, pcells, rmask, roff, n_rows,
                      nodes);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ path columns (kvcol.h)
+// element rows of family f = 1 + blockIdx.y per wave group: the most any lane of the group needs
+__global__ __launch_bounds__(KV_WG) void kv_pcol_rows_kernel(const DevBatch* __restrict__ Bp,
+                                                             const ColDesc* __restrict__ cols,
+                                                             const ColFam* __restrict__ fams) {
+  const uint32_t r = blockIdx.x * KV_WG + threadIdx.x, f = 1u + blockIdx.y;
+  uint32_t v = col_rows(*Bp, cols, fams, f, r);
+#pragma unroll
+  for (int m = 1; m < (int)KV_LANES; m <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, m, (int)KV_LANES));
+  if ((threadIdx.x & (KV_LANES - 1)) == 0) fams[f].erow[r >> 6] = v;
+}
+
+// exclusive prefix of each family's per-group element rows (one workgroup per family; its
+// total lands at erow[n_groups])
+__global__ __launch_bounds__(1024) void kv_pcol_scan_kernel(const ColFam* __restrict__ fams, uint32_t n_groups) {
+  __shared__ uint32_t s_sum[1024];
+  uint32_t* __restrict__ e = fams[1u + blockIdx.x].erow;
+  const uint32_t per = (n_groups + 1023u) / 1024u, a = threadIdx.x * per, b = min(a + per, n_groups);
+  uint32_t t = 0;
+  for (uint32_t i = a; i < b; i++) t += e[i];
+  s_sum[threadIdx.x] = t;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024u; o <<= 1) {  // inclusive scan of the chunk sums
+    const uint32_t x = threadIdx.x >= o ? s_sum[threadIdx.x - o] : 0u;
+    __syncthreads();
+    s_sum[threadIdx.x] += x;
+    __syncthreads();
+  }
+  uint32_t run = s_sum[threadIdx.x] - t;
+  for (uint32_t i = a; i < b; i++) {
+    const uint32_t c = e[i];
+    e[i] = run;
+    run += c;
+  }
+  if (threadIdx.x == 1023u) e[n_groups] = s_sum[1023];
+}
+
+// cells of columns [c0, c0 + gridDim.y) for every lane (family-0 columns, or element columns
+// after them: their family arrays' cells must be built)
+__global__ __launch_bounds__(KV_WG) void kv_pcol_build_kernel(const DevBatch* __restrict__ Bp,
+                                                              const ColDesc* __restrict__ cols,
+                                                              const ColFam* __restrict__ fams, uint32_t j0,
+                                                              uint32_t c0, uint32_t elem, Node* __restrict__ pool) {
+  const uint32_t r = blockIdx.x * KV_WG + threadIdx.x, c = c0 + blockIdx.y;
+  if (elem) col_build_elem(*Bp, cols, fams, j0, c, r, pool);
+  else col_build_root(*Bp, cols, fams, j0, c, r, pool);
+}
+
+hipError_t launch_pcol_rows(const DevBatch* B, const ColDesc* cols, const ColFam* fams, uint32_t n_fam,
+                            uint32_t n_groups, hipStream_t stream) {
+  if (n_fam < 2 || n_groups == 0) return hipSuccess;
+  hipLaunchKernelGGL(kv_pcol_rows_kernel, dim3(n_groups * KV_LANES / KV_WG, n_fam - 1), dim3(KV_WG), 0, stream, B, cols,
+                     fams);
+  if (hipError_t e = hipGetLastError()) return e;
+  hipLaunchKernelGGL(kv_pcol_scan_kernel, dim3(n_fam - 1), dim3(1024), 0, stream, fams, n_groups);
+  return hipGetLastError();
+}
+
+hipError_t launch_pcol_build(const DevBatch* B, const ColDesc* cols, const ColFam* fams, uint32_t j0, uint32_t c0,
+                             uint32_t n, uint32_t n_groups, bool elem, Node* pool, hipStream_t stream) {
+  if (n == 0 || n_groups == 0) return hipSuccess;
+  if (n > 65535u) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kv_pcol_build_kernel, dim3(n_groups * KV_LANES / KV_WG, n), dim3(KV_WG), 0, stream, B, cols, fams,
+                     j0, c0, elem ? 1u : 0u, pool);
   return hipGetLastError();
 }
 

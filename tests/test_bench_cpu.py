@@ -62,3 +62,42 @@ def test_scope_union_remap_matches_report_reindexing():
     u, c = report.allreduce_scope_counts(names, counts, None)
     assert u == sorted(names)
     assert np.array_equal(c[u.index("ns-a")], counts[2])
+
+
+def test_inprocess_bench_refuses_a_wrong_rccl_rank_count(monkeypatch):
+    """bench.py --gpus N (in process) must prove that RCCL reduced over one rank per distinct
+    device: a parts session whose communicator reports another count ends the run non-zero
+    before the timed region."""
+    import pytest
+
+    import bench
+    from kyverno_amd import batch, workloads
+
+    bench.check_rccl(8, range(8))  # 8 parts on 8 devices: 8 ranks
+    bench.check_rccl(0, [0, 0, 0, 0])  # logical parts on one device: host sum
+    for ranks, devs in [(0, range(8)), (4, range(8)), (1, [0, 0]), (2, [0, 1, 1, 1, 2])]:
+        with pytest.raises(SystemExit):
+            bench.check_rccl(ranks, devs)
+
+    class FakeSession:
+        n_parts = 2
+
+        def attach_part(self, k, b, device):
+            pass
+
+        def rccl_ranks(self):
+            return 1  # wrong: two distinct devices need two ranks
+
+        def scope_names(self):
+            return []
+
+    monkeypatch.setattr(batch.Session, "parts", classmethod(lambda cls, ps, n, mode=0, ctx=None: FakeSession()))
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--n-res", "300", "--config", "c5", "--mode",
+                                      "counts", "--no-cpu-baseline", "--no-e2e", "--no-traffic"])
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    orig = batch.PolicySet  # (the bytecode engine: no hiprtc compile on this CPU-only check)
+    monkeypatch.setattr(batch, "PolicySet", lambda pols, specialize=False: orig(pols))
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert "RCCL communicator has 1 ranks, expected 2" in str(e.value)
+
