@@ -84,7 +84,7 @@ def pmc_traffic(args) -> dict | None:
     one rocprofv3 --pmc run per counter group, kernel-trace/stats only). Per MI355X_MICROARCH.md
     (HBM section): the counters are KB, and on gfx950 FETCH_SIZE counts half the bytes of coalesced
     reads, so it is doubled. Sum over the pass's kernels (the record-compaction kernels kv_rec_*
-    run at fetch, outside the pass)."""
+    run at fetch, outside the pass; the row expansion and path-column build run once per batch)."""
     import csv
     import collections
     import glob
@@ -126,10 +126,10 @@ def pmc_traffic(args) -> dict | None:
         for f in sorted(set(glob.glob(os.path.join(out, "**", f"{ctr}*counter_collection.csv"), recursive=True))):
             for r in csv.DictReader(open(f)):
                 k = r.get("Kernel_Name", "")
-                # the pass's kernels: not the record compaction of a fetch (kv_rec_*) nor the
-                # row expansion of the batch upload (kv_expand_rows), which run once per batch
+                # the pass's kernels: not the record compaction of a fetch (kv_rec_*) nor what the
+                # batch upload runs once per batch (kv_expand_rows, the path-column build kv_pcol_*)
                 if r["Counter_Name"] == ctr and k.startswith(("kv_", "kvj_", "kv::")) and "kv_rec_" not in k \
-                        and "kv_expand_rows" not in k:
+                        and "kv_expand_rows" not in k and "kv_pcol_" not in k:
                     agg[k] += float(r["Counter_Value"])
         if not agg:
             return None
@@ -207,6 +207,7 @@ def e2e_stream(ps, n_res: int, kind_mix: int, device: int, seed: int, chunk: int
     chunks = [batch.synth(seed, min(chunk, n_res - k), kind_mix, first=k) for k in range(0, n_res, chunk)]
     mode = batch.MODE_STATUS | batch.MODE_ERRORS
     results, t_ing, t_val = [], [0.0], [0.0]
+    inflight = 2  # chunks being uploaded / evaluated / fetched while the next one is ingested
 
     def evaluate(b):
         t = time.perf_counter()
@@ -215,23 +216,23 @@ def e2e_stream(ps, n_res: int, kind_mix: int, device: int, seed: int, chunk: int
         return r
 
     t0 = time.perf_counter()
-    with cf.ThreadPoolExecutor(max_workers=1) as ex:
-        pending = None
+    with cf.ThreadPoolExecutor(max_workers=inflight) as ex:
+        pending = []
         for data in chunks:
             t = time.perf_counter()
             b = batch.Batch(ps, data)
             t_ing[0] += time.perf_counter() - t
-            if pending is not None:
-                results.append(pending.result())
-            pending = ex.submit(evaluate, b)
-        results.append(pending.result())
+            while len(pending) >= inflight:
+                results.append(pending.pop(0).result())
+            pending.append(ex.submit(evaluate, b))
+        results.extend(f.result() for f in pending)
     secs = time.perf_counter() - t0
     n_rules = ps.n_rules
     return {"seconds": secs, "evals_per_s": n_res * n_rules / secs, "resources_per_s": n_res / secs,
-            "chunks": len(chunks), "chunk_resources": chunk, "ingest_seconds": t_ing[0],
+            "chunks": len(chunks), "chunk_resources": chunk, "in_flight": inflight, "ingest_seconds": t_ing[0],
             "validate_seconds": t_val[0],
-            "includes": "NDJSON -> kv_ingest (host threads) overlapped with kv_validate of the previous chunk "
-                        "(H2D + pass + D2H of statuses and records)"}
+            "includes": "NDJSON -> kv_ingest (host threads) overlapped with kv_validate of the previous chunks "
+                        "(H2D + pass + D2H of statuses and records, two in flight)"}
 
 
 def main():
@@ -342,6 +343,11 @@ def main():
     else:
         data = batch.synth(workloads.SEED, args.n_res, kind_mix, first=rank * args.n_res)
         ndjson_bytes = len(data)
+        # a long-running caller page-locks its store / result arena once at startup (kv_host_reserve),
+        # not inside the first batch's ingest: about 2.5x the NDJSON for the store, plus the status
+        # matrix and records of a FULL fetch
+        reserve = int(2.5 * ndjson_bytes) + (10 * ps.n_rules * args.n_res if args.mode == "full" else 0)
+        batch.host_reserve(min(reserve, 96 << 30))
         t1 = time.time()
         b = batch.Batch(ps, data)
         del data
@@ -464,7 +470,7 @@ def main():
         del r2, b2
         # the same stream as a caller would push it: ingest overlapped with upload + pass + fetch
         out["e2e_stream"] = e2e_stream(ps, args.n_res, kind_mix, local, workloads.SEED + 13,
-                                       max(KV_LANES_CHUNK, args.n_res // 4))
+                                       max(KV_LANES_CHUNK, args.n_res // 8))
     if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
         # every core this process may run on (the GPU box grants a share of the machine's cores;
         # nproc and the CPU model are recorded beside it)

@@ -119,6 +119,11 @@ int kv_validate_devices(const kv_policyset* ps, const kv_batch* b, const char* c
 int kv_result_status(const kv_result* r, const uint8_t** status, uint64_t* n_rules, uint64_t* n_res);
 /* counts[rule * 8 + status] */
 int kv_result_counts(const kv_result* r, const int64_t** counts);
+/* Page-lock `bytes` of host memory for the library's store and result arrays up front (once per
+ * process; a later call only reports whether the reserve is at least that large), so the ingest of
+ * a process's first batch and its first results find page-locked memory instead of pinning it
+ * then. 0 on success, KV_E_DEVICE without a device or when the host refuses the memory. */
+int kv_host_reserve(uint64_t bytes);
 /* phase i of the kv_validate that produced r: its name ("upload", "setup", "pass", "host_alloc",
  * "status_d2h", "records_count", "records_scatter_d2h", ...) and wall-clock milliseconds;
  * KV_E_RANGE past the last phase. Diagnostics of the host boundary (no reference counterpart). */

@@ -388,6 +388,12 @@ class Session:
             self._h = None
 
 
+def host_reserve(nbytes: int) -> bool:
+    """Page-lock `nbytes` of host memory for the library's store and result arrays once, before the
+    first batch (kv_host_reserve); False without a device."""
+    return lib().kv_host_reserve(int(nbytes)) == 0
+
+
 def synth(seed: int, n: int, kind_mix: int = 0, first: int = 0) -> bytes:
     """NDJSON of resources [first, first + n) of the synthetic stream `seed` (kv_synth_range)."""
     p = ctypes.c_void_p()

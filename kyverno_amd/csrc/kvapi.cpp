@@ -206,14 +206,37 @@ namespace {
 // Page-locked host blocks are expensive to create (pinning), so released result
 // buffers are kept for the next result of the process (up to 8 GiB): a host that
 // validates batch after batch pays the pinning once.
+// A caller that knows its batches' size can page-lock an arena up front (kv_host_reserve, outside
+// ingest): blocks are then carved from it (first fit, 2 MiB granules, freed ranges coalesce) before
+// any new block is page-locked, so even a process's first batch ingests into page-locked memory
+// that is already there.
 struct PinnedPool {
   std::mutex mu;
   std::multimap<size_t, void*> free;  // capacity -> block
   size_t held = 0;
+  char* arena = nullptr;
+  size_t arena_bytes = 0;
+  std::map<size_t, size_t> arena_free;  // offset -> bytes
+  static constexpr size_t kGran = 2u << 20;
   static PinnedPool& get() {
     static PinnedPool* p = new PinnedPool();  // never destroyed: blocks may outlive static teardown
     return *p;
   }
+  bool reserve(size_t bytes) {
+    std::lock_guard<std::mutex> g(mu);
+    if (arena) return arena_bytes >= bytes;
+    bytes = (bytes + kGran - 1) / kGran * kGran;
+    void* p = nullptr;
+    if (!bytes || hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    arena = (char*)p;
+    arena_bytes = bytes;
+    arena_free[0] = bytes;
+    return true;
+  }
+  bool in_arena(const void* p) const { return arena && (const char*)p >= arena && (const char*)p < arena + arena_bytes; }
   void* take(size_t bytes, size_t* cap) {
     {
       std::lock_guard<std::mutex> g(mu);
@@ -224,6 +247,17 @@ struct PinnedPool {
         held -= it->first;
         free.erase(it);
         return p;
+      }
+      if (arena) {
+        const size_t want = (bytes + kGran - 1) / kGran * kGran;
+        for (auto a = arena_free.begin(); a != arena_free.end(); ++a)
+          if (a->second >= want) {
+            const size_t off = a->first, left = a->second - want;
+            arena_free.erase(a);
+            if (left) arena_free[off + want] = left;
+            *cap = want;
+            return arena + off;
+          }
       }
     }
     // headroom (+1/8, 16 MiB granules) so the next batch's slightly larger result fits the block
@@ -238,6 +272,24 @@ struct PinnedPool {
   }
   void give(void* p, size_t cap) {
     std::lock_guard<std::mutex> g(mu);
+    if (in_arena(p)) {  // back into the arena, merged with its free neighbours
+      size_t off = (size_t)((char*)p - arena), len = cap;
+      auto nx = arena_free.lower_bound(off);
+      if (nx != arena_free.end() && nx->first == off + len) {
+        len += nx->second;
+        nx = arena_free.erase(nx);
+      }
+      if (nx != arena_free.begin()) {
+        auto pv = std::prev(nx);
+        if (pv->first + pv->second == off) {
+          off = pv->first;
+          len += pv->second;
+          arena_free.erase(pv);
+        }
+      }
+      arena_free[off] = len;
+      return;
+    }
     if (held + cap > (8ull << 30)) {
       (void)hipHostFree(p);
       return;
@@ -920,6 +972,7 @@ struct DevSession {
   DevBuf r_offs, r_tot, r_base, r_out8, r_outw, r_wide;  // record compaction (fetch)
   DevBuf inv_d, stc;                                     // caller-order statuses (fetch)
   DevBuf ord_d, r_mask;                                  // caller-order records: batch order, record lanes
+  DevBuf stamps;                                         // KVGPU_STAMPS diagnostics
   uint32_t mt_words = 0, mt_entities = 0;
   uint32_t *mt_ns = nullptr, *mt_ann = nullptr, *mt_sel = nullptr;
   uint32_t nscopes = 0, nvals = 0;
@@ -1022,6 +1075,19 @@ struct DevSession {
       O.scounts = (unsigned long long*)scn.p;
       if (dp.specialized()) O.full |= 8;
     }
+    if (getenv("KVGPU_JIT_STAMPS") && dp.specialized()) {  // diagnostics: segment stamps of the rule kernels' waves
+      const uint64_t n = (nres + KV_WG - 1) / KV_WG * (KV_WG / 64) * kJitStamps;
+      stamps.alloc(std::max<uint64_t>(n, 1) * sizeof(unsigned long long), device);
+      HIPCHK(hipMemset(stamps.p, 0, stamps.n));
+      for (hipModule_t m : dp.mods) {  // the kernels' global kvj_stamps -> this buffer
+        hipDeviceptr_t g = nullptr;
+        size_t gs = 0;
+        if (hipModuleGetGlobal(&g, &gs, m, "kvj_stamps") == hipSuccess && gs == sizeof(void*))
+          HIPCHK(hipMemcpy(g, &stamps.p, sizeof(void*), hipMemcpyHostToDevice));
+        else
+          (void)hipGetLastError();
+      }
+    }
     HIPCHK(hipStreamCreate(&stream));
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
@@ -1098,7 +1164,34 @@ struct DevSession {
     HIPCHK(hipEventSynchronize(e1));
     float t = 0;
     HIPCHK(hipEventElapsedTime(&t, e0, e1));
+    if (stamps.p) report_stamps();
     return t;
+  }
+  // mean shader cycles per wave between consecutive stamps of the last rule kernel (segment k: from
+  // stamp k - 1 to stamp k), and the mean wave lifetime
+  void report_stamps() {
+    std::vector<unsigned long long> h(stamps.n / sizeof(unsigned long long));
+    HIPCHK(hipMemcpy(h.data(), stamps.p, stamps.n, hipMemcpyDeviceToHost));
+    double seg[kJitStamps] = {}, life = 0;
+    uint64_t n[kJitStamps] = {}, nl = 0;
+    for (size_t w = 0; w + kJitStamps <= h.size(); w += kJitStamps) {
+      const unsigned long long* x = &h[w];
+      uint32_t last = 0;
+      for (uint32_t k = 1; k < kJitStamps; k++)
+        if (x[k] && x[last]) {
+          seg[k] += (double)(x[k] - x[last]);
+          n[k]++;
+          last = k;
+        }
+      if (x[0] && x[last] && last) {
+        life += (double)(x[last] - x[0]);
+        nl++;
+      }
+    }
+    fprintf(stderr, "[kvgpu] stamps: wave lifetime %.0f cycles;", nl ? life / nl : 0.0);
+    for (uint32_t k = 1; k < kJitStamps; k++)
+      if (n[k]) fprintf(stderr, " seg%u %.0f", k, seg[k] / n[k]);
+    fprintf(stderr, "\n");
   }
   // one launch per rule kernel of the specialized kernels, 256 resources per workgroup
   void launch_specialized() {
@@ -1735,6 +1828,14 @@ int kv_result_status(const kv_result* r, const uint8_t** status, uint64_t* n_rul
   if (n_rules) *n_rules = r->n_rules;
   if (n_res) *n_res = r->n_res;
   return 0;
+}
+
+int kv_host_reserve(uint64_t bytes) {
+  try {
+    return PinnedStore::enabled() && PinnedPool::get().reserve(bytes) ? 0 : KV_E_DEVICE;
+  } catch (const std::exception&) {
+    return KV_E_DEVICE;
+  }
 }
 
 int kv_result_phase(const kv_result* r, uint32_t i, const char** name, double* ms) {

@@ -1927,6 +1927,7 @@ struct Gen {
     const uint32_t nr = (uint32_t)rules.size();
     KernelText kt(*this, name);
     o << block_decls;
+    if (getenv("KVGPU_JIT_STAMPS")) o << "__device__ unsigned long long* kvj_stamps;\n";
     o << "__device__ const uint32_t " << name << "_rules[" << nr << "] = {";
     for (uint32_t q = 0; q < nr; q++) o << (q ? ", " : "") << u32(rules[q]);
     o << "};\n";
@@ -1964,6 +1965,16 @@ struct Gen {
       << "  uint8_t* s_w = (uint8_t*)s_stw;\n"
       // every status row starts as NOMATCH (0xFF past the batch): only matched lanes store
       << "  kv_prefill_rows(s_stw, " << nr << "u, r - threadIdx.x, n_res);\n";
+    // diagnostics (KVGPU_JIT_STAMPS): a wave's shader clock at the start, after each block and
+    // after the flush, into the program's global kvj_stamps ([workgroup][wave][kJitStamps], set by
+    // kvapi.cpp)
+    const bool stamps = getenv("KVGPU_JIT_STAMPS") != nullptr;
+    auto stamp = [&](size_t k) {
+      if (stamps && k < kJitStamps)
+        o << "  if (kvj_stamps && (threadIdx.x & 63u) == 0u) kvj_stamps[((size_t)blockIdx.x * 4u + (threadIdx.x >> 6)) * "
+          << kJitStamps << "u + " << k << "u] = __builtin_amdgcn_s_memtime();\n";
+    };
+    stamp(0);
     for (size_t bi = 0; bi < blocks.size(); bi++) {
       // the block's match words (bits of its rules, kv_mtup_kernel); a wave none of whose resources
       // matches any rule of the block skips it whole (every rule NOMATCH on every lane)
@@ -1980,12 +1991,15 @@ struct Gen {
       // (the rows of a skipped block keep their NOMATCH prefill)
       o << "  if (__ballot((" << any << ") != 0u) != 0ull) {\n" << blocks[bi] << "  }\n";
       o << "  }\n";
+      stamp(bi + 1);
     }
     // statuses to the status matrix, per-rule (and per-scope) histograms
     o << "  const uint32_t wg0_ = r - threadIdx.x;\n"
       << "  kv_end_flush(O, s_stw, " << nr << "u, " << name << "_rules, n_res, r, valid, "
          "(O.full & 8u) && valid ? O.scope[r] : 0xFFFFFFFFu, (O.full & 8u) && wg0_ < n_res ? O.scope[wg0_] : 0xFFFFFFFFu, "
-         "P.n_rules);\n}\n\n";
+         "P.n_rules);\n";
+    stamp(std::min<size_t>(blocks.size() + 1, kJitStamps - 1));
+    o << "}\n\n";
     hist_lds = false;
     return rules;
   }

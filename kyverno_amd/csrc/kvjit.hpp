@@ -63,6 +63,8 @@ struct JitImage {
 // `chunk_rules` rules per kernel).
 // most rules per kernel (one fused block): KVGPU_JIT_CHUNK, default 128
 uint32_t jit_chunk_rules();
+// diagnostics (KVGPU_JIT_STAMPS): stamps per wave of the rule kernels' segment boundaries
+constexpr uint32_t kJitStamps = 16;
 void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out);
 // Compile every kernel program with hiprtc for gfx950, on parallel host threads
 // (KVGPU_JIT_THREADS, default: hardware threads), through the code-object cache

@@ -6,6 +6,7 @@
 #   BENCH=1        the default bench line (C2: e2e leg, CPU baseline, in-run PMC traffic)
 #   PROF=1         rocprofv3 kernel stats of the default bench
 #   CONFIGS="c3 c4 c5"  one bench line per config with in-run PMC traffic + rocprofv3 kernel stats
+#   STAMPS=1       per-segment shader-clock stamps of the rule kernels' waves (STAMPS_CFG, default c2)
 #   PMC=1          the SQ / cache counter passes of C2 (tools/gpu_abpmc.sh), PMC_CFG selects the config
 # Output under gpurun_out/$OUT (default r4).
 set -o pipefail
@@ -50,6 +51,18 @@ for c in $CONFIGS; do
      > "$R/$O/${c}_prof.json" 2> "$R/$O/${c}_prof.err") || { echo "prof $c failed"; tail "$O/${c}_prof.err"; exit 1; }
   kstats "$O/prof_$c"
 done
+if [ -n "$MODES" ]; then  # the C2 kernel in COUNTS mode (no status matrix, no records) beside FULL
+  for m in counts full; do
+    timeout -k 10 300 python -u bench.py --mode $m --steps 20 --warmup 3 --no-cpu-baseline --no-e2e --no-traffic \
+      > "$O/mode_$m.json" 2> "$O/mode_$m.err" || { echo "mode $m failed"; tail "$O/mode_$m.err"; exit 1; }
+    python -c "import json; d=json.load(open('$O/mode_$m.json')); print('mode $m', round(d['kernel_ms_per_step'], 4))"
+  done
+fi
+if [ -n "$STAMPS" ]; then  # segment stamps of the rule kernels' waves (KVGPU_JIT_STAMPS; compiled on the box)
+  KVGPU_JIT_STAMPS=1 timeout -k 10 400 python -u bench.py --config ${STAMPS_CFG:-c2} --steps 5 --warmup 1 --no-cpu-baseline \
+    --no-e2e --no-traffic > "$O/stamps.json" 2> "$O/stamps.err" || { echo "stamps failed"; tail "$O/stamps.err"; exit 1; }
+  grep "stamps:" "$O/stamps.err" | tail -2
+fi
 if [ -n "$PMC" ]; then
   CFG=${PMC_CFG:-c2} OUTDIR="${OUT:-r4}/pmc" bash tools/gpu_abpmc.sh - > "$O/pmc.txt" 2>&1 \
     || { echo "pmc failed"; tail "$O/pmc.txt"; exit 1; }
