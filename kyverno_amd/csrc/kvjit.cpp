@@ -91,6 +91,8 @@ struct Gen {
   explicit Gen(const PolicySet& p) : ps(p), rec_slot(p.rules.size(), 0) {
     const char* c = getenv("KVGPU_JIT_COLS");
     cols_on = !(c && !strcmp(c, "0"));
+    const char* gd = getenv("KVGPU_JIT_GUARDS");
+    guards_on = gd && !strcmp(gd, "1");
     fams.emplace_back();
     col_of(0, "R");  // column 0 of family 0: the root
   }
@@ -996,7 +998,21 @@ struct Gen {
   // + LDS atomics per rule and wave
   bool hist_lds = false;
 
-  void emit_region(RGen& g, const Region& R, std::ostringstream& w) {
+  // Fast-path guards (KVGPU_JIT_GUARDS=1; measured, not shipped): a run of ops that only test hoisted
+  // values (type checks, presence of hoisted keys, hoisted leaf bits) and assign cursors is
+  // preceded by one test of all their exit conditions; a lane none of them fires for takes the
+  // run's assignments and jumps past it, so a wave none of whose lanes fails there runs one
+  // branch instead of one per check. Exact: the conditions are pure functions of the hoisted
+  // values, and with none true the run falls through every check to its end. Round 5
+  // (gpurun_out/r5f, ms per pass, guards / none): C2 0.681 / 0.669, C4 1.068 / 1.044, C5 3.31 /
+  // 3.29, C3 7.56 / 7.58 -- the kernels are not bound by these branches.
+  bool guards_on = false;
+  void emit_region(RGen& g, const Region& R, std::ostringstream& wout) {
+    struct OpOut {
+      std::string code, cond, assign;
+      bool guardable = false;
+    };
+    std::vector<OpOut> outs;
     const std::string& s = g.s;
     auto C = [&](uint32_t d) { return "c" + std::to_string(d) + s; };
     auto L = [&](uint32_t pc) { return "R" + std::to_string(g.ri) + "_L" + std::to_string(pc); };
@@ -1095,30 +1111,54 @@ struct Gen {
       const std::string cd = C(d), cn = C(d + 1);
       const uint32_t lv = aux & 3;
       const std::string L_lv = std::to_string(lv);
+      std::ostringstream w;
+      OpOut oo;  // this op's code and, for the fast-path guards, its exit condition / assignments
       w << L(pc) << ":;\n";
       switch (op) {
         case OP_MAPCHK:
         case OP_ARRCHK: {
           const char* t = op == OP_MAPCHK ? "NT_MAP" : "NT_ARR";
-          if (known(d)) w << "  if (node_type(" << NODE(d) << ".kt) != " << t << ") ";
-          else w << "  if (" << cd << " == ABSENT || node_type(N[" << cd << "].kt) != " << t << ") ";
+          if (known(d)) {
+            w << "  if (node_type(" << NODE(d) << ".kt) != " << t << ") ";
+            oo.guardable = true;
+            oo.cond = "(node_type(" + NODE(d) + ".kt) != " + t + ")";
+          } else {
+            w << "  if (" << cd << " == ABSENT || node_type(N[" << cd << "].kt) != " << t << ") ";
+          }
           w << raise(op == OP_MAPCHK ? E_TYPE_MAP : E_TYPE_ARR, in.a, in.c) << "\n";
           break;
         }
         case OP_AREG: {
           const std::string bit = "(1ull << " + std::to_string(aux & 63) + ")";
-          w << "  areg" << s << " |= " << bit << "; if (" << lookup(d, in.a, aux, false) << " != ABSENT) apres" << s
-            << " |= " << bit << ";\n";
+          const bool h = known(d) && table_for(d);
+          const std::string st = "  areg" + s + " |= " + bit + "; if (" + lookup(d, in.a, aux, false) + " != ABSENT) apres" +
+                                 s + " |= " + bit + ";\n";
+          w << st;
+          if (h) {
+            oo.guardable = true;
+            oo.assign = st;
+          }
           break;
         }
         case OP_KEY: {
+          const bool h = known(d) && table_for(d);
           std::string x = lookup(d, in.a, aux, true);
           w << "  " << cn << " = " << x << "; if (" << cn << " == ABSENT) " << jump(in.b) << "\n";
+          if (h) {
+            oo.guardable = true;
+            oo.cond = "(" + x + " == ABSENT)";
+            oo.assign = "  " + cn + " = " + x + ";\n";
+          }
           break;
         }
         case OP_KEYV: {
+          const bool h = known(d) && table_for(d);
           std::string x = lookup(d, in.a, aux, true);
           w << "  " << cn << " = " << x << ";\n";
+          if (h) {
+            oo.guardable = true;
+            oo.assign = "  " + cn + " = " + x + ";\n";
+          }
           break;
         }
         case OP_KEYGLOB:
@@ -1128,7 +1168,10 @@ struct Gen {
             << u32(in.c) << ", &nd_, &kn" << s << ")) " << jump(in.b) << " " << cn << " = nd_; }\n";
           break;
         case OP_SCOPE_END:
-          if (G) break;  // groups carry no pending error (decided where raised)
+          if (G) {  // groups carry no pending error (decided where raised)
+            oo.guardable = true;
+            break;
+          }
           if (in.c == 0) w << "  if (" << kindof << ") " << ek << " |= " << u32(aux << 4) << ";\n";
           else w << "  if (" << kindof << ") { " << ek << " |= " << u32(aux << 4) << "; " << jump(in.c, true) << " }\n";
           break;
@@ -1137,12 +1180,24 @@ struct Gen {
           w << "  if (" << kindof << ") { if (" << ek << " & " << u32(EF_COND << 4) << ") " << ek << " = 0u; else "
             << jump(in.c, true) << " }\n";
           break;
-        case OP_NEG:
-          w << "  if (" << lookup(d, in.a, aux, false) << " != ABSENT) " << raise(E_NEG, in.b, in.c) << "\n";
+        case OP_NEG: {
+          const bool h = known(d) && table_for(d);
+          const std::string x = lookup(d, in.a, aux, false);
+          w << "  if (" << x << " != ABSENT) " << raise(E_NEG, in.b, in.c) << "\n";
+          if (h) {
+            oo.guardable = true;
+            oo.cond = "(" + x + " != ABSENT)";
+          }
           break;
+        }
         case OP_STAR:
-          if (known(d + 1)) w << "  if (node_type(" << NODE(d + 1) << ".kt) == NT_NULL) ";
-          else w << "  if (" << cn << " == ABSENT || node_type(N[" << cn << "].kt) == NT_NULL) ";
+          if (known(d + 1)) {
+            w << "  if (node_type(" << NODE(d + 1) << ".kt) == NT_NULL) ";
+            oo.guardable = true;
+            oo.cond = "(node_type(" + NODE(d + 1) + ".kt) == NT_NULL)";
+          } else {
+            w << "  if (" << cn << " == ABSENT || node_type(N[" << cn << "].kt) == NT_NULL) ";
+          }
           w << raise(E_STAR, in.b, in.c) << "\n";
           break;
         case OP_LEAF: {
@@ -1166,8 +1221,16 @@ struct Gen {
             w << "  { const uint32_t f_ = " << al << " & ~((" << wx << " >> " << u32(slot % 32) << ") & " << hex32(mask)
               << ");\n    if (f_) { " << gfin("f_", E_VALUE, in.b, in.c) << " " << al << " &= ~f_; if (!" << al << ") "
               << gdone() << " } }\n";
+            if (T) {
+              oo.guardable = true;
+              oo.cond = "((" + al + " & ~((" + wx + " >> " + u32(slot % 32) + ") & " + hex32(mask) + ")) != 0u)";
+            }
           } else {
             w << "  if (!(((" << wx << " >> " << u32(slot % 32) << ") & 1u) != 0u)) " << raise(E_VALUE, in.b, in.c) << "\n";
+            if (T) {
+              oo.guardable = true;
+              oo.cond = "(((" + wx + " >> " + u32(slot % 32) + ") & 1u) == 0u)";
+            }
           }
           break;
         }
@@ -1183,15 +1246,28 @@ struct Gen {
           w << "  " << raise(in.b, in.a, in.c) << "\n";
           break;
         case OP_EXISTCHK:
-          if (known(d)) w << "  if (node_type(" << NODE(d) << ".kt) != NT_ARR) ";
-          else w << "  if (" << cd << " == ABSENT || node_type(N[" << cd << "].kt) != NT_ARR) ";
+          if (known(d)) {
+            w << "  if (node_type(" << NODE(d) << ".kt) != NT_ARR) ";
+            oo.guardable = true;
+            oo.cond = "(node_type(" + NODE(d) + ".kt) != NT_ARR)";
+          } else {
+            w << "  if (" << cd << " == ABSENT || node_type(N[" << cd << "].kt) != NT_ARR) ";
+          }
           w << raise(E_EXIST_RESTYPE, in.a, in.c) << "\n";
           break;
         case OP_LENCHK:
           w << "  if (" << NODE(d) << ".b < " << u32(in.a) << ") " << raise(E_LEN, in.b, in.c) << "\n";
+          if (known(d)) {
+            oo.guardable = true;
+            oo.cond = "(" + NODE(d) + ".b < " + u32(in.a) + ")";
+          }
           break;
         case OP_INDEX:
           w << "  " << cn << " = ni(" << NODE(d) << ".a + " << u32(in.a) << ");\n";
+          if (known(d)) {
+            oo.guardable = true;
+            oo.assign = "  " + cn + " = ni(" + NODE(d) + ".a + " + u32(in.a) + ");\n";
+          }
           set_unknown(d + 1);
           break;
         case OP_LOOP_BEGIN:
@@ -1255,8 +1331,26 @@ struct Gen {
           w << "k_ == E_LEN ? ST_ERROR : ST_FAIL);\n    goto " << R.se << "; }\n";
           break;
         default:  // OP_NOP, OP_METACHK (handled per resource by RF_BAD_META)
+          oo.guardable = true;
           break;
       }
+      oo.code = w.str();
+      outs.push_back(std::move(oo));
+    }
+    // the runs of guardable ops with at least two exit conditions get a fast path to their end
+    for (size_t i = 0; i < outs.size();) {
+      size_t j = i, nc = 0;
+      while (j < outs.size() && outs[j].guardable) nc += !outs[j++].cond.empty();
+      if (guards_on && nc >= 2) {
+        wout << "  if (!(false";
+        for (size_t k = i; k < j; k++)
+          if (!outs[k].cond.empty()) wout << "\n      | " << outs[k].cond;
+        wout << ")) {\n";
+        for (size_t k = i; k < j; k++) wout << outs[k].assign;
+        wout << "    goto " << L(R.rb + (uint32_t)j) << ";\n  }\n";
+      }
+      for (size_t k = i; k < std::max(j, i + 1); k++) wout << outs[k].code;
+      i = std::max(j, i + 1);
     }
   }
 
@@ -2628,7 +2722,8 @@ bool jit_plan_spills(JitImage* img) {
     size_t big = 0;
     for (size_t b = 1; b < np.blocks.size(); b++)
       if (np.blocks[b] > np.blocks[big]) big = b;
-    if (kp.waves > 6 && np.blocks.size() > 1) {
+    static const bool keep_waves = getenv("KVGPU_JIT_KEEPWAVES") != nullptr;  // (A/B: split blocks first)
+    if (kp.waves > 6 && np.blocks.size() > 1 && !(keep_waves && np.blocks[big] > 1)) {
       // the blocks met the bound alone (jit_refine_blocks) and the kernel still does not: the
       // pressure crosses blocks, which splitting one block at a time fixes only slowly (C4:
       // 20+ recompiles); a kernel of multi-block form gives up a wave first (down to 6)
@@ -2745,6 +2840,7 @@ std::string cache_file(const JitImage& img, size_t i, uint64_t hcommon) {
 std::string jit_plan_key(const JitImage& img) {
   uint64_t h = common_hash(img);
   for (size_t i = 0; i < img.kernel_src.size(); i++) h = fnv1a64(img.kernel_src[i], fnv1a64(img.kernel_name[i], h));
+  if (getenv("KVGPU_JIT_KEEPWAVES")) h = fnv1a64("keepwaves", h);  // (the re-plan policy changes the plan)
   char key[40];
   snprintf(key, sizeof key, "%016llx", (unsigned long long)h);
   return key;
