@@ -52,6 +52,20 @@ __device__ __forceinline__ T kv_gld(const T* p, size_t i) {
 #endif
 }
 
+// A node through a global-address-space pointer (kv_gld for a struct: the copy goes through a
+// native vector, the fields the caller reads are the ones loaded). The path columns (DevBatch::
+// pcol) are read this way: through the generic pointer they compiled to flat loads (C2: 100 of
+// 305 loads), whose waits also drain the LDS / scalar counter.
+__device__ __forceinline__ Node kv_ldn(const Node* p, size_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef uint32_t u32x4_ __attribute__((ext_vector_type(4)));
+  const u32x4_ v = ((const __attribute__((address_space(1))) u32x4_*)p)[i];
+  return Node{v.x, v.y, v.z, v.w};
+#else
+  return p[i];
+#endif
+}
+
 // node index of this lane's cell in a row (wave-group layout, kv_layout.h)
 __device__ __forceinline__ uint32_t ni(uint32_t row) { return row * KV_LANES + (threadIdx.x & (KV_LANES - 1)); }
 
@@ -762,7 +776,7 @@ __device__ __forceinline__ void kv_final(const DevOut& O, uint32_t ri, uint32_t 
 // (C4's and C5's rules) takes the wave-level add of a single rule: 64 lanes adding to one LDS
 // word serialise.
 // V: the finalization variant of the generated kernels (kvjit.cpp, KVGPU_JIT_GFIN)
-template <int V = 0>
+template <int V = 0, bool TB = false>
 __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_t r, bool valid, uint32_t m, uint32_t st,
                                         uint32_t ekx, uint32_t i0, uint32_t i1, uint32_t i2, uint32_t i3,
                                         uint8_t* s_row0, uint32_t row0, const uint32_t* tab, uint32_t n, uint32_t ri0,
@@ -770,8 +784,8 @@ __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_
 #if defined(KV_JIT_PRELUDE) && !defined(KVEMU)
   if (n == 1u && !slot) {  // a one-member group ends like a single rule (one wave-level add)
     if (m & 1u) {
-      const uint32_t ri = __builtin_amdgcn_readfirstlane(tab ? tab[0] : ri0);
-      const uint32_t ek = ekx ? ekx + ((tab ? tab[1] : 0u) << 8) : 0u;
+      const uint32_t ri = __builtin_amdgcn_readfirstlane(TB ? tab[0] : ri0);
+      const uint32_t ek = ekx ? ekx + ((TB ? tab[1] : 0u) << 8) : 0u;
       const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
       kv_final(O, ri, n_res, r, valid, st, e, s_row0, row0);
     }
@@ -786,10 +800,10 @@ __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_
   for (uint32_t mm = m; mm; mm &= mm - 1u) {
     const uint32_t j = (uint32_t)__builtin_ctz(mm), row = row0 + j;
     if (rec) {
-      const uint32_t ri = tab ? tab[j] : ri0 + j * sri;
+      const uint32_t ri = TB ? tab[j] : ri0 + j * sri;
       uint32_t z = 0u, rr = r;
       asm volatile("" : "+v"(rr), "+v"(z));
-      const uint32_t ek = ekx ? ekx + ((tab ? tab[n + j] : j * spn) << 8) : 0u;
+      const uint32_t ek = ekx ? ekx + ((TB ? tab[n + j] : j * spn) << 8) : 0u;
       const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
       if (slot) {
         ((uint2*)(O.err8 + (size_t)ri * n_res))[rr] = err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, rr);
@@ -808,18 +822,18 @@ __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_
     if (act == 0ull) break;
     const uint32_t j = __builtin_amdgcn_readlane((uint32_t)__builtin_ctz(mm | 0x80000000u), (uint32_t)__builtin_ctzll(act));
     if ((mm >> j) & 1u) {
-      const uint32_t ri = __builtin_amdgcn_readfirstlane(tab ? tab[j] : ri0 + j * sri);
+      const uint32_t ri = __builtin_amdgcn_readfirstlane(TB ? tab[j] : ri0 + j * sri);
       if (slot) {
         const bool rec = valid && (O.full & 2) && !(O.full & 4) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP);
         if (rec) {
           uint32_t z = 0u, rr = r;
           asm volatile("" : "+v"(rr), "+v"(z));
-          const uint32_t ek = ekx ? ekx + ((tab ? tab[n + j] : j * spn) << 8) : 0u;
+          const uint32_t ek = ekx ? ekx + ((TB ? tab[n + j] : j * spn) << 8) : 0u;
           ((uint2*)(O.err8 + (size_t)ri * n_res))[rr] = err8_pack((ek & 15u) + z, (ek >> 4) & 15u, (ek >> 8) + z, ABSENT, i0, i1, i2, i3, rr);
         }
         s_row0[j * KV_RSTRIDE + threadIdx.x] = valid ? (uint8_t)st : (uint8_t)0xFFu;
       } else {
-        const uint32_t ek = ekx ? ekx + ((tab ? tab[n + j] : j * spn) << 8) : 0u;
+        const uint32_t ek = ekx ? ekx + ((TB ? tab[n + j] : j * spn) << 8) : 0u;
         const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
         kv_final(O, ri, n_res, r, valid, st, e, s_row0 + j * KV_RSTRIDE, row0 + j);
       }
@@ -848,11 +862,13 @@ __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_
   for (uint32_t j = 0; j < n; j++) {  // uniform over the members (scalar rule ids and rows)
     if (!((m >> j) & 1u)) continue;
     // (j is uniform, so is the member's rule id: named so, the compiler keeps it scalar)
-    const uint32_t ri = __builtin_amdgcn_readfirstlane(tab ? tab[j] : ri0 + j * sri);
+    uint32_t ri = __builtin_amdgcn_readfirstlane(TB ? tab[j] : ri0 + j * sri);
     if (rec) {
       uint32_t z = 0u, rr = r;
-      asm volatile("" : "+v"(rr), "+v"(z));
-      const uint32_t ek = ekx ? ekx + ((tab ? tab[n + j] : j * spn) << 8) : 0u;
+      // (ri named opaque here: the member's record row address is formed at its store, not
+      // hoisted to the kernel entry as one live scalar pair per member: C2 spilled 319 SGPRs)
+      asm volatile("" : "+v"(rr), "+v"(z), "+s"(ri));
+      const uint32_t ek = ekx ? ekx + ((TB ? tab[n + j] : j * spn) << 8) : 0u;
       const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
       if (slot)
         ((uint2*)(O.err8 + (size_t)ri * n_res))[rr] = err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, rr);
@@ -865,8 +881,8 @@ __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_
 #else
   for (uint32_t j = 0; j < n; j++) {
     if (!((m >> j) & 1u)) continue;
-    const uint32_t ri = __builtin_amdgcn_readfirstlane(tab ? tab[j] : ri0 + j * sri);
-    const uint32_t ek = ekx ? ekx + ((tab ? tab[n + j] : j * spn) << 8) : 0u;
+    const uint32_t ri = __builtin_amdgcn_readfirstlane(TB ? tab[j] : ri0 + j * sri);
+    const uint32_t ek = ekx ? ekx + ((TB ? tab[n + j] : j * spn) << 8) : 0u;
     const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
     kv_final(O, ri, n_res, r, valid, st, e, s_row0 + j * KV_RSTRIDE, row0 + j);
   }

@@ -954,7 +954,7 @@ struct Gen {
     if (j != kNoCol) {
       // the node from its path column (absent: the zero cell); the index only where the
       // lookup's presence (or a map's own index: wildcard keys) is asked for
-      c << "  const Node " << h.node << " = PC[" << T.cell0 << " + " << u32(j * KV_LANES) << "];\n"
+      c << "  const Node " << h.node << " = kv_ldn(PC, " << T.cell0 << " + " << u32(j * KV_LANES) << ");\n"
         << "  const uint32_t " << h.idx << " = " << h.node << ".kt == 0u ? ABSENT : node_type(" << h.node
         << ".kt) == NT_MAP ? " << h.node << ".c : 0u;\n";
       T.code.push_back(c.str());
@@ -1051,7 +1051,7 @@ struct Gen {
         if (g.uses_anchor) st = "((areg" + s + " & ~apres" + s + ") ? ST_ERROR : " + st + ")";
       }
       std::ostringstream r;
-      r << "kv_gfin<KVJ_GFIN>(O, n_res, r, valid, " << m << ", " << st << ", " << u32(kind | (pcn.flags << 4) | (pn << 8));
+      r << "kv_gfin<KVJ_GFIN, " << (g.gtab.empty() ? "false" : "true") << ">(O, n_res, r, valid, " << m << ", " << st << ", " << u32(kind | (pcn.flags << 4) | (pn << 8));
       for (uint32_t lv = 0; lv < 4; lv++) r << ", " << (lv <= g.max_level ? li(lv) : std::string("0u"));
       r << ", s_w + " << u32(KV_ROW0 + g.grow * KV_RSTRIDE) << ", " << u32(g.grow) << ", " << (g.gtab.empty() ? std::string("nullptr") : g.gtab) << ", "
         << u32(g.gn) << ", " << u32(g.gri[0]) << ", " << u32(g.gsri) << ", " << u32(g.gspn) << ", "
@@ -1933,7 +1933,7 @@ struct Gen {
              << "      const uint32_t el" << tag << " = ni(ff" << tag << " + fli" << tag << ");\n";
         if (fam != kNoCol)  // the element's column-0 cell: element row fe + i of its family
           body << "      const uint32_t ec" << tag << " = fe" << tag << " + fli" << tag << " * (KVC_J" << fam
-               << " * " << u32(KV_LANES) << ") + ln_;\n      const Node eln" << tag << " = PC[ec" << tag << "];\n";
+               << " * " << u32(KV_LANES) << ") + ln_;\n      const Node eln" << tag << " = kv_ldn(PC, ec" << tag << ");\n";
         else
           body << "      const Node eln" << tag << " = N[el" << tag << "];\n";
         body << T.flush() << bodies.str() << "    }\n";
@@ -2046,12 +2046,12 @@ struct Gen {
       << "  const bool valid = r < n_res;\n"
       << "  const Res* __restrict__ R = B.res + (valid ? r : 0u);\n"
       << "  uint32_t root = ABSENT, rkind = KEY_NONE, rflags = 0u, rtup = 0u;\n"
-      << "  if (valid) { root = ni(R->root); rkind = R->kind; rflags = R->flags; rtup = R->tup; }\n"
+      << "  if (valid) { root = ni(kv_gld(&R->root, 0)); rkind = kv_gld(&R->kind, 0); rflags = kv_gld(&R->flags, 0); rtup = kv_gld(&R->tup, 0); }\n"
       << "  Node rootn{0u, 0u, 0u, 0u};\n";
     if (cols_on)  // path columns (kvdevtypes.h): cell offset of this lane's family-0 columns; column 0 = the root
       o << "  const Node* __restrict__ PC = B.pcol;\n"
         << "  const uint32_t ln_ = threadIdx.x & " << u32(KV_LANES - 1) << ", gc_ = (r >> 6) * (KVC_J0 * " << u32(KV_LANES)
-        << ") + ln_;\n  if (valid) rootn = PC[gc_];\n";
+        << ") + ln_;\n  if (valid) rootn = kv_ldn(PC, gc_);\n";
     else
       o << "  if (valid) rootn = N[root];\n";
     o
@@ -2079,7 +2079,7 @@ struct Gen {
       for (uint32_t w = p0 / 32u; w * 32u < p1; w++) {
         const uint32_t lo = std::max(p0, w * 32u) - w * 32u, hi = std::min(p1, w * 32u + 32u) - w * 32u;
         const uint32_t m = hi - lo == 32u ? 0xFFFFFFFFu : ((1u << (hi - lo)) - 1u) << lo;
-        o << "  const uint32_t mw" << w << " = valid ? mtr_[(size_t)" << w << "u * ntup_] : 0u;\n";
+        o << "  const uint32_t mw" << w << " = valid ? kv_gld(mtr_, (size_t)" << w << "u * ntup_) : 0u;\n";
         any += " | (mw" + std::to_string(w) + " & " + u32(m) + ")";
       }
       // (the rows of a skipped block keep their NOMATCH prefill)
