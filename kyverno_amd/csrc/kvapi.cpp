@@ -132,7 +132,9 @@ struct DevBuf {
 
 struct DevPolicySet {
   DevBuf prog, preds, alts, conjs, atoms, rules, filters, kinds, strrefs, strpairs, sels, sellabels, selexprs, kgs,
-      gsegs, gwords, pstr, fword, fbit, flist, frule, rcompact;
+      gsegs, gwords, pstr, fword, fbit, flist, frule, rcompact, gsdesc, gsmem;
+  // site-record groups of the specialized kernels (kvdevtypes.h GSiteDesc)
+  uint32_t gs_groups = 0, gs_members = 0;
   DevPS view{};
   // specialized kernels (KV_COMPILE_SPECIALIZE): one module per kernel program, one
   // function per rule chunk
@@ -181,7 +183,9 @@ struct kv_batch {
   Batch b;
   const kv_policyset* owner = nullptr;
   std::mutex mu;
-  std::map<int, std::unique_ptr<DevBatchRes>> dev;
+  // device copies, shared with the sessions that use them (a session keeps its copy alive when
+  // the batch drops it: kv_batch_free, a parts session's detach)
+  std::map<int, std::shared_ptr<DevBatchRes>> dev;
   std::once_flag dyn_once;
   DynHost dyn;  // pattern-variable tables (build_dyn), on first use
   const DynHost& dyn_host(const PolicySet& ps) {
@@ -603,6 +607,12 @@ DevPolicySet& dev_ps(kv_policyset* s, int device) {
       }
     }
     d->rcompact.upload(J.rec_compact, device);  // record layout per rule (JitImage::rec_compact)
+    if (!J.gs_desc.empty()) {
+      d->gs_groups = (uint32_t)(J.gs_desc.size() / 4u);
+      d->gs_members = J.gs_members;
+      d->gsdesc.upload(J.gs_desc, device);
+      d->gsmem.upload(J.gs_mem, device);
+    }
     if (J.mtup_words) {  // factored-match descriptors of the kernels' match bits
       d->mtup_words = J.mtup_words;
       d->fac_slots = J.fac_slots;
@@ -680,11 +690,11 @@ void build_pcol(const JitImage& J, const Batch& b, DevBatchRes* d, int device) {
             cells * sizeof(Node) / 1e6, d->pcol_ms);
 }
 
-DevBatchRes& dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
+std::shared_ptr<DevBatchRes> dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
   std::lock_guard<std::mutex> g(bt->mu);
   auto it = bt->dev.find(device);
-  if (it != bt->dev.end()) return *it->second;
-  auto d = std::make_unique<DevBatchRes>();
+  if (it != bt->dev.end()) return it->second;
+  auto d = std::make_shared<DevBatchRes>();
   const Batch& b = bt->b;
   if (b.rmask.size() != b.n_rows || b.roff.size() != b.n_rows)
     throw std::runtime_error("batch: packed row arrays do not match the row count");
@@ -771,9 +781,8 @@ DevBatchRes& dev_batch(kv_batch* bt, const PolicySet& ps, int device) {
     build_pcol(*bt->owner->jit, b, d.get(), device);
     d->view_dev.upload_raw(&d->view, sizeof(DevBatch), device);
   }
-  auto& ref = *d;
-  bt->dev[device] = std::move(d);
-  return ref;
+  bt->dev[device] = d;
+  return d;
 }
 
 // Path segments from the pattern root to pnode p: keys (resolved wildcard keys
@@ -967,13 +976,16 @@ struct DevSession {
   DevBuf fflags, pview, st, er8, er, cn, scope, scn, ptab, mtab, mtbf, mtup, ftab;
   uint32_t fac_entities = 0, ntup = 0;
   bool rec_compact = false;  // the last pass wrote records per wave segment (specialized kernels)
-  // a part of a parts session owns its batch's device copy (detach_batch): the caller's
-  // host batch may be freed once the part is attached
-  std::unique_ptr<DevBatchRes> own_batch;
+  // the batch's device copy, shared with the batch's cache and other sessions on it; a part of a
+  // parts session keeps it after dropping the batch (detach_batch): the caller's host batch may
+  // be freed once the part is attached
+  std::shared_ptr<DevBatchRes> batch_ref;
   DevBuf r_offs, r_tot, r_base, r_out8, r_outw, r_wide;  // record compaction (fetch)
   DevBuf inv_d, stc;                                     // caller-order statuses (fetch)
   DevBuf ord_d, r_mask;                                  // caller-order records: batch order, record lanes
   DevBuf stamps;                                         // KVGPU_STAMPS diagnostics
+  DevBuf gsite, gcnt;                                    // site records of rule groups (pass)
+  DevBuf sflag;                                          // written status segments (specialized)
   uint32_t mt_words = 0, mt_entities = 0;
   uint32_t *mt_ns = nullptr, *mt_ann = nullptr, *mt_sel = nullptr;
   uint32_t nscopes = 0, nvals = 0;
@@ -994,7 +1006,8 @@ struct DevSession {
     HIPCHK(hipSetDevice(device));
     const auto tc0 = std::chrono::steady_clock::now();
     DevPolicySet& dp = dev_ps(ps, device);
-    DevBatchRes& db = dev_batch(bt, ps->ps, device);
+    batch_ref = dev_batch(bt, ps->ps, device);
+    DevBatchRes& db = *batch_ref;
     upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc0).count();
     if (getenv("KVGPU_VERBOSE")) fprintf(stderr, "[kvgpu] session: policy set + batch upload %.1f ms\n", upload_ms);
     bview = (const DevBatch*)db.view_dev.p;
@@ -1056,12 +1069,24 @@ struct DevSession {
       st.alloc(nrules * nres, device);
       O.status = (uint8_t*)st.p;
       O.full |= 1;
+      if (dp.specialized() && !getenv("KVGPU_NO_SFLAG")) {  // (flags of every segment, set by each pass)
+        sflag.alloc(std::max<uint64_t>(nrules * ((nres + KV_WG - 1) / KV_WG), 1), device);
+        HIPCHK(hipMemset(sflag.p, 1, sflag.n));
+        O.sflag = (uint8_t*)sflag.p;
+      }
     }
     if (mode & KV_MODE_ERRORS) {
       er8.alloc(nrules * nres * sizeof(ErrRec8), device);
       O.err8 = (ErrRec8*)er8.p;
       O.err = nullptr;  // full records: allocated by fetch() for the re-run pass, if some record is wide
       O.full |= 2;
+      if (dp.gs_groups) {  // 64 x members 16 B slots per wave and group, a count per (group, wave)
+        const uint64_t nw = (nres + 63) / 64;
+        gsite.alloc(std::max<uint64_t>((uint64_t)dp.gs_members * nw * 64u * 16u, 16), device);
+        gcnt.alloc(std::max<uint64_t>((uint64_t)dp.gs_groups * nw * sizeof(uint32_t), 4), device);
+        O.gsite = (uint32_t*)gsite.p;
+        O.gcnt = (uint32_t*)gcnt.p;
+      }
     }
     cn.alloc(std::max<uint64_t>(nrules, 1) * KV_HIST * sizeof(unsigned long long), device);
     O.counts = (unsigned long long*)cn.p;
@@ -1096,17 +1121,10 @@ struct DevSession {
     HIPCHK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
   }
-  // take the batch's device copy out of the kv_batch (parts sessions: the host batch is the
-  // caller's, and may be freed after kv_session_attach_part)
-  void detach_batch() {
-    std::lock_guard<std::mutex> g(bt->mu);
-    auto it = bt->dev.find(device);
-    if (it != bt->dev.end()) {
-      own_batch = std::move(it->second);
-      bt->dev.erase(it);
-    }
-    bt = nullptr;
-  }
+  // drop the kv_batch (parts sessions: the host batch is the caller's, and may be freed after
+  // kv_session_attach_part); the session keeps the device copy through batch_ref, and so does
+  // every other session using it (the batch's cache keeps its entry for later sessions)
+  void detach_batch() { bt = nullptr; }
   // renumber the scope of every resource through map (batch namespace -> session scope) and
   // size the per-scope counts for n_total scopes
   void remap_scopes(const std::vector<uint32_t>& map, uint32_t n_total) {
@@ -1251,11 +1269,19 @@ struct DevSession {
       if (verbose) fprintf(stderr, "[kvgpu] fetch: %s %.1f ms\n", what, ms);
     };
     const bool want_st = O.status && (mode & (KV_MODE_STATUS | KV_MODE_ERRORS)) && nres && nrules;
+    if (O.status && O.sflag && rec_compact && nres && nrules) {  // the segments the pass left NOMATCH
+      HIPCHK(launch_status_fill(O.status, O.sflag, (uint32_t)nres, (uint32_t)nrules, stream));
+      lap("status_fill");
+    }
     // A permuted batch fetched whole comes back in the caller's order: the statuses are gathered on
     // the device (stc[rule][j] = st[rule][store index of j]) and the records scattered to the
     // caller's (rule, resource) order, so one status matrix crosses PCIe and the host permutes
     // nothing. Its copy runs on the side stream, beside the record kernels.
-    const bool caller = want_st && bt && lo == 0 && nres == n_total && !bt->b.order.empty();
+    bool caller = want_st && bt && lo == 0 && nres == n_total && !bt->b.order.empty();
+    if (caller && !stc.p) {  // the gathered copy is a second status matrix: only with room to spare
+      size_t fr = 0, tot = 0;
+      if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < nrules * nres + nres * 8u + (512ull << 20)) caller = false;
+    }
     bool side_copy = false;
     if (caller) {
       if (!inv_d.p) inv_d.upload_raw(bt->inverse(), nres * sizeof(uint32_t), device);
@@ -1303,6 +1329,9 @@ struct DevSession {
       const uint64_t total = part->base[nrules];
       if (r_out8.n < total * sizeof(ErrRec8)) r_out8.alloc(std::max<uint64_t>(total, 1) * sizeof(ErrRec8), device);
       HIPCHK(hipMemsetAsync(r_wide.p, 0, sizeof(uint32_t), stream));
+      if (rec_compact && O.gsite)  // the groups' site records to their members' slots
+        HIPCHK(launch_gsite_expand(O.gsite, O.gcnt, (const GSiteDesc*)dps->gsdesc.p, (const uint32_t*)dps->gsmem.p,
+                                   dps->gs_groups, (uint32_t)nres, O.err8, stream));
       HIPCHK(launch_rec_compact(O.status, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                 nullptr, (unsigned long long*)r_base.p, (ErrRec8*)r_out8.p, nullptr,
                                 (uint32_t*)r_wide.p, 1, rec_compact ? (const uint8_t*)dps->rcompact.p : nullptr, ord,
@@ -2028,8 +2057,9 @@ int kv_result_failures(const kv_result* cr, uint64_t* n, const uint32_t** rule, 
       }
       if (!r->b->b.order.empty() && !r->caller_order) {
         // caller order: by rule, then caller resource index. Each rule's pairs are a subset of
-        // [0, n_res) with distinct caller indices: scattered into a per-thread slot array and
-        // swept in order (rules split over host threads; no comparison sort)
+        // [0, n_res) with distinct caller indices: a rule with pairs on 1/16 of the resources or more
+        // is scattered into a per-thread slot array and swept in order, a sparser one sorted
+        // (rules split over host threads)
         std::vector<size_t> rb(r->n_rules + 1, 0);
         for (size_t i = 0; i < r->f_rule.size(); i++) rb[r->f_rule[i] + 1]++;
         for (uint32_t rl = 0; rl < r->n_rules; rl++) rb[rl + 1] += rb[rl];
@@ -2042,6 +2072,17 @@ int kv_result_failures(const kv_result* cr, uint64_t* n, const uint32_t** rule, 
             std::vector<uint32_t> slot;  // caller index -> path id + 1 (0: no pair)
             for (uint32_t rl = t; rl < r->n_rules; rl += T) {
               if (rb[rl] == rb[rl + 1]) continue;
+              if ((rb[rl + 1] - rb[rl]) * 16u < r->n_res) {
+                std::vector<std::pair<uint64_t, uint32_t>> v;
+                v.reserve(rb[rl + 1] - rb[rl]);
+                for (size_t i = rb[rl]; i < rb[rl + 1]; i++) v.push_back({r->f_res[i], r->f_path[i]});
+                std::sort(v.begin(), v.end());
+                for (size_t i = 0; i < v.size(); i++) {
+                  fs[rb[rl] + i] = v[i].first;
+                  fp[rb[rl] + i] = v[i].second;
+                }
+                continue;
+              }
               if (slot.empty()) slot.assign(r->n_res, 0u);
               for (size_t i = rb[rl]; i < rb[rl + 1]; i++) slot[r->f_res[i]] = r->f_path[i] + 1u;
               size_t o = rb[rl];

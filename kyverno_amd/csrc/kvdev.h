@@ -40,6 +40,13 @@ hipError_t launch_remap_u32(uint32_t* a, uint64_t n, const uint32_t* map, hipStr
 // store-order `status` to out8[base[rule] + offs[rule][tile] + rank]; *wide |= 1 if a compact
 // record is flagged ERR8_WIDE. With `order` (store index -> caller index) phase 0 ran over the
 // caller-order statuses and phase 1 puts each record at its caller index's place.
+// NOMATCH into the status segments the specialized kernels did not write (DevOut::sflag)
+hipError_t launch_status_fill(uint8_t* status, const uint8_t* sflag, uint32_t n_res, uint32_t n_rules,
+                              hipStream_t stream);
+// site records of the specialized rule groups -> the members' records at their slots (kvdevtypes.h
+// GSiteDesc; fetch time, before launch_rec_compact's scatter)
+hipError_t launch_gsite_expand(const uint32_t* gsite, const uint32_t* gcnt, const GSiteDesc* desc, const uint32_t* mem,
+                               uint32_t n_groups, uint32_t n_res, ErrRec8* err8, hipStream_t stream);
 hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const ErrRec* errw, uint32_t n_res,
                               uint32_t n_rules, uint32_t* offs, unsigned long long* totals, unsigned long long* base,
                               ErrRec8* out8, ErrRec* outw, uint32_t* wide, int phase, const uint8_t* compact,

@@ -775,12 +775,18 @@ __device__ __forceinline__ void kv_final(const DevOut& O, uint32_t ri, uint32_t 
 // instead (no counter; partial lines: C3 writes 7.55 -> 9.74 GB) 8.22 ms. A one-member group
 // (C4's and C5's rules) takes the wave-level add of a single rule: 64 lanes adding to one LDS
 // word serialise.
-// V: the finalization variant of the generated kernels (kvjit.cpp, KVGPU_JIT_GFIN)
-template <int V = 0, bool TB = false>
+// V: the finalization variant of the generated kernels (kvjit.cpp, KVGPU_JIT_GFIN).
+// SITE (groups of 2+ members, kvjit.cpp KVGPU_JIT_GSITE): one site record per lane for all the
+// members `m` it ends here (kvdevtypes.h GSiteDesc), appended through the wave's counter s_gc[wave]
+// to the wave's segment of the group's area (gpre: the group's first record / (64 x waves)); the
+// members' records are expanded at fetch (kv_gsite_expand_kernel). C2's image-glob groups end 20
+// of their 21 members at one leaf site on most lanes: one store there instead of 20.
+template <int V = 0, bool TB = false, bool SITE = false>
 __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_t r, bool valid, uint32_t m, uint32_t st,
                                         uint32_t ekx, uint32_t i0, uint32_t i1, uint32_t i2, uint32_t i3,
                                         uint8_t* s_row0, uint32_t row0, const uint32_t* tab, uint32_t n, uint32_t ri0,
-                                        uint32_t sri, uint32_t spn, bool slot) {
+                                        uint32_t sri, uint32_t spn, bool slot, uint32_t* s_gc = nullptr,
+                                        uint32_t gpre = 0u) {
 #if defined(KV_JIT_PRELUDE) && !defined(KVEMU)
   if (n == 1u && !slot) {  // a one-member group ends like a single rule (one wave-level add)
     if (m & 1u) {
@@ -789,6 +795,24 @@ __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_
       const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
       kv_final(O, ri, n_res, r, valid, st, e, s_row0, row0);
     }
+    return;
+  }
+  if constexpr (SITE) {
+    const uint8_t st8 = valid ? (uint8_t)st : (uint8_t)0xFFu;
+    if (m != 0u && valid && (O.full & 2) && !(O.full & 4) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP)) {
+      uint32_t z = 0u, rr = r;
+      asm volatile("" : "+v"(rr), "+v"(z));
+      const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+      const uint32_t fits = (i0 < 1024u) & (i1 < 256u) & (i2 < 256u) & (i3 == 0u);
+      const uint32_t y = (i0 & 1023u) | ((i1 & 255u) << 10) | ((i2 & 255u) << 18) | ((rr & 63u) << 26);
+      // (a wave-uniform LDS address: the atomic optimizer issues one add of the wave's lanes)
+      const uint32_t k = atomicAdd(s_gc + w, 1u);
+      const uint32_t nw = (n_res + 63u) >> 6;
+      uint4* seg = (uint4*)O.gsite + ((size_t)gpre * nw + (size_t)(rr >> 6) * n) * 64u;
+      seg[k] = make_uint4(ekx + z, y, m, fits ^ 1u);
+    }
+    for (uint32_t j = 0; j < n; j++)
+      if ((m >> j) & 1u) s_row0[j * KV_RSTRIDE + threadIdx.x] = st8;
     return;
   }
   if constexpr (V == 1) {
@@ -870,7 +894,11 @@ __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_
       asm volatile("" : "+v"(rr), "+v"(z), "+s"(ri));
       const uint32_t ek = ekx ? ekx + ((TB ? tab[n + j] : j * spn) << 8) : 0u;
       const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
-      if (slot)
+      if constexpr (V == 3) {  // (diagnostic: records built, not stored)
+        const uint2 w = err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, rr);
+        const uint32_t sl = (uint32_t)(old[((row0 + j) >> 3) - w0] >> (8u * ((row0 + j) & 7u))) & 0xFFu;
+        asm volatile("" ::"v"(w.x), "v"(w.y), "v"(sl), "s"(ri));
+      } else if (slot)
         ((uint2*)(O.err8 + (size_t)ri * n_res))[rr] = err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, rr);
       else
         kv_rec_put(O, ri, n_res, rr, (uint32_t)(old[((row0 + j) >> 3) - w0] >> (8u * ((row0 + j) & 7u))) & 0xFFu, e, z);
@@ -978,9 +1006,20 @@ __device__ __forceinline__ void kv_end_flush(const DevOut& O, uint32_t* s_stw, u
     // 16 B per lane, 16 lanes per row: each wave store writes 4 rows of the workgroup (C3 9.10
     // -> 8.96 ms per pass against a byte per lane and row); a partial workgroup, or rows not
     // 16 B aligned: a byte per lane
+    // A row segment of the workgroup that is NOMATCH throughout (72 % of C3's statuses) is not
+    // written: its flag says so (O.sflag) and the fetch fills it
     const uint32_t l = threadIdx.x & 63u, c16 = (l & 15u) * 16u;
+    const size_t nwg = (n_res + (uint32_t)KV_WG - 1u) / (uint32_t)KV_WG;
     for (uint32_t q = (threadIdx.x >> 4); q < nr; q += (uint32_t)KV_WG / 16u) {
-      *(uint4*)(O.status + (size_t)rules[q] * n_res + wg0 + c16) = *(const uint4*)(s_b + q * KV_RSTRIDE + c16);
+      const uint4 v = *(const uint4*)(s_b + q * KV_RSTRIDE + c16);
+      if (O.sflag) {
+        constexpr uint32_t NM4 = 0x01010101u * (uint32_t)ST_NOMATCH;
+        const bool nm = v.x == NM4 && v.y == NM4 && v.z == NM4 && v.w == NM4;
+        const bool any = ((__ballot(!nm) >> (l & 48u)) & 0xFFFFull) != 0ull;  // the row's 16 lanes
+        if ((l & 15u) == 0u) O.sflag[(size_t)rules[q] * nwg + wg0 / (uint32_t)KV_WG] = any ? 1u : 0u;
+        if (!any) continue;
+      }
+      *(uint4*)(O.status + (size_t)rules[q] * n_res + wg0 + c16) = v;
     }
     // (a wave copies the other waves' segments, which they overwrite with counts below; the
     // condition is uniform over the workgroup)
@@ -990,6 +1029,8 @@ __device__ __forceinline__ void kv_end_flush(const DevOut& O, uint32_t* s_stw, u
   if ((O.full & 1u) && valid) {
 #pragma unroll 4
     for (uint32_t q = 0; q < nr; q++) O.status[(size_t)rules[q] * n_res + r] = s_b[q * KV_RSTRIDE + threadIdx.x];
+    if (O.sflag && (r & ((uint32_t)KV_WG - 1u)) == 0u)  // (the workgroup's first lane: rows written)
+      for (uint32_t q = 0; q < nr; q++) O.sflag[(size_t)rules[q] * ((n_res + (uint32_t)KV_WG - 1u) / (uint32_t)KV_WG) + r / (uint32_t)KV_WG] = 1u;
   }
 #ifndef KVEMU
   const uint32_t l = threadIdx.x & 63u, w = threadIdx.x >> 6;

@@ -175,6 +175,25 @@ struct DevOut {
                                // bit3 per-scope counts (specialized kernels: counted in the pass)
   unsigned long long* scounts; // [scope][rule][8] (bit3)
   const uint32_t* scope;       // scope of every resource (bit3)
+  // site records of the specialized rule groups (bit1, below; null without such groups)
+  uint32_t* gsite;             // 16 B records, [group area][wave][64 x members]
+  uint32_t* gcnt;              // [group][wave] records written
+  // specialized kernels (bit0): 1 = the workgroup's 256 statuses of the rule were written, 0 = all
+  // NOMATCH and not written (kv_end_flush; the fetch fills them, kv_status_fill_kernel)
+  uint8_t* sflag;              // [rule][workgroup]
+};
+
+// Site records (specialized kernels, rule groups of 2+ members; kvdevfn.h kv_gfin): the members a
+// lane ends at one error site share the site's record but for their pattern nodes (the group's
+// representative's node + the member's shift), so the kernel writes one 16 B record per (lane,
+// site) - {kind | flags << 4 | pn << 8 of the representative (0: none), ErrRec8::w1, member mask,
+// indices do not fit} - appended to the wave's segment of the group's area (64 x members slots per
+// wave: a member ends once per lane), and the count per (group, wave) when the wave ends. At fetch
+// kv_gsite_expand_kernel writes each member's ErrRec8 to its [rule][res] slot. Group g's area
+// starts at record gpre * 64 * waves (gpre = members of the groups before it); its members are
+// gs_mem[2 * (moff + j)] (rule) and [2 * (moff + j) + 1] (pattern-node shift).
+struct GSiteDesc {
+  uint32_t n, gpre, moff, pad;
 };
 
 constexpr int KV_WG = 256;

@@ -93,6 +93,8 @@ struct Gen {
     cols_on = !(c && !strcmp(c, "0"));
     const char* gd = getenv("KVGPU_JIT_GUARDS");
     guards_on = gd && !strcmp(gd, "1");
+    const char* gsv = getenv("KVGPU_JIT_GSITE");
+    gsite_on = !(gsv && !strcmp(gsv, "0"));
     fams.emplace_back();
     col_of(0, "R");  // column 0 of family 0: the root
   }
@@ -106,6 +108,13 @@ struct Gen {
   // column count of each family is a macro (KVC_J<f>) defined at the head of every kernel
   // program once the whole image is generated.
   bool cols_on = true;
+  // Site records of rule groups (kvdevtypes.h GSiteDesc; KVGPU_JIT_GSITE=0: the members' own
+  // records, A/B): per group of 2+ members its descriptor (n, gpre, moff, 0) in gs_desc and its
+  // members' (rule, pattern-node shift) in gs_mem, numbered in generation order over the image;
+  // k_gs0 / k_gsn: the first group and the groups of the kernel being generated
+  bool gsite_on = true;
+  std::vector<uint32_t> gs_desc, gs_mem;
+  uint32_t gs_members = 0, k_gs0 = 0, k_gsn = 0;
   struct Fam {
     std::string arr;                          // family array expr (family 0: "")
     std::map<std::string, uint32_t> idx;      // relative expr -> column
@@ -938,6 +947,8 @@ struct Gen {
     std::vector<uint32_t> gri, gdpn;                    // member rule ids, pattern-node shifts
     std::map<uint32_t, uint32_t> gslot;                 // representative LEAF pc -> slot of member 0
     std::string gtab;                                   // member table (empty: arithmetic)
+    bool gsite = false;                                 // site records (gl: its counter in the kernel)
+    uint32_t gl = 0, gpre = 0;
     uint32_t max_level = 0;
     std::string s;                                      // "_<ri>"
   };
@@ -1051,11 +1062,14 @@ struct Gen {
         if (g.uses_anchor) st = "((areg" + s + " & ~apres" + s + ") ? ST_ERROR : " + st + ")";
       }
       std::ostringstream r;
-      r << "kv_gfin<KVJ_GFIN, " << (g.gtab.empty() ? "false" : "true") << ">(O, n_res, r, valid, " << m << ", " << st << ", " << u32(kind | (pcn.flags << 4) | (pn << 8));
+      r << "kv_gfin<KVJ_GFIN, " << (g.gtab.empty() ? "false" : "true") << ", " << (g.gsite ? "true" : "false")
+        << ">(O, n_res, r, valid, " << m << ", " << st << ", " << u32(kind | (pcn.flags << 4) | (pn << 8));
       for (uint32_t lv = 0; lv < 4; lv++) r << ", " << (lv <= g.max_level ? li(lv) : std::string("0u"));
       r << ", s_w + " << u32(KV_ROW0 + g.grow * KV_RSTRIDE) << ", " << u32(g.grow) << ", " << (g.gtab.empty() ? std::string("nullptr") : g.gtab) << ", "
         << u32(g.gn) << ", " << u32(g.gri[0]) << ", " << u32(g.gsri) << ", " << u32(g.gspn) << ", "
-        << (g.gn >= gslot_members() ? "true" : "false") << ");";
+        << (!g.gsite && g.gn >= gslot_members() ? "true" : "false");
+      if (g.gsite) r << ", s_gc_ + " << u32(4u * g.gl) << ", " << u32(g.gpre);
+      r << ");";
       return r.str();
     };
     auto raise = [&](uint32_t kind, uint32_t pn, uint32_t catch_pc) {
@@ -1603,7 +1617,16 @@ struct Gen {
         g.gn = (uint32_t)G.members.size();
         g.gri = G.members;
         g.gdpn = G.dpn;
-        if (g.gn >= gslot_members())
+        if (gsite_on && g.gn >= 2u) {
+          g.gsite = true;
+          g.gl = k_gsn++;
+          g.gpre = gs_members;
+          gs_desc.insert(gs_desc.end(), {g.gn, gs_members, (uint32_t)(gs_mem.size() / 2u), 0u});
+          for (uint32_t j = 0; j < g.gn; j++) gs_mem.insert(gs_mem.end(), {G.members[j], G.dpn[j]});
+          gs_members += g.gn;
+        }
+        // (site-record members get their records expanded to their resource slots at fetch)
+        if (g.gsite || g.gn >= gslot_members())
           for (uint32_t m : G.members) rec_slot.at(m) = 1;
         g.grow = hbase + q;
         for (const auto& m : G.preds)
@@ -2010,6 +2033,8 @@ struct Gen {
     if (nr_all > KV_KROWS) throw std::runtime_error("kvjit: at most KV_KROWS rules per kernel (KVGPU_JIT_CHUNK)");
     block_decls.clear();
     mt_kbase = (uint32_t)(mt_bits.size() / 32u);
+    k_gs0 = (uint32_t)(gs_desc.size() / 4u);
+    k_gsn = 0;
     for (const JitChunk* c : chs) {
       std::vector<uint32_t> ord;
       rows.push_back({(uint32_t)rules.size(), (uint32_t)c->rules.size()});
@@ -2033,7 +2058,7 @@ struct Gen {
       << "(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp, const Node* __restrict__ N, "
          "const Val* __restrict__ V, const uint8_t* __restrict__ S, DevOut O, uint32_t r0) {\n"
       << "  constexpr uint32_t FIN_ = " << u32(FIN) << ", ACT_ = " << u32(ACT) << ", ST_STORED_ = 0x7Eu;\n"
-      << "  __shared__ unsigned long long s_stq[" << kernel_lds(nr) / 8 << "];\n  uint32_t* s_stw = (uint32_t*)s_stq;\n"
+      << "  __shared__ unsigned long long s_stq[" << kernel_lds(nr) / 8 + 2u * k_gsn << "];\n  uint32_t* s_stw = (uint32_t*)s_stq;\n"
       << "  const DevPS& P = *Pp;\n  const DevBatch& B = *Bp;\n  const uint8_t* __restrict__ pstr = P.pstr;\n";
     // Workgroup b runs tile (b % 8) * n/8 + b / 8, so each XCD (blocks b, b+8, ... share one)
     // walks a contiguous resource range and its L2 sees the values those resources share
@@ -2058,6 +2083,10 @@ struct Gen {
       << "  const uint32_t* __restrict__ mtr_ = P.mtup + rtup;\n  const uint32_t ntup_ = B.n_tup;\n"
       << "  uint8_t* s_w = (uint8_t*)s_stw;\n"
       // every status row starts as NOMATCH (0xFF past the batch): only matched lanes store
+      // site-record counters of the kernel's groups, [group][wave] after the rows (zeroed before
+      // the prefill's barrier)
+      << "  uint32_t* const s_gc_ = s_stw + " << u32(kernel_lds(nr) / 4u) << ";\n"
+      << (k_gsn ? "  if (threadIdx.x < " + u32(4u * k_gsn) + ") s_gc_[threadIdx.x] = 0u;\n" : std::string())
       << "  kv_prefill_rows(s_stw, " << nr << "u, r - threadIdx.x, n_res);\n";
     // diagnostics (KVGPU_JIT_STAMPS): a wave's shader clock at the start, after each block and
     // after the flush, into the program's global kvj_stamps ([workgroup][wave][kJitStamps], set by
@@ -2088,8 +2117,13 @@ struct Gen {
       stamp(bi + 1);
     }
     // statuses to the status matrix, per-rule (and per-scope) histograms
-    o << "  const uint32_t wg0_ = r - threadIdx.x;\n"
-      << "  kv_end_flush(O, s_stw, " << nr << "u, " << name << "_rules, n_res, r, valid, "
+    o << "  const uint32_t wg0_ = r - threadIdx.x;\n";
+    // each wave's site-record counts (lane l: the kernel's group l)
+    if (k_gsn)
+      o << "#ifndef KVEMU\n  if ((O.full & 2u) && !(O.full & 4u) && (threadIdx.x & 63u) < " << u32(k_gsn)
+        << " && r - (threadIdx.x & 63u) < n_res)\n    O.gcnt[(size_t)(" << u32(k_gs0)
+        << " + (threadIdx.x & 63u)) * ((n_res + 63u) >> 6) + (r >> 6)] = s_gc_[(threadIdx.x & 63u) * 4u + (threadIdx.x >> 6)];\n#endif\n";
+    o << "  kv_end_flush(O, s_stw, " << nr << "u, " << name << "_rules, n_res, r, valid, "
          "(O.full & 8u) && valid ? O.scope[r] : 0xFFFFFFFFu, (O.full & 8u) && wg0_ < n_res ? O.scope[wg0_] : 0xFFFFFFFFu, "
          "P.n_rules);\n";
     stamp(std::min<size_t>(blocks.size() + 1, kJitStamps - 1));
@@ -2371,6 +2405,9 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   if (out->mtup_words && !out->probe) g.build_fac(out);
   out->rec_compact.assign(n, 1);
   for (uint32_t ri = 0; ri < n; ri++) out->rec_compact[ri] = g.rec_slot[ri] ? 0 : 1;
+  out->gs_desc = g.gs_desc;
+  out->gs_mem = g.gs_mem;
+  out->gs_members = g.gs_members;
   std::string cdefs;  // the column count of every path-column family (KVC_J<f>)
   g.col_plan(out, &cdefs);
   // group finalization (kvdevfn.h kv_gfin): 0 members unrolled, 1 per-lane member loop, 2 uniform

@@ -49,8 +49,13 @@ struct JitImage {
   std::vector<uint32_t> fac_word, fac_bit, fac_flist, fac_rule;
   uint32_t fac_slots = 0;
   // per rule: 1 = its records are appended to its wave's 64-slot segment (lane in the record),
-  // 0 = at the resource's slot (members of large rule groups; kvjit.cpp gslot_members)
+  // 0 = at the resource's slot (members of large rule groups, kvjit.cpp gslot_members; members of
+  // groups with site records, expanded there at fetch)
   std::vector<uint8_t> rec_compact;
+  // site-record groups (kvdevtypes.h GSiteDesc): 4 words per group, (rule, node shift) per member,
+  // members in all
+  std::vector<uint32_t> gs_desc, gs_mem;
+  uint32_t gs_members = 0;
   // path columns the kernels read (kvdevtypes.h ColDesc, built per batch by kvcol.h): every
   // column; per family its array's column in family 0 and its column count
   std::vector<kv::ColDesc> cols;

@@ -585,6 +585,66 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_scatter_kernel(const uint8_t* __
   if (e.w0 & ERR8_WIDE) atomicOr(wide, 1u);
 }
 
+// Site records -> the members' ErrRec8 at their [rule][res] slots (kvdevtypes.h GSiteDesc): one
+// wave per (group, wave of resources), lane k handles records k, k + 64, ... of the segment.
+__global__ __launch_bounds__(KV_WG) void kv_gsite_expand_kernel(const uint4* __restrict__ gsite,
+                                                                 const uint32_t* __restrict__ gcnt,
+                                                                 const GSiteDesc* __restrict__ desc,
+                                                                 const uint32_t* __restrict__ mem, uint32_t n_res,
+                                                                 ErrRec8* __restrict__ err8) {
+  const uint32_t nw = (n_res + 63u) >> 6, w = blockIdx.x * (KV_WG / 64) + (threadIdx.x >> 6), g = blockIdx.y;
+  if (w >= nw) return;
+  const GSiteDesc d = desc[g];
+  const uint32_t cnt = gcnt[(size_t)g * nw + w];
+  const uint4* seg = gsite + ((size_t)d.gpre * nw + (size_t)w * d.n) * 64u;
+  for (uint32_t k = threadIdx.x & 63u; k < cnt; k += 64u) {
+    const uint4 x = seg[k];  // {ekx, w1, member mask, indices do not fit}
+    const uint32_t r = w * 64u + (x.y >> 26);
+    for (uint32_t m = x.z; m; m &= m - 1u) {
+      const uint32_t j = (uint32_t)__builtin_ctz(m);
+      const uint32_t ri = mem[2u * (d.moff + j)];
+      // the member's error: the representative's node shifted (ekx 0: no error node)
+      const uint32_t pn = x.x ? (x.x >> 8) + mem[2u * (d.moff + j) + 1u] : 0u;
+      const uint32_t wide = x.w | (pn >= (1u << 25) ? 1u : 0u);
+      ErrRec8 e;
+      e.w0 = (x.x & 15u) | (((x.x >> 4) & 15u) << 4) | (wide << 6) | (pn << 7);
+      e.w1 = x.y;
+      err8[(size_t)ri * n_res + r] = e;
+    }
+  }
+}
+
+hipError_t launch_gsite_expand(const uint32_t* gsite, const uint32_t* gcnt, const GSiteDesc* desc, const uint32_t* mem,
+                               uint32_t n_groups, uint32_t n_res, ErrRec8* err8, hipStream_t stream) {
+  if (n_res == 0 || n_groups == 0) return hipSuccess;
+  const uint32_t nw = (n_res + 63u) >> 6;
+  hipLaunchKernelGGL(kv_gsite_expand_kernel, dim3((nw + KV_WG / 64 - 1) / (KV_WG / 64), n_groups), dim3(KV_WG), 0, stream,
+                     (const uint4*)gsite, gcnt, desc, mem, n_res, err8);
+  return hipGetLastError();
+}
+
+// NOMATCH into the status segments the specialized kernels left unwritten (DevOut::sflag): one
+// wave per (workgroup segment, rule), 16 B per lane of the first 16 lanes
+__global__ __launch_bounds__(KV_WG) void kv_status_fill_kernel(uint8_t* __restrict__ status,
+                                                                const uint8_t* __restrict__ sflag, uint32_t n_res,
+                                                                uint32_t n_rules) {
+  const uint32_t nwg = (n_res + KV_WG - 1) / KV_WG, g = blockIdx.x * (KV_WG / 64) + (threadIdx.x >> 6);
+  const uint32_t rule = blockIdx.y, l = threadIdx.x & 63u;
+  if (g >= nwg || l >= 16u || sflag[(size_t)rule * nwg + g]) return;
+  const uint32_t nm = 0x01010101u * (uint32_t)ST_NOMATCH;
+  // (an unwritten segment is a whole workgroup: n_res % 16 == 0 and the segment inside the batch)
+  *(uint4*)(status + (size_t)rule * n_res + (size_t)g * KV_WG + l * 16u) = make_uint4(nm, nm, nm, nm);
+}
+
+hipError_t launch_status_fill(uint8_t* status, const uint8_t* sflag, uint32_t n_res, uint32_t n_rules,
+                              hipStream_t stream) {
+  if (n_res == 0 || n_rules == 0) return hipSuccess;
+  const uint32_t nwg = (n_res + KV_WG - 1) / KV_WG;
+  hipLaunchKernelGGL(kv_status_fill_kernel, dim3((nwg + KV_WG / 64 - 1) / (KV_WG / 64), n_rules), dim3(KV_WG), 0, stream,
+                     status, sflag, n_res, n_rules);
+  return hipGetLastError();
+}
+
 hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const ErrRec* errw, uint32_t n_res,
                               uint32_t n_rules, uint32_t* offs, unsigned long long* totals, unsigned long long* base,
                               ErrRec8* out8, ErrRec* outw, uint32_t* wide, int phase, const uint8_t* compact,
