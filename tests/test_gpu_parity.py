@@ -287,3 +287,40 @@ def test_glob_stress_long_values(orc, spec):
     mism, r, ost = compare(orc, pols, ress, specialize=spec)
     assert not mism, "\n".join(mism)
     assert (r.status == 0).sum() > 1000 and (r.status == 1).sum() > 1000
+
+
+@engines
+def test_group_site_records(orc, spec):
+    """Rule groups (rules of one form differing only in constants, run once with a bit per member)
+    write one site record per lane and error site for every member ending there, expanded to the
+    members' records at fetch (kvdevtypes.h GSiteDesc): members failing at different leaves and at
+    different loop indices on one resource, a group of 40 members (two groups of at most 32), loop
+    indices that overflow the compact record (the full-record re-run) and ERROR statuses."""
+    import random
+
+    rnd = random.Random(11)
+    regs = [f"reg{k}.io" for k in range(40)]
+    rules = [{"name": f"img-{k}", "match": {"resources": {"kinds": ["Pod"]}},
+              "validate": {"pattern": {"spec": {"containers": [{"image": f"{regs[k]}/*", "name": f"c{k % 7}*"}]}}}}
+             for k in range(40)]
+    # an array where a map is expected: the representative's structural check fails for every member
+    rules += [{"name": f"lim-{k}", "match": {"resources": {"kinds": ["Pod"]}},
+               "validate": {"pattern": {"spec": {"volumes": [{"name": f"v{k}*"}]}}}} for k in range(6)]
+    pol = {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "grp"}, "spec": {"rules": rules}}
+
+    def pod(n, big=None):
+        cs = [{"name": f"c{rnd.randrange(9)}x", "image": f"{rnd.choice(regs)}/app:{i}"} for i in range(n)]
+        if big is not None:
+            cs[big]["image"] = "other.io/x"
+        vols = rnd.choice([[{"name": f"v{rnd.randrange(8)}a"}], [], "notalist", [{"name": "v1"}, {"name": "z"}]])
+        return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p"}, "spec": {"containers": cs, "volumes": vols}}
+
+    ress = [pod(rnd.randrange(1, 6)) for _ in range(300)] + [pod(1100, big=1050), pod(1100, big=1023), pod(3)]
+    mism, r, ost = compare(orc, [pol], ress, check_paths=True, max_path_checks=3000, specialize=spec)
+    assert not mism, "\n".join(mism)
+    assert (r.status == 1).sum() > 5000 and (r.status == 0).sum() > 100
+    for j in (300, 301):  # every failing path of the 1100-container Pods (wide and compact indices)
+        ov = orc.validate(pol, ress[j], None)
+        for k in range(len(rules)):
+            if r.status[k, j] == 1:
+                assert r.path(k, j) == ov["rules"][k]["path"], (k, j)
