@@ -40,9 +40,114 @@ struct HipError : std::runtime_error {
 
 bool pinned_src(const void* src, size_t bytes);  // page-locked store array (PinnedStore)
 
+// Device allocations are expensive to create and to free (hipMalloc maps pages, hipFree also
+// waits for the device), and a host that validates batch after batch allocates the same store,
+// column and result buffers for every batch. Released buffers are therefore kept per device (up
+// to 64 GiB of the 288 GiB HBM) and handed to the next allocation of a similar size; when a
+// hipMalloc fails, the device's kept buffers are freed and the allocation is retried.
+// KVGPU_DEVPOOL=0: plain hipMalloc / hipFree.
+struct DevPool {
+  std::mutex mu;
+  std::map<int, std::multimap<size_t, void*>> free;  // device -> capacity -> block
+  std::map<int, size_t> held;
+  static constexpr size_t kHold = 64ull << 30;
+  static DevPool& get() {
+    static DevPool* p = new DevPool();  // never destroyed: buffers may be released during static teardown
+    return *p;
+  }
+  static bool enabled() {
+    static const bool on = !(getenv("KVGPU_DEVPOOL") && getenv("KVGPU_DEVPOOL")[0] == '0');
+    return on;
+  }
+  // a block of at least `bytes` on the current device `dev` (its capacity in *cap)
+  void* take(int dev, size_t bytes, size_t* cap) {
+    if (enabled()) {
+      std::lock_guard<std::mutex> g(mu);
+      auto& f = free[dev];
+      auto it = f.lower_bound(bytes);
+      if (it != f.end() && it->first <= bytes + bytes / 4 + (2u << 20)) {
+        void* p = it->second;
+        *cap = it->first;
+        held[dev] -= it->first;
+        f.erase(it);
+        return p;
+      }
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      trim(dev);
+      HIPCHK(hipMalloc(&p, bytes));
+    }
+    *cap = bytes;
+    return p;
+  }
+  // the block goes back once the device is idle (hipFree's own semantics: no kernel or copy
+  // still using it can see it handed out again)
+  void give(int dev, void* p, size_t cap) {
+    (void)hipDeviceSynchronize();
+    if (enabled()) {
+      std::lock_guard<std::mutex> g(mu);
+      if (held[dev] + cap <= kHold) {
+        free[dev].emplace(cap, p);
+        held[dev] += cap;
+        return;
+      }
+    }
+    (void)hipFree(p);
+  }
+  size_t held_on(int dev) {
+    std::lock_guard<std::mutex> g(mu);
+    return held[dev];
+  }
+  void trim(int dev) {
+    std::multimap<size_t, void*> f;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      f.swap(free[dev]);
+      held[dev] = 0;
+    }
+    for (auto& [c, p] : f) (void)hipFree(p);
+  }
+};
+
+// HIP streams cost milliseconds to create and to destroy on this runtime (hipStreamCreate* 2.3-3.8
+// ms, hipStreamDestroy 1.8-2.6 ms per call in the rocprofv3 HIP API trace of a C2 kv_validate: 15 of
+// its 44 ms), so sessions and staged uploads take idle streams from a per-(device, flags) pool and
+// give them back instead.
+struct StreamPool {
+  std::mutex mu;
+  std::map<std::pair<int, unsigned>, std::vector<hipStream_t>> free;
+  static StreamPool& get() {
+    static StreamPool* p = new StreamPool();  // never destroyed (streams die with the process)
+    return *p;
+  }
+  // a stream of the current device `dev`
+  hipStream_t take(int dev, unsigned flags) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      auto& v = free[{dev, flags}];
+      if (!v.empty()) {
+        hipStream_t s = v.back();
+        v.pop_back();
+        return s;
+      }
+    }
+    hipStream_t s = nullptr;
+    HIPCHK(hipStreamCreateWithFlags(&s, flags));
+    return s;
+  }
+  void give(int dev, unsigned flags, hipStream_t s) {
+    if (!s) return;
+    (void)hipStreamSynchronize(s);
+    std::lock_guard<std::mutex> g(mu);
+    free[{dev, flags}].push_back(s);
+  }
+};
+
 struct DevBuf {
   void* p = nullptr;
-  size_t n = 0;
+  size_t n = 0, cap = 0;
   int dev = -1;
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
@@ -53,11 +158,20 @@ struct DevBuf {
     upload_raw(v.data(), v.size() * sizeof(T), device);
   }
   void upload_raw(const void* src, size_t bytes, int device) {
-    release();
-    dev = device;
-    n = bytes;
-    HIPCHK(hipMalloc(&p, std::max<size_t>(bytes, 16)));
+    alloc(bytes, device);
     if (bytes) upload_h2d(p, src, bytes);
+  }
+  // a page-locked source is copied asynchronously on `st` (the caller synchronizes `st` before
+  // the source may change or the buffer is read elsewhere); a pageable one as upload_raw
+  template <class T, class A>
+  void upload_async(const std::vector<T, A>& v, int device, hipStream_t st) {
+    const size_t bytes = v.size() * sizeof(T);
+    alloc(bytes, device);
+    if (!bytes) return;
+    if (pinned_src(v.data(), bytes))
+      HIPCHK(hipMemcpyAsync(p, v.data(), bytes, hipMemcpyHostToDevice, st));
+    else
+      upload_h2d(p, v.data(), bytes);
   }
   // Host-to-device copy of a (pageable) host range. Large ranges go through a pinned staging
   // ring: host threads copy chunk i into a page-locked buffer while the DMA engine moves chunk
@@ -84,8 +198,9 @@ struct DevBuf {
         }
       }
     }
-    hipStream_t st;
-    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    int sdev = 0;
+    HIPCHK(hipGetDevice(&sdev));
+    hipStream_t st = StreamPool::get().take(sdev, hipStreamNonBlocking);
     hipEvent_t ev[kRing];
     for (int i = 0; i < kRing; i++) HIPCHK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
     bool used[kRing] = {};
@@ -109,24 +224,25 @@ struct DevBuf {
     }
     HIPCHK(hipStreamSynchronize(st));
     for (int i = 0; i < kRing; i++) (void)hipEventDestroy(ev[i]);
-    (void)hipStreamDestroy(st);
+    StreamPool::get().give(sdev, hipStreamNonBlocking, st);
   }
-  void alloc(size_t bytes, int device) {  // (a buffer allocated before is freed first)
+  void alloc(size_t bytes, int device) {  // (a buffer allocated before is released first)
     release();
     dev = device;
     n = bytes;
-    HIPCHK(hipMalloc(&p, std::max<size_t>(bytes, 16)));
+    p = DevPool::get().take(device, std::max<size_t>(bytes, 16), &cap);
   }
   void release() {
     if (!p) return;
     int cur;
     if (hipGetDevice(&cur) == hipSuccess) {
       (void)hipSetDevice(dev);
-      (void)hipFree(p);
+      DevPool::get().give(dev, p, cap);
       (void)hipSetDevice(cur);
     }
     p = nullptr;
     n = 0;
+    cap = 0;
   }
 };
 
@@ -698,20 +814,20 @@ std::shared_ptr<DevBatchRes> dev_batch(kv_batch* bt, const PolicySet& ps, int de
   const Batch& b = bt->b;
   if (b.rmask.size() != b.n_rows || b.roff.size() != b.n_rows)
     throw std::runtime_error("batch: packed row arrays do not match the row count");
-  {
-    // packed rows: upload the non-zero cells, masks and row offsets, then expand to the
-    // wave-group layout on the device
-    DevBuf pc, rm, ro;
-    pc.upload(b.pcells, device);
-    rm.upload(b.rmask, device);
-    ro.upload(b.roff, device);
-    d->nodes.alloc(b.n_cells() * sizeof(Node), device);
-    HIPCHK(launch_expand_rows((const Node*)pc.p, (const uint64_t*)rm.p, (const uint32_t*)ro.p, b.n_rows,
-                              (Node*)d->nodes.p, nullptr));
-    HIPCHK(hipStreamSynchronize(nullptr));
-  }
-  d->vals.upload(b.vals, device);
-  d->res.upload(b.res, device);
+  // packed rows: upload the non-zero cells, masks and row offsets, then expand to the
+  // wave-group layout on the device. The page-locked arrays (rows, values, resources) go as
+  // asynchronous copies on one stream, the expansion behind them, while this thread uploads the
+  // pageable ones (strings, key table, match inputs) through the staging path beside them.
+  hipStream_t us = StreamPool::get().take(device, hipStreamNonBlocking);
+  DevBuf pc, rm, ro;
+  pc.upload_async(b.pcells, device, us);
+  rm.upload_async(b.rmask, device, us);
+  ro.upload_async(b.roff, device, us);
+  d->nodes.alloc(b.n_cells() * sizeof(Node), device);
+  HIPCHK(launch_expand_rows((const Node*)pc.p, (const uint64_t*)rm.p, (const uint32_t*)ro.p, b.n_rows,
+                            (Node*)d->nodes.p, us));
+  d->vals.upload_async(b.vals, device, us);
+  d->res.upload_async(b.res, device, us);
   d->kvs.upload(b.kvs, device);
   d->bstr.upload_raw(b.strs.data(), b.strs.size(), device);
   d->nsbits.upload(b.ns_bits, device);
@@ -777,6 +893,11 @@ std::shared_ptr<DevBatchRes> dev_batch(kv_batch* bt, const PolicySet& ps, int de
     v.dyn_st = (const uint8_t*)d->dynst.p;
   }
   d->view_dev.upload_raw(&d->view, sizeof(DevBatch), device);
+  HIPCHK(hipStreamSynchronize(us));
+  StreamPool::get().give(device, hipStreamNonBlocking, us);
+  pc.release();
+  rm.release();
+  ro.release();
   if (bt->owner && bt->owner->jit && !bt->owner->jit->cols.empty() && !b.res.empty()) {
     build_pcol(*bt->owner->jit, b, d.get(), device);
     d->view_dev.upload_raw(&d->view, sizeof(DevBatch), device);
@@ -1114,10 +1235,10 @@ struct DevSession {
           (void)hipGetLastError();
       }
     }
-    HIPCHK(hipStreamCreate(&stream));
+    stream = StreamPool::get().take(device, hipStreamDefault);
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
-    HIPCHK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    side = StreamPool::get().take(device, hipStreamNonBlocking);
     HIPCHK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
   }
@@ -1144,8 +1265,8 @@ struct DevSession {
     if (e1) (void)hipEventDestroy(e1);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
-    if (side) (void)hipStreamDestroy(side);
-    if (stream) (void)hipStreamDestroy(stream);
+    StreamPool::get().give(device, hipStreamNonBlocking, side);
+    StreamPool::get().give(device, hipStreamDefault, stream);
   }
   // enqueue `iters` passes, wait, return HIP-event milliseconds of all passes
   // vm: run the passes on the bytecode engine even when the policy set has specialized kernels
@@ -1280,7 +1401,9 @@ struct DevSession {
     bool caller = want_st && bt && lo == 0 && nres == n_total && !bt->b.order.empty();
     if (caller && !stc.p) {  // the gathered copy is a second status matrix: only with room to spare
       size_t fr = 0, tot = 0;
-      if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < nrules * nres + nres * 8u + (512ull << 20)) caller = false;
+      if (hipMemGetInfo(&fr, &tot) != hipSuccess) caller = false;
+      fr += DevPool::get().held_on(device);  // (kept buffers are freed when an allocation needs them)
+      if (fr < nrules * nres + nres * 8u + (512ull << 20)) caller = false;
     }
     bool side_copy = false;
     if (caller) {
