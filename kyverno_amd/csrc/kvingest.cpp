@@ -1032,7 +1032,7 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
       decltype(q.rmask)().swap(q.rmask);
       decltype(q.roff)().swap(q.roff);
       decltype(q.kvs)().swap(q.kvs);
-      std::string().swap(q.strs);
+      HeapStr().swap(q.strs);
     });
   for (auto& t : th) t.join();
 }

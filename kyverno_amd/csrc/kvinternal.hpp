@@ -255,6 +255,8 @@ struct StoreAlloc {
 };
 template <class T>
 using StoreVec = std::vector<T, StoreAlloc<T>>;
+// the string heap: page-locked in the merged batch (one direct DMA), huge pages in the parts
+using HeapStr = std::basic_string<char, std::char_traits<char>, StoreAlloc<char>>;
 
 // Ingested batch (host mirror of the HBM store)
 struct Batch {
@@ -294,9 +296,10 @@ struct Batch {
     pcells = StoreVec<kv::Node>(StoreAlloc<kv::Node>(true));
     rmask = StoreVec<uint64_t>(StoreAlloc<uint64_t>(true));
     roff = StoreVec<uint32_t>(StoreAlloc<uint32_t>(true));
+    strs = HeapStr(StoreAlloc<char>(true));
   }
   std::vector<kv::KV> kvs;
-  std::string strs;                  // string heap
+  HeapStr strs;                      // string heap
   std::vector<std::string> dyn_keys; // key ids >= ps.keys.size()
   std::vector<std::string> namespaces;
   std::vector<kv::StrRef> nsms;      // distinct checkNameSpace strings (Res::nsm)
