@@ -1095,6 +1095,16 @@ struct DevSession {
   uint32_t mode = 0;
   uint64_t nrules = 0, nres = 0;
   DevBuf fflags, pview, st, er8, er, cn, scope, scn, ptab, mtab, mtbf, mtup, ftab;
+  // Value-predicate tables of consecutive passes are double-buffered (ptab / ptab1, read through
+  // pview / pview1): pass i + 1's table (kvj_ptab, on `pside`) is built while pass i's rule
+  // kernels run, waiting only for pass i - 1's rule kernels (the last readers of its buffer), so
+  // its waves fill the workgroup slots the rule kernels' last round leaves idle. ev_pt[b]: table
+  // b built; ev_rk[b]: the rule kernels that read table b done. KVGPU_PTAB_PIPE=0: one table,
+  // built on the session stream ahead of each pass's rule kernels.
+  DevBuf ptab1, pview1;
+  hipStream_t pside = nullptr;
+  hipEvent_t ev_pt[2] = {nullptr, nullptr}, ev_rk[2] = {nullptr, nullptr};
+  bool ptab_pipe = false;
   uint32_t fac_entities = 0, ntup = 0;
   bool rec_compact = false;  // the last pass wrote records per wave segment (specialized kernels)
   // the batch's device copy, shared with the batch's cache and other sessions on it; a part of a
@@ -1180,6 +1190,12 @@ struct DevSession {
       P.fac_tab = (uint32_t*)ftab.p;
     }
     pview.upload_raw(&P, sizeof(DevPS), device);  // read through a uniform pointer (scalar loads)
+    ptab_pipe = dp.ptab_fn && !(getenv("KVGPU_PTAB_PIPE") && getenv("KVGPU_PTAB_PIPE")[0] == '0');
+    if (ptab_pipe) {
+      ptab1.alloc(ptab.n, device);
+      P.ptab = (const uint32_t*)ptab1.p;
+      pview1.upload_raw(&P, sizeof(DevPS), device);
+    }
     nrules = ps->ps.rules.size();
     nres = bt->b.res.size();
     ntup = (uint32_t)bt->b.tup_rep.size();
@@ -1239,6 +1255,13 @@ struct DevSession {
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
     side = StreamPool::get().take(device, hipStreamNonBlocking);
+    if (ptab_pipe) {
+      pside = StreamPool::get().take(device, hipStreamNonBlocking);
+      for (int b = 0; b < 2; b++) {
+        HIPCHK(hipEventCreateWithFlags(&ev_pt[b], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ev_rk[b], hipEventDisableTiming));
+      }
+    }
     HIPCHK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
   }
@@ -1265,6 +1288,11 @@ struct DevSession {
     if (e1) (void)hipEventDestroy(e1);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
+    for (int b = 0; b < 2; b++) {
+      if (ev_pt[b]) (void)hipEventDestroy(ev_pt[b]);
+      if (ev_rk[b]) (void)hipEventDestroy(ev_rk[b]);
+    }
+    StreamPool::get().give(device, hipStreamNonBlocking, pside);
     StreamPool::get().give(device, hipStreamNonBlocking, side);
     StreamPool::get().give(device, hipStreamDefault, stream);
   }
@@ -1274,6 +1302,11 @@ struct DevSession {
   double run(int iters, bool vm = false) {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipEventRecord(e0, stream));
+    const bool pipe = ptab_pipe && dps->specialized() && !vm && nres;
+    if (pipe && iters > 0) {  // pass 0's table, after the start event
+      HIPCHK(hipStreamWaitEvent(pside, e0, 0));
+      launch_ptab(0);
+    }
     for (int i = 0; i < iters; i++) {
       rec_compact = dps->specialized() && !vm;
       // the match tables on the side stream, forked from and joined back into `stream`
@@ -1287,7 +1320,12 @@ struct DevSession {
       if (mode & KV_MODE_SCOPES) HIPCHK(hipMemsetAsync(scn.p, 0, scn.n, ms));
       HIPCHK(launch_mtab((const DevPS*)pview.p, bview, mt_words, mt_entities, mt_ns, mt_ann, mt_sel, ms));
       if (rec_compact) {
-        launch_specialized();  // (per-scope counts inside the rule kernels)
+        launch_specialized(pipe ? (i & 1) : -1);  // (per-scope counts inside the rule kernels)
+        if (pipe && i + 1 < iters) {  // the next pass's table, once pass i - 1's kernels are done with it
+          const int nb = (i + 1) & 1;
+          if (i >= 1) HIPCHK(hipStreamWaitEvent(pside, ev_rk[nb], 0));
+          launch_ptab(nb);
+        }
         if (O.full & 8u)  // per-rule totals from the per-scope counts (the kernels add only those)
           HIPCHK(launch_scope_totals((const unsigned long long*)scn.p, nscopes, (uint32_t)nrules,
                                      (unsigned long long*)cn.p, stream));
@@ -1334,18 +1372,33 @@ struct DevSession {
     fprintf(stderr, "\n");
   }
   // one launch per rule kernel of the specialized kernels, 256 resources per workgroup
-  void launch_specialized() {
+  // the value-predicate table b of a pipelined pass, on `pside`, then its event
+  void launch_ptab(int b) {
+    const DevPS* P = (const DevPS*)(b ? pview1.p : pview.p);
+    const Val* V = bhost->vals;
+    const uint8_t* S = bhost->bstr;
+    uint32_t NV = nvals;
+    uint32_t* PT = (uint32_t*)(b ? ptab1.p : ptab.p);
+    void* targs[] = {(void*)&P, (void*)&V, (void*)&S, (void*)&NV, (void*)&PT};
+    HIPCHK(hipModuleLaunchKernel(dps->ptab_fn, (NV + KV_PTAB_PSEUDO + KV_WG - 1) / KV_WG, dps->ptab_rows, 1, KV_WG, 1, 1, 0,
+                                 pside, targs, nullptr));
+    HIPCHK(hipEventRecord(ev_pt[b], pside));
+  }
+  // pb: the pipelined table this pass reads (launch_ptab), -1: build the table here
+  void launch_specialized(int pb = -1) {
     if (nres == 0) {  // (join the side stream's table work all the same)
       HIPCHK(hipEventRecord(ev_join, side));
       HIPCHK(hipStreamWaitEvent(stream, ev_join, 0));
       return;
     }
     const uint32_t blocks = (uint32_t)((nres + KV_WG - 1) / KV_WG);
-    const DevPS* P = (const DevPS*)pview.p;
+    const DevPS* P = (const DevPS*)(pb == 1 ? pview1.p : pview.p);
     const Node* N = bhost->nodes;
     const Val* V = bhost->vals;
     const uint8_t* S = bhost->bstr;
-    if (dps->ptab_fn) {  // every leaf predicate once per distinct value (+ pseudo columns), before the rule kernels
+    if (pb >= 0) {
+      HIPCHK(hipStreamWaitEvent(stream, ev_pt[pb], 0));
+    } else if (dps->ptab_fn) {  // every leaf predicate once per distinct value (+ pseudo columns), before the rule kernels
       uint32_t NV = nvals;
       uint32_t* PT = (uint32_t*)ptab.p;
       void* targs[] = {(void*)&P, (void*)&V, (void*)&S, (void*)&NV, (void*)&PT};
@@ -1360,6 +1413,7 @@ struct DevSession {
     uint32_t r0 = 0;
     void* args[] = {(void*)&P, (void*)&bview, (void*)&N, (void*)&V, (void*)&S, (void*)&Ov, (void*)&r0};
     for (hipFunction_t f : dps->fns) HIPCHK(hipModuleLaunchKernel(f, blocks, 1, 1, KV_WG, 1, 1, 0, stream, args, nullptr));
+    if (pb >= 0) HIPCHK(hipEventRecord(ev_rk[pb], stream));
   }
   std::vector<int64_t> read_counts() {
     HIPCHK(hipSetDevice(device));
