@@ -1095,13 +1095,16 @@ struct DevSession {
   uint32_t mode = 0;
   uint64_t nrules = 0, nres = 0;
   DevBuf fflags, pview, st, er8, er, cn, scope, scn, ptab, mtab, mtbf, mtup, ftab;
-  // Value-predicate tables of consecutive passes are double-buffered (ptab / ptab1, read through
-  // pview / pview1): pass i + 1's table (kvj_ptab, on `pside`) is built while pass i's rule
-  // kernels run, waiting only for pass i - 1's rule kernels (the last readers of its buffer), so
-  // its waves fill the workgroup slots the rule kernels' last round leaves idle. ev_pt[b]: table
-  // b built; ev_rk[b]: the rule kernels that read table b done. KVGPU_PTAB_PIPE=0: one table,
-  // built on the session stream ahead of each pass's rule kernels.
-  DevBuf ptab1, pview1;
+  // The per-pass tables of the specialized kernels (value-predicate table kvj_ptab, match tables
+  // kv_mtab / kv_mfac / kv_mtup) are double-buffered between consecutive passes (ptab / ptab1,
+  // mtab / mtab1, ... read through pview / pview1): pass i + 1's tables are built on `pside` while
+  // pass i's rule kernels run, waiting only for pass i - 1's rule kernels (the last readers of
+  // their buffers), so their waves fill the workgroup slots the rule kernels' last round leaves
+  // idle. ev_pt[b]: tables b built; ev_rk[b]: the rule kernels that read tables b done.
+  // KVGPU_PTAB_PIPE=0: one set, built ahead of each pass's rule kernels (ptab on the session
+  // stream, the match tables on `side`).
+  DevBuf ptab1, pview1, mtab1, mtup1, ftab1;
+  uint32_t *mt1_ns = nullptr, *mt1_ann = nullptr, *mt1_sel = nullptr;
   hipStream_t pside = nullptr;
   hipEvent_t ev_pt[2] = {nullptr, nullptr}, ev_rk[2] = {nullptr, nullptr};
   bool ptab_pipe = false;
@@ -1190,10 +1193,25 @@ struct DevSession {
       P.fac_tab = (uint32_t*)ftab.p;
     }
     pview.upload_raw(&P, sizeof(DevPS), device);  // read through a uniform pointer (scalar loads)
-    ptab_pipe = dp.ptab_fn && !(getenv("KVGPU_PTAB_PIPE") && getenv("KVGPU_PTAB_PIPE")[0] == '0');
-    if (ptab_pipe) {
-      ptab1.alloc(ptab.n, device);
-      P.ptab = (const uint32_t*)ptab1.p;
+    ptab_pipe = dp.specialized() && !(getenv("KVGPU_PTAB_PIPE") && getenv("KVGPU_PTAB_PIPE")[0] == '0');
+    if (ptab_pipe) {  // the second set of per-pass tables
+      if (dp.ptab_fn) {
+        ptab1.alloc(ptab.n, device);
+        P.ptab = (const uint32_t*)ptab1.p;
+      }
+      mtab1.alloc(mtab.n, device);
+      mt1_ns = (uint32_t*)mtab1.p;
+      mt1_ann = mt1_ns + (mt_ann - mt_ns);
+      mt1_sel = mt1_ns + (mt_sel - mt_ns);
+      P.mt_ns = mt1_ns;
+      P.mt_ann = mt1_ann;
+      P.mt_sel = mt1_sel;
+      if (dp.mtup_words) {
+        mtup1.alloc(mtup.n, device);
+        P.mtup = (const uint32_t*)mtup1.p;
+        ftab1.alloc(ftab.n, device);
+        P.fac_tab = (uint32_t*)ftab1.p;
+      }
       pview1.upload_raw(&P, sizeof(DevPS), device);
     }
     nrules = ps->ps.rules.size();
@@ -1303,12 +1321,26 @@ struct DevSession {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipEventRecord(e0, stream));
     const bool pipe = ptab_pipe && dps->specialized() && !vm && nres;
-    if (pipe && iters > 0) {  // pass 0's table, after the start event
+    if (pipe && iters > 0) {  // pass 0's tables, after the start event
       HIPCHK(hipStreamWaitEvent(pside, e0, 0));
-      launch_ptab(0);
+      launch_tables(0);
     }
     for (int i = 0; i < iters; i++) {
       rec_compact = dps->specialized() && !vm;
+      if (pipe) {  // counts zeroed behind pass i - 1's kernels; tables from launch_tables
+        HIPCHK(hipMemsetAsync(cn.p, 0, cn.n, stream));
+        if (mode & KV_MODE_SCOPES) HIPCHK(hipMemsetAsync(scn.p, 0, scn.n, stream));
+        launch_specialized(i & 1);
+        if (O.full & 8u)
+          HIPCHK(launch_scope_totals((const unsigned long long*)scn.p, nscopes, (uint32_t)nrules,
+                                     (unsigned long long*)cn.p, stream));
+        if (i + 1 < iters) {  // the next pass's tables, once pass i - 1's kernels are done with them
+          const int nb = (i + 1) & 1;
+          if (i >= 1) HIPCHK(hipStreamWaitEvent(pside, ev_rk[nb], 0));
+          launch_tables(nb);
+        }
+        continue;
+      }
       // the match tables on the side stream, forked from and joined back into `stream`
       // (specialized passes; the bytecode engine runs everything in order on `stream`)
       hipStream_t ms = rec_compact ? side : stream;
@@ -1320,12 +1352,7 @@ struct DevSession {
       if (mode & KV_MODE_SCOPES) HIPCHK(hipMemsetAsync(scn.p, 0, scn.n, ms));
       HIPCHK(launch_mtab((const DevPS*)pview.p, bview, mt_words, mt_entities, mt_ns, mt_ann, mt_sel, ms));
       if (rec_compact) {
-        launch_specialized(pipe ? (i & 1) : -1);  // (per-scope counts inside the rule kernels)
-        if (pipe && i + 1 < iters) {  // the next pass's table, once pass i - 1's kernels are done with it
-          const int nb = (i + 1) & 1;
-          if (i >= 1) HIPCHK(hipStreamWaitEvent(pside, ev_rk[nb], 0));
-          launch_ptab(nb);
-        }
+        launch_specialized();  // (per-scope counts inside the rule kernels)
         if (O.full & 8u)  // per-rule totals from the per-scope counts (the kernels add only those)
           HIPCHK(launch_scope_totals((const unsigned long long*)scn.p, nscopes, (uint32_t)nrules,
                                      (unsigned long long*)cn.p, stream));
@@ -1372,16 +1399,24 @@ struct DevSession {
     fprintf(stderr, "\n");
   }
   // one launch per rule kernel of the specialized kernels, 256 resources per workgroup
-  // the value-predicate table b of a pipelined pass, on `pside`, then its event
-  void launch_ptab(int b) {
+  // the per-pass tables of set b (match tables, factored match, value-predicate table) of a
+  // pipelined pass, on `pside`, then their event
+  void launch_tables(int b) {
     const DevPS* P = (const DevPS*)(b ? pview1.p : pview.p);
-    const Val* V = bhost->vals;
-    const uint8_t* S = bhost->bstr;
-    uint32_t NV = nvals;
-    uint32_t* PT = (uint32_t*)(b ? ptab1.p : ptab.p);
-    void* targs[] = {(void*)&P, (void*)&V, (void*)&S, (void*)&NV, (void*)&PT};
-    HIPCHK(hipModuleLaunchKernel(dps->ptab_fn, (NV + KV_PTAB_PSEUDO + KV_WG - 1) / KV_WG, dps->ptab_rows, 1, KV_WG, 1, 1, 0,
-                                 pside, targs, nullptr));
+    HIPCHK(launch_mtab(P, bview, mt_words, mt_entities, b ? mt1_ns : mt_ns, b ? mt1_ann : mt_ann, b ? mt1_sel : mt_sel,
+                       pside));
+    if (dps->mtup_words && ntup)
+      HIPCHK(launch_mfac(P, bview, dps->fac_slots, fac_entities, dps->mtup_words, ntup,
+                         (uint32_t*)(b ? mtup1.p : mtup.p), pside));
+    if (dps->ptab_fn) {
+      const Val* V = bhost->vals;
+      const uint8_t* S = bhost->bstr;
+      uint32_t NV = nvals;
+      uint32_t* PT = (uint32_t*)(b ? ptab1.p : ptab.p);
+      void* targs[] = {(void*)&P, (void*)&V, (void*)&S, (void*)&NV, (void*)&PT};
+      HIPCHK(hipModuleLaunchKernel(dps->ptab_fn, (NV + KV_PTAB_PSEUDO + KV_WG - 1) / KV_WG, dps->ptab_rows, 1, KV_WG, 1, 1,
+                                   0, pside, targs, nullptr));
+    }
     HIPCHK(hipEventRecord(ev_pt[b], pside));
   }
   // pb: the pipelined table this pass reads (launch_ptab), -1: build the table here
@@ -1398,7 +1433,8 @@ struct DevSession {
     const uint8_t* S = bhost->bstr;
     if (pb >= 0) {
       HIPCHK(hipStreamWaitEvent(stream, ev_pt[pb], 0));
-    } else if (dps->ptab_fn) {  // every leaf predicate once per distinct value (+ pseudo columns), before the rule kernels
+    } else {
+    if (dps->ptab_fn) {  // every leaf predicate once per distinct value (+ pseudo columns), before the rule kernels
       uint32_t NV = nvals;
       uint32_t* PT = (uint32_t*)ptab.p;
       void* targs[] = {(void*)&P, (void*)&V, (void*)&S, (void*)&NV, (void*)&PT};
@@ -1409,6 +1445,7 @@ struct DevSession {
       HIPCHK(launch_mfac(P, bview, dps->fac_slots, fac_entities, dps->mtup_words, ntup, (uint32_t*)mtup.p, side));
     HIPCHK(hipEventRecord(ev_join, side));
     HIPCHK(hipStreamWaitEvent(stream, ev_join, 0));
+    }
     DevOut Ov = O;
     uint32_t r0 = 0;
     void* args[] = {(void*)&P, (void*)&bview, (void*)&N, (void*)&V, (void*)&S, (void*)&Ov, (void*)&r0};
