@@ -12,6 +12,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <tuple>
 #include <stdexcept>
 #include <thread>
 #include <string>
@@ -117,16 +118,18 @@ struct DevPool {
 // give them back instead.
 struct StreamPool {
   std::mutex mu;
-  std::map<std::pair<int, unsigned>, std::vector<hipStream_t>> free;
+  std::map<std::tuple<int, unsigned, int>, std::vector<hipStream_t>> free;
   static StreamPool& get() {
     static StreamPool* p = new StreamPool();  // never destroyed (streams die with the process)
     return *p;
   }
-  // a stream of the current device `dev`
-  hipStream_t take(int dev, unsigned flags) {
+  // a stream of the current device `dev`; low: the lowest scheduling priority (its workgroups are
+  // dispatched when the other queues' kernels leave slots free)
+  hipStream_t take(int dev, unsigned flags, bool low = false) {
+    const int prio = low ? lowest() : 0;
     {
       std::lock_guard<std::mutex> g(mu);
-      auto& v = free[{dev, flags}];
+      auto& v = free[{dev, flags, prio}];
       if (!v.empty()) {
         hipStream_t s = v.back();
         v.pop_back();
@@ -134,14 +137,24 @@ struct StreamPool {
       }
     }
     hipStream_t s = nullptr;
-    HIPCHK(hipStreamCreateWithFlags(&s, flags));
+    if (low) HIPCHK(hipStreamCreateWithPriority(&s, flags, prio));
+    else HIPCHK(hipStreamCreateWithFlags(&s, flags));
     return s;
   }
-  void give(int dev, unsigned flags, hipStream_t s) {
+  void give(int dev, unsigned flags, hipStream_t s, bool low = false) {
     if (!s) return;
     (void)hipStreamSynchronize(s);
+    const int prio = low ? lowest() : 0;
     std::lock_guard<std::mutex> g(mu);
-    free[{dev, flags}].push_back(s);
+    free[{dev, flags, prio}].push_back(s);
+  }
+  static int lowest() {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) {
+      (void)hipGetLastError();
+      return 0;
+    }
+    return least;
   }
 };
 
@@ -225,6 +238,12 @@ struct DevBuf {
     HIPCHK(hipStreamSynchronize(st));
     for (int i = 0; i < kRing; i++) (void)hipEventDestroy(ev[i]);
     StreamPool::get().give(sdev, hipStreamNonBlocking, st);
+  }
+  void swap(DevBuf& o) {
+    std::swap(p, o.p);
+    std::swap(n, o.n);
+    std::swap(cap, o.cap);
+    std::swap(dev, o.dev);
   }
   void alloc(size_t bytes, int device) {  // (a buffer allocated before is released first)
     release();
@@ -1103,7 +1122,7 @@ struct DevSession {
   // idle. ev_pt[b]: tables b built; ev_rk[b]: the rule kernels that read tables b done.
   // KVGPU_PTAB_PIPE=0: one set, built ahead of each pass's rule kernels (ptab on the session
   // stream, the match tables on `side`).
-  DevBuf ptab1, pview1, mtab1, mtup1, ftab1;
+  DevBuf ptab1, pview1, mtab1, mtup1, ftab1, cn1, scn1;  // (counts of set 1: zeroed with its tables)
   uint32_t *mt1_ns = nullptr, *mt1_ann = nullptr, *mt1_sel = nullptr;
   hipStream_t pside = nullptr;
   hipEvent_t ev_pt[2] = {nullptr, nullptr}, ev_rk[2] = {nullptr, nullptr};
@@ -1245,6 +1264,7 @@ struct DevSession {
     }
     cn.alloc(std::max<uint64_t>(nrules, 1) * KV_HIST * sizeof(unsigned long long), device);
     O.counts = (unsigned long long*)cn.p;
+    if (ptab_pipe) cn1.alloc(cn.n, device);
     if (mode & KV_MODE_SCOPES) {
       // scope of every resource = its namespace index in the batch namespace table
       std::vector<uint32_t> sc(nres);
@@ -1252,6 +1272,7 @@ struct DevSession {
       nscopes = (uint32_t)bt->b.namespaces.size();
       scope.upload(sc, device);
       scn.alloc(std::max<uint64_t>((uint64_t)nscopes * nrules, 1) * KV_HIST * sizeof(unsigned long long), device);
+      if (ptab_pipe) scn1.alloc(scn.n, device);
       O.scope = (const uint32_t*)scope.p;
       O.scounts = (unsigned long long*)scn.p;
       if (dp.specialized()) O.full |= 8;
@@ -1274,7 +1295,7 @@ struct DevSession {
     HIPCHK(hipEventCreate(&e1));
     side = StreamPool::get().take(device, hipStreamNonBlocking);
     if (ptab_pipe) {
-      pside = StreamPool::get().take(device, hipStreamNonBlocking);
+      pside = StreamPool::get().take(device, hipStreamNonBlocking, !(getenv("KVGPU_PIPE_PRIO") && getenv("KVGPU_PIPE_PRIO")[0] == '0'));
       for (int b = 0; b < 2; b++) {
         HIPCHK(hipEventCreateWithFlags(&ev_pt[b], hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ev_rk[b], hipEventDisableTiming));
@@ -1298,6 +1319,7 @@ struct DevSession {
     HIPCHK(hipStreamSynchronize(stream));
     nscopes = n_total;
     scn.alloc(std::max<uint64_t>((uint64_t)nscopes * nrules, 1) * KV_HIST * sizeof(unsigned long long), device);
+    if (ptab_pipe) scn1.alloc(scn.n, device);
     O.scounts = (unsigned long long*)scn.p;
   }
   ~DevSession() {
@@ -1310,7 +1332,7 @@ struct DevSession {
       if (ev_pt[b]) (void)hipEventDestroy(ev_pt[b]);
       if (ev_rk[b]) (void)hipEventDestroy(ev_rk[b]);
     }
-    StreamPool::get().give(device, hipStreamNonBlocking, pside);
+    StreamPool::get().give(device, hipStreamNonBlocking, pside, !(getenv("KVGPU_PIPE_PRIO") && getenv("KVGPU_PIPE_PRIO")[0] == '0'));
     StreamPool::get().give(device, hipStreamNonBlocking, side);
     StreamPool::get().give(device, hipStreamDefault, stream);
   }
@@ -1327,13 +1349,12 @@ struct DevSession {
     }
     for (int i = 0; i < iters; i++) {
       rec_compact = dps->specialized() && !vm;
-      if (pipe) {  // counts zeroed behind pass i - 1's kernels; tables from launch_tables
-        HIPCHK(hipMemsetAsync(cn.p, 0, cn.n, stream));
-        if (mode & KV_MODE_SCOPES) HIPCHK(hipMemsetAsync(scn.p, 0, scn.n, stream));
-        launch_specialized(i & 1);
+      if (pipe) {  // tables and zeroed counts of set i & 1 from launch_tables
+        const int b = i & 1;
+        launch_specialized(b);
         if (O.full & 8u)
-          HIPCHK(launch_scope_totals((const unsigned long long*)scn.p, nscopes, (uint32_t)nrules,
-                                     (unsigned long long*)cn.p, stream));
+          HIPCHK(launch_scope_totals((const unsigned long long*)(b ? scn1.p : scn.p), nscopes, (uint32_t)nrules,
+                                     (unsigned long long*)(b ? cn1.p : cn.p), stream));
         if (i + 1 < iters) {  // the next pass's tables, once pass i - 1's kernels are done with them
           const int nb = (i + 1) & 1;
           if (i >= 1) HIPCHK(hipStreamWaitEvent(pside, ev_rk[nb], 0));
@@ -1367,6 +1388,12 @@ struct DevSession {
     }
     HIPCHK(hipEventRecord(e1, stream));
     HIPCHK(hipEventSynchronize(e1));
+    if (pipe && iters > 0 && ((iters - 1) & 1)) {  // the last pass counted into set 1: it becomes set 0
+      cn.swap(cn1);
+      scn.swap(scn1);
+      O.counts = (unsigned long long*)cn.p;
+      if (mode & KV_MODE_SCOPES) O.scounts = (unsigned long long*)scn.p;
+    }
     float t = 0;
     HIPCHK(hipEventElapsedTime(&t, e0, e1));
     if (stamps.p) report_stamps();
@@ -1403,6 +1430,12 @@ struct DevSession {
   // pipelined pass, on `pside`, then their event
   void launch_tables(int b) {
     const DevPS* P = (const DevPS*)(b ? pview1.p : pview.p);
+    DevBuf& c = b ? cn1 : cn;
+    HIPCHK(hipMemsetAsync(c.p, 0, c.n, pside));
+    if (mode & KV_MODE_SCOPES) {
+      DevBuf& sc = b ? scn1 : scn;
+      HIPCHK(hipMemsetAsync(sc.p, 0, sc.n, pside));
+    }
     HIPCHK(launch_mtab(P, bview, mt_words, mt_entities, b ? mt1_ns : mt_ns, b ? mt1_ann : mt_ann, b ? mt1_sel : mt_sel,
                        pside));
     if (dps->mtup_words && ntup)
@@ -1447,6 +1480,10 @@ struct DevSession {
     HIPCHK(hipStreamWaitEvent(stream, ev_join, 0));
     }
     DevOut Ov = O;
+    if (pb == 1) {  // counts of set 1
+      Ov.counts = (unsigned long long*)cn1.p;
+      if (mode & KV_MODE_SCOPES) Ov.scounts = (unsigned long long*)scn1.p;
+    }
     uint32_t r0 = 0;
     void* args[] = {(void*)&P, (void*)&bview, (void*)&N, (void*)&V, (void*)&S, (void*)&Ov, (void*)&r0};
     for (hipFunction_t f : dps->fns) HIPCHK(hipModuleLaunchKernel(f, blocks, 1, 1, KV_WG, 1, 1, 0, stream, args, nullptr));
