@@ -811,14 +811,19 @@ void build_pcol(const JitImage& J, const Batch& b, DevBatchRes* d, int device) {
   // (the kernels index cells with 32 bits)
   if (cells >= (1ull << 32)) throw std::runtime_error("path columns: more than 2^32 cells");
   HIPCHK(hipMemcpy(d->pfam.p, fams.data(), fams.size() * sizeof(ColFam), hipMemcpyHostToDevice));
+  // two planes (kvcol.h col_put): (kt, a, c) 12 B per cell, then b 4 B per cell
   d->pcol.alloc(cells * sizeof(Node), device);
-  if (cells > root_cells)  // element rows past a lane's own elements stay zero
-    HIPCHK(hipMemset((Node*)d->pcol.p + root_cells, 0, (cells - root_cells) * sizeof(Node)));
-  HIPCHK(launch_pcol_build(Bd, cd, (const ColFam*)d->pfam.p, j0, 0, j0, groups, false, (Node*)d->pcol.p, nullptr));
+  uint32_t* pool = (uint32_t*)d->pcol.p;
+  if (cells > root_cells) {  // element rows past a lane's own elements stay zero (both planes)
+    HIPCHK(hipMemset(pool + 3 * root_cells, 0, (cells - root_cells) * 12u));
+    HIPCHK(hipMemset(pool + 3 * cells + root_cells, 0, (cells - root_cells) * 4u));
+  }
+  HIPCHK(launch_pcol_build(Bd, cd, (const ColFam*)d->pfam.p, j0, 0, j0, groups, false, pool, cells, nullptr));
   HIPCHK(launch_pcol_build(Bd, cd, (const ColFam*)d->pfam.p, j0, j0, (uint32_t)J.cols.size() - j0, groups, true,
-                           (Node*)d->pcol.p, nullptr));
+                           pool, cells, nullptr));
   HIPCHK(hipStreamSynchronize(nullptr));
-  d->view.pcol = (const Node*)d->pcol.p;
+  d->view.pcol = pool;
+  d->view.pcolb = pool + 3 * cells;
   d->pcol_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (getenv("KVGPU_VERBOSE"))
     fprintf(stderr, "[kvgpu] path columns: %zu columns in %u families, %.1f MB, built in %.2f ms\n", J.cols.size(), nf,

@@ -62,6 +62,18 @@ KV_FN Node col_cell(const Node& n, uint32_t idx, uint32_t arr_c) {
 
 KV_FN uint64_t col_fam_off(const ColFam& F) { return (uint64_t)F.off_lo | (uint64_t)F.off_hi << 32; }
 
+// cell i of a pool of `cells` cells in two planes (DevBatch::pcol): (kt, a, c) at word 3i, b at
+// word 3 cells + i
+KV_FN void col_put(uint32_t* __restrict__ pool, uint64_t cells, uint64_t i, const Node& n) {
+  pool[3 * i] = n.kt;
+  pool[3 * i + 1] = n.a;
+  pool[3 * i + 2] = n.c;
+  pool[3 * cells + i] = n.b;
+}
+KV_FN Node col_get(const uint32_t* __restrict__ pool, uint64_t cells, uint64_t i) {
+  return Node{pool[3 * i], pool[3 * i + 1], pool[3 * cells + i], pool[3 * i + 2]};
+}
+
 // element rows lane r needs in family f (its array's element count; 0 without an array)
 KV_FN uint32_t col_rows(const DevBatch& B, const ColDesc* cols, const ColFam* fams, uint32_t f, uint32_t r) {
   if (r >= B.n_res) return 0u;
@@ -72,7 +84,7 @@ KV_FN uint32_t col_rows(const DevBatch& B, const ColDesc* cols, const ColFam* fa
 
 // cell of family-0 column `c` for lane r (r >= n_res: the zero cell), written into the pool
 KV_FN void col_build_root(const DevBatch& B, const ColDesc* cols, const ColFam* fams, uint32_t j0, uint32_t c,
-                          uint32_t r, Node* __restrict__ pool) {
+                          uint32_t r, uint32_t* __restrict__ pool, uint64_t cells) {
   const ColDesc& d = cols[c];
   Node cell{0u, 0u, 0u, 0u};
   if (r < B.n_res) {
@@ -85,20 +97,20 @@ KV_FN void col_build_root(const DevBatch& B, const ColDesc* cols, const ColFam* 
     }
     cell = col_cell(n, idx, arr_c);
   }
-  pool[((size_t)(r >> 6) * j0 + d.j) * KV_LANES + (r & (KV_LANES - 1))] = cell;
+  col_put(pool, cells, ((size_t)(r >> 6) * j0 + d.j) * KV_LANES + (r & (KV_LANES - 1)), cell);
 }
 
 // cells of element column `c` (family f > 0) for every element of lane r's family array
 KV_FN void col_build_elem(const DevBatch& B, const ColDesc* cols, const ColFam* fams, uint32_t j0, uint32_t c,
-                          uint32_t r, Node* __restrict__ pool) {
+                          uint32_t r, uint32_t* __restrict__ pool, uint64_t cells) {
   const ColDesc& d = cols[c];
   const ColFam& F = fams[d.fam];
   const uint32_t lane = r & (KV_LANES - 1);
-  const Node a = pool[((size_t)(r >> 6) * j0 + F.arr_col) * KV_LANES + lane];
+  const Node a = col_get(pool, cells, ((size_t)(r >> 6) * j0 + F.arr_col) * KV_LANES + lane);
   if (node_type(a.kt) != NT_ARR || a.kt == 0u) return;
   for (uint32_t i = 0; i < a.b; i++) {
     uint32_t idx;
     const Node n = col_walk(B.nodes, ni(a.a + i), d, &idx);
-    pool[(size_t)a.c + ((size_t)i * F.ncols + d.j) * KV_LANES + lane] = col_cell(n, idx, 0u);
+    col_put(pool, cells, (size_t)a.c + ((size_t)i * F.ncols + d.j) * KV_LANES + lane, col_cell(n, idx, 0u));
   }
 }

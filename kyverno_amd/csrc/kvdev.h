@@ -74,6 +74,6 @@ hipError_t launch_expand_rows(const Node* pcells, const uint64_t* rmask, const u
 hipError_t launch_pcol_rows(const DevBatch* B, const ColDesc* cols, const ColFam* fams, uint32_t n_fam,
                             uint32_t n_groups, hipStream_t stream);
 hipError_t launch_pcol_build(const DevBatch* B, const ColDesc* cols, const ColFam* fams, uint32_t j0, uint32_t c0,
-                             uint32_t n, uint32_t n_groups, bool elem, Node* pool, hipStream_t stream);
+                             uint32_t n, uint32_t n_groups, bool elem, uint32_t* pool, uint64_t cells, hipStream_t stream);
 
 }  // namespace kv

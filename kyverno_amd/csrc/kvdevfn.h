@@ -66,6 +66,20 @@ __device__ __forceinline__ Node kv_ldn(const Node* p, size_t i) {
 #endif
 }
 
+// path-column cell i (DevBatch::pcol / pcolb planes): its (kt, a, c) words as one 12-byte
+// global-address-space load and its b word (an array's element count) as a 4-byte one, which
+// only array cells need (a caller that never reads .b leaves it dead)
+__device__ __forceinline__ Node kv_ldc(const uint32_t* pa, const uint32_t* pb, size_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef uint32_t u32x3_ __attribute__((ext_vector_type(3)));
+  const u32x3_ x = *(const __attribute__((address_space(1))) u32x3_*)((const __attribute__((address_space(1))) char*)pa + 12u * i);
+  const uint32_t y = ((const __attribute__((address_space(1))) uint32_t*)pb)[i];
+  return Node{x.x, x.y, y, x.z};
+#else
+  return Node{pa[3 * i], pa[3 * i + 1], pb[i], pa[3 * i + 2]};
+#endif
+}
+
 // node index of this lane's cell in a row (wave-group layout, kv_layout.h)
 __device__ __forceinline__ uint32_t ni(uint32_t row) { return row * KV_LANES + (threadIdx.x & (KV_LANES - 1)); }
 

@@ -131,8 +131,11 @@ struct DevBatch {
   const DevPS* dps;
   const uint32_t* dleaf;
   const uint8_t* dyn_st;
-  // path columns of the specialized kernels (kvcol.h; null without them)
-  const Node* pcol;
+  // path columns of the specialized kernels (kvcol.h; null without them), in two planes: the
+  // (kt, a, c) words of every cell, then its b words (pcolb = pcol + 3 x cells), so a lookup
+  // of a map or a scalar (everything but an array's element count) loads 12 of its 16 bytes
+  const uint32_t* pcol;
+  const uint32_t* pcolb;
 };
 
 // ------------------------------------------------------------------ path columns

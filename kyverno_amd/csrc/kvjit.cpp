@@ -965,7 +965,7 @@ struct Gen {
     if (j != kNoCol) {
       // the node from its path column (absent: the zero cell); the index only where the
       // lookup's presence (or a map's own index: wildcard keys) is asked for
-      c << "  const Node " << h.node << " = kv_ldn(PC, " << T.cell0 << " + " << u32(j * KV_LANES) << ");\n"
+      c << "  const Node " << h.node << " = kv_ldc(PC, PCB, " << T.cell0 << " + " << u32(j * KV_LANES) << ");\n"
         << "  const uint32_t " << h.idx << " = " << h.node << ".kt == 0u ? ABSENT : node_type(" << h.node
         << ".kt) == NT_MAP ? " << h.node << ".c : 0u;\n";
       T.code.push_back(c.str());
@@ -1956,7 +1956,7 @@ struct Gen {
              << "      const uint32_t el" << tag << " = ni(ff" << tag << " + fli" << tag << ");\n";
         if (fam != kNoCol)  // the element's column-0 cell: element row fe + i of its family
           body << "      const uint32_t ec" << tag << " = fe" << tag << " + fli" << tag << " * (KVC_J" << fam
-               << " * " << u32(KV_LANES) << ") + ln_;\n      const Node eln" << tag << " = kv_ldn(PC, ec" << tag << ");\n";
+               << " * " << u32(KV_LANES) << ") + ln_;\n      const Node eln" << tag << " = kv_ldc(PC, PCB, ec" << tag << ");\n";
         else
           body << "      const Node eln" << tag << " = N[el" << tag << "];\n";
         body << T.flush() << bodies.str() << "    }\n";
@@ -2074,9 +2074,9 @@ struct Gen {
       << "  if (valid) { root = ni(kv_gld(&R->root, 0)); rkind = kv_gld(&R->kind, 0); rflags = kv_gld(&R->flags, 0); rtup = kv_gld(&R->tup, 0); }\n"
       << "  Node rootn{0u, 0u, 0u, 0u};\n";
     if (cols_on)  // path columns (kvdevtypes.h): cell offset of this lane's family-0 columns; column 0 = the root
-      o << "  const Node* __restrict__ PC = B.pcol;\n"
+      o << "  const uint32_t* __restrict__ PC = B.pcol;\n  const uint32_t* __restrict__ PCB = B.pcolb;\n"
         << "  const uint32_t ln_ = threadIdx.x & " << u32(KV_LANES - 1) << ", gc_ = (r >> 6) * (KVC_J0 * " << u32(KV_LANES)
-        << ") + ln_;\n  if (valid) rootn = kv_ldn(PC, gc_);\n";
+        << ") + ln_;\n  if (valid) rootn = kv_ldc(PC, PCB, gc_);\n";
     else
       o << "  if (valid) rootn = N[root];\n";
     o

@@ -820,10 +820,10 @@ __global__ __launch_bounds__(1024) void kv_pcol_scan_kernel(const ColFam* __rest
 __global__ __launch_bounds__(KV_WG) void kv_pcol_build_kernel(const DevBatch* __restrict__ Bp,
                                                               const ColDesc* __restrict__ cols,
                                                               const ColFam* __restrict__ fams, uint32_t j0,
-                                                              uint32_t c0, uint32_t elem, Node* __restrict__ pool) {
+                                                              uint32_t c0, uint32_t elem, uint32_t* __restrict__ pool, uint64_t cells) {
   const uint32_t r = blockIdx.x * KV_WG + threadIdx.x, c = c0 + blockIdx.y;
-  if (elem) col_build_elem(*Bp, cols, fams, j0, c, r, pool);
-  else col_build_root(*Bp, cols, fams, j0, c, r, pool);
+  if (elem) col_build_elem(*Bp, cols, fams, j0, c, r, pool, cells);
+  else col_build_root(*Bp, cols, fams, j0, c, r, pool, cells);
 }
 
 hipError_t launch_pcol_rows(const DevBatch* B, const ColDesc* cols, const ColFam* fams, uint32_t n_fam,
@@ -837,11 +837,12 @@ hipError_t launch_pcol_rows(const DevBatch* B, const ColDesc* cols, const ColFam
 }
 
 hipError_t launch_pcol_build(const DevBatch* B, const ColDesc* cols, const ColFam* fams, uint32_t j0, uint32_t c0,
-                             uint32_t n, uint32_t n_groups, bool elem, Node* pool, hipStream_t stream) {
+                             uint32_t n, uint32_t n_groups, bool elem, uint32_t* pool, uint64_t cells,
+                             hipStream_t stream) {
   if (n == 0 || n_groups == 0) return hipSuccess;
   if (n > 65535u) return hipErrorInvalidValue;
   hipLaunchKernelGGL(kv_pcol_build_kernel, dim3(n_groups * KV_LANES / KV_WG, n), dim3(KV_WG), 0, stream, B, cols, fams,
-                     j0, c0, elem ? 1u : 0u, pool);
+                     j0, c0, elem ? 1u : 0u, pool, cells);
   return hipGetLastError();
 }
 

@@ -39,7 +39,7 @@ thread_local kvemu_dim3 threadIdx, blockIdx, gridDim;
 extern "C" void kvemu_mtab(const DevPS* P, const DevBatch* B, uint32_t words, uint32_t max_entities, uint32_t* ns,
                            uint32_t* an, uint32_t* sl);
 
-std::vector<Node> kvemu_pcol(const DevBatch* B, const std::vector<ColDesc>& cols, const std::vector<uint32_t>& fam_arr,
+std::vector<uint32_t> kvemu_pcol(const DevBatch* B, const std::vector<ColDesc>& cols, const std::vector<uint32_t>& fam_arr,
                              const std::vector<uint32_t>& fam_ncols, std::vector<uint32_t>* erow);
 typedef void (*ptab_fn)(const DevPS*, const Val*, const uint8_t*, uint32_t, uint32_t*);
 extern "C" void kvemu_mfac(const DevPS* P, const DevBatch* B, uint32_t* mtup);
@@ -221,10 +221,11 @@ int main(int argc, char** argv) {
     B.dyn_st = dyn.dyn_st.data();
     // path columns of the image (as dev_batch: built once per batch)
     std::vector<uint32_t> pcol_erow;
-    std::vector<Node> pcol;
+    std::vector<uint32_t> pcol;  // two planes (kvcol.h col_put)
     if (!img.cols.empty() && B.n_res) {
       pcol = kvemu_pcol(&B, img.cols, img.fam_arr, img.fam_ncols, &pcol_erow);
       B.pcol = pcol.data();
+      B.pcolb = pcol.data() + pcol.size() / 4 * 3;
     }
     // match tables (as kv_session: one allocation, three [word][entity] tables)
     P.mt_ns_words = (ps.n_nss_bits + 31) / 32;

@@ -28,7 +28,7 @@ extern "C" void kvemu_mfac(const DevPS* P, const DevBatch* B, uint32_t* mtup) {
 // path columns (as build_pcol in kvapi.cpp, the kv_pcol_* kernels lane by lane): family 0,
 // the element rows of every wave group and family (max over the group's lanes, exclusive
 // prefix), the families' offsets, then the element columns; returns the pool
-std::vector<Node> kvemu_pcol(const DevBatch* B, const std::vector<ColDesc>& cols, const std::vector<uint32_t>& fam_arr,
+std::vector<uint32_t> kvemu_pcol(const DevBatch* B, const std::vector<ColDesc>& cols, const std::vector<uint32_t>& fam_arr,
                              const std::vector<uint32_t>& fam_ncols, std::vector<uint32_t>* erow) {
   const uint32_t nf = (uint32_t)fam_ncols.size(), j0 = fam_ncols.at(0);
   const uint32_t groups = (uint32_t)((B->n_res + KV_WG - 1) / KV_WG * (KV_WG / KV_LANES));
@@ -59,12 +59,14 @@ std::vector<Node> kvemu_pcol(const DevBatch* B, const std::vector<ColDesc>& cols
     cells += (uint64_t)fams[f].erow[groups] * fams[f].ncols * KV_LANES;
   }
   if (cells >= (1ull << 32)) throw std::runtime_error("kvemu: more than 2^32 column cells");
-  std::vector<Node> pool(std::max<uint64_t>(cells, 1), Node{0u, 0u, 0u, 0u});
+  // two planes: (kt, a, c) 12 B per cell, then b 4 B per cell
+  const uint64_t nc = std::max<uint64_t>(cells, 1);
+  std::vector<uint32_t> pool(4 * nc, 0u);
   for (uint32_t c = 0; c < cols.size(); c++)
     for (uint32_t r = 0; r < groups * KV_LANES; r++) {
       threadIdx.x = r % KV_WG;
-      if (c < j0) col_build_root(*B, cols.data(), fams.data(), j0, c, r, pool.data());
-      else col_build_elem(*B, cols.data(), fams.data(), j0, c, r, pool.data());
+      if (c < j0) col_build_root(*B, cols.data(), fams.data(), j0, c, r, pool.data(), nc);
+      else col_build_elem(*B, cols.data(), fams.data(), j0, c, r, pool.data(), nc);
     }
   return pool;
 }
