@@ -371,6 +371,13 @@ def main():
         dist.barrier()
     wall = te - ts
     kernel_ms = event_ms / args.steps
+    # The K timed passes re-validate the resident batch: pass i + 1's per-pass tables are built on a
+    # low-priority stream beside pass i's rule kernels (DESIGN.md §4 Streams). A caller validating
+    # each batch once runs one pass with its tables in order: single_pass_ms (median of 5, untimed
+    # for `value`).
+    single = sorted(sess.run(1) for _ in range(5))
+    single_ms = single[len(single) // 2]
+    status_written = sess.status_bytes() if args.mode == "full" else 0
     t_max = wall
     if dist is not None:
         import torch
@@ -400,7 +407,9 @@ def main():
     # the rare records that do not fit also write 32 B, not counted); scopes: the 4 B scope index of
     # every resource (the rule kernels count per scope inside the pass; the per-scope counts
     # themselves are KB-scale)
-    out_bytes = {"full": n_pairs_rank + 8 * n_fail // n_devs, "counts": 0,
+    # (full: the status bytes the pass wrote — a 256-resource segment of a rule whose statuses are all
+    # NOMATCH is not written but flagged, and filled at fetch; kv_session_status_bytes)
+    out_bytes = {"full": status_written // n_devs + 8 * n_fail // n_devs, "counts": 0,
                  "scopes": 4 * n_res_total // n_devs}[args.mode]
     b_alg = store_bytes // n_devs + prog_bytes + out_bytes  # per GPU (the slowest part's event time below)
     achieved = b_alg / (kernel_ms / 1e3) / 1e9
@@ -427,9 +436,13 @@ def main():
                                       else ")")) if inproc else f"resource-shard x{world}",
                    "engine": args.engine},
         "kernel_ms_per_step": kernel_ms,
+        "pipelined": True,
+        "single_pass_ms": single_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "bytes_per_launch": b_alg, "bytes_per_eval": b_alg / n_pairs_rank},
+                     "bytes_per_launch": b_alg, "bytes_per_eval": b_alg / n_pairs_rank,
+                     "output_bytes": out_bytes, "status_bytes_written": status_written // n_devs,
+                     "single_pass_frac": b_alg / (single_ms / 1e3) / 1e9 / HBM_PEAK_GBS},
         "status_counts": {n: int(counts[:, i].sum()) for i, n in enumerate(batch.STATUS_NAMES)},
     }
     if scopes is not None:

@@ -124,6 +124,14 @@ int kv_result_counts(const kv_result* r, const int64_t** counts);
  * a process's first batch and its first results find page-locked memory instead of pinning it
  * then. 0 on success, KV_E_DEVICE without a device or when the host refuses the memory. */
 int kv_host_reserve(uint64_t bytes);
+/* Device buffers released by batches, results and sessions are kept per device and handed to the
+ * next allocation of a similar size (a released buffer is reused only after the work queued before
+ * its release has finished). kv_device_pool_limit sets how many bytes are kept per device (default
+ * 32 GiB; 0 keeps none); kv_device_trim frees what device `device` keeps now, e.g. before another
+ * allocator in the process (torch) needs the memory. No reference counterpart (Go frees nothing
+ * on a device). 0 on success, KV_E_DEVICE for a bad device. */
+int kv_device_pool_limit(uint64_t bytes);
+int kv_device_trim(int device);
 /* phase i of the kv_validate that produced r: its name ("upload", "setup", "pass", "host_alloc",
  * "status_d2h", "records_count", "records_scatter_d2h", ...) and wall-clock milliseconds;
  * KV_E_RANGE past the last phase. Diagnostics of the host boundary (no reference counterpart). */
@@ -208,6 +216,11 @@ const char* kv_session_scope_name(const kv_session* s, uint32_t i);
  * logical parts of one device) and the HIP-event ms of each part's last kv_session_run */
 int kv_session_rccl_ranks(const kv_session* s, int* ranks);
 int kv_session_part_ms(const kv_session* s, double* ms /* [n_parts] */);
+/* status-matrix bytes the last pass wrote: the specialized kernels write a rule's statuses of a
+ * 256-resource workgroup only when one of them is not NOMATCH and flag the segment (an unwritten
+ * segment is filled with NOMATCH at fetch); the bytecode engine writes the whole matrix. The
+ * output bytes of a pass for the roofline accounting (no reference counterpart). */
+int kv_session_status_bytes(kv_session* s, uint64_t* bytes);
 
 /* Synthetic resource generator for the benchmark configs:
  * kind_mix 0 = Pods; 1 = Pods/Deployments/Services 60/25/15 (64 namespaces each);

@@ -74,6 +74,8 @@ def lib():
         L.kv_result_counts.argtypes = [vp, ctypes.POINTER(vp)]
         L.kv_result_phase.argtypes = [vp, u32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double)]
         L.kv_host_reserve.argtypes = [u64]
+        L.kv_device_pool_limit.argtypes = [u64]
+        L.kv_device_trim.argtypes = [i32]
         L.kv_result_path.argtypes = [vp, u32, u64, ctypes.c_char_p, sz]
         L.kv_result_error.argtypes = [vp, u32, u64, ctypes.POINTER(u32), ctypes.POINTER(u32)]
         L.kv_result_error_message.argtypes = [vp, u32, u64, ctypes.c_char_p, sz, ctypes.c_char_p, sz]
@@ -106,6 +108,7 @@ def lib():
         L.kv_session_scope_name.restype = ctypes.c_char_p
         L.kv_session_rccl_ranks.argtypes = [vp, ctypes.POINTER(i32)]
         L.kv_session_part_ms.argtypes = [vp, vp]
+        L.kv_session_status_bytes.argtypes = [vp, ctypes.POINTER(u64)]
         for fn in ("kv_free_policyset", "kv_free_batch", "kv_free_result", "kv_free_buffer", "kv_free_session"):
             getattr(L, fn).argtypes = [vp]
             getattr(L, fn).restype = None
@@ -118,14 +121,14 @@ def lib():
 EXPORTED_SYMBOLS = [
     "kv_compile", "kv_policyset_info", "kv_policyset_jit_info", "kv_rule_info_get", "kv_ingest", "kv_batch_info", "kv_validate",
     "kv_result_status", "kv_result_counts", "kv_result_path", "kv_result_error", "kv_result_error_message",
-    "kv_result_subst_error", "kv_result_phase", "kv_host_reserve",
+    "kv_result_subst_error", "kv_result_phase", "kv_host_reserve", "kv_device_pool_limit", "kv_device_trim",
     "kv_result_kernel_ms",
     "kv_bench", "kv_synth", "kv_synth_range", "kv_free_policyset", "kv_free_batch", "kv_free_result", "kv_free_error",
     "kv_free_buffer", "kv_session_create", "kv_session_run", "kv_session_counts", "kv_free_session",
     "kv_session_scope_counts", "kv_result_scope_counts", "kv_batch_namespaces", "kv_batch_namespace",
     "kv_validate_devices", "kv_session_create_devices", "kv_session_parts", "kv_session_fetch", "kv_result_failures",
     "kv_path_string", "kv_session_create_parts", "kv_session_attach_part", "kv_session_scopes", "kv_session_scope_name",
-    "kv_session_rccl_ranks", "kv_session_part_ms",
+    "kv_session_rccl_ranks", "kv_session_part_ms", "kv_session_status_bytes",
 ]
 
 

@@ -343,6 +343,13 @@ class Session:
             raise _native.KvError(-3, "kv_session_rccl_ranks failed")
         return n.value
 
+    def status_bytes(self) -> int:
+        """Status-matrix bytes the last run()'s pass wrote (unwritten segments are all NOMATCH)."""
+        n = ctypes.c_uint64()
+        if lib().kv_session_status_bytes(self._h, ctypes.byref(n)) != 0:
+            raise _native.KvError(-3, "kv_session_status_bytes failed")
+        return n.value
+
     def part_ms(self) -> list[float]:
         """HIP-event milliseconds of each part's last run()."""
         out = np.zeros(self.n_parts, dtype=np.float64)

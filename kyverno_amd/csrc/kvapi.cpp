@@ -41,17 +41,84 @@ struct HipError : std::runtime_error {
 
 bool pinned_src(const void* src, size_t bytes);  // page-locked store array (PinnedStore)
 
+// HIP streams cost milliseconds to create and to destroy on this runtime (hipStreamCreate* 2.3-3.8
+// ms, hipStreamDestroy 1.8-2.6 ms per call in the rocprofv3 HIP API trace of a C2 kv_validate: 15 of
+// its 44 ms), so sessions and staged uploads take idle streams from a per-(device, flags) pool and
+// give them back instead. The pool also knows every stream it ever created per device (`all`): a
+// released device buffer becomes reusable once an event recorded on each of them has completed
+// (DevPool below).
+struct StreamPool {
+  std::mutex mu;
+  std::map<std::tuple<int, unsigned, int>, std::vector<hipStream_t>> free;
+  std::map<int, std::vector<hipStream_t>> all;
+  static StreamPool& get() {
+    static StreamPool* p = new StreamPool();  // never destroyed (streams die with the process)
+    return *p;
+  }
+  std::vector<hipStream_t> streams_of(int dev) {
+    std::lock_guard<std::mutex> g(mu);
+    return all[dev];
+  }
+  // a stream of the current device `dev`; low: the lowest scheduling priority (its workgroups are
+  // dispatched when the other queues' kernels leave slots free)
+  hipStream_t take(int dev, unsigned flags, bool low = false) {
+    const int prio = low ? lowest() : 0;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      auto& v = free[{dev, flags, prio}];
+      if (!v.empty()) {
+        hipStream_t s = v.back();
+        v.pop_back();
+        return s;
+      }
+    }
+    hipStream_t s = nullptr;
+    if (low) HIPCHK(hipStreamCreateWithPriority(&s, flags, prio));
+    else HIPCHK(hipStreamCreateWithFlags(&s, flags));
+    std::lock_guard<std::mutex> g(mu);
+    all[dev].push_back(s);
+    return s;
+  }
+  void give(int dev, unsigned flags, hipStream_t s, bool low = false) {
+    if (!s) return;
+    (void)hipStreamSynchronize(s);
+    const int prio = low ? lowest() : 0;
+    std::lock_guard<std::mutex> g(mu);
+    free[{dev, flags, prio}].push_back(s);
+  }
+  static int lowest() {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) {
+      (void)hipGetLastError();
+      return 0;
+    }
+    return least;
+  }
+};
+
 // Device allocations are expensive to create and to free (hipMalloc maps pages, hipFree also
 // waits for the device), and a host that validates batch after batch allocates the same store,
-// column and result buffers for every batch. Released buffers are therefore kept per device (up
-// to 64 GiB of the 288 GiB HBM) and handed to the next allocation of a similar size; when a
-// hipMalloc fails, the device's kept buffers are freed and the allocation is retried.
+// column and result buffers for every batch. Released buffers are therefore kept per device and
+// handed to the next allocation of a similar size. A released block is reusable once the work
+// queued before its release has finished (hipFree's own guarantee, without blocking the releasing
+// thread or any other session on the device): give() records an event on every stream the library
+// created on the device and on the null stream, and take() hands the block out only when all of
+// them have completed. At most kv_device_pool_limit() bytes are kept (default 32 GiB of the 288 GiB
+// HBM); when a hipMalloc fails the device's kept buffers are freed and the allocation retried, and
+// kv_device_trim() returns them to the device for co-resident allocators (e.g. torch).
 // KVGPU_DEVPOOL=0: plain hipMalloc / hipFree.
 struct DevPool {
+  struct Pending {
+    void* p;
+    size_t cap;
+    std::vector<hipEvent_t> ev;
+  };
   std::mutex mu;
   std::map<int, std::multimap<size_t, void*>> free;  // device -> capacity -> block
-  std::map<int, size_t> held;
-  static constexpr size_t kHold = 64ull << 30;
+  std::map<int, std::vector<Pending>> pending;        // released, maybe still in use by queued work
+  std::map<int, size_t> held;                         // free + pending bytes
+  std::map<int, std::vector<hipEvent_t>> evs;         // idle events per device
+  size_t hold = 32ull << 30;
   static DevPool& get() {
     static DevPool* p = new DevPool();  // never destroyed: buffers may be released during static teardown
     return *p;
@@ -60,10 +127,34 @@ struct DevPool {
     static const bool on = !(getenv("KVGPU_DEVPOOL") && getenv("KVGPU_DEVPOOL")[0] == '0');
     return on;
   }
+  // (mu held) pending blocks whose events have all completed move to the free list
+  void settle(int dev) {
+    auto& pv = pending[dev];
+    for (size_t i = 0; i < pv.size();) {
+      bool done = true;
+      for (hipEvent_t e : pv[i].ev) {
+        const hipError_t q = hipEventQuery(e);
+        if (q == hipErrorNotReady) {
+          done = false;
+          break;
+        }
+        if (q != hipSuccess) (void)hipGetLastError();
+      }
+      if (!done) {
+        i++;
+        continue;
+      }
+      for (hipEvent_t e : pv[i].ev) evs[dev].push_back(e);
+      free[dev].emplace(pv[i].cap, pv[i].p);
+      pv[i] = std::move(pv.back());
+      pv.pop_back();
+    }
+  }
   // a block of at least `bytes` on the current device `dev` (its capacity in *cap)
   void* take(int dev, size_t bytes, size_t* cap) {
     if (enabled()) {
       std::lock_guard<std::mutex> g(mu);
+      settle(dev);
       auto& f = free[dev];
       auto it = f.lower_bound(bytes);
       if (it != f.end() && it->first <= bytes + bytes / 4 + (2u << 20)) {
@@ -83,78 +174,66 @@ struct DevPool {
     *cap = bytes;
     return p;
   }
-  // the block goes back once the device is idle (hipFree's own semantics: no kernel or copy
-  // still using it can see it handed out again)
+  // `dev` is the current device
   void give(int dev, void* p, size_t cap) {
-    (void)hipDeviceSynchronize();
     if (enabled()) {
+      std::vector<hipStream_t> st = StreamPool::get().streams_of(dev);
+      st.push_back(nullptr);  // (the null stream: synchronous copies, RCCL setup)
       std::lock_guard<std::mutex> g(mu);
-      if (held[dev] + cap <= kHold) {
-        free[dev].emplace(cap, p);
-        held[dev] += cap;
-        return;
+      if (held[dev] + cap <= hold) {
+        Pending pe{p, cap, {}};
+        bool ok = true;
+        for (hipStream_t s : st) {
+          hipEvent_t e = nullptr;
+          auto& idle = evs[dev];
+          if (!idle.empty()) {
+            e = idle.back();
+            idle.pop_back();
+          } else if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            ok = false;
+            break;
+          }
+          pe.ev.push_back(e);
+          if (hipEventRecord(e, s) != hipSuccess) {
+            (void)hipGetLastError();
+            ok = false;
+            break;
+          }
+        }
+        if (ok) {
+          pending[dev].push_back(std::move(pe));
+          held[dev] += cap;
+          return;
+        }
+        for (hipEvent_t e : pe.ev) evs[dev].push_back(e);
       }
     }
+    (void)hipDeviceSynchronize();  // (hipFree waits for the device anyway)
     (void)hipFree(p);
   }
   size_t held_on(int dev) {
     std::lock_guard<std::mutex> g(mu);
     return held[dev];
   }
+  // free every kept block of `dev` (the current device): waits for the device first
   void trim(int dev) {
     std::multimap<size_t, void*> f;
+    std::vector<Pending> pv;
     {
       std::lock_guard<std::mutex> g(mu);
       f.swap(free[dev]);
+      pv.swap(pending[dev]);
       held[dev] = 0;
     }
+    if (f.empty() && pv.empty()) return;
+    (void)hipDeviceSynchronize();
     for (auto& [c, p] : f) (void)hipFree(p);
-  }
-};
-
-// HIP streams cost milliseconds to create and to destroy on this runtime (hipStreamCreate* 2.3-3.8
-// ms, hipStreamDestroy 1.8-2.6 ms per call in the rocprofv3 HIP API trace of a C2 kv_validate: 15 of
-// its 44 ms), so sessions and staged uploads take idle streams from a per-(device, flags) pool and
-// give them back instead.
-struct StreamPool {
-  std::mutex mu;
-  std::map<std::tuple<int, unsigned, int>, std::vector<hipStream_t>> free;
-  static StreamPool& get() {
-    static StreamPool* p = new StreamPool();  // never destroyed (streams die with the process)
-    return *p;
-  }
-  // a stream of the current device `dev`; low: the lowest scheduling priority (its workgroups are
-  // dispatched when the other queues' kernels leave slots free)
-  hipStream_t take(int dev, unsigned flags, bool low = false) {
-    const int prio = low ? lowest() : 0;
-    {
-      std::lock_guard<std::mutex> g(mu);
-      auto& v = free[{dev, flags, prio}];
-      if (!v.empty()) {
-        hipStream_t s = v.back();
-        v.pop_back();
-        return s;
-      }
-    }
-    hipStream_t s = nullptr;
-    if (low) HIPCHK(hipStreamCreateWithPriority(&s, flags, prio));
-    else HIPCHK(hipStreamCreateWithFlags(&s, flags));
-    return s;
-  }
-  void give(int dev, unsigned flags, hipStream_t s, bool low = false) {
-    if (!s) return;
-    (void)hipStreamSynchronize(s);
-    const int prio = low ? lowest() : 0;
     std::lock_guard<std::mutex> g(mu);
-    free[{dev, flags, prio}].push_back(s);
-  }
-  static int lowest() {
-    int least = 0, greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) {
-      (void)hipGetLastError();
-      return 0;
+    for (Pending& pe : pv) {
+      (void)hipFree(pe.p);
+      for (hipEvent_t e : pe.ev) evs[dev].push_back(e);
     }
-    return least;
   }
 };
 
@@ -1360,6 +1439,9 @@ struct DevSession {
         if (O.full & 8u)
           HIPCHK(launch_scope_totals((const unsigned long long*)(b ? scn1.p : scn.p), nscopes, (uint32_t)nrules,
                                      (unsigned long long*)(b ? cn1.p : cn.p), stream));
+        // set b's last readers (rule kernels) and writers (scope totals) are done after this event:
+        // launch_tables(b) of pass i + 2 zeroes its counts behind it
+        HIPCHK(hipEventRecord(ev_rk[b], stream));
         if (i + 1 < iters) {  // the next pass's tables, once pass i - 1's kernels are done with them
           const int nb = (i + 1) & 1;
           if (i >= 1) HIPCHK(hipStreamWaitEvent(pside, ev_rk[nb], 0));
@@ -1492,7 +1574,21 @@ struct DevSession {
     uint32_t r0 = 0;
     void* args[] = {(void*)&P, (void*)&bview, (void*)&N, (void*)&V, (void*)&S, (void*)&Ov, (void*)&r0};
     for (hipFunction_t f : dps->fns) HIPCHK(hipModuleLaunchKernel(f, blocks, 1, 1, KV_WG, 1, 1, 0, stream, args, nullptr));
-    if (pb >= 0) HIPCHK(hipEventRecord(ev_rk[pb], stream));
+  }
+  // status-matrix bytes the last pass wrote: the (rule, workgroup) segments whose flag it set (a
+  // segment left unwritten is all NOMATCH and filled at fetch), or the whole matrix without flags
+  uint64_t written_status_bytes() {
+    if (!O.status) return 0;
+    if (!O.sflag || !dps->specialized()) return nrules * nres;
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamSynchronize(stream));
+    std::vector<uint8_t> f(sflag.n);
+    if (!f.empty()) HIPCHK(hipMemcpy(f.data(), sflag.p, f.size(), hipMemcpyDeviceToHost));
+    const uint64_t nwg = (nres + KV_WG - 1) / KV_WG, last = nres - (nwg - 1) * KV_WG;
+    uint64_t bytes = 0;
+    for (uint64_t i = 0; i < nrules * nwg && i < f.size(); i++)
+      if (f[i]) bytes += (i % nwg == nwg - 1) ? last : KV_WG;
+    return bytes;
   }
   std::vector<int64_t> read_counts() {
     HIPCHK(hipSetDevice(device));
@@ -1960,6 +2056,12 @@ int kv_compile(const char* policies_json, size_t len, uint32_t flags, kv_policys
             throw std::runtime_error("kvjit: the register plan did not settle (kernels still spill after 64 re-plans)");
           s->jit->compile_ms = ms;
           jit_save_plan(pkey, *s->jit);
+          if (const char* dump = getenv("KVGPU_JIT_DUMP")) {  // (the source of the final plan)
+            if (FILE* f = fopen(dump, "w")) {
+              fwrite(s->jit->source.data(), 1, s->jit->source.size(), f);
+              fclose(f);
+            }
+          }
         }
         if (const char* dump = getenv("KVGPU_JIT_DUMP_CO")) {  // gfx950 code objects (llvm-objdump / readelf)
           for (size_t i = 0; i < s->jit->codes.size(); i++) {
@@ -2122,6 +2224,28 @@ int kv_host_reserve(uint64_t bytes) {
   } catch (const std::exception&) {
     return KV_E_DEVICE;
   }
+}
+
+int kv_device_pool_limit(uint64_t bytes) {
+  DevPool& p = DevPool::get();
+  std::lock_guard<std::mutex> g(p.mu);
+  p.hold = (size_t)bytes;
+  return 0;
+}
+
+int kv_device_trim(int device) {
+  int n = 0, cur = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n || hipGetDevice(&cur) != hipSuccess) {
+    (void)hipGetLastError();
+    return KV_E_DEVICE;
+  }
+  if (hipSetDevice(device) != hipSuccess) {
+    (void)hipGetLastError();
+    return KV_E_DEVICE;
+  }
+  DevPool::get().trim(device);
+  (void)hipSetDevice(cur);
+  return 0;
 }
 
 int kv_result_phase(const kv_result* r, uint32_t i, const char** name, double* ms) {
@@ -2457,6 +2581,19 @@ int kv_session_rccl_ranks(const kv_session* s, int* ranks) {
   if (!s || !ranks) return KV_E_INVALID;
   *ranks = s->set.rccl_ranks();
   return *ranks < 0 ? KV_E_DEVICE : 0;
+}
+
+int kv_session_status_bytes(kv_session* s, uint64_t* bytes) {
+  if (!s || !bytes) return KV_E_INVALID;
+  try {
+    uint64_t t = 0;
+    for (auto& p : s->set.parts)
+      if (p) t += p->written_status_bytes();
+    *bytes = t;
+    return 0;
+  } catch (const std::exception&) {
+    return KV_E_DEVICE;
+  }
 }
 
 int kv_session_part_ms(const kv_session* s, double* ms) {

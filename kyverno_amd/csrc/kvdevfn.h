@@ -71,7 +71,8 @@ __device__ __forceinline__ Node kv_ldn(const Node* p, size_t i) {
 // only array cells need (a caller that never reads .b leaves it dead)
 __device__ __forceinline__ Node kv_ldc(const uint32_t* pa, const uint32_t* pb, size_t i) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  typedef uint32_t u32x3_ __attribute__((ext_vector_type(3)));
+  // (a 12-byte cell is 4-byte aligned: the type says so, gfx950 loads it as one dwordx3)
+  typedef uint32_t u32x3_ __attribute__((ext_vector_type(3), aligned(4)));
   const u32x3_ x = *(const __attribute__((address_space(1))) u32x3_*)((const __attribute__((address_space(1))) char*)pa + 12u * i);
   const uint32_t y = ((const __attribute__((address_space(1))) uint32_t*)pb)[i];
   return Node{x.x, x.y, y, x.z};

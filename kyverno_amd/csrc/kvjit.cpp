@@ -2044,6 +2044,9 @@ struct Gen {
     mt_bits.insert(mt_bits.end(), rules.begin(), rules.end());
     while (mt_bits.size() % 32u) mt_bits.push_back(0xFFFFFFFFu);
     const uint32_t nr = (uint32_t)rules.size();
+    // a wave's lane l zeroes / writes the site-record counters of the kernel's group l (groups have
+    // 2+ members and a kernel at most KV_KROWS rules: at most 64 groups)
+    if (k_gsn > 64u) throw std::runtime_error("kvjit: more than 64 site-record groups in one kernel");
     KernelText kt(*this, name);
     o << block_decls;
     if (getenv("KVGPU_JIT_STAMPS")) o << "__device__ unsigned long long* kvj_stamps;\n";

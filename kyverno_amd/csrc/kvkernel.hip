@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "kvdev.h"
 
 using namespace kv;
@@ -585,14 +587,16 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_scatter_kernel(const uint8_t* __
   if (e.w0 & ERR8_WIDE) atomicOr(wide, 1u);
 }
 
+constexpr uint32_t kMaxGridY = 65535u;
+
 // Site records -> the members' ErrRec8 at their [rule][res] slots (kvdevtypes.h GSiteDesc): one
 // wave per (group, wave of resources), lane k handles records k, k + 64, ... of the segment.
 __global__ __launch_bounds__(KV_WG) void kv_gsite_expand_kernel(const uint4* __restrict__ gsite,
                                                                  const uint32_t* __restrict__ gcnt,
                                                                  const GSiteDesc* __restrict__ desc,
                                                                  const uint32_t* __restrict__ mem, uint32_t n_res,
-                                                                 ErrRec8* __restrict__ err8) {
-  const uint32_t nw = (n_res + 63u) >> 6, w = blockIdx.x * (KV_WG / 64) + (threadIdx.x >> 6), g = blockIdx.y;
+                                                                 ErrRec8* __restrict__ err8, uint32_t g0) {
+  const uint32_t nw = (n_res + 63u) >> 6, w = blockIdx.x * (KV_WG / 64) + (threadIdx.x >> 6), g = g0 + blockIdx.y;
   if (w >= nw) return;
   const GSiteDesc d = desc[g];
   const uint32_t cnt = gcnt[(size_t)g * nw + w];
@@ -618,18 +622,21 @@ hipError_t launch_gsite_expand(const uint32_t* gsite, const uint32_t* gcnt, cons
                                uint32_t n_groups, uint32_t n_res, ErrRec8* err8, hipStream_t stream) {
   if (n_res == 0 || n_groups == 0) return hipSuccess;
   const uint32_t nw = (n_res + 63u) >> 6;
-  hipLaunchKernelGGL(kv_gsite_expand_kernel, dim3((nw + KV_WG / 64 - 1) / (KV_WG / 64), n_groups), dim3(KV_WG), 0, stream,
-                     (const uint4*)gsite, gcnt, desc, mem, n_res, err8);
-  return hipGetLastError();
+  for (uint32_t g0 = 0; g0 < n_groups; g0 += kMaxGridY) {  // (grid y holds at most 65535 groups)
+    hipLaunchKernelGGL(kv_gsite_expand_kernel, dim3((nw + KV_WG / 64 - 1) / (KV_WG / 64), std::min(kMaxGridY, n_groups - g0)),
+                       dim3(KV_WG), 0, stream, (const uint4*)gsite, gcnt, desc, mem, n_res, err8, g0);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 // NOMATCH into the status segments the specialized kernels left unwritten (DevOut::sflag): one
 // wave per (workgroup segment, rule), 16 B per lane of the first 16 lanes
 __global__ __launch_bounds__(KV_WG) void kv_status_fill_kernel(uint8_t* __restrict__ status,
                                                                 const uint8_t* __restrict__ sflag, uint32_t n_res,
-                                                                uint32_t n_rules) {
+                                                                uint32_t n_rules, uint32_t rule0) {
   const uint32_t nwg = (n_res + KV_WG - 1) / KV_WG, g = blockIdx.x * (KV_WG / 64) + (threadIdx.x >> 6);
-  const uint32_t rule = blockIdx.y, l = threadIdx.x & 63u;
+  const uint32_t rule = rule0 + blockIdx.y, l = threadIdx.x & 63u;
   if (g >= nwg || l >= 16u || sflag[(size_t)rule * nwg + g]) return;
   const uint32_t nm = 0x01010101u * (uint32_t)ST_NOMATCH;
   // (an unwritten segment is a whole workgroup: n_res % 16 == 0 and the segment inside the batch)
@@ -640,9 +647,12 @@ hipError_t launch_status_fill(uint8_t* status, const uint8_t* sflag, uint32_t n_
                               hipStream_t stream) {
   if (n_res == 0 || n_rules == 0) return hipSuccess;
   const uint32_t nwg = (n_res + KV_WG - 1) / KV_WG;
-  hipLaunchKernelGGL(kv_status_fill_kernel, dim3((nwg + KV_WG / 64 - 1) / (KV_WG / 64), n_rules), dim3(KV_WG), 0, stream,
-                     status, sflag, n_res, n_rules);
-  return hipGetLastError();
+  for (uint32_t q0 = 0; q0 < n_rules; q0 += kMaxGridY) {  // (grid y holds at most 65535 rules)
+    hipLaunchKernelGGL(kv_status_fill_kernel, dim3((nwg + KV_WG / 64 - 1) / (KV_WG / 64), std::min(kMaxGridY, n_rules - q0)),
+                       dim3(KV_WG), 0, stream, status, sflag, n_res, n_rules, q0);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const ErrRec* errw, uint32_t n_res,
