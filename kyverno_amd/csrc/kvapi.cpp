@@ -354,6 +354,13 @@ struct DevPolicySet {
   // function per rule chunk
   std::vector<hipModule_t> mods;
   std::vector<hipFunction_t> fns;
+  // output-mode variants (JitImage::variants): DevOut::full value -> a function per rule kernel
+  // (the variant where it compiled within the plan's registers, else the generic kernel)
+  std::map<uint32_t, std::vector<hipFunction_t>> vfns;
+  const std::vector<hipFunction_t>& fns_for(uint32_t full) const {
+    auto it = vfns.find(full);
+    return it == vfns.end() ? fns : it->second;
+  }
   hipFunction_t ptab_fn = nullptr;  // value-predicate table builder (kvj_ptab)
   uint32_t mtup_words = 0;          // match words per tuple (kv_mfac + kv_mtup, factored match)
   uint32_t fac_slots = 0;
@@ -806,6 +813,23 @@ DevPolicySet& dev_ps(kv_policyset* s, int device) {
       hipFunction_t f;
       HIPCHK(hipModuleGetFunction(&f, m, J.kernel_name[i].c_str()));
       byname[J.kernel_name[i]] = f;
+    }
+    for (const JitImage::Variant& v : J.variants) {
+      std::map<std::string, hipFunction_t> vname;
+      for (size_t i = 0; i < v.codes.size() && i < J.kernel_name.size(); i++) {
+        if (v.codes[i].empty()) continue;
+        hipModule_t m;
+        HIPCHK(hipModuleLoadData(&m, v.codes[i].data()));
+        d->mods.push_back(m);
+        hipFunction_t f;
+        HIPCHK(hipModuleGetFunction(&f, m, J.kernel_name[i].c_str()));
+        vname[J.kernel_name[i]] = f;
+      }
+      std::vector<hipFunction_t>& fv = d->vfns[v.full];
+      for (auto& ch : J.chunks) {
+        auto it = vname.find(ch.name);
+        fv.push_back(it != vname.end() ? it->second : byname.at(ch.name));
+      }
     }
     for (auto& ch : J.chunks) {
       auto it = byname.find(ch.name);
@@ -1327,8 +1351,8 @@ struct DevSession {
       st.alloc(nrules * nres, device);
       O.status = (uint8_t*)st.p;
       O.full |= 1;
-      if (dp.specialized() && !getenv("KVGPU_NO_SFLAG")) {  // (flags of every segment, set by each pass)
-        sflag.alloc(std::max<uint64_t>(nrules * ((nres + KV_WG - 1) / KV_WG), 1), device);
+      if (dp.specialized()) {  // (flags of every segment, set by each pass)
+        sflag.alloc(std::max<uint64_t>(nrules * ((nres + KV_RWG - 1) / KV_RWG), 1), device);
         HIPCHK(hipMemset(sflag.p, 1, sflag.n));
         O.sflag = (uint8_t*)sflag.p;
       }
@@ -1362,7 +1386,7 @@ struct DevSession {
       if (dp.specialized()) O.full |= 8;
     }
     if (getenv("KVGPU_JIT_STAMPS") && dp.specialized()) {  // diagnostics: segment stamps of the rule kernels' waves
-      const uint64_t n = (nres + KV_WG - 1) / KV_WG * (KV_WG / 64) * kJitStamps;
+      const uint64_t n = (nres + KV_RWG - 1) / KV_RWG * KV_RWAVES * kJitStamps;
       stamps.alloc(std::max<uint64_t>(n, 1) * sizeof(unsigned long long), device);
       HIPCHK(hipMemset(stamps.p, 0, stamps.n));
       for (hipModule_t m : dp.mods) {  // the kernels' global kvj_stamps -> this buffer
@@ -1379,7 +1403,7 @@ struct DevSession {
     HIPCHK(hipEventCreate(&e1));
     side = StreamPool::get().take(device, hipStreamNonBlocking);
     if (ptab_pipe) {
-      pside = StreamPool::get().take(device, hipStreamNonBlocking, !(getenv("KVGPU_PIPE_PRIO") && getenv("KVGPU_PIPE_PRIO")[0] == '0'));
+      pside = StreamPool::get().take(device, hipStreamNonBlocking, true);  // (the lowest priority)
       for (int b = 0; b < 2; b++) {
         HIPCHK(hipEventCreateWithFlags(&ev_pt[b], hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ev_rk[b], hipEventDisableTiming));
@@ -1416,7 +1440,7 @@ struct DevSession {
       if (ev_pt[b]) (void)hipEventDestroy(ev_pt[b]);
       if (ev_rk[b]) (void)hipEventDestroy(ev_rk[b]);
     }
-    StreamPool::get().give(device, hipStreamNonBlocking, pside, !(getenv("KVGPU_PIPE_PRIO") && getenv("KVGPU_PIPE_PRIO")[0] == '0'));
+    StreamPool::get().give(device, hipStreamNonBlocking, pside, true);
     StreamPool::get().give(device, hipStreamNonBlocking, side);
     StreamPool::get().give(device, hipStreamDefault, stream);
   }
@@ -1546,7 +1570,7 @@ struct DevSession {
       HIPCHK(hipStreamWaitEvent(stream, ev_join, 0));
       return;
     }
-    const uint32_t blocks = (uint32_t)((nres + KV_WG - 1) / KV_WG);
+    const uint32_t blocks = (uint32_t)((nres + KV_RWG - 1) / KV_RWG);
     const DevPS* P = (const DevPS*)(pb == 1 ? pview1.p : pview.p);
     const Node* N = bhost->nodes;
     const Val* V = bhost->vals;
@@ -1573,7 +1597,8 @@ struct DevSession {
     }
     uint32_t r0 = 0;
     void* args[] = {(void*)&P, (void*)&bview, (void*)&N, (void*)&V, (void*)&S, (void*)&Ov, (void*)&r0};
-    for (hipFunction_t f : dps->fns) HIPCHK(hipModuleLaunchKernel(f, blocks, 1, 1, KV_WG, 1, 1, 0, stream, args, nullptr));
+    for (hipFunction_t f : dps->fns_for(Ov.full))
+      HIPCHK(hipModuleLaunchKernel(f, blocks, 1, 1, KV_RWG, 1, 1, 0, stream, args, nullptr));
   }
   // status-matrix bytes the last pass wrote: the (rule, workgroup) segments whose flag it set (a
   // segment left unwritten is all NOMATCH and filled at fetch), or the whole matrix without flags
@@ -1584,10 +1609,10 @@ struct DevSession {
     HIPCHK(hipStreamSynchronize(stream));
     std::vector<uint8_t> f(sflag.n);
     if (!f.empty()) HIPCHK(hipMemcpy(f.data(), sflag.p, f.size(), hipMemcpyDeviceToHost));
-    const uint64_t nwg = (nres + KV_WG - 1) / KV_WG, last = nres - (nwg - 1) * KV_WG;
+    const uint64_t nwg = (nres + KV_RWG - 1) / KV_RWG, last = nres - (nwg - 1) * KV_RWG;
     uint64_t bytes = 0;
     for (uint64_t i = 0; i < nrules * nwg && i < f.size(); i++)
-      if (f[i]) bytes += (i % nwg == nwg - 1) ? last : KV_WG;
+      if (f[i]) bytes += (i % nwg == nwg - 1) ? last : KV_RWG;
     return bytes;
   }
   std::vector<int64_t> read_counts() {
@@ -2054,6 +2079,9 @@ int kv_compile(const char* policies_json, size_t len, uint32_t flags, kv_policys
           }
           if (!settled)
             throw std::runtime_error("kvjit: the register plan did not settle (kernels still spill after 64 re-plans)");
+          const double c0 = s->jit->compile_ms;
+          jit_compile_variants(s->jit.get());  // (output-mode variants of the final kernels)
+          ms += s->jit->compile_ms - c0;
           s->jit->compile_ms = ms;
           jit_save_plan(pkey, *s->jit);
           if (const char* dump = getenv("KVGPU_JIT_DUMP")) {  // (the source of the final plan)
@@ -2070,6 +2098,15 @@ int kv_compile(const char* policies_json, size_t len, uint32_t flags, kv_policys
               fclose(f);
             }
           }
+          for (const JitImage::Variant& v : s->jit->variants)  // (output-mode variants: <name>.m<full>)
+            for (size_t i = 0; i < v.codes.size(); i++) {
+              if (v.codes[i].empty()) continue;
+              const std::string fn = std::string(dump) + "." + s->jit->kernel_name[i] + ".m" + std::to_string(v.full) + ".co";
+              if (FILE* f = fopen(fn.c_str(), "wb")) {
+                fwrite(v.codes[i].data(), 1, v.codes[i].size(), f);
+                fclose(f);
+              }
+            }
         }
       }
     } catch (...) {

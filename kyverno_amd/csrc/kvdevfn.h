@@ -52,6 +52,15 @@ __device__ __forceinline__ T kv_gld(const T* p, size_t i) {
 #endif
 }
 
+// Output mode of the launch (DevOut::full): a rule-kernel program compiled for one mode
+// (kvjit.cpp output-mode variants, KVJ_FULL) has it as a constant, so the code of outputs its
+// launches never write (records in SCOPES mode, the status copy in COUNTS mode) is not there
+#ifdef KVJ_FULL
+#define KV_OFULL(O) ((uint32_t)(KVJ_FULL))
+#else
+#define KV_OFULL(O) ((O).full)
+#endif
+
 // A node through a global-address-space pointer (kv_gld for a struct: the copy goes through a
 // native vector, the fields the caller reads are the ones loaded). The path columns (DevBatch::
 // pcol) are read this way: through the generic pointer they compiled to flat loads (C2: 100 of
@@ -680,7 +689,7 @@ struct EState {
 
 // error record of a FAIL / ERROR / SKIP pair (kvdevtypes.h ErrRec8): the 8 B
 // compact form, flagged `wide` when the indices / key do not fit. Passes with
-// O.full bit 2 (re-run by the host only when some record was wide) write the
+// KV_OFULL(O) bit 2 (re-run by the host only when some record was wide) write the
 // full 32 B form instead; the flag is uniform, so this is a scalar branch.
 // compact record words (kvdevtypes.h ErrRec8) of an error at loop indices i0..i3 on the
 // resource of lane r % 64; `wide` when they do not fit
@@ -702,9 +711,9 @@ __device__ __forceinline__ void store_err(const DevOut& O, uint32_t ri, uint32_t
   // specialized kernels write compact records only: the host re-runs a pass that needs full
   // records on the bytecode engine (kvapi.cpp DevSession::fetch), which keeps the code of
   // every record site of these kernels small
-  if (O.full & 4) return;
+  if (KV_OFULL(O) & 4) return;
 #else
-  if (O.full & 4) {
+  if (KV_OFULL(O) & 4) {
     uint4* x = (uint4*)(O.err + (size_t)ri * n_res) + 2u * r;
     x[0] = make_uint4(kind | (flags << 16), pn, key, res);
     x[1] = make_uint4(i0, i1, i2, i3);
@@ -733,6 +742,9 @@ __device__ __forceinline__ uint32_t kv_ptab_col(const DevPS& P, uint32_t type, u
 // for an empty array)
 __device__ __forceinline__ uint32_t kv_leaf_word(const DevPS& P, const Node* __restrict__ N, const Node& n, uint32_t w) {
   const uint32_t t = node_type(n.kt);
+#ifdef KV_DIAG_XPTAB
+  if (t != NT_ARR) return (n.a * 0x9E3779B9u) ^ (w * 0x85EBCA6Bu);  // (diagnostics: no table read)
+#endif
   if (t != NT_ARR) return kv_gld(P.ptab, (size_t)w * P.n_vals + kv_ptab_col(P, t, n.a));
   uint32_t x = 0xFFFFFFFFu;
   for (uint32_t k = 0; k < n.b; k++) {
@@ -746,6 +758,24 @@ __device__ __forceinline__ uint32_t kv_leaf_word(const DevPS& P, const Node* __r
 // (slot < 64: a rule ends once per lane)
 __device__ __forceinline__ void kv_rec_put(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, uint32_t slot,
                                            const EState& e, uint32_t z) {
+#ifdef KV_DIAG_NORECST
+  asm volatile("" ::"v"(slot));
+  return;
+#endif
+#ifdef KV_DIAG_RECADDR
+  // (diagnostics: the record stored at a per-lane address with no rule / segment term)
+  ((uint2*)O.err8)[(threadIdx.x & 63u) + (slot & 63u)] = err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, r);
+  return;
+#endif
+#ifdef KV_DIAG_RECLDS
+  {  // (diagnostics: the record's address and payload formed, written to LDS instead of memory)
+    __shared__ uint32_t kv_sink_[64];
+    const uint2 w = err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, r);
+    const uint2* a = (uint2*)(O.err8 + (size_t)ri * n_res) + (r & ~63u) + (slot & 63u);
+    *(volatile uint32_t*)&kv_sink_[threadIdx.x & 63u] = w.x ^ w.y ^ (uint32_t)(uintptr_t)a ^ (uint32_t)((uintptr_t)a >> 32);
+    return;
+  }
+#endif
   ((uint2*)(O.err8 + (size_t)ri * n_res))[(r & ~63u) + (slot & 63u)] =
       err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, r);
 }
@@ -756,7 +786,11 @@ __device__ __forceinline__ void kv_rec_put(const DevOut& O, uint32_t ri, uint32_
 // record row through the wave's counter byte of the row (ErrRec8 layout)
 __device__ __forceinline__ void kv_final(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, bool valid,
                                          uint32_t st, const EState& e, uint8_t* s_row, uint32_t row) {
-  if (valid && (O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP)) {
+#ifdef KV_DIAG_NOREC
+  if (false) {
+#else
+  if (valid && (KV_OFULL(O) & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP)) {
+#endif
     uint32_t z = 0u;  // an opaque zero: the site's constant record words are built here, not
                       // hoisted out of the loops as one constant register tuple per site
 #ifndef KVEMU
@@ -764,7 +798,7 @@ __device__ __forceinline__ void kv_final(const DevOut& O, uint32_t ri, uint32_t 
     asm volatile("" : "+s"(ri));
 #endif
 #if defined(KV_JIT_PRELUDE) && !defined(KVEMU)
-    if (!(O.full & 4)) {  // (full records come from a bytecode-engine re-run)
+    if (!(KV_OFULL(O) & 4)) {  // (full records come from a bytecode-engine re-run)
       // the row's byte of the wave's counter word; the increment is wave-uniform, so the atomic
       // optimizer issues one LDS add of popcount(exec) << sh per wave
       uint8_t* s_c = s_row - KV_ROW0 - row * KV_RSTRIDE + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * KV_KROWS;
@@ -790,13 +824,14 @@ __device__ __forceinline__ void kv_final(const DevOut& O, uint32_t ri, uint32_t 
 // instead (no counter; partial lines: C3 writes 7.55 -> 9.74 GB) 8.22 ms. A one-member group
 // (C4's and C5's rules) takes the wave-level add of a single rule: 64 lanes adding to one LDS
 // word serialise.
-// V: the finalization variant of the generated kernels (kvjit.cpp, KVGPU_JIT_GFIN).
-// SITE (groups of 2+ members, kvjit.cpp KVGPU_JIT_GSITE): one site record per lane for all the
+// Round 5 A/B of two other finalizations (C2 / C5 ms per pass, gpurun_out/s17): this lane's members
+// one after the other, and a uniform loop over the members some lane ends: neutral, removed.
+// SITE (groups of 2+ members): one site record per lane for all the
 // members `m` it ends here (kvdevtypes.h GSiteDesc), appended through the wave's counter s_gc[wave]
 // to the wave's segment of the group's area (gpre: the group's first record / (64 x waves)); the
 // members' records are expanded at fetch (kv_gsite_expand_kernel). C2's image-glob groups end 20
 // of their 21 members at one leaf site on most lanes: one store there instead of 20.
-template <int V = 0, bool TB = false, bool SITE = false>
+template <bool TB = false, bool SITE = false>
 __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_t r, bool valid, uint32_t m, uint32_t st,
                                         uint32_t ekx, uint32_t i0, uint32_t i1, uint32_t i2, uint32_t i3,
                                         uint8_t* s_row0, uint32_t row0, const uint32_t* tab, uint32_t n, uint32_t ri0,
@@ -814,7 +849,11 @@ __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_
   }
   if constexpr (SITE) {
     const uint8_t st8 = valid ? (uint8_t)st : (uint8_t)0xFFu;
-    if (m != 0u && valid && (O.full & 2) && !(O.full & 4) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP)) {
+#ifdef KV_DIAG_NOREC
+    if (false) {
+#else
+    if (m != 0u && valid && (KV_OFULL(O) & 2) && !(KV_OFULL(O) & 4) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP)) {
+#endif
       uint32_t z = 0u, rr = r;
       asm volatile("" : "+v"(rr), "+v"(z));
       const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -824,63 +863,28 @@ __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_
       const uint32_t k = atomicAdd(s_gc + w, 1u);
       const uint32_t nw = (n_res + 63u) >> 6;
       uint4* seg = (uint4*)O.gsite + ((size_t)gpre * nw + (size_t)(rr >> 6) * n) * 64u;
+#if defined(KV_DIAG_NORECST)
+      asm volatile("" ::"v"(k), "v"(y));
+#elif defined(KV_DIAG_RECLDS)
+      {
+        __shared__ uint32_t kv_sink2_[64];
+        const uintptr_t a = (uintptr_t)(seg + k);
+        *(volatile uint32_t*)&kv_sink2_[threadIdx.x & 63u] = (ekx + z) ^ y ^ m ^ (uint32_t)a ^ (uint32_t)(a >> 32);
+      }
+#else
       seg[k] = make_uint4(ekx + z, y, m, fits ^ 1u);
+#endif
     }
     for (uint32_t j = 0; j < n; j++)
       if ((m >> j) & 1u) s_row0[j * KV_RSTRIDE + threadIdx.x] = st8;
     return;
   }
-  if constexpr (V == 1) {
-  // this lane's members one after the other (a member's record slot: one lane-level LDS add on
-  // its row's counter byte); rule ids and rows per lane
-  const bool rec = valid && (O.full & 2) && !(O.full & 4) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP);
-  const uint8_t st8 = valid ? (uint8_t)st : (uint8_t)0xFFu;
-  uint8_t* s_c = s_row0 - KV_ROW0 - row0 * KV_RSTRIDE + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * KV_KROWS;
-  for (uint32_t mm = m; mm; mm &= mm - 1u) {
-    const uint32_t j = (uint32_t)__builtin_ctz(mm), row = row0 + j;
-    if (rec) {
-      const uint32_t ri = TB ? tab[j] : ri0 + j * sri;
-      uint32_t z = 0u, rr = r;
-      asm volatile("" : "+v"(rr), "+v"(z));
-      const uint32_t ek = ekx ? ekx + ((TB ? tab[n + j] : j * spn) << 8) : 0u;
-      const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
-      if (slot) {
-        ((uint2*)(O.err8 + (size_t)ri * n_res))[rr] = err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, rr);
-      } else {
-        const uint32_t sh = 8u * (row & 3u);
-        kv_rec_put(O, ri, n_res, rr, (atomicAdd((uint32_t*)(s_c + (row & ~3u)), 1u << sh) >> sh) & 0xFFu, e, z);
-      }
-    }
-    s_row0[j * KV_RSTRIDE + threadIdx.x] = st8;
-  }
-  } else if constexpr (V == 2) {
-  // the members some lane of the wave ends here, one after the other: a uniform loop (scalar rule
-  // ids and rows, the wave-level counter add of a single rule), as many rounds as distinct members
-  for (uint32_t mm = m;;) {
-    const unsigned long long act = __ballot(mm != 0u);
-    if (act == 0ull) break;
-    const uint32_t j = __builtin_amdgcn_readlane((uint32_t)__builtin_ctz(mm | 0x80000000u), (uint32_t)__builtin_ctzll(act));
-    if ((mm >> j) & 1u) {
-      const uint32_t ri = __builtin_amdgcn_readfirstlane(TB ? tab[j] : ri0 + j * sri);
-      if (slot) {
-        const bool rec = valid && (O.full & 2) && !(O.full & 4) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP);
-        if (rec) {
-          uint32_t z = 0u, rr = r;
-          asm volatile("" : "+v"(rr), "+v"(z));
-          const uint32_t ek = ekx ? ekx + ((TB ? tab[n + j] : j * spn) << 8) : 0u;
-          ((uint2*)(O.err8 + (size_t)ri * n_res))[rr] = err8_pack((ek & 15u) + z, (ek >> 4) & 15u, (ek >> 8) + z, ABSENT, i0, i1, i2, i3, rr);
-        }
-        s_row0[j * KV_RSTRIDE + threadIdx.x] = valid ? (uint8_t)st : (uint8_t)0xFFu;
-      } else {
-        const uint32_t ek = ekx ? ekx + ((TB ? tab[n + j] : j * spn) << 8) : 0u;
-        const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
-        kv_final(O, ri, n_res, r, valid, st, e, s_row0 + j * KV_RSTRIDE, row0 + j);
-      }
-    }
-    mm &= ~(1u << j);
-  }
-  } else {
-  const bool rec = valid && (O.full & 2) && !(O.full & 4) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP);
+  {
+#ifdef KV_DIAG_NOREC
+  const bool rec = false;
+#else
+  const bool rec = valid && (KV_OFULL(O) & 2) && !(KV_OFULL(O) & 4) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP);
+#endif
   constexpr uint32_t NW = 5u;  // 64-bit counter words a group of < 32 rows touches
   const uint32_t w0 = row0 >> 3;
   unsigned long long old[NW] = {0ull, 0ull, 0ull, 0ull, 0ull};
@@ -909,13 +913,18 @@ __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_
       asm volatile("" : "+v"(rr), "+v"(z), "+s"(ri));
       const uint32_t ek = ekx ? ekx + ((TB ? tab[n + j] : j * spn) << 8) : 0u;
       const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
-      if constexpr (V == 3) {  // (diagnostic: records built, not stored)
-        const uint2 w = err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, rr);
-        const uint32_t sl = (uint32_t)(old[((row0 + j) >> 3) - w0] >> (8u * ((row0 + j) & 7u))) & 0xFFu;
-        asm volatile("" ::"v"(w.x), "v"(w.y), "v"(sl), "s"(ri));
-      } else if (slot)
+      if (slot) {
+#if defined(KV_DIAG_RECLDS)
+        {
+          __shared__ uint32_t kv_sink3_[64];
+          const uint2 w = err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, rr);
+          const uintptr_t a = (uintptr_t)((uint2*)(O.err8 + (size_t)ri * n_res) + rr);
+          *(volatile uint32_t*)&kv_sink3_[threadIdx.x & 63u] = w.x ^ w.y ^ (uint32_t)a ^ (uint32_t)(a >> 32);
+        }
+#elif !defined(KV_DIAG_NORECST)
         ((uint2*)(O.err8 + (size_t)ri * n_res))[rr] = err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, rr);
-      else
+#endif
+      } else
         kv_rec_put(O, ri, n_res, rr, (uint32_t)(old[((row0 + j) >> 3) - w0] >> (8u * ((row0 + j) & 7u))) & 0xFFu, e, z);
     }
     s_row0[j * KV_RSTRIDE + threadIdx.x] = valid ? (uint8_t)st : (uint8_t)0xFFu;
@@ -934,7 +943,7 @@ __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_
 
 // ------------------------------------------------------------------ status rows
 // The rule kernels stage one status byte per (rule, lane) in LDS rows of the workgroup
-// (KV_RSTRIDE bytes per rule: KV_WG status bytes + a record counter byte per wave), prefilled
+// (KV_RSTRIDE bytes per rule: KV_RWG status bytes; the record counter bytes per wave before them), prefilled
 // with NOMATCH (kv_prefill_rows); matched lanes store their status (kv_final); a fused block
 // that no lane of a wave matches costs that wave nothing. When the kernel ends each wave copies
 // its statuses to the status matrix and counts its segment of every row (kv_end_flush).
@@ -958,13 +967,15 @@ __device__ __forceinline__ void kv_prefill_rows(uint32_t* s_stw, uint32_t nr, ui
   for (uint32_t q = 0; q < nr; q++)
     ((uint8_t*)s_stw)[KV_ROW0 + q * KV_RSTRIDE + threadIdx.x] = threadIdx.x < nv ? (uint8_t)ST_NOMATCH : (uint8_t)0xFFu;
 #else
-  if (threadIdx.x < KV_ROW0 / 4u) s_stw[threadIdx.x] = 0u;
-  // thread t writes status word t % 64 of rows t / 64, t / 64 + 4, ... (one pattern per thread)
+  for (uint32_t t = threadIdx.x; t < KV_ROW0 / 4u; t += (uint32_t)KV_RWG) s_stw[t] = 0u;
+  // thread t writes status word t % WPR of rows t / WPR, t / WPR + KV_RWG / WPR, ... (one pattern
+  // per thread; WPR words per row)
+  constexpr uint32_t WPR = KV_RSTRIDE / 4u;
   uint32_t* rows = s_stw + KV_ROW0 / 4u;
-  const uint32_t k = threadIdx.x & 63u, l = k * 4u;
+  const uint32_t k = threadIdx.x % WPR, l = k * 4u;
   uint32_t x = 0u;
   for (uint32_t j = 0u; j < 4u; j++) x |= (l + j < nv ? (uint32_t)ST_NOMATCH : 0xFFu) << (8u * j);
-  for (uint32_t q = threadIdx.x >> 6; q < nr; q += (uint32_t)KV_WG / 64u) rows[q * (KV_RSTRIDE / 4u) + k] = x;
+  for (uint32_t q = threadIdx.x / WPR; q < nr; q += (uint32_t)KV_RWG / WPR) rows[q * WPR + k] = x;
   __syncthreads();
 #endif
 }
@@ -1003,8 +1014,8 @@ __device__ __forceinline__ void kv_count_seg(const uint32_t* w, uint64_t m, uint
 }
 
 // End of the rule kernel for this wave: its statuses of the nr rules (kernel rules
-// rules[0..nr)) go to the status matrix (O.full & 1); lane q counts the wave's segment of row q
-// (every lane, and with per-scope counts, O.full & 8, the lanes of the workgroup's scope wsc;
+// rules[0..nr)) go to the status matrix (KV_OFULL(O) & 1); lane q counts the wave's segment of row q
+// (every lane, and with per-scope counts, KV_OFULL(O) & 8, the lanes of the workgroup's scope wsc;
 // lanes of other scopes go straight to O.scounts) and leaves the 16 counts in that segment
 // (counts[KV_HIST], scope counts[KV_HIST]); after a workgroup barrier one thread per (rule,
 // count) sums the four waves' segments into O.counts / O.scounts with a global atomic. The
@@ -1017,21 +1028,27 @@ __device__ __forceinline__ void kv_end_flush(const DevOut& O, uint32_t* s_stw, u
   __syncthreads();  // (the waves read each other's rows)
 #ifndef KVEMU
   const uint32_t wg0 = r - threadIdx.x;
-  if ((O.full & 1u) && wg0 + (uint32_t)KV_WG <= n_res && (n_res & 15u) == 0u) {
-    // 16 B per lane, 16 lanes per row: each wave store writes 4 rows of the workgroup (C3 9.10
-    // -> 8.96 ms per pass against a byte per lane and row); a partial workgroup, or rows not
-    // 16 B aligned: a byte per lane
-    // A row segment of the workgroup that is NOMATCH throughout (72 % of C3's statuses) is not
-    // written: its flag says so (O.sflag) and the fetch fills it
-    const uint32_t l = threadIdx.x & 63u, c16 = (l & 15u) * 16u;
-    const size_t nwg = (n_res + (uint32_t)KV_WG - 1u) / (uint32_t)KV_WG;
-    for (uint32_t q = (threadIdx.x >> 4); q < nr; q += (uint32_t)KV_WG / 16u) {
+#ifdef KV_DIAG_NOCOPY
+  if (false) {
+#else
+  if ((KV_OFULL(O) & 1u) && wg0 + (uint32_t)KV_RWG <= n_res && (n_res & 15u) == 0u) {
+#endif
+    // 16 B per lane, LPR lanes per row (a row = the workgroup's KV_RWG statuses of a rule): each
+    // wave store writes 64 / LPR rows of the workgroup (C3 9.10 -> 8.96 ms per pass against a
+    // byte per lane and row, round 4); a partial workgroup, or rows not 16 B aligned: a byte per
+    // lane. A row segment of the workgroup that is NOMATCH throughout (72 % of C3's statuses) is
+    // not written: its flag says so (O.sflag) and the fetch fills it
+    constexpr uint32_t LPR = KV_RSTRIDE / 16u;
+    const uint32_t l = threadIdx.x & 63u, c16 = (threadIdx.x % LPR) * 16u;
+    const size_t nwg = (n_res + (uint32_t)KV_RWG - 1u) / (uint32_t)KV_RWG;
+    for (uint32_t q = threadIdx.x / LPR; q < nr; q += (uint32_t)KV_RWG / LPR) {
       const uint4 v = *(const uint4*)(s_b + q * KV_RSTRIDE + c16);
       if (O.sflag) {
         constexpr uint32_t NM4 = 0x01010101u * (uint32_t)ST_NOMATCH;
         const bool nm = v.x == NM4 && v.y == NM4 && v.z == NM4 && v.w == NM4;
-        const bool any = ((__ballot(!nm) >> (l & 48u)) & 0xFFFFull) != 0ull;  // the row's 16 lanes
-        if ((l & 15u) == 0u) O.sflag[(size_t)rules[q] * nwg + wg0 / (uint32_t)KV_WG] = any ? 1u : 0u;
+        // the row's LPR lanes
+        const bool any = ((__ballot(!nm) >> (l & (64u - LPR))) & ((1ull << LPR) - 1ull)) != 0ull;
+        if ((l % LPR) == 0u) O.sflag[(size_t)rules[q] * nwg + wg0 / (uint32_t)KV_RWG] = any ? 1u : 0u;
         if (!any) continue;
       }
       *(uint4*)(O.status + (size_t)rules[q] * n_res + wg0 + c16) = v;
@@ -1041,17 +1058,20 @@ __device__ __forceinline__ void kv_end_flush(const DevOut& O, uint32_t* s_stw, u
     __syncthreads();
   } else
 #endif
-  if ((O.full & 1u) && valid) {
+  if ((KV_OFULL(O) & 1u) && valid) {
 #pragma unroll 4
     for (uint32_t q = 0; q < nr; q++) O.status[(size_t)rules[q] * n_res + r] = s_b[q * KV_RSTRIDE + threadIdx.x];
-    if (O.sflag && (r & ((uint32_t)KV_WG - 1u)) == 0u)  // (the workgroup's first lane: rows written)
-      for (uint32_t q = 0; q < nr; q++) O.sflag[(size_t)rules[q] * ((n_res + (uint32_t)KV_WG - 1u) / (uint32_t)KV_WG) + r / (uint32_t)KV_WG] = 1u;
+    if (O.sflag && (r & ((uint32_t)KV_RWG - 1u)) == 0u)  // (the workgroup's first lane: rows written)
+      for (uint32_t q = 0; q < nr; q++) O.sflag[(size_t)rules[q] * ((n_res + (uint32_t)KV_RWG - 1u) / (uint32_t)KV_RWG) + r / (uint32_t)KV_RWG] = 1u;
   }
+#ifdef KV_DIAG_NOCOUNT
+  return;
+#endif
 #ifndef KVEMU
   const uint32_t l = threadIdx.x & 63u, w = threadIdx.x >> 6;
   const uint64_t vm = __ballot(valid);
   uint64_t mw = 0ull;  // the wave's lanes of the workgroup's scope
-  if (O.full & 8u) {
+  if (KV_OFULL(O) & 8u) {
     uint64_t rem = vm;
     while (rem) {  // one pass per distinct scope among the wave's resources
       const uint32_t s = __builtin_amdgcn_readlane(sc, (uint32_t)__builtin_ctzll(rem));
@@ -1083,15 +1103,19 @@ __device__ __forceinline__ void kv_end_flush(const DevOut& O, uint32_t* s_stw, u
     }
   }
   __syncthreads();
-  for (uint32_t t = threadIdx.x; t < nr * 2u * KV_HIST; t += (uint32_t)KV_WG) {
+  for (uint32_t t = threadIdx.x; t < nr * 2u * KV_HIST; t += (uint32_t)KV_RWG) {
     const uint32_t q = t / (2u * KV_HIST), k = t % (2u * KV_HIST);
     uint32_t v = 0u;
-    for (uint32_t x = 0; x < (uint32_t)KV_WG / 64u; x++) v += ((const uint32_t*)(s_b + q * KV_RSTRIDE + x * 64u))[k];
+    for (uint32_t x = 0; x < KV_RWAVES; x++) v += ((const uint32_t*)(s_b + q * KV_RSTRIDE + x * 64u))[k];
+#ifdef KV_DIAG_NOATOM
+    asm volatile("" ::"v"(v));
+    continue;
+#endif
     if (!v) continue;
     if (k < (uint32_t)KV_HIST) {
       // (with per-scope counts the per-rule totals are their sum, kv_scope_totals_kernel)
-      if (!(O.full & 8u)) atomicAdd(&O.counts[(size_t)rules[q] * KV_HIST + k], (unsigned long long)v);
-    } else if ((O.full & 8u) && wsc != 0xFFFFFFFFu)
+      if (!(KV_OFULL(O) & 8u)) atomicAdd(&O.counts[(size_t)rules[q] * KV_HIST + k], (unsigned long long)v);
+    } else if ((KV_OFULL(O) & 8u) && wsc != 0xFFFFFFFFu)
       atomicAdd(&O.scounts[((size_t)wsc * n_rules + rules[q]) * KV_HIST + (k - KV_HIST)], (unsigned long long)v);
   }
 #else
@@ -1103,10 +1127,10 @@ __device__ __forceinline__ void kv_end_flush(const DevOut& O, uint32_t* s_stw, u
 // common statuses counted by one ballot each (fused specialized kernels)
 __device__ __forceinline__ void store_result2(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, bool valid,
                                               uint32_t st, const EState& e, uint32_t* hist) {
-  if (valid && (O.full & 1)) {
+  if (valid && (KV_OFULL(O) & 1)) {
     const size_t o = (size_t)ri * n_res + r;
     O.status[o] = (uint8_t)st;
-    if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP))
+    if ((KV_OFULL(O) & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP))
       store_err(O, ri, n_res, r, e.kind, e.flags, e.pn, e.key, e.res, e.i0, e.i1, e.i2, e.i3);
   }
   const uint64_t m_pass = __ballot(valid && st == ST_PASS), m_fail = __ballot(valid && st == ST_FAIL);
@@ -1130,10 +1154,10 @@ __device__ __forceinline__ void store_result2(const DevOut& O, uint32_t ri, uint
 // status histogram (one LDS atomic per wave and status)
 __device__ __forceinline__ void store_result(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, bool valid,
                                              uint32_t st, const EState& e, uint32_t* hist) {
-  if (valid && (O.full & 1)) {
+  if (valid && (KV_OFULL(O) & 1)) {
     const size_t o = (size_t)ri * n_res + r;
     O.status[o] = (uint8_t)st;
-    if ((O.full & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP))
+    if ((KV_OFULL(O) & 2) && (st == ST_FAIL || st == ST_ERROR || st == ST_SKIP))
       store_err(O, ri, n_res, r, e.kind, e.flags, e.pn, e.key, e.res, e.i0, e.i1, e.i2, e.i3);
   }
   for (uint32_t s = 0; s < 7; s++) {

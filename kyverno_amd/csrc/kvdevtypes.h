@@ -200,11 +200,18 @@ struct GSiteDesc {
 };
 
 constexpr int KV_WG = 256;
+// Workgroup of the specialized rule kernels: one wave. A workgroup's LDS (its status rows) is
+// released when its last wave ends, so with four waves per workgroup a wave that finished its
+// blocks early held its slot until the slowest wave of the four reached the end-of-kernel flush
+// (C2: 14 % of wave lifetime at that barrier, KVGPU_JIT_STAMPS); one-wave workgroups hand their
+// LDS and registers to the next workgroup as soon as they end.
+constexpr int KV_RWG = 256;
+constexpr uint32_t KV_RWAVES = (uint32_t)KV_RWG / 64u;
 // LDS of a specialized rule kernel: the waves' record counters (a byte per (wave, row), wave
 // stride KV_KROWS), then one status row per rule of the kernel (KV_RSTRIDE bytes: a byte per lane)
-constexpr uint32_t KV_RSTRIDE = KV_WG;
-constexpr uint32_t KV_KROWS = 128u;             // most rules (rows) per specialized kernel
-constexpr uint32_t KV_ROW0 = 4u * KV_KROWS;     // byte offset of row 0
+constexpr uint32_t KV_RSTRIDE = KV_RWG;
+constexpr uint32_t KV_KROWS = 128u;                  // most rules (rows) per specialized kernel
+constexpr uint32_t KV_ROW0 = KV_RWAVES * KV_KROWS;   // byte offset of row 0
 constexpr uint32_t KV_PTAB_PSEUDO = 3;  // ptab columns of a null, a map and an array node
 constexpr int KV_HIST = 8;
 

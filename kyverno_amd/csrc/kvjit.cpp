@@ -91,10 +91,6 @@ struct Gen {
   explicit Gen(const PolicySet& p) : ps(p), rec_slot(p.rules.size(), 0) {
     const char* c = getenv("KVGPU_JIT_COLS");
     cols_on = !(c && !strcmp(c, "0"));
-    const char* gd = getenv("KVGPU_JIT_GUARDS");
-    guards_on = gd && !strcmp(gd, "1");
-    const char* gsv = getenv("KVGPU_JIT_GSITE");
-    gsite_on = !(gsv && !strcmp(gsv, "0"));
     fams.emplace_back();
     col_of(0, "R");  // column 0 of family 0: the root
   }
@@ -108,11 +104,10 @@ struct Gen {
   // column count of each family is a macro (KVC_J<f>) defined at the head of every kernel
   // program once the whole image is generated.
   bool cols_on = true;
-  // Site records of rule groups (kvdevtypes.h GSiteDesc; KVGPU_JIT_GSITE=0: the members' own
-  // records, A/B): per group of 2+ members its descriptor (n, gpre, moff, 0) in gs_desc and its
-  // members' (rule, pattern-node shift) in gs_mem, numbered in generation order over the image;
-  // k_gs0 / k_gsn: the first group and the groups of the kernel being generated
-  bool gsite_on = true;
+  // Site records of rule groups (kvdevtypes.h GSiteDesc): per group of 2+ members its descriptor
+  // (n, gpre, moff, 0) in gs_desc and its members' (rule, pattern-node shift) in gs_mem, numbered
+  // in generation order over the image; k_gs0 / k_gsn: the first group and the groups of the kernel
+  // being generated (round 5, with the unwritten NOMATCH segments: C3 writes 9.4 -> 2.9 GB per pass).
   std::vector<uint32_t> gs_desc, gs_mem;
   uint32_t gs_members = 0, k_gs0 = 0, k_gsn = 0;
   struct Fam {
@@ -1009,19 +1004,9 @@ struct Gen {
   // + LDS atomics per rule and wave
   bool hist_lds = false;
 
-  // Fast-path guards (KVGPU_JIT_GUARDS=1; measured, not shipped): a run of ops that only test hoisted
-  // values (type checks, presence of hoisted keys, hoisted leaf bits) and assign cursors is
-  // preceded by one test of all their exit conditions; a lane none of them fires for takes the
-  // run's assignments and jumps past it, so a wave none of whose lanes fails there runs one
-  // branch instead of one per check. Exact: the conditions are pure functions of the hoisted
-  // values, and with none true the run falls through every check to its end. Round 5
-  // (gpurun_out/r5f, ms per pass, guards / none): C2 0.681 / 0.669, C4 1.068 / 1.044, C5 3.31 /
-  // 3.29, C3 7.56 / 7.58 -- the kernels are not bound by these branches.
-  bool guards_on = false;
   void emit_region(RGen& g, const Region& R, std::ostringstream& wout) {
     struct OpOut {
-      std::string code, cond, assign;
-      bool guardable = false;
+      std::string code;
     };
     std::vector<OpOut> outs;
     const std::string& s = g.s;
@@ -1062,13 +1047,13 @@ struct Gen {
         if (g.uses_anchor) st = "((areg" + s + " & ~apres" + s + ") ? ST_ERROR : " + st + ")";
       }
       std::ostringstream r;
-      r << "kv_gfin<KVJ_GFIN, " << (g.gtab.empty() ? "false" : "true") << ", " << (g.gsite ? "true" : "false")
+      r << "kv_gfin<" << (g.gtab.empty() ? "false" : "true") << ", " << (g.gsite ? "true" : "false")
         << ">(O, n_res, r, valid, " << m << ", " << st << ", " << u32(kind | (pcn.flags << 4) | (pn << 8));
       for (uint32_t lv = 0; lv < 4; lv++) r << ", " << (lv <= g.max_level ? li(lv) : std::string("0u"));
       r << ", s_w + " << u32(KV_ROW0 + g.grow * KV_RSTRIDE) << ", " << u32(g.grow) << ", " << (g.gtab.empty() ? std::string("nullptr") : g.gtab) << ", "
         << u32(g.gn) << ", " << u32(g.gri[0]) << ", " << u32(g.gsri) << ", " << u32(g.gspn) << ", "
         << (!g.gsite && g.gn >= gslot_members() ? "true" : "false");
-      if (g.gsite) r << ", s_gc_ + " << u32(4u * g.gl) << ", " << u32(g.gpre);
+      if (g.gsite) r << ", s_gc_ + " << u32(KV_RWAVES * g.gl) << ", " << u32(g.gpre);
       r << ");";
       return r.str();
     };
@@ -1134,8 +1119,6 @@ struct Gen {
           const char* t = op == OP_MAPCHK ? "NT_MAP" : "NT_ARR";
           if (known(d)) {
             w << "  if (node_type(" << NODE(d) << ".kt) != " << t << ") ";
-            oo.guardable = true;
-            oo.cond = "(node_type(" + NODE(d) + ".kt) != " + t + ")";
           } else {
             w << "  if (" << cd << " == ABSENT || node_type(N[" << cd << "].kt) != " << t << ") ";
           }
@@ -1149,8 +1132,6 @@ struct Gen {
                                  s + " |= " + bit + ";\n";
           w << st;
           if (h) {
-            oo.guardable = true;
-            oo.assign = st;
           }
           break;
         }
@@ -1159,9 +1140,6 @@ struct Gen {
           std::string x = lookup(d, in.a, aux, true);
           w << "  " << cn << " = " << x << "; if (" << cn << " == ABSENT) " << jump(in.b) << "\n";
           if (h) {
-            oo.guardable = true;
-            oo.cond = "(" + x + " == ABSENT)";
-            oo.assign = "  " + cn + " = " + x + ";\n";
           }
           break;
         }
@@ -1170,8 +1148,6 @@ struct Gen {
           std::string x = lookup(d, in.a, aux, true);
           w << "  " << cn << " = " << x << ";\n";
           if (h) {
-            oo.guardable = true;
-            oo.assign = "  " + cn + " = " + x + ";\n";
           }
           break;
         }
@@ -1183,7 +1159,6 @@ struct Gen {
           break;
         case OP_SCOPE_END:
           if (G) {  // groups carry no pending error (decided where raised)
-            oo.guardable = true;
             break;
           }
           if (in.c == 0) w << "  if (" << kindof << ") " << ek << " |= " << u32(aux << 4) << ";\n";
@@ -1199,16 +1174,12 @@ struct Gen {
           const std::string x = lookup(d, in.a, aux, false);
           w << "  if (" << x << " != ABSENT) " << raise(E_NEG, in.b, in.c) << "\n";
           if (h) {
-            oo.guardable = true;
-            oo.cond = "(" + x + " != ABSENT)";
           }
           break;
         }
         case OP_STAR:
           if (known(d + 1)) {
             w << "  if (node_type(" << NODE(d + 1) << ".kt) == NT_NULL) ";
-            oo.guardable = true;
-            oo.cond = "(node_type(" + NODE(d + 1) + ".kt) == NT_NULL)";
           } else {
             w << "  if (" << cn << " == ABSENT || node_type(N[" << cn << "].kt) == NT_NULL) ";
           }
@@ -1236,14 +1207,10 @@ struct Gen {
               << ");\n    if (f_) { " << gfin("f_", E_VALUE, in.b, in.c) << " " << al << " &= ~f_; if (!" << al << ") "
               << gdone() << " } }\n";
             if (T) {
-              oo.guardable = true;
-              oo.cond = "((" + al + " & ~((" + wx + " >> " + u32(slot % 32) + ") & " + hex32(mask) + ")) != 0u)";
             }
           } else {
             w << "  if (!(((" << wx << " >> " << u32(slot % 32) << ") & 1u) != 0u)) " << raise(E_VALUE, in.b, in.c) << "\n";
             if (T) {
-              oo.guardable = true;
-              oo.cond = "(((" + wx + " >> " + u32(slot % 32) + ") & 1u) == 0u)";
             }
           }
           break;
@@ -1262,8 +1229,6 @@ struct Gen {
         case OP_EXISTCHK:
           if (known(d)) {
             w << "  if (node_type(" << NODE(d) << ".kt) != NT_ARR) ";
-            oo.guardable = true;
-            oo.cond = "(node_type(" + NODE(d) + ".kt) != NT_ARR)";
           } else {
             w << "  if (" << cd << " == ABSENT || node_type(N[" << cd << "].kt) != NT_ARR) ";
           }
@@ -1272,15 +1237,11 @@ struct Gen {
         case OP_LENCHK:
           w << "  if (" << NODE(d) << ".b < " << u32(in.a) << ") " << raise(E_LEN, in.b, in.c) << "\n";
           if (known(d)) {
-            oo.guardable = true;
-            oo.cond = "(" + NODE(d) + ".b < " + u32(in.a) + ")";
           }
           break;
         case OP_INDEX:
           w << "  " << cn << " = ni(" << NODE(d) << ".a + " << u32(in.a) << ");\n";
           if (known(d)) {
-            oo.guardable = true;
-            oo.assign = "  " + cn + " = ni(" + NODE(d) + ".a + " + u32(in.a) + ");\n";
           }
           set_unknown(d + 1);
           break;
@@ -1345,27 +1306,12 @@ struct Gen {
           w << "k_ == E_LEN ? ST_ERROR : ST_FAIL);\n    goto " << R.se << "; }\n";
           break;
         default:  // OP_NOP, OP_METACHK (handled per resource by RF_BAD_META)
-          oo.guardable = true;
           break;
       }
       oo.code = w.str();
       outs.push_back(std::move(oo));
     }
-    // the runs of guardable ops with at least two exit conditions get a fast path to their end
-    for (size_t i = 0; i < outs.size();) {
-      size_t j = i, nc = 0;
-      while (j < outs.size() && outs[j].guardable) nc += !outs[j++].cond.empty();
-      if (guards_on && nc >= 2) {
-        wout << "  if (!(false";
-        for (size_t k = i; k < j; k++)
-          if (!outs[k].cond.empty()) wout << "\n      | " << outs[k].cond;
-        wout << ")) {\n";
-        for (size_t k = i; k < j; k++) wout << outs[k].assign;
-        wout << "    goto " << L(R.rb + (uint32_t)j) << ";\n  }\n";
-      }
-      for (size_t k = i; k < std::max(j, i + 1); k++) wout << outs[k].code;
-      i = std::max(j, i + 1);
-    }
+    for (const auto& x : outs) wout << x.code;
   }
 
   RGen analyze(uint32_t ri) {
@@ -1617,7 +1563,7 @@ struct Gen {
         g.gn = (uint32_t)G.members.size();
         g.gri = G.members;
         g.gdpn = G.dpn;
-        if (gsite_on && g.gn >= 2u) {
+        if (g.gn >= 2u) {
           g.gsite = true;
           g.gl = k_gsn++;
           g.gpre = gs_members;
@@ -2015,12 +1961,12 @@ struct Gen {
   // wave-private rows (round 4, first build) freed the LDS but cost C5 25 flushes per wave:
   // 3.91 against 3.25 ms per pass.
   static uint32_t kernel_lds(uint32_t nr) { return KV_ROW0 + nr * KV_RSTRIDE; }
-  // workgroups of 4 waves a CU's 160 KB LDS admits (= waves per SIMD): allocations are made in
-  // 1280 B granules (C3's 124-rule kernels, 32 240 B, ran at 4 workgroups per CU and 1.3x the
-  // time of the 123-rule ones at 31 980 B; round 4, gpurun_out/r4h)
+  // waves per SIMD a CU's 160 KB LDS admits (workgroups of KV_RWAVES waves): allocations are made
+  // in 1280 B granules (C3's 124-rule kernels, 32 240 B, ran at 4 workgroups of 4 waves per CU and
+  // 1.3x the time of the 123-rule ones at 31 980 B; round 4, gpurun_out/r4h)
   static int lds_waves(uint32_t nr) {
     const uint32_t g = 1280u, b = (kernel_lds(nr) + g - 1u) / g * g;
-    return (int)std::max<uint32_t>(1u, (160u * 1024u) / std::max(b, g));
+    return (int)std::max<uint32_t>(1u, (160u * 1024u) / std::max(b, g) * KV_RWAVES / 4u);
   }
   std::vector<uint32_t> group_kernel(const std::string& name, const std::vector<const JitChunk*>& chs, int waves) {
     std::vector<std::string> blocks;
@@ -2056,12 +2002,13 @@ struct Gen {
     // Occupancy over registers: the rule kernels are latency-bound on dependent
     // tree loads, so they ask for 8 waves per SIMD (<= 64 VGPRs) unless the plan
     // relaxes it for a kernel that would spill (jit_plan_spills).
-    const std::string lb = waves > 0 ? "KV_WG, " + std::to_string(waves) : "KV_WG";
+    const std::string lb = waves > 0 ? "KV_RWG, " + std::to_string(waves) : "KV_RWG";
     o << "extern \"C\" __global__ __launch_bounds__(" << lb << ") void " << name
       << "(const DevPS* __restrict__ Pp, const DevBatch* __restrict__ Bp, const Node* __restrict__ N, "
          "const Val* __restrict__ V, const uint8_t* __restrict__ S, DevOut O, uint32_t r0) {\n"
       << "  constexpr uint32_t FIN_ = " << u32(FIN) << ", ACT_ = " << u32(ACT) << ", ST_STORED_ = 0x7Eu;\n"
-      << "  __shared__ unsigned long long s_stq[" << kernel_lds(nr) / 8 + 2u * k_gsn << "];\n  uint32_t* s_stw = (uint32_t*)s_stq;\n"
+      << "  __shared__ unsigned long long s_stq[" << kernel_lds(nr) / 8 + (KV_RWAVES * k_gsn + 1u) / 2u
+      << "];\n  uint32_t* s_stw = (uint32_t*)s_stq;\n"
       << "  const DevPS& P = *Pp;\n  const DevBatch& B = *Bp;\n  const uint8_t* __restrict__ pstr = P.pstr;\n";
     // Workgroup b runs tile (b % 8) * n/8 + b / 8, so each XCD (blocks b, b+8, ... share one)
     // walks a contiguous resource range and its L2 sees the values those resources share
@@ -2069,7 +2016,7 @@ struct Gen {
     // per pass, traffic -1 %
     o << "  const uint32_t nb_ = gridDim.x, x_ = blockIdx.x & 7u, per_ = nb_ >> 3, rem_ = nb_ & 7u;\n"
       << "  const uint32_t bx_ = x_ * per_ + (x_ < rem_ ? x_ : rem_) + (blockIdx.x >> 3);\n";
-    o << "  const uint32_t r = r0 + bx_ * KV_WG + threadIdx.x;\n"
+    o << "  const uint32_t r = r0 + bx_ * KV_RWG + threadIdx.x;\n"
       << "  const uint32_t n_res = B.n_res;\n"
       << "  const bool valid = r < n_res;\n"
       << "  const Res* __restrict__ R = B.res + (valid ? r : 0u);\n"
@@ -2089,7 +2036,8 @@ struct Gen {
       // site-record counters of the kernel's groups, [group][wave] after the rows (zeroed before
       // the prefill's barrier)
       << "  uint32_t* const s_gc_ = s_stw + " << u32(kernel_lds(nr) / 4u) << ";\n"
-      << (k_gsn ? "  if (threadIdx.x < " + u32(4u * k_gsn) + ") s_gc_[threadIdx.x] = 0u;\n" : std::string())
+      << (k_gsn ? "  for (uint32_t t_ = threadIdx.x; t_ < " + u32(KV_RWAVES * k_gsn) + "; t_ += KV_RWG) s_gc_[t_] = 0u;\n"
+                : std::string())
       << "  kv_prefill_rows(s_stw, " << nr << "u, r - threadIdx.x, n_res);\n";
     // diagnostics (KVGPU_JIT_STAMPS): a wave's shader clock at the start, after each block and
     // after the flush, into the program's global kvj_stamps ([workgroup][wave][kJitStamps], set by
@@ -2097,7 +2045,7 @@ struct Gen {
     const bool stamps = getenv("KVGPU_JIT_STAMPS") != nullptr;
     auto stamp = [&](size_t k) {
       if (stamps && k < kJitStamps)
-        o << "  if (kvj_stamps && (threadIdx.x & 63u) == 0u) kvj_stamps[((size_t)blockIdx.x * 4u + (threadIdx.x >> 6)) * "
+        o << "  if (kvj_stamps && (threadIdx.x & 63u) == 0u) kvj_stamps[((size_t)blockIdx.x * KV_RWAVES + (threadIdx.x >> 6)) * "
           << kJitStamps << "u + " << k << "u] = __builtin_amdgcn_s_memtime();\n";
     };
     stamp(0);
@@ -2123,11 +2071,11 @@ struct Gen {
     o << "  const uint32_t wg0_ = r - threadIdx.x;\n";
     // each wave's site-record counts (lane l: the kernel's group l)
     if (k_gsn)
-      o << "#ifndef KVEMU\n  if ((O.full & 2u) && !(O.full & 4u) && (threadIdx.x & 63u) < " << u32(k_gsn)
+      o << "#ifndef KVEMU\n  if ((KV_OFULL(O) & 2u) && !(KV_OFULL(O) & 4u) && (threadIdx.x & 63u) < " << u32(k_gsn)
         << " && r - (threadIdx.x & 63u) < n_res)\n    O.gcnt[(size_t)(" << u32(k_gs0)
-        << " + (threadIdx.x & 63u)) * ((n_res + 63u) >> 6) + (r >> 6)] = s_gc_[(threadIdx.x & 63u) * 4u + (threadIdx.x >> 6)];\n#endif\n";
+        << " + (threadIdx.x & 63u)) * ((n_res + 63u) >> 6) + (r >> 6)] = s_gc_[(threadIdx.x & 63u) * KV_RWAVES + (threadIdx.x >> 6)];\n#endif\n";
     o << "  kv_end_flush(O, s_stw, " << nr << "u, " << name << "_rules, n_res, r, valid, "
-         "(O.full & 8u) && valid ? O.scope[r] : 0xFFFFFFFFu, (O.full & 8u) && wg0_ < n_res ? O.scope[wg0_] : 0xFFFFFFFFu, "
+         "(KV_OFULL(O) & 8u) && valid ? O.scope[r] : 0xFFFFFFFFu, (KV_OFULL(O) & 8u) && wg0_ < n_res ? O.scope[wg0_] : 0xFFFFFFFFu, "
          "P.n_rules);\n";
     stamp(std::min<size_t>(blocks.size() + 1, kJitStamps - 1));
     o << "}\n\n";
@@ -2337,8 +2285,21 @@ uint32_t jit_chunk_rules() {
 void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   auto t0 = std::chrono::steady_clock::now();
   Gen g(ps);
+  // KVGPU_JIT_DIAG=A,B: diagnostics-only kernel variants (#define KV_DIAG_A ... ahead of the
+  // prelude; their results are wrong)
+  std::string diag;
+  if (const char* dg = getenv("KVGPU_JIT_DIAG")) {
+    const std::string d = dg;
+    for (size_t at = 0; at <= d.size();) {
+      const size_t nx = d.find(',', at);
+      const std::string t = d.substr(at, nx == std::string::npos ? std::string::npos : nx - at);
+      if (!t.empty()) diag += "#define KV_DIAG_" + t + " 1\n";
+      if (nx == std::string::npos) break;
+      at = nx + 1;
+    }
+  }
   const std::string prelude =
-      kPrelude + std::string("\nusing namespace kv;\n\n") +
+      diag + kPrelude + std::string("\nusing namespace kv;\n\n") +
       "__device__ __noinline__ bool kv_dleaf_impl(const DevBatch& B, const Node* __restrict__ N, uint32_t dp, Node vn);\n\n";
   for (uint32_t ri = 0; ri < ps.rules.size(); ri++)
     if (ps.rules[ri].route == 0) g.leaf_classes(ri);
@@ -2413,12 +2374,7 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   out->gs_members = g.gs_members;
   std::string cdefs;  // the column count of every path-column family (KVC_J<f>)
   g.col_plan(out, &cdefs);
-  // group finalization (kvdevfn.h kv_gfin): 0 members unrolled, 1 per-lane member loop, 2 uniform
-  // loop over the members some lane ends (KVGPU_JIT_GFIN, A/B)
-  {
-    const char* gf = getenv("KVGPU_JIT_GFIN");
-    cdefs = "#define KVJ_GFIN " + std::to_string(gf ? atoi(gf) : 0) + "\n" + cdefs;
-  }
+
   if (!g.cols_on) {
     out->cols.clear();
     out->fam_arr.clear();
@@ -2762,8 +2718,7 @@ bool jit_plan_spills(JitImage* img) {
     size_t big = 0;
     for (size_t b = 1; b < np.blocks.size(); b++)
       if (np.blocks[b] > np.blocks[big]) big = b;
-    static const bool keep_waves = getenv("KVGPU_JIT_KEEPWAVES") != nullptr;  // (A/B: split blocks first)
-    if (kp.waves > 6 && np.blocks.size() > 1 && !(keep_waves && np.blocks[big] > 1)) {
+    if (kp.waves > 6 && np.blocks.size() > 1) {
       // the blocks met the bound alone (jit_refine_blocks) and the kernel still does not: the
       // pressure crosses blocks, which splitting one block at a time fixes only slowly (C4:
       // 20+ recompiles); a kernel of multi-block form gives up a wave first (down to 6)
@@ -2789,6 +2744,41 @@ bool jit_plan_spills(JitImage* img) {
   }
   if (changed) img->plan = next;
   return changed;
+}
+
+void jit_compile_variants(JitImage* img) {
+  img->variants.clear();
+  for (uint32_t full : {3u, 8u}) {
+    JitImage v;
+    v.common = "#define KVJ_FULL " + std::to_string(full) + "u\n" + img->common;
+    std::vector<size_t> at;  // program of each variant program
+    for (size_t i = 0; i < img->kernel_name.size(); i++)
+      if (img->kernel_name[i].rfind("kvj_r", 0) == 0) {
+        v.kernel_name.push_back(img->kernel_name[i]);
+        v.kernel_src.push_back(img->kernel_src[i]);
+        at.push_back(i);
+      }
+    if (at.empty()) return;
+    jit_compile(&v);
+    img->compile_ms += v.compile_ms;
+    JitImage::Variant out;
+    out.full = full;
+    out.codes.resize(img->kernel_name.size());
+    for (size_t j = 0; j < at.size(); j++) {
+      // the plan's bound of this kernel; the variant ships only where it meets the same register
+      // rules as the generic kernel (no scratch, within the bound's registers)
+      int waves = 0;
+      for (size_t k = 0; k < img->chunks.size() && k < img->plan.size(); k++)
+        if (img->chunks[k].name == v.kernel_name[j]) waves = img->plan[k].waves;
+      uint32_t priv = 0, vgprs = 0;
+      uint64_t code = 0;
+      if (!co_kernel_info(v.codes[j], v.kernel_name[j], &priv, &code, &vgprs)) continue;
+      const bool calls = v.kernel_src[j].find("kv_dleaf_impl") != std::string::npos;
+      if ((priv != 0 && !(calls && waves == 0)) || (waves > 0 && vgprs > 512u / (uint32_t)waves)) continue;
+      out.codes[at[j]] = std::move(v.codes[j]);
+    }
+    img->variants.push_back(std::move(out));
+  }
 }
 
 void jit_refine_blocks(const PolicySet& ps, uint32_t chunk_rules, JitImage* img) {
@@ -2880,7 +2870,6 @@ std::string cache_file(const JitImage& img, size_t i, uint64_t hcommon) {
 std::string jit_plan_key(const JitImage& img) {
   uint64_t h = common_hash(img);
   for (size_t i = 0; i < img.kernel_src.size(); i++) h = fnv1a64(img.kernel_src[i], fnv1a64(img.kernel_name[i], h));
-  if (getenv("KVGPU_JIT_KEEPWAVES")) h = fnv1a64("keepwaves", h);  // (the re-plan policy changes the plan)
   char key[40];
   snprintf(key, sizeof key, "%016llx", (unsigned long long)h);
   return key;
@@ -2936,6 +2925,15 @@ void jit_save_plan(const std::string& key, const JitImage& img) {
   // intermediate probes and re-plans)
   const uint64_t hc = common_hash(img);
   for (size_t i = 0; i < img.kernel_src.size(); i++) t += "co " + cache_file(img, i, hc) + "\n";
+  for (const JitImage::Variant& v : img.variants) {  // (the output-mode variants' code objects)
+    JitImage w;
+    w.common = "#define KVJ_FULL " + std::to_string(v.full) + "u\n" + img.common;
+    w.kernel_src = img.kernel_src;
+    w.kernel_name = img.kernel_name;
+    const uint64_t hv = common_hash(w);
+    for (size_t i = 0; i < img.kernel_src.size(); i++)
+      if (i < v.codes.size() && !v.codes[i].empty()) t += "co " + cache_file(w, i, hv) + "\n";
+  }
   write_file_atomic(dir, dir + "/plan-" + key + ".txt", std::vector<char>(t.begin(), t.end()));
 }
 

@@ -62,6 +62,15 @@ struct JitImage {
   std::vector<uint32_t> fam_arr, fam_ncols;
   bool probe = false;      // a block-probe image (jit_refine_blocks): rule kernels only
   double gen_ms = 0, compile_ms = 0;
+  // Output-mode variants (jit_compile_variants): the final plan's rule kernels compiled once more
+  // per DevOut::full value the benchmarks and callers run most (KVJ_FULL a constant), so a kernel
+  // carries no code for outputs its launches never write. codes[i] is program i's variant; empty
+  // where the program is not a rule kernel or its variant spilled (the generic code runs there).
+  struct Variant {
+    uint32_t full = 0;
+    std::vector<std::vector<char>> codes;
+  };
+  std::vector<Variant> variants;
 };
 
 // Generate the specialized source for every rule of `ps` (chunks of at most
@@ -86,6 +95,9 @@ uint64_t code_bytes(const JitImage& img);
 // Returns true when the plan changed (regenerate + compile again; the kernels that did not
 // change come from the code-object cache).
 bool jit_plan_spills(JitImage* img);
+// The output-mode variants of the final plan (JitImage::variants): FULL (status + records, DevOut::
+// full 3) and SCOPES-only (per-scope counts, 8); through the code-object cache.
+void jit_compile_variants(JitImage* img);
 // Block sizes of the plan from probe compiles: every multi-rule block of a multi-block kernel
 // is compiled alone under its kernel's bound, and the blocks that spill or exceed the bound's
 // registers are split in two, until every probe meets its bound (then regenerate the image).

@@ -630,25 +630,26 @@ hipError_t launch_gsite_expand(const uint32_t* gsite, const uint32_t* gcnt, cons
   return hipSuccess;
 }
 
-// NOMATCH into the status segments the specialized kernels left unwritten (DevOut::sflag): one
-// wave per (workgroup segment, rule), 16 B per lane of the first 16 lanes
+// NOMATCH into the status segments (KV_RWG statuses of a rule kernel's workgroup) the specialized
+// kernels left unwritten (DevOut::sflag): 16 B per lane, KV_RWG / 16 lanes per segment
 __global__ __launch_bounds__(KV_WG) void kv_status_fill_kernel(uint8_t* __restrict__ status,
                                                                 const uint8_t* __restrict__ sflag, uint32_t n_res,
                                                                 uint32_t n_rules, uint32_t rule0) {
-  const uint32_t nwg = (n_res + KV_WG - 1) / KV_WG, g = blockIdx.x * (KV_WG / 64) + (threadIdx.x >> 6);
-  const uint32_t rule = rule0 + blockIdx.y, l = threadIdx.x & 63u;
-  if (g >= nwg || l >= 16u || sflag[(size_t)rule * nwg + g]) return;
+  constexpr uint32_t LPS = (uint32_t)KV_RWG / 16u;
+  const uint32_t nwg = (n_res + KV_RWG - 1) / KV_RWG, g = blockIdx.x * (KV_WG / LPS) + threadIdx.x / LPS;
+  const uint32_t rule = rule0 + blockIdx.y, l = threadIdx.x % LPS;
+  if (g >= nwg || sflag[(size_t)rule * nwg + g]) return;
   const uint32_t nm = 0x01010101u * (uint32_t)ST_NOMATCH;
   // (an unwritten segment is a whole workgroup: n_res % 16 == 0 and the segment inside the batch)
-  *(uint4*)(status + (size_t)rule * n_res + (size_t)g * KV_WG + l * 16u) = make_uint4(nm, nm, nm, nm);
+  *(uint4*)(status + (size_t)rule * n_res + (size_t)g * KV_RWG + l * 16u) = make_uint4(nm, nm, nm, nm);
 }
 
 hipError_t launch_status_fill(uint8_t* status, const uint8_t* sflag, uint32_t n_res, uint32_t n_rules,
                               hipStream_t stream) {
   if (n_res == 0 || n_rules == 0) return hipSuccess;
-  const uint32_t nwg = (n_res + KV_WG - 1) / KV_WG;
+  const uint32_t nwg = (n_res + KV_RWG - 1) / KV_RWG, per = (uint32_t)KV_WG / ((uint32_t)KV_RWG / 16u);
   for (uint32_t q0 = 0; q0 < n_rules; q0 += kMaxGridY) {  // (grid y holds at most 65535 rules)
-    hipLaunchKernelGGL(kv_status_fill_kernel, dim3((nwg + KV_WG / 64 - 1) / (KV_WG / 64), std::min(kMaxGridY, n_rules - q0)),
+    hipLaunchKernelGGL(kv_status_fill_kernel, dim3((nwg + per - 1) / per, std::min(kMaxGridY, n_rules - q0)),
                        dim3(KV_WG), 0, stream, status, sflag, n_res, n_rules, q0);
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   }

@@ -131,3 +131,72 @@ def test_c3_scope_counts_full_policy_set(orc):
         np.add.at(want[idx[ns]], (np.arange(ost.shape[0]), ost[:, j]), 1)
     assert len(nss) > 900  # the C3 stream spreads 2 500 resources over ~1 000 namespaces
     assert np.array_equal(res.scope_counts, want)
+
+
+def _scope_want(ost, ns_index, n_scopes):
+    """Per-(scope, rule, status) counts of the oracle's per-pair statuses, the resources grouped by
+    scope (namespace index), summed with bincount over blocks of rules."""
+    nr = ost.shape[0]
+    want = np.zeros(n_scopes * nr * 8, np.int64)
+    ns = ns_index.astype(np.int64)[None, :]
+    for q0 in range(0, nr, 128):
+        q1 = min(nr, q0 + 128)
+        key = (ns * nr + np.arange(q0, q1, dtype=np.int64)[:, None]) * 8 + ost[q0:q1].astype(np.int64)
+        want += np.bincount(key.ravel(), minlength=want.size)
+    return want.reshape(n_scopes, nr, 8)
+
+
+def _ns_index(data, nss):
+    idx = {n: i for i, n in enumerate(nss)}
+    return np.array([idx[json.loads(line)["metadata"].get("namespace", "")] for line in data.split(b"\n")],
+                    np.int64)
+
+
+def test_c3_bench_scale(orc):
+    """C3 at bench scale: the 1 000-policy / 1 973-rule set x 100 000 mixed resources over the C3
+    stream's 1 000 namespaces (about 100 resources per namespace, so the rule kernels' per-scope
+    counts add whole waves of one scope): full status matrix and sampled failing paths against the
+    oracle, then the per-namespace PolicyReport counts of SCOPES mode (the counts of
+    pkg/kyverno/apply/report.go:80-87, pkg/policyreport/builder.go:245-261) against the oracle's
+    statuses grouped by namespace."""
+    from kyverno_amd import batch, workloads
+
+    pols = workloads.c3_policies(1000)
+    data = batch.synth(workloads.SEED + 31, 100_000, workloads.C3_KIND_MIX).strip()
+    r = _check(orc, pols, data, n_paths=200, n_msgs=50)
+    assert r.n_rules == 1973
+    ps = batch.PolicySet(pols, specialize=True)
+    b = batch.Batch(ps, data)
+    nss = b.namespaces
+    assert len(nss) >= 900 and 100_000 / len(nss) >= 50
+    ost = r.status  # (equal to the oracle's, checked above)
+    want = _scope_want(ost, _ns_index(data, nss), len(nss))
+    res = batch.validate(ps, b, mode=batch.MODE_COUNTS | batch.MODE_SCOPES)
+    assert np.array_equal(res.scope_counts, want)
+    assert np.array_equal(res.counts[:, :7], want.sum(axis=0)[:, :7])
+
+
+def test_c5_bench_scale(orc):
+    """C5 at bench scale: the chart after autogen (105 rules) x 300 000 mixed Pods / Deployments /
+    Services in SCOPES mode (the background-scan counts the bench times: no status matrix, per-scope
+    counts inside the rule kernels) against the oracle's per-pair statuses grouped by namespace; the
+    full status matrix of the same batch against the oracle."""
+    from kyverno_amd import batch, workloads
+
+    pols = workloads.c5_policies()
+    data = batch.synth(workloads.SEED + 32, 300_000, kind_mix=1).strip()
+    ps = batch.PolicySet(pols, specialize=True)
+    b = batch.Batch(ps, data)
+    ost, _ = orc.validate_ndjson(json.dumps(pols), data, nthreads=_threads())
+    ost[ost == 7] = 6
+    nss = b.namespaces
+    want = _scope_want(ost, _ns_index(data, nss), len(nss))
+    res = batch.validate(ps, b, mode=batch.MODE_COUNTS | batch.MODE_SCOPES)
+    assert np.array_equal(res.scope_counts, want)
+    sess = batch.Session(ps, b, mode=batch.MODE_COUNTS | batch.MODE_SCOPES)
+    sess.run(3)  # (pipelined passes)
+    assert np.array_equal(sess.scope_counts(len(nss)), want)
+    st = batch.validate(ps, b, mode=batch.MODE_STATUS)
+    bad = np.argwhere(st.status != ost)
+    assert not len(bad), bad[:10]
+    assert (ost == 1).sum() > 10_000 and (ost == 0).sum() > 10_000

@@ -42,7 +42,8 @@ tot = collections.Counter()
 print(f"{'kernel':24s} {'vgpr':>4s} {'sgpr':>4s} {'spill':>5s} {'priv':>4s} {'KB':>6s} {'salu':>6s} {'exec':>6s} "
       f"{'valu':>6s} {'lane':>5s} {'vmem':>5s} {'lds':>5s}")
 for f in sorted(glob.glob(os.path.join(d, "k.*.co"))):
-    name = f.split("k.", 1)[1][:-3]
+    label = f.split("k.", 1)[1][:-3]
+    name = label.split(".m")[0]  # (output-mode variants: <name>.m<full>)
     if not name.startswith("kvj_r"):
         continue
     notes = subprocess.run([READELF, "--notes", f], capture_output=True, text=True).stdout
@@ -70,7 +71,7 @@ for f in sorted(glob.glob(os.path.join(d, "k.*.co"))):
             c["vmem"] += 1
     size = os.path.getsize(f)
     tot.update(c)
-    print(f"{name[:24]:24s} {meta('vgpr_count'):4d} {meta('sgpr_count'):4d} {meta('sgpr_spill_count'):5d} "
+    print(f"{label[:24]:24s} {meta('vgpr_count'):4d} {meta('sgpr_count'):4d} {meta('sgpr_spill_count'):5d} "
           f"{meta('private_segment_fixed_size'):4d} {size / 1024:6.0f} {c['salu']:6d} {c['exec']:6d} {c['valu']:6d} "
           f"{c['lane']:5d} {c['vmem']:5d} {c['lds']:5d}")
 print("total", dict(tot))

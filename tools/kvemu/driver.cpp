@@ -65,7 +65,7 @@ static uint64_t fnv1a(const std::string& s) {
 
 // every (block, lane) of a grid, blocks spread over host threads
 template <class F>
-static void grid(uint32_t bx, uint32_t by, F f) {
+static void grid(uint32_t bx, uint32_t by, F f, uint32_t lanes = (uint32_t)KV_WG) {
   const uint32_t T = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
   std::atomic<uint64_t> next{0};
   const uint64_t total = (uint64_t)bx * by;
@@ -75,7 +75,7 @@ static void grid(uint32_t bx, uint32_t by, F f) {
       for (uint64_t i; (i = next++) < total;) {
         blockIdx = {(uint32_t)(i % bx), (uint32_t)(i / bx), 0};
         gridDim = {bx, by, 1};
-        for (uint32_t x = 0; x < (uint32_t)KV_WG; x++) {
+        for (uint32_t x = 0; x < lanes; x++) {
           threadIdx = {x, 0, 0};
           f();
         }
@@ -265,9 +265,9 @@ int main(int argc, char** argv) {
       if (!f) throw std::runtime_error(c.name + " not linked in");
       fns.push_back(f);
     }
-    const uint32_t blocks = (uint32_t)((nres + KV_WG - 1) / KV_WG);
+    const uint32_t blocks = (uint32_t)((nres + KV_RWG - 1) / KV_RWG);
     auto pass = [&]() {
-      for (chunk_fn f : fns) grid(blocks, 1, [&]() { f(&P, &B, B.nodes, B.vals, B.bstr, O, 0u); });
+      for (chunk_fn f : fns) grid(blocks, 1, [&]() { f(&P, &B, B.nodes, B.vals, B.bstr, O, 0u); }, (uint32_t)KV_RWG);
     };
     if (nres) pass();
     bool wide = false;
