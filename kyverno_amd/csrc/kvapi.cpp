@@ -638,8 +638,20 @@ struct ResultPart {
   HostArray<uint32_t> offs;         // [rule][tile] exclusive record offsets within the rule (page-locked:
                                     // C3's 38 MB crossed PCIe through a staging copy at ~1 GB/s)
   std::vector<uint64_t> base;       // [rule + 1] record offsets of the rules
-  HostArray<ErrRec8> rec;           // compact records
+  HostArray<ErrRec8> rec;           // compact records (with `uni`: only the rules that are not uniform)
   HostArray<ErrRec> recw;           // full records, parallel to rec (only when some record is wide)
+  // Per-rule deduplication (kv_rec_uniform_kernel): a rule whose records all agree but for their
+  // lane field crosses PCIe as one record, urec[rule]; the others' records are rec[nbase[rule] ...).
+  // Empty: rec holds every record.
+  std::vector<uint8_t> uni;
+  std::vector<ErrRec8> urec;
+  std::vector<uint64_t> nbase;
+  uint64_t n_rec() const { return base.empty() ? 0 : base.back(); }
+  // record i of rule `rule` (base[rule] <= i < base[rule + 1])
+  ErrRec8 r8(uint32_t rule, uint64_t i) const {
+    if (uni.empty()) return rec[i];
+    return uni[rule] ? urec[rule] : rec[nbase[rule] + (i - base[rule])];
+  }
 };
 
 struct kv_result {
@@ -736,8 +748,9 @@ struct kv_result {
     const ResultPart* p = part_of(res);
     if (!p || !errors) return false;
     const uint64_t i = rec_index(*p, rule, res);
-    if (i >= p->rec.size()) return false;
-    *e = (p->rec[i].w0 & ERR8_WIDE) && !p->recw.empty() ? p->recw[i] : decode(p->rec[i]);
+    if (i >= p->n_rec() || i < p->base[rule] || i >= p->base[rule + 1]) return false;
+    const ErrRec8 c = p->r8(rule, i);
+    *e = (c.w0 & ERR8_WIDE) && !p->recw.empty() ? p->recw[i] : decode(c);
     *bt = &batch_of(*p);
     return true;
   }
@@ -1242,6 +1255,7 @@ struct DevSession {
   // be freed once the part is attached
   std::shared_ptr<DevBatchRes> batch_ref;
   DevBuf r_offs, r_tot, r_base, r_out8, r_outw, r_wide;  // record compaction (fetch)
+  DevBuf r_uni, r_urec, r_nbase, r_out8b;                // per-rule record deduplication (fetch)
   DevBuf inv_d, stc;                                     // caller-order statuses (fetch)
   DevBuf ord_d, r_mask;                                  // caller-order records: batch order, record lanes
   DevBuf stamps;                                         // KVGPU_STAMPS diagnostics
@@ -1358,7 +1372,8 @@ struct DevSession {
       }
     }
     if (mode & KV_MODE_ERRORS) {
-      er8.alloc(nrules * nres * sizeof(ErrRec8), device);
+      // ([rule][res] for the bytecode engine, [wave][rule][64] for the specialized kernels)
+      er8.alloc(nrules * ((nres + 63) & ~63ull) * sizeof(ErrRec8), device);
       O.err8 = (ErrRec8*)er8.p;
       O.err = nullptr;  // full records: allocated by fetch() for the re-run pass, if some record is wide
       O.full |= 2;
@@ -1695,7 +1710,8 @@ struct DevSession {
       const uint8_t* rank_st = caller ? (const uint8_t*)stc.p : O.status;
       HIPCHK(launch_rec_compact(rank_st, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                 (unsigned long long*)r_tot.p, (unsigned long long*)r_base.p, nullptr, nullptr, nullptr,
-                                0, rec_compact ? (const uint8_t*)dps->rcompact.p : nullptr, nullptr, masks, stream));
+                                0, rec_compact ? (const uint8_t*)dps->rcompact.p : nullptr, nullptr, masks,
+                                rec_compact ? (uint32_t)nrules : 0u, stream));
       part->base.resize(nrules + 1);
       part->offs.alloc((size_t)nrules * tiles);
       HIPCHK(hipMemcpyAsync(part->base.data(), r_base.p, part->base.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
@@ -1708,22 +1724,64 @@ struct DevSession {
       HIPCHK(hipMemsetAsync(r_wide.p, 0, sizeof(uint32_t), stream));
       if (rec_compact && O.gsite)  // the groups' site records to their members' slots
         HIPCHK(launch_gsite_expand(O.gsite, O.gcnt, (const GSiteDesc*)dps->gsdesc.p, (const uint32_t*)dps->gsmem.p,
-                                   dps->gs_groups, (uint32_t)nres, O.err8, stream));
+                                   dps->gs_groups, (uint32_t)nres, O.err8, (uint32_t)nrules, dps->gs_members, stream));
       HIPCHK(launch_rec_compact(O.status, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                 nullptr, (unsigned long long*)r_base.p, (ErrRec8*)r_out8.p, nullptr,
                                 (uint32_t*)r_wide.p, 1, rec_compact ? (const uint8_t*)dps->rcompact.p : nullptr, ord,
-                                masks, stream));
+                                masks, rec_compact ? (uint32_t)nrules : 0u, stream));
+      uint32_t wide = 0;
+      HIPCHK(hipMemcpyAsync(&wide, r_wide.p, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
       lap("records_scatter");
+      // Per-rule deduplication: a rule whose records agree in all but their lane crosses as one
+      // record (C3: most of its 454 M records per pass); skipped when some record is wide (the full
+      // records of the re-run below are kept parallel to every compact record)
+      const ErrRec8* src = (const ErrRec8*)r_out8.p;
+      uint64_t keep = total;
+      if (!wide && total && nrules) {
+        if (!r_uni.p) {
+          r_uni.alloc(nrules * sizeof(uint32_t), device);
+          r_urec.alloc(nrules * sizeof(ErrRec8), device);
+          r_nbase.alloc(nrules * sizeof(unsigned long long), device);
+        }
+        HIPCHK(hipMemsetAsync(r_uni.p, 1, r_uni.n, stream));
+        HIPCHK(launch_rec_dedup((const ErrRec8*)r_out8.p, (const unsigned long long*)r_base.p, (uint32_t)nrules,
+                                (uint32_t*)r_uni.p, (ErrRec8*)r_urec.p, nullptr, nullptr, 0, stream));
+        std::vector<uint32_t> uni(nrules);
+        part->urec.resize(nrules);
+        HIPCHK(hipMemcpyAsync(uni.data(), r_uni.p, nrules * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(part->urec.data(), r_urec.p, nrules * sizeof(ErrRec8), hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        part->uni.assign(nrules, 0);
+        part->nbase.assign(nrules, 0);
+        keep = 0;
+        for (uint64_t q = 0; q < nrules; q++) {
+          part->uni[q] = uni[q] ? 1 : 0;
+          part->nbase[q] = keep;
+          if (!uni[q]) keep += part->base[q + 1] - part->base[q];
+        }
+        if (keep * 10 >= total * 9) {  // (little to gain: every record crosses)
+          part->uni.clear();
+          part->urec.clear();
+          part->nbase.clear();
+          keep = total;
+        } else if (keep) {
+          if (r_out8b.n < keep * sizeof(ErrRec8)) r_out8b.alloc(keep * sizeof(ErrRec8), device);
+          HIPCHK(hipMemcpyAsync(r_nbase.p, part->nbase.data(), nrules * sizeof(unsigned long long),
+                                hipMemcpyHostToDevice, stream));
+          HIPCHK(launch_rec_dedup((const ErrRec8*)r_out8.p, (const unsigned long long*)r_base.p, (uint32_t)nrules,
+                                  (uint32_t*)r_uni.p, nullptr, (const unsigned long long*)r_nbase.p,
+                                  (ErrRec8*)r_out8b.p, 1, stream));
+          src = (const ErrRec8*)r_out8b.p;
+        }
+        lap("records_dedup");
+      }
       const auto th0 = std::chrono::steady_clock::now();
-      part->rec.alloc(total);
+      part->rec.alloc(keep);
       if (part == &out->parts[0])
         out->phases.push_back(
             {"host_alloc", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count()});
       tl = std::chrono::steady_clock::now();
-      if (total)
-        HIPCHK(hipMemcpyAsync(part->rec.data(), r_out8.p, total * sizeof(ErrRec8), hipMemcpyDeviceToHost, stream));
-      uint32_t wide = 0;
-      HIPCHK(hipMemcpyAsync(&wide, r_wide.p, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+      if (keep) HIPCHK(hipMemcpyAsync(part->rec.data(), src, keep * sizeof(ErrRec8), hipMemcpyDeviceToHost, stream));
       lap("records_d2h");
       if (wide) {  // re-run the pass once writing full records (same statuses), compact those too
         if (!er.p) er.alloc(nrules * nres * sizeof(ErrRec), device);
@@ -1734,7 +1792,7 @@ struct DevSession {
         if (r_outw.n < total * sizeof(ErrRec)) r_outw.alloc(std::max<uint64_t>(total, 1) * sizeof(ErrRec), device);
         HIPCHK(launch_rec_compact(O.status, O.err8, O.err, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                   nullptr, (unsigned long long*)r_base.p, (ErrRec8*)r_out8.p, (ErrRec*)r_outw.p,
-                                  (uint32_t*)r_wide.p, 1, nullptr, ord, masks, stream));
+                                  (uint32_t*)r_wide.p, 1, nullptr, ord, masks, 0u, stream));
         part->recw.alloc(total);
         HIPCHK(hipMemcpyAsync(part->recw.data(), r_outw.p, total * sizeof(ErrRec), hipMemcpyDeviceToHost, stream));
         lap("records_wide_rerun");
@@ -2440,7 +2498,7 @@ int kv_result_failures(const kv_result* cr, uint64_t* n, const uint32_t** rule, 
             if (st != ST_FAIL && st != ST_ERROR && st != ST_SKIP) continue;
             uint32_t id = KV_PATH_NONE;
             if (st == ST_FAIL) {
-              const ErrRec8 c = p.rec[i];
+              const ErrRec8 c = p.r8(rl, i);
               if ((c.w0 & ERR8_WIDE) && !p.recw.empty()) {
                 const std::string path = render_path(ps, r->batch_of(p), p.recw[i]);
                 auto it = rendered.find(path);
