@@ -1372,8 +1372,7 @@ struct DevSession {
       }
     }
     if (mode & KV_MODE_ERRORS) {
-      // ([rule][res] for the bytecode engine, [wave][rule][64] for the specialized kernels)
-      er8.alloc(nrules * ((nres + 63) & ~63ull) * sizeof(ErrRec8), device);
+      er8.alloc(nrules * nres * sizeof(ErrRec8), device);
       O.err8 = (ErrRec8*)er8.p;
       O.err = nullptr;  // full records: allocated by fetch() for the re-run pass, if some record is wide
       O.full |= 2;
@@ -1710,8 +1709,7 @@ struct DevSession {
       const uint8_t* rank_st = caller ? (const uint8_t*)stc.p : O.status;
       HIPCHK(launch_rec_compact(rank_st, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                 (unsigned long long*)r_tot.p, (unsigned long long*)r_base.p, nullptr, nullptr, nullptr,
-                                0, rec_compact ? (const uint8_t*)dps->rcompact.p : nullptr, nullptr, masks,
-                                rec_compact ? (uint32_t)nrules : 0u, stream));
+                                0, rec_compact ? (const uint8_t*)dps->rcompact.p : nullptr, nullptr, masks, stream));
       part->base.resize(nrules + 1);
       part->offs.alloc((size_t)nrules * tiles);
       HIPCHK(hipMemcpyAsync(part->base.data(), r_base.p, part->base.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
@@ -1724,11 +1722,11 @@ struct DevSession {
       HIPCHK(hipMemsetAsync(r_wide.p, 0, sizeof(uint32_t), stream));
       if (rec_compact && O.gsite)  // the groups' site records to their members' slots
         HIPCHK(launch_gsite_expand(O.gsite, O.gcnt, (const GSiteDesc*)dps->gsdesc.p, (const uint32_t*)dps->gsmem.p,
-                                   dps->gs_groups, (uint32_t)nres, O.err8, (uint32_t)nrules, dps->gs_members, stream));
+                                   dps->gs_groups, (uint32_t)nres, O.err8, stream));
       HIPCHK(launch_rec_compact(O.status, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                 nullptr, (unsigned long long*)r_base.p, (ErrRec8*)r_out8.p, nullptr,
                                 (uint32_t*)r_wide.p, 1, rec_compact ? (const uint8_t*)dps->rcompact.p : nullptr, ord,
-                                masks, rec_compact ? (uint32_t)nrules : 0u, stream));
+                                masks, stream));
       uint32_t wide = 0;
       HIPCHK(hipMemcpyAsync(&wide, r_wide.p, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
       lap("records_scatter");
@@ -1792,7 +1790,7 @@ struct DevSession {
         if (r_outw.n < total * sizeof(ErrRec)) r_outw.alloc(std::max<uint64_t>(total, 1) * sizeof(ErrRec), device);
         HIPCHK(launch_rec_compact(O.status, O.err8, O.err, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                   nullptr, (unsigned long long*)r_base.p, (ErrRec8*)r_out8.p, (ErrRec*)r_outw.p,
-                                  (uint32_t*)r_wide.p, 1, nullptr, ord, masks, 0u, stream));
+                                  (uint32_t*)r_wide.p, 1, nullptr, ord, masks, stream));
         part->recw.alloc(total);
         HIPCHK(hipMemcpyAsync(part->recw.data(), r_outw.p, total * sizeof(ErrRec), hipMemcpyDeviceToHost, stream));
         lap("records_wide_rerun");

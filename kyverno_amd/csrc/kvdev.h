@@ -43,18 +43,14 @@ hipError_t launch_remap_u32(uint32_t* a, uint64_t n, const uint32_t* map, hipStr
 // NOMATCH into the status segments the specialized kernels did not write (DevOut::sflag)
 hipError_t launch_status_fill(uint8_t* status, const uint8_t* sflag, uint32_t n_res, uint32_t n_rules,
                               hipStream_t stream);
-// site records of the specialized rule groups (gsite [wave][gm members][64]) -> the members'
-// records at their slots of err8 [wave][nrw rules][64] (kvdevtypes.h GSiteDesc; fetch time, before
-// launch_rec_compact's scatter)
+// site records of the specialized rule groups -> the members' records at their slots (kvdevtypes.h
+// GSiteDesc; fetch time, before launch_rec_compact's scatter)
 hipError_t launch_gsite_expand(const uint32_t* gsite, const uint32_t* gcnt, const GSiteDesc* desc, const uint32_t* mem,
-                               uint32_t n_groups, uint32_t n_res, ErrRec8* err8, uint32_t nrw, uint32_t gm,
-                               hipStream_t stream);
-// err8 layout: nrw > 0 -> [wave][nrw rules][64] (specialized kernels), 0 -> [rule][res] (bytecode
-// engine); errw (full records) is always [rule][res]
+                               uint32_t n_groups, uint32_t n_res, ErrRec8* err8, hipStream_t stream);
 hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const ErrRec* errw, uint32_t n_res,
                               uint32_t n_rules, uint32_t* offs, unsigned long long* totals, unsigned long long* base,
                               ErrRec8* out8, ErrRec* outw, uint32_t* wide, int phase, const uint8_t* compact,
-                              const uint32_t* order, unsigned long long* masks, uint32_t nrw, hipStream_t stream);
+                              const uint32_t* order, unsigned long long* masks, hipStream_t stream);
 
 // Per-rule record deduplication of a compacted record array (rule-major, rule r at
 // [base[r], base[r + 1])): phase 0 sets uni[rule] = 0 unless every record of the rule equals its

@@ -754,28 +754,6 @@ __device__ __forceinline__ uint32_t kv_leaf_word(const DevPS& P, const Node* __r
   return x;
 }
 
-// Records of the specialized kernels: err8 [wave][KVJ_NR rules][64 slots] (and the site records of
-// rule groups, gsite [wave][KVJ_GM members][64]): a wave's record rows are one block, so a record's
-// address is the wave's base + rule * 512 + slot * 8 instead of a rule-row base err8 + rule * n_res
-// per record site (C2: 3 % of the pass, KVGPU_JIT_DIAG round 6). The kernel prologue moves its
-// copy of O.err8 / O.gsite to the wave's block once (kv_rec_waves); kv_rec_wave is that base. The
-// bytecode engine keeps err8 [rule][resource].
-#ifndef KVJ_NR
-#define KVJ_NR 0u
-#define KVJ_GM 0u
-#endif
-__device__ __forceinline__ void kv_rec_waves(DevOut& O, uint32_t r) {
-#if !defined(KVEMU)
-  const size_t w = (size_t)__builtin_amdgcn_readfirstlane(r >> 6);
-  O.err8 = (ErrRec8*)((uint2*)O.err8 + w * (KVJ_NR * 64u));
-  O.gsite = (uint32_t*)((uint4*)O.gsite + w * (KVJ_GM * 64u));
-#endif
-}
-__device__ __forceinline__ uint2* kv_rec_wave(const DevOut& O, uint32_t r) {
-  (void)r;
-  return (uint2*)O.err8;
-}
-
 // record `e` of rule ri on resource r at `slot` of its wave's segment of the rule's record row
 // (slot < 64: a rule ends once per lane)
 __device__ __forceinline__ void kv_rec_put(const DevOut& O, uint32_t ri, uint32_t n_res, uint32_t r, uint32_t slot,
@@ -784,7 +762,8 @@ __device__ __forceinline__ void kv_rec_put(const DevOut& O, uint32_t ri, uint32_
   asm volatile("" ::"v"(slot));
   return;
 #endif
-  kv_rec_wave(O, r)[ri * 64u + (slot & 63u)] = err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, r);
+  ((uint2*)(O.err8 + (size_t)ri * n_res))[(r & ~63u) + (slot & 63u)] =
+      err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, r);
 }
 
 // final status of one rule on this lane: its byte in status row `row` of the workgroup (s_row;
@@ -868,9 +847,8 @@ __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_
       const uint32_t y = (i0 & 1023u) | ((i1 & 255u) << 10) | ((i2 & 255u) << 18) | ((rr & 63u) << 26);
       // (a wave-uniform LDS address: the atomic optimizer issues one add of the wave's lanes)
       const uint32_t k = atomicAdd(s_gc + w, 1u);
-      // the wave's segment of the group's site area: gsite [wave][KVJ_GM members][64] (O.gsite: the
-      // wave's block, kv_rec_waves)
-      uint4* seg = (uint4*)O.gsite + (size_t)gpre * 64u;
+      const uint32_t nw = (n_res + 63u) >> 6;
+      uint4* seg = (uint4*)O.gsite + ((size_t)gpre * nw + (size_t)(rr >> 6) * n) * 64u;
 #if defined(KV_DIAG_NORECST)
       asm volatile("" ::"v"(k), "v"(y));
 #else
@@ -917,7 +895,7 @@ __device__ __forceinline__ void kv_gfin(const DevOut& O, uint32_t n_res, uint32_
       const EState e{ek & 15u, (ek >> 4) & 15u, ek >> 8, ABSENT, ABSENT, i0, i1, i2, i3};
       if (slot) {
 #if !defined(KV_DIAG_NORECST)
-        kv_rec_wave(O, rr)[ri * 64u + (rr & 63u)] = err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, rr);
+        ((uint2*)(O.err8 + (size_t)ri * n_res))[rr] = err8_pack(e.kind + z, e.flags, e.pn + z, e.key + z, e.i0, e.i1, e.i2, e.i3, rr);
 #endif
       } else
         kv_rec_put(O, ri, n_res, rr, (uint32_t)(old[((row0 + j) >> 3) - w0] >> (8u * ((row0 + j) & 7u))) & 0xFFu, e, z);

@@ -2017,7 +2017,6 @@ struct Gen {
     o << "  const uint32_t nb_ = gridDim.x, x_ = blockIdx.x & 7u, per_ = nb_ >> 3, rem_ = nb_ & 7u;\n"
       << "  const uint32_t bx_ = x_ * per_ + (x_ < rem_ ? x_ : rem_) + (blockIdx.x >> 3);\n";
     o << "  const uint32_t r = r0 + bx_ * KV_RWG + threadIdx.x;\n"
-      << "  kv_rec_waves(O, r);\n"
       << "  const uint32_t n_res = B.n_res;\n"
       << "  const bool valid = r < n_res;\n"
       << "  const Res* __restrict__ R = B.res + (valid ? r : 0u);\n"
@@ -2423,12 +2422,10 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
       }
     }
   };
-  // the record layout constants of the specialized kernels (kvdevfn.h kv_rec_wave): rules of the
-  // policy set and site-record group members of the image, ahead of the prelude
-  out->common = "#define KVJ_NR " + std::to_string(n) + "u\n#define KVJ_GM " + std::to_string(g.gs_members) + "u\n" + prelude;
+  out->common = prelude;
   out->kernel_name.clear();
   out->kernel_src.clear();
-  out->source = out->common + cdefs + helpers;
+  out->source = prelude + cdefs + helpers;
   for (auto& k : g.kernels) {
     std::vector<char> used(defs.size(), 0);
     std::vector<size_t> stack;

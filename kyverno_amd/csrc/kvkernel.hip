@@ -547,13 +547,10 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_scatter_kernel(const uint8_t* __
                                                                 uint32_t* __restrict__ wide,
                                                                 const uint8_t* __restrict__ compact,
                                                                 const uint32_t* __restrict__ order,
-                                                                const unsigned long long* __restrict__ masks,
-                                                                uint32_t nrw) {
+                                                                const unsigned long long* __restrict__ masks) {
   __shared__ uint32_t s_w[KV_WG / 64];
   const uint32_t rule = blockIdx.y, r = blockIdx.x * KV_WG + threadIdx.x, lane = threadIdx.x & 63;
   const size_t o = (size_t)rule * n_res + r;
-  // err8 of the specialized kernels: [wave][nrw rules][64] (kvdevfn.h kv_rec_wave); nrw 0: [rule][res]
-  const size_t o8 = nrw ? ((size_t)(r >> 6) * nrw + rule) * 64u + lane : o;
   const bool f = r < n_res && has_record(status[o]);
   const uint64_t m = __ballot(f);
   if (lane == 0) s_w[threadIdx.x >> 6] = (uint32_t)__popcll(m);
@@ -576,7 +573,7 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_scatter_kernel(const uint8_t* __
     // slot `lane` of the wave's segment holds the wave's lane-th record written; its lane field
     // gives its rank among the wave's record lanes
     if (lane >= (uint32_t)__popcll(m)) return;
-    const ErrRec8 e = err8[o8];
+    const ErrRec8 e = err8[o];
     const uint32_t l = e.w1 >> 26;
     out8[dest((r & ~63u) + l, (uint32_t)__popcll(m & ((1ull << l) - 1ull)))] = e;
     if (e.w0 & ERR8_WIDE) atomicOr(wide, 1u);
@@ -584,7 +581,7 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_scatter_kernel(const uint8_t* __
   }
   if (!f) return;
   const unsigned long long idx = dest(r, (uint32_t)__popcll(m & ((1ull << lane) - 1ull)));
-  const ErrRec8 e = err8[o8];
+  const ErrRec8 e = err8[o];
   out8[idx] = e;
   if (outw) outw[idx] = errw[o];
   if (e.w0 & ERR8_WIDE) atomicOr(wide, 1u);
@@ -651,13 +648,12 @@ __global__ __launch_bounds__(KV_WG) void kv_gsite_expand_kernel(const uint4* __r
                                                                  const uint32_t* __restrict__ gcnt,
                                                                  const GSiteDesc* __restrict__ desc,
                                                                  const uint32_t* __restrict__ mem, uint32_t n_res,
-                                                                 ErrRec8* __restrict__ err8, uint32_t g0, uint32_t nrw,
-                                                                 uint32_t gm) {
+                                                                 ErrRec8* __restrict__ err8, uint32_t g0) {
   const uint32_t nw = (n_res + 63u) >> 6, w = blockIdx.x * (KV_WG / 64) + (threadIdx.x >> 6), g = g0 + blockIdx.y;
   if (w >= nw) return;
   const GSiteDesc d = desc[g];
   const uint32_t cnt = gcnt[(size_t)g * nw + w];
-  const uint4* seg = gsite + ((size_t)w * gm + d.gpre) * 64u;  // (gsite [wave][gm members][64])
+  const uint4* seg = gsite + ((size_t)d.gpre * nw + (size_t)w * d.n) * 64u;
   for (uint32_t k = threadIdx.x & 63u; k < cnt; k += 64u) {
     const uint4 x = seg[k];  // {ekx, w1, member mask, indices do not fit}
     const uint32_t r = w * 64u + (x.y >> 26);
@@ -670,19 +666,18 @@ __global__ __launch_bounds__(KV_WG) void kv_gsite_expand_kernel(const uint4* __r
       ErrRec8 e;
       e.w0 = (x.x & 15u) | (((x.x >> 4) & 15u) << 4) | (wide << 6) | (pn << 7);
       e.w1 = x.y;
-      err8[((size_t)w * nrw + ri) * 64u + (r & 63u)] = e;  // (err8 [wave][nrw rules][64])
+      err8[(size_t)ri * n_res + r] = e;
     }
   }
 }
 
 hipError_t launch_gsite_expand(const uint32_t* gsite, const uint32_t* gcnt, const GSiteDesc* desc, const uint32_t* mem,
-                               uint32_t n_groups, uint32_t n_res, ErrRec8* err8, uint32_t nrw, uint32_t gm,
-                               hipStream_t stream) {
+                               uint32_t n_groups, uint32_t n_res, ErrRec8* err8, hipStream_t stream) {
   if (n_res == 0 || n_groups == 0) return hipSuccess;
   const uint32_t nw = (n_res + 63u) >> 6;
   for (uint32_t g0 = 0; g0 < n_groups; g0 += kMaxGridY) {  // (grid y holds at most 65535 groups)
     hipLaunchKernelGGL(kv_gsite_expand_kernel, dim3((nw + KV_WG / 64 - 1) / (KV_WG / 64), std::min(kMaxGridY, n_groups - g0)),
-                       dim3(KV_WG), 0, stream, (const uint4*)gsite, gcnt, desc, mem, n_res, err8, g0, nrw, gm);
+                       dim3(KV_WG), 0, stream, (const uint4*)gsite, gcnt, desc, mem, n_res, err8, g0);
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -717,7 +712,7 @@ hipError_t launch_status_fill(uint8_t* status, const uint8_t* sflag, uint32_t n_
 hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const ErrRec* errw, uint32_t n_res,
                               uint32_t n_rules, uint32_t* offs, unsigned long long* totals, unsigned long long* base,
                               ErrRec8* out8, ErrRec* outw, uint32_t* wide, int phase, const uint8_t* compact,
-                              const uint32_t* order, unsigned long long* masks, uint32_t nrw, hipStream_t stream) {
+                              const uint32_t* order, unsigned long long* masks, hipStream_t stream) {
   if (n_res == 0 || n_rules == 0) return hipSuccess;
   const uint32_t tiles = (n_res + KV_WG - 1) / KV_WG;
   if (phase == 0) {  // offsets and bases
@@ -727,7 +722,7 @@ hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const 
     hipLaunchKernelGGL(kv_rec_base_kernel, dim3(1), dim3(KV_WG), 0, stream, totals, n_rules, base);
   } else {
     hipLaunchKernelGGL(kv_rec_scatter_kernel, dim3(tiles, n_rules), dim3(KV_WG), 0, stream, status, err8, errw, n_res,
-                       tiles, offs, base, out8, outw, wide, compact, order, masks, nrw);
+                       tiles, offs, base, out8, outw, wide, compact, order, masks);
   }
   return hipGetLastError();
 }
