@@ -10,6 +10,7 @@
 // Resource identity for match/exclude follows unstructured accessors
 // (GetKind/GetName/GetNamespace/GetLabels/GetAnnotations, GroupVersionKind).
 #include <algorithm>
+#include <atomic>
 #include <array>
 #include <chrono>
 #include <cstdio>
@@ -1061,6 +1062,18 @@ std::string_view raw_string_of(const char* p, size_t n, const char* key, size_t 
   return {};
 }
 
+// occurrences of `key` (kl bytes) in a resource's JSON text
+size_t count_of(const char* p, size_t n, const char* key, size_t kl) {
+  size_t c = 0;
+  for (const char* e = p + n; p < e;) {
+    const char* k = (const char*)memmem(p, (size_t)(e - p), key, kl);
+    if (!k) break;
+    c++;
+    p = k + kl;
+  }
+  return c;
+}
+
 // Store order from per-resource (kind, namespace) keys: kinds in order of first appearance,
 // inside a kind its namespaces in order of first appearance, input order inside a (kind,
 // namespace) run (stable counting sort, per-thread key tables merged in thread order); empty
@@ -1070,8 +1083,14 @@ std::string_view raw_string_of(const char* p, size_t n, const char* key, size_t 
 // resources of one namespace share waves and workgroups, so the rule kernels count per-scope
 // PolicyReport results for a whole wave at once (kv_end_flush) and neighbouring resources share
 // match tuples.
+// Inside a wave group, the resources of one (kind, namespace) run are ordered by descending
+// element weight (`weight`: the "image" keys of each document, i.e. its containers, init and
+// ephemeral containers): a fused loop over an array then runs its iteration i on a prefix of the
+// group's lanes, so the active cells of the element rows of the path columns share cache lines
+// (C2: 19.9 -> 12.9 of the 128-byte lines a containers column touches per wave, initContainers 5.4
+// -> 3.8; round 6).
 std::vector<uint32_t> store_order(const std::vector<std::string_view>& kinds, const std::vector<std::string_view>& nss,
-                                  unsigned T) {
+                                  const std::vector<uint8_t>* weight, unsigned T) {
   struct KeyHash {
     size_t operator()(const std::pair<std::string_view, std::string_view>& k) const {
       return std::hash<std::string_view>()(k.first) * 1000003u ^ std::hash<std::string_view>()(k.second);
@@ -1117,7 +1136,7 @@ std::vector<uint32_t> store_order(const std::vector<std::string_view>& kinds, co
       }
       remap[c].push_back(it->second);
     }
-  if (gid.size() < 2) return {};
+  if (gid.size() < 2 && !weight) return {};
   std::sort(rank.begin(), rank.end());
   std::vector<uint32_t> slot(gid.size());  // key id -> position of its run
   for (size_t q = 0; q < rank.size(); q++) slot[rank[q].second] = (uint32_t)q;
@@ -1141,6 +1160,31 @@ std::vector<uint32_t> store_order(const std::vector<std::string_view>& kinds, co
   run([&](size_t c) {
     for (size_t i = c * per; i < std::min(n, (c + 1) * per); i++) order[cnt[c][key[i]]++] = (uint32_t)i;
   });
+  if (weight && weight->size() == n) {  // descending weight inside each (wave group, run) segment
+    std::atomic<bool> moved{false};
+    const size_t groups = (n + KV_LANES - 1) / KV_LANES, gper = (groups + C - 1) / C;
+    run([&](size_t c) {
+      bool any = false;
+      for (size_t g = c * gper; g < std::min(groups, (c + 1) * gper); g++) {
+        const size_t e = std::min(n, (g + 1) * KV_LANES);
+        for (size_t a = g * KV_LANES; a < e;) {
+          size_t b = a + 1;
+          while (b < e && key[order[b]] == key[order[a]]) b++;
+          const bool sorted = std::is_sorted(order.begin() + a, order.begin() + b, [&](uint32_t x, uint32_t y) {
+            return (*weight)[x] > (*weight)[y];
+          });
+          if (!sorted) {
+            std::stable_sort(order.begin() + a, order.begin() + b,
+                             [&](uint32_t x, uint32_t y) { return (*weight)[x] > (*weight)[y]; });
+            any = true;
+          }
+          a = b;
+        }
+      }
+      if (any) moved = true;
+    });
+    if (!moved && gid.size() < 2) return {};
+  }
   return order;
 }
 
@@ -1303,6 +1347,7 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
     const size_t P = (nres + per - 1) / per;
     {  // store order: resources grouped by kind, then namespace
       std::vector<std::string_view> kinds(nres), nss(nres);
+      std::vector<uint8_t> weight(nres);
       std::vector<std::thread> kt;
       for (size_t k = 0; k < P; k++)
         kt.emplace_back([&, k]() {
@@ -1310,10 +1355,11 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
             const size_t end = i + 1 < nres ? starts[i + 1] : len;
             kinds[i] = raw_string_of(json + starts[i], end - starts[i], "\"kind\"", 6);
             nss[i] = raw_string_of(json + starts[i], end - starts[i], "\"namespace\"", 11);
+            weight[i] = (uint8_t)std::min<size_t>(255, count_of(json + starts[i], end - starts[i], "\"image\"", 7));
           }
         });
       for (auto& t : kt) t.join();
-      b->order = store_order(kinds, nss, T);
+      b->order = store_order(kinds, nss, &weight, T);
     }
     if (verbose) fprintf(stderr, "[kvgpu] ingest: store order %.1f ms\n", ms());
     const std::vector<uint32_t>& order = b->order;
@@ -1393,7 +1439,7 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
         const int64_t ns = m >= 0 && d.at((uint32_t)m).t == J_MAP ? d.get((uint32_t)m, "namespace") : -1;
         if (ns >= 0 && d.at((uint32_t)ns).t == J_STR) nss[i] = d.sval(d.at((uint32_t)ns));
       }
-      b->order = store_order(kinds, nss, 1);
+      b->order = store_order(kinds, nss, nullptr, 1);
       for (size_t q = 0; q < docs.size(); q++) in.take(docs[b->order.empty() ? q : b->order[q]]);
     } else {
       parse_json_stream(json, len, NUM_UNSTRUCTURED, [&](JDoc& d) { in.take(d); });
