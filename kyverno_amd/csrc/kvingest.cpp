@@ -11,6 +11,8 @@
 // (GetKind/GetName/GetNamespace/GetLabels/GetAnnotations, GroupVersionKind).
 #include <algorithm>
 #include <atomic>
+
+#include <emmintrin.h>
 #include <array>
 #include <chrono>
 #include <cstdio>
@@ -1062,16 +1064,36 @@ std::string_view raw_string_of(const char* p, size_t n, const char* key, size_t 
   return {};
 }
 
-// occurrences of `key` (kl bytes) in a resource's JSON text
-size_t count_of(const char* p, size_t n, const char* key, size_t kl) {
-  size_t c = 0;
-  for (const char* e = p + n; p < e;) {
-    const char* k = (const char*)memmem(p, (size_t)(e - p), key, kl);
-    if (!k) break;
-    c++;
-    p = k + kl;
+// The store-order weight of a resource from its JSON text, one pass over its quotes: the
+// "image" keys (its containers) above a "volumes" key above the "securityContext", "resources"
+// and "ports" keys (the containers' optional parts), so like resources sort together
+uint32_t shape_weight(const char* p, size_t n) {
+  uint32_t img = 0, vol = 0, sc = 0, rs = 0, po = 0;
+  const char* e = p + n;
+  auto key = [&](const char* q) {  // q: the byte after a quote
+    auto is = [&](const char* k, size_t kl) { return (size_t)(e - q) >= kl && memcmp(q, k, kl) == 0; };
+    switch (*q) {
+      case 'i': img += is("image\"", 6); break;
+      case 'v': vol |= is("volumes\"", 8); break;
+      case 's': sc += is("securityContext\"", 16); break;
+      case 'r': rs += is("resources\"", 10); break;
+      case 'p': po += is("ports\"", 6); break;
+      default: break;
+    }
+  };
+  const __m128i qq = _mm_set1_epi8('"');  // quotes 16 bytes at a time (SSE2)
+  const char* q = p;
+  for (; q + 16 <= e; q += 16) {
+    unsigned m = (unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128((const __m128i*)q), qq));
+    while (m) {
+      const unsigned b = (unsigned)__builtin_ctz(m);
+      m &= m - 1;
+      if (q + b + 1 < e) key(q + b + 1);
+    }
   }
-  return c;
+  for (; q < e; q++)
+    if (*q == '"' && q + 1 < e) key(q + 1);
+  return std::min(img, 255u) << 24 | vol << 23 | std::min(sc, 15u) << 16 | std::min(rs, 15u) << 12 | std::min(po, 15u) << 8;
 }
 
 // Store order from per-resource (kind, namespace) keys: kinds in order of first appearance,
@@ -1083,16 +1105,17 @@ size_t count_of(const char* p, size_t n, const char* key, size_t kl) {
 // resources of one namespace share waves and workgroups, so the rule kernels count per-scope
 // PolicyReport results for a whole wave at once (kv_end_flush) and neighbouring resources share
 // match tuples.
-// Inside a (kind, namespace) run the resources are ordered by descending element weight
-// (`weight`: twice the "image" keys of each document, i.e. its containers, init and ephemeral
-// containers, plus one with a "volumes" key), input order among equals. A fused loop over an array
+// Inside a (kind, namespace) run the resources are ordered by descending weight (`weight`,
+// shape_weight: the "image" keys of each document, i.e. its containers, init and ephemeral
+// containers, then a "volumes" key, then the containers' optional parts), input order among
+// equals. A fused loop over an array
 // runs as many iterations as the wave's largest array: waves of like resources run fewer of them
 // (C2: most waves held a 4-container Pod, ran 4 iterations for 1.75 containers per Pod on average),
 // and iteration i runs on a prefix of the lanes, so the active cells of the element rows of the path
 // columns share cache lines (round 6: sorting inside each wave group alone took C2 0.517 -> 0.483,
 // C4 0.844 -> 0.786, C5 2.57 -> 2.445 ms per pass).
 std::vector<uint32_t> store_order(const std::vector<std::string_view>& kinds, const std::vector<std::string_view>& nss,
-                                  const std::vector<uint8_t>* weight, unsigned T) {
+                                  const std::vector<uint32_t>* weight, unsigned T) {
   struct KeyHash {
     size_t operator()(const std::pair<std::string_view, std::string_view>& k) const {
       return std::hash<std::string_view>()(k.first) * 1000003u ^ std::hash<std::string_view>()(k.second);
@@ -1345,7 +1368,7 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
     const size_t P = (nres + per - 1) / per;
     {  // store order: resources grouped by kind, then namespace
       std::vector<std::string_view> kinds(nres), nss(nres);
-      std::vector<uint8_t> weight(nres);
+      std::vector<uint32_t> weight(nres);
       std::vector<std::thread> kt;
       for (size_t k = 0; k < P; k++)
         kt.emplace_back([&, k]() {
@@ -1353,9 +1376,7 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
             const size_t end = i + 1 < nres ? starts[i + 1] : len;
             kinds[i] = raw_string_of(json + starts[i], end - starts[i], "\"kind\"", 6);
             nss[i] = raw_string_of(json + starts[i], end - starts[i], "\"namespace\"", 11);
-            const size_t img = std::min<size_t>(127, count_of(json + starts[i], end - starts[i], "\"image\"", 7));
-            const bool vol = memmem(json + starts[i], end - starts[i], "\"volumes\"", 9) != nullptr;
-            weight[i] = (uint8_t)(img * 2 + (vol ? 1 : 0));
+            weight[i] = shape_weight(json + starts[i], end - starts[i]);
           }
         });
       for (auto& t : kt) t.join();
