@@ -80,11 +80,12 @@ def cpu_baseline(policies, pairs: float, threads: int, kind_mix: int = 0, label:
 
 def pmc_traffic(args) -> dict | None:
     """HBM bytes per pass of this workload from rocprofv3 PMC counters, measured by this command:
-    two child runs of this script (2 passes + the first), one counter each (FETCH_SIZE, WRITE_SIZE;
-    one rocprofv3 --pmc run per counter group, kernel-trace/stats only). Per MI355X_MICROARCH.md
-    (HBM section): the counters are KB, and on gfx950 FETCH_SIZE counts half the bytes of coalesced
-    reads, so it is doubled. Sum over the pass's kernels (the record-compaction kernels kv_rec_*
-    run at fetch, outside the pass; the row expansion and path-column build run once per batch)."""
+    two child runs of this script, one counter group each (kernel-trace/stats only): the L2's
+    memory-side read requests by size class (TCC_EA0_RDREQ_128B / _64B / _32B: bytes = 128 / 64 / 32
+    per request; FETCH_SIZE tallies a 128-byte request at 64 B, MI355X_MICROARCH.md HBM section) and
+    WRITE_SIZE. Per kernel the counters are averaged over its dispatches (every kernel of a pass runs
+    once per pass), then summed over the pass's kernels (not the record compaction of a fetch,
+    kv_rec_*, nor the row expansion and path-column build that run once per batch)."""
     import csv
     import collections
     import glob
@@ -102,14 +103,15 @@ def pmc_traffic(args) -> dict | None:
         log("pmc: running under a profiler, in-run traffic skipped")
         return None
     out = tempfile.mkdtemp(prefix="kvpmc.", dir=os.environ.get("TMPDIR", "/tmp"))
-    passes = 3  # the child's first pass + --warmup 0 + --steps 2
     child = [sys.executable, "-u", os.path.abspath(__file__), "--config", args.config, "--n-res", str(args.n_res),
              "--mode", args.mode, "--engine", args.engine, "--steps", "2", "--warmup", "0", "--no-cpu-baseline",
              "--no-e2e", "--no-traffic"]
+    groups = {"read": {"TCC_EA0_RDREQ_128B_sum": 128, "TCC_EA0_RDREQ_64B_sum": 64, "TCC_EA0_RDREQ_32B_sum": 32},
+              "write": {"WRITE_SIZE": 1024}}
     vals = {}
-    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+    for name, ctrs in groups.items():
         launcher = [sys.executable, rp] if open(rp, "rb").read(2) == b"#!" else [rp]
-        cmd = launcher + ["--pmc", ctr, "--kernel-trace", "--stats", "-d", out, "-o", ctr, "--output-format", "csv",
+        cmd = launcher + ["--pmc", *ctrs, "--kernel-trace", "--stats", "-d", out, "-o", name, "--output-format", "csv",
                           "--"] + child
         p = subprocess.Popen(cmd, cwd=out, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, start_new_session=True)
         try:
@@ -117,28 +119,28 @@ def pmc_traffic(args) -> dict | None:
         except subprocess.TimeoutExpired:
             os.killpg(p.pid, signal.SIGKILL)
             p.wait()
-            log(f"pmc {ctr}: timed out")
+            log(f"pmc {name}: timed out")
             return None
         if p.returncode != 0:
-            log(f"pmc {ctr}: rocprofv3 exit {p.returncode}: {err.decode(errors='replace')[-400:]}")
+            log(f"pmc {name}: rocprofv3 exit {p.returncode}: {err.decode(errors='replace')[-400:]}")
             return None
         agg = collections.defaultdict(float)
-        for f in sorted(set(glob.glob(os.path.join(out, "**", f"{ctr}*counter_collection.csv"), recursive=True))):
+        disp = collections.defaultdict(set)
+        for f in sorted(set(glob.glob(os.path.join(out, "**", f"{name}*counter_collection.csv"), recursive=True))):
             for r in csv.DictReader(open(f)):
                 k = r.get("Kernel_Name", "")
-                # the pass's kernels: not the record compaction of a fetch (kv_rec_*) nor what the
-                # batch upload runs once per batch (kv_expand_rows, the path-column build kv_pcol_*)
-                if r["Counter_Name"] == ctr and k.startswith(("kv_", "kvj_", "kv::")) and "kv_rec_" not in k \
+                if r["Counter_Name"] in ctrs and k.startswith(("kv_", "kvj_", "kv::")) and "kv_rec_" not in k \
                         and "kv_expand_rows" not in k and "kv_pcol_" not in k:
-                    agg[k] += float(r["Counter_Value"])
+                    agg[k] += float(r["Counter_Value"]) * ctrs[r["Counter_Name"]]
+                    disp[k].add(r.get("Dispatch_Id", ""))
         if not agg:
             return None
-        vals[ctr] = {k: v * 1024 / passes for k, v in agg.items()}
+        vals[name] = {k: v / max(1, len(disp[k])) for k, v in agg.items()}
     shutil.rmtree(out, ignore_errors=True)
-    fetch = 2 * sum(vals["FETCH_SIZE"].values())
-    write = sum(vals["WRITE_SIZE"].values())
+    fetch = sum(vals["read"].values())
+    write = sum(vals["write"].values())
     return {"bytes_per_pass": fetch + write, "read_bytes": fetch, "write_bytes": write,
-            "per_kernel_read": {k: 2 * v for k, v in sorted(vals["FETCH_SIZE"].items())},
+            "per_kernel_read": dict(sorted(vals["read"].items())),
             "run_id": f"in-run PMC, pid {os.getpid()}, {time.strftime('%Y-%m-%dT%H:%M:%SZ', time.gmtime())}"}
 
 
@@ -499,7 +501,8 @@ def main():
         t = pmc_traffic(args)
         if t is not None:
             out["roofline"]["traffic"] = t["bytes_per_pass"]
-            out["roofline"]["traffic_source"] = t["run_id"] + " (2 x FETCH_SIZE + WRITE_SIZE, rocprofv3 --pmc)"
+            out["roofline"]["traffic_source"] = t["run_id"] + (" (TCC_EA0_RDREQ 128B/64B/32B x size + WRITE_SIZE, "
+                                                               "rocprofv3 --pmc, per dispatch)")
             out["roofline"]["traffic_over_alg"] = t["bytes_per_pass"] / b_alg
             out["roofline"]["traffic_detail"] = {"read": t["read_bytes"], "write": t["write_bytes"],
                                                  "per_kernel_read": t["per_kernel_read"]}
