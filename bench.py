@@ -214,6 +214,7 @@ def e2e_stream(ps, n_res: int, kind_mix: int, device: int, seed: int, chunk: int
     def evaluate(b):
         t = time.perf_counter()
         r = batch.validate(ps, b, device=device, mode=mode, copy=False)
+        _ = r.status  # the dense status matrix on the host (materialised from the transfer form)
         t_val[0] += time.perf_counter() - t
         return r
 
@@ -234,7 +235,7 @@ def e2e_stream(ps, n_res: int, kind_mix: int, device: int, seed: int, chunk: int
             "chunks": len(chunks), "chunk_resources": chunk, "in_flight": inflight, "ingest_seconds": t_ing[0],
             "validate_seconds": t_val[0],
             "includes": "NDJSON -> kv_ingest (host threads) overlapped with kv_validate of the previous chunks "
-                        "(H2D + pass + D2H of statuses and records, two in flight)"}
+                        "(H2D + pass + D2H of statuses and records + the dense status matrix, two in flight)"}
 
 
 def main():
@@ -474,14 +475,22 @@ def main():
         rw = batch.validate(ps, bw, device=local, copy=False)
         del rw, bw
         b2 = batch.Batch(ps, batch.synth(workloads.SEED, args.n_res, kind_mix, first=rank * args.n_res))
+        xfer = b2.transfer_bytes
         te0 = time.perf_counter()
         r2 = batch.validate(ps, b2, device=local, copy=False)  # statuses stay in the result's pinned buffer
         te1 = time.perf_counter()
+        _ = r2.status  # the dense caller-order matrix, materialised on the host from the transfer form
+        te2 = time.perf_counter()
         out["e2e_kv_validate"] = {"seconds": te1 - te0, "evals_per_s": n_pairs_rank / (te1 - te0),
                                   "kernel_ms": r2.kernel_ms,
                                   "phases_ms": {k: round(v, 3) for k, v in r2.phases.items()},
-                                  "includes": "H2D store upload + 1 pass + D2H status/error records "
-                                              "(steady state: after one untimed kv_validate of another batch)"}
+                                  "status_matrix_ms": round(1e3 * (te2 - te1), 3),
+                                  "upload_bytes": xfer, "upload_bytes_per_resource": round(xfer / args.n_res, 1),
+                                  "includes": "H2D store upload + 1 pass + D2H statuses (transfer form: the "
+                                              "segments the pass wrote, 4 bits a status) and error records "
+                                              "(1-byte codes into per-rule tables); status_matrix_ms: the "
+                                              "dense [rule][res] matrix built from it on first read (steady "
+                                              "state: after one untimed kv_validate of another batch)"}
         del r2, b2
         # the same stream as a caller would push it: ingest overlapped with upload + pass + fetch
         out["e2e_stream"] = e2e_stream(ps, args.n_res, kind_mix, local, workloads.SEED + 13,

@@ -92,6 +92,10 @@ int kv_rule_info_get(const kv_policyset* ps, uint32_t rule, kv_rule_info* out);
 int kv_ingest(const kv_policyset* ps, const char* resources_json, size_t len, const char* ns_labels_json,
               kv_batch** out, kv_error** err);
 int kv_batch_info(const kv_batch* b, uint64_t* n_res, uint64_t* store_bytes);
+/* bytes the batch's store crosses PCIe in (kv_validate's upload: the populated cells in their
+ * 8-byte transfer form, row masks, values, resource headers, strings, match inputs); no
+ * reference counterpart (the reference evaluates in the process that decoded the resource) */
+int kv_batch_transfer_bytes(const kv_batch* b, uint64_t* bytes);
 /* namespace table of a batch (first-seen order; index = scope of kv_result_scope_counts);
  * the name lives as long as the batch. Reference: resource.GetNamespace() keys the report
  * scope in buildPolicyResults (pkg/kyverno/apply/report.go:80-87). */

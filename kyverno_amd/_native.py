@@ -69,6 +69,7 @@ def lib():
         L.kv_rule_info_get.argtypes = [vp, u32, ctypes.POINTER(RuleInfo)]
         L.kv_ingest.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_char_p, ctypes.POINTER(vp), errpp]
         L.kv_batch_info.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]
+        L.kv_batch_transfer_bytes.argtypes = [vp, ctypes.POINTER(u64)]
         L.kv_validate.argtypes = [vp, vp, ctypes.c_char_p, i32, u32, ctypes.POINTER(vp), errpp]
         L.kv_result_status.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(u64), ctypes.POINTER(u64)]
         L.kv_result_counts.argtypes = [vp, ctypes.POINTER(vp)]
@@ -119,7 +120,7 @@ def lib():
 
 
 EXPORTED_SYMBOLS = [
-    "kv_compile", "kv_policyset_info", "kv_policyset_jit_info", "kv_rule_info_get", "kv_ingest", "kv_batch_info", "kv_validate",
+    "kv_compile", "kv_policyset_info", "kv_policyset_jit_info", "kv_rule_info_get", "kv_ingest", "kv_batch_info", "kv_batch_transfer_bytes", "kv_validate",
     "kv_result_status", "kv_result_counts", "kv_result_path", "kv_result_error", "kv_result_error_message",
     "kv_result_subst_error", "kv_result_phase", "kv_host_reserve", "kv_device_pool_limit", "kv_device_trim",
     "kv_result_kernel_ms",

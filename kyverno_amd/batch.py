@@ -116,6 +116,13 @@ class Batch:
         self.n_res, self.store_bytes = n.value, b.value
 
     @property
+    def transfer_bytes(self) -> int:
+        """Bytes the store crosses PCIe in (kv_batch_transfer_bytes: 8-byte transfer cells)."""
+        n = ctypes.c_uint64()
+        lib().kv_batch_transfer_bytes(self._h, ctypes.byref(n))
+        return n.value
+
+    @property
     def namespaces(self) -> list[str]:
         """Batch namespace table: index = scope of per-scope counts ("" = cluster scope)."""
         n = ctypes.c_uint32()
@@ -164,20 +171,12 @@ class Result:
         self.policyset = policyset
         self.batch = batch
         L = lib()
-        p = ctypes.c_void_p()
         nr, nn = ctypes.c_uint64(), ctypes.c_uint64()
-        L.kv_result_status(h, ctypes.byref(p), ctypes.byref(nr), ctypes.byref(nn))
+        L.kv_result_status(h, None, ctypes.byref(nr), ctypes.byref(nn))
         self.n_rules, self.n_res = nr.value, nn.value
-        if p.value:
-            buf = (ctypes.c_uint8 * (self.n_rules * self.n_res)).from_address(p.value)
-            buf._kv_owner = self._owner  # the view outlives this Result only together with the handle
-            self.status = np.frombuffer(buf, dtype=np.uint8).reshape(self.n_rules, self.n_res)
-            if copy:
-                self.status = self.status.copy()
-            else:
-                self.status.flags.writeable = False
-        else:
-            self.status = None
+        self._copy = copy
+        self._status = None
+        self._status_read = False
         c = ctypes.c_void_p()
         L.kv_result_counts(h, ctypes.byref(c))
         cb = (ctypes.c_int64 * (self.n_rules * 8)).from_address(c.value) if self.n_rules else []
@@ -196,6 +195,27 @@ class Result:
         if L.kv_result_scope_counts(h, ctypes.byref(sc), ctypes.byref(ns)) == 0 and self.n_rules and ns.value:
             buf = (ctypes.c_int64 * (ns.value * self.n_rules * 8)).from_address(sc.value)
             self.scope_counts = np.frombuffer(buf, dtype=np.int64).reshape(ns.value, self.n_rules, 8).copy()
+
+    @property
+    def status(self):
+        """uint8 [rule][res] statuses in the caller's order, or None for a counts-only result. The
+        library materialises the matrix on first use from the form the statuses crossed PCIe in
+        (kv_result_status; the segments a specialized pass wrote, 4 bits a status)."""
+        if not self._status_read:
+            p = ctypes.c_void_p()
+            if lib().kv_result_status(self._h, ctypes.byref(p), None, None) != 0:
+                raise MemoryError("kv_result_status: no host memory for the status matrix")
+            if p.value:
+                buf = (ctypes.c_uint8 * (self.n_rules * self.n_res)).from_address(p.value)
+                buf._kv_owner = self._owner  # the view outlives this Result only together with the handle
+                st = np.frombuffer(buf, dtype=np.uint8).reshape(self.n_rules, self.n_res)
+                if self._copy:
+                    st = st.copy()
+                else:
+                    st.flags.writeable = False
+                self._status = st
+            self._status_read = True
+        return self._status
 
     def path(self, rule: int, res: int) -> str | None:
         buf = ctypes.create_string_buffer(4096)

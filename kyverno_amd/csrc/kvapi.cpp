@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <emmintrin.h>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -640,17 +641,48 @@ struct ResultPart {
   std::vector<uint64_t> base;       // [rule + 1] record offsets of the rules
   HostArray<ErrRec8> rec;           // compact records (with `uni`: only the rules that are not uniform)
   HostArray<ErrRec> recw;           // full records, parallel to rec (only when some record is wide)
-  // Per-rule deduplication (kv_rec_uniform_kernel): a rule whose records all agree but for their
-  // lane field crosses PCIe as one record, urec[rule]; the others' records are rec[nbase[rule] ...).
-  // Empty: rec holds every record.
-  std::vector<uint8_t> uni;
-  std::vector<ErrRec8> urec;
+  // Record codes (kv_rec_code_kernel): record i of a coded rule is its rule's table entry
+  // tab[rule * KV_REC_CODES + code[i]] (the lane field left out); a raw rule's records are
+  // rec[nbase[rule] ...). Empty `raw`: rec holds every record.
+  std::vector<uint8_t> raw;
+  std::vector<ErrRec8> tab;
+  HostArray<uint8_t> code;
   std::vector<uint64_t> nbase;
+  // Status transfer form (kv_status_pack_kernel): the flags of the (rule, KV_RWG-status segment)s
+  // the pass wrote, their statuses at 4 bits (KV_RWG / 2 bytes a segment, rule-major), the first
+  // packed segment of each rule; the other segments are NOMATCH. Empty sflag: the part's statuses
+  // crossed as dense rows of kv_result::status.
+  HostArray<uint8_t> sflag, spack;
+  std::vector<uint64_t> sbase;
+  uint64_t nwg = 0;
+  // statuses [lo, lo + n) of rule `rule` from the transfer form into dst[0, n)
+  void unpack_row(uint32_t rule, uint8_t* dst) const {
+    const uint8_t* f = sflag.data() + (size_t)rule * nwg;
+    const uint8_t* src = spack.data() + sbase[rule] * (KV_RWG / 2);
+    const __m128i lo4 = _mm_set1_epi8(0x0F);
+    for (uint64_t g = 0; g < nwg; g++) {
+      const uint64_t q0 = g * KV_RWG, m = std::min<uint64_t>(KV_RWG, n - q0);
+      uint8_t* d = dst + q0;
+      if (!f[g]) {
+        memset(d, ST_NOMATCH, m);
+        continue;
+      }
+      uint64_t i = 0;
+      for (; i + 32 <= m; i += 32) {
+        const __m128i b = _mm_loadu_si128((const __m128i*)(src + i / 2));
+        const __m128i l = _mm_and_si128(b, lo4), h = _mm_and_si128(_mm_srli_epi16(b, 4), lo4);
+        _mm_storeu_si128((__m128i*)(d + i), _mm_unpacklo_epi8(l, h));
+        _mm_storeu_si128((__m128i*)(d + i + 16), _mm_unpackhi_epi8(l, h));
+      }
+      for (; i < m; i++) d[i] = (src[i / 2] >> (4 * (i & 1))) & 15u;
+      src += KV_RWG / 2;
+    }
+  }
   uint64_t n_rec() const { return base.empty() ? 0 : base.back(); }
   // record i of rule `rule` (base[rule] <= i < base[rule + 1])
   ErrRec8 r8(uint32_t rule, uint64_t i) const {
-    if (uni.empty()) return rec[i];
-    return uni[rule] ? urec[rule] : rec[nbase[rule] + (i - base[rule])];
+    if (raw.empty()) return rec[i];
+    return raw[rule] ? rec[nbase[rule] + (i - base[rule])] : tab[(size_t)rule * KV_REC_CODES + code[i]];
   }
 };
 
@@ -664,6 +696,10 @@ struct kv_result {
   HostArray<uint8_t> status;
   std::once_flag sc_once;
   HostArray<uint8_t> status_c;
+  // the parts hold their statuses in the transfer form (ResultPart::sflag) until an accessor
+  // materialises `status` (st_store) or the caller-order copy (status_caller)
+  bool sparse = false;
+  std::once_flag st_once;
   // statuses and records were fetched in the caller's order (a permuted batch fetched whole:
   // DevSession::fetch); `status` is then the caller order and `res` below a caller index
   bool caller_order = false;
@@ -692,22 +728,63 @@ struct kv_result {
   }
   // caller index of status / record index `s`
   uint64_t cidx(uint64_t s) const { return caller_order || b->b.order.empty() ? s : b->b.order[s]; }
-  // the statuses in caller order: rows of the store-order matrix scattered through the batch
-  // order, rules split over host threads (a permuted batch only)
+  bool has_status() const { return sparse || !status.empty(); }
+  static unsigned host_threads() { return std::max(1u, std::min<unsigned>(16u, std::thread::hardware_concurrency())); }
+  // out[c] = row[inv[c]] (a gather: sequential 8-byte stores, reads from a row that stays in the
+  // core's cache; 2.5x the rate of the scatter out[ord[q]] = row[q] on this host's cores)
+  static void gather_row(const uint8_t* row, const uint32_t* inv, uint64_t n, uint8_t* out) {
+    uint64_t c = 0;
+    for (; c + 8 <= n; c += 8) {
+      uint64_t v = 0;
+      for (int k = 0; k < 8; k++) v |= (uint64_t)row[inv[c + k]] << (8 * k);
+      memcpy(out + c, &v, 8);
+    }
+    for (; c < n; c++) out[c] = row[inv[c]];
+  }
+  // rows [rule][0, n_res) of dst from the parts' transfer form, rules split over host threads;
+  // with `inv` (caller index -> store index) each row is unpacked in store order and gathered
+  void unpack_rows(uint8_t* dst, const uint32_t* inv) const {
+    const unsigned T = host_threads();
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < T; t++)
+      th.emplace_back([&, t]() {
+        std::vector<uint8_t> tmp(inv ? n_res : 0);
+        for (uint64_t rl = t; rl < n_rules; rl += T) {
+          uint8_t* row = inv ? tmp.data() : dst + rl * n_res;
+          for (const ResultPart& p : parts) p.unpack_row((uint32_t)rl, row + p.lo);
+          if (inv) gather_row(row, inv, n_res, dst + rl * n_res);
+        }
+      });
+    for (auto& x : th) x.join();
+  }
+  // the status matrix in the records' order (store order unless caller_order), materialised from
+  // the transfer form on first use
+  const uint8_t* st_store() {
+    if (sparse)
+      std::call_once(st_once, [this]() {
+        status.alloc(n_rules * n_res);
+        unpack_rows(status.data(), nullptr);
+      });
+    return status.empty() ? nullptr : status.data();
+  }
+  // the statuses in caller order: rows of the store-order matrix gathered through the batch's
+  // inverse order, rules split over host threads (a permuted batch only); from the transfer form directly
+  // when the store-order matrix was not materialised
   const uint8_t* status_caller() {
-    if (b->b.order.empty() || status.empty() || caller_order) return status.empty() ? nullptr : status.data();
+    if (b->b.order.empty() || !has_status() || caller_order) return st_store();
     std::call_once(sc_once, [this]() {
-      status_c.alloc(status.size());
-      const uint32_t* ord = b->b.order.data();
-      const unsigned T = std::max(1u, std::min<unsigned>(16u, std::thread::hardware_concurrency()));
+      status_c.alloc(n_rules * n_res);
+      const uint32_t* inv = const_cast<kv_batch*>(b)->inverse();
+      if (status.empty()) {
+        unpack_rows(status_c.data(), inv);
+        return;
+      }
+      const unsigned T = host_threads();
       std::vector<std::thread> th;
       for (unsigned t = 0; t < T; t++)
         th.emplace_back([&, t]() {
-          for (uint64_t rl = t; rl < n_rules; rl += T) {
-            const uint8_t* in = status.data() + rl * n_res;
-            uint8_t* out = status_c.data() + rl * n_res;
-            for (uint64_t q = 0; q < n_res; q++) out[ord[q]] = in[q];
-          }
+          for (uint64_t rl = t; rl < n_rules; rl += T)
+            gather_row(status.data() + rl * n_res, inv, n_res, status_c.data() + rl * n_res);
         });
       for (auto& x : th) x.join();
     });
@@ -736,7 +813,7 @@ struct kv_result {
     const uint64_t local = res - p.lo;
     const uint64_t tile = local / KV_WG;
     uint64_t idx = p.base[rule] + p.offs[(size_t)rule * p.tiles + tile];
-    const uint8_t* row = status.data() + (size_t)rule * n_res;
+    const uint8_t* row = const_cast<kv_result*>(this)->st_store() + (size_t)rule * n_res;
     for (uint64_t q = p.lo + tile * KV_WG; q < res; q++) {
       const uint8_t s = row[q];
       idx += s == ST_FAIL || s == ST_ERROR || s == ST_SKIP;
@@ -952,21 +1029,22 @@ std::shared_ptr<DevBatchRes> dev_batch(kv_batch* bt, const PolicySet& ps, int de
   if (it != bt->dev.end()) return it->second;
   auto d = std::make_shared<DevBatchRes>();
   const Batch& b = bt->b;
-  if (b.rmask.size() != b.n_rows || b.roff.size() != b.n_rows)
+  if (b.rmask.size() != b.n_rows || b.rwide.size() != b.n_rows || b.roff.size() != b.n_rows)
     throw std::runtime_error("batch: packed row arrays do not match the row count");
   // packed rows: upload the non-zero cells, masks and row offsets, then expand to the
   // wave-group layout on the device. The page-locked arrays (rows, values, resources) go as
   // asynchronous copies on one stream, the expansion behind them, while this thread uploads the
   // pageable ones (strings, key table, match inputs) through the staging path beside them.
   hipStream_t us = StreamPool::get().take(device, hipStreamNonBlocking);
-  DevBuf pc, rm, ro;
-  pc.upload_async(b.pcells, device, us);
+  DevBuf pc, rm, rw, ro;
+  pc.upload_async(b.tcells, device, us);
   rm.upload_async(b.rmask, device, us);
+  rw.upload_async(b.rwide, device, us);
   ro.upload_async(b.roff, device, us);
-  d->nodes.alloc(b.n_cells() * sizeof(Node), device);
-  HIPCHK(launch_expand_rows((const Node*)pc.p, (const uint64_t*)rm.p, (const uint32_t*)ro.p, b.n_rows,
-                            (Node*)d->nodes.p, us));
   d->vals.upload_async(b.vals, device, us);
+  d->nodes.alloc(b.n_cells() * sizeof(Node), device);
+  HIPCHK(launch_expand_rows((const uint64_t*)pc.p, (const uint64_t*)rm.p, (const uint64_t*)rw.p, (const uint32_t*)ro.p,
+                            (const Val*)d->vals.p, b.n_rows, (Node*)d->nodes.p, us));
   d->res.upload_async(b.res, device, us);
   d->kvs.upload(b.kvs, device);
   d->bstr.upload_raw(b.strs.data(), b.strs.size(), device);
@@ -1037,6 +1115,7 @@ std::shared_ptr<DevBatchRes> dev_batch(kv_batch* bt, const PolicySet& ps, int de
   StreamPool::get().give(device, hipStreamNonBlocking, us);
   pc.release();
   rm.release();
+  rw.release();
   ro.release();
   if (bt->owner && bt->owner->jit && !bt->owner->jit->cols.empty() && !b.res.empty()) {
     build_pcol(*bt->owner->jit, b, d.get(), device);
@@ -1255,7 +1334,8 @@ struct DevSession {
   // be freed once the part is attached
   std::shared_ptr<DevBatchRes> batch_ref;
   DevBuf r_offs, r_tot, r_base, r_out8, r_outw, r_wide;  // record compaction (fetch)
-  DevBuf r_uni, r_urec, r_nbase, r_out8b;                // per-rule record deduplication (fetch)
+  DevBuf r_tkey, r_raw, r_nbase, r_code, r_out8b;        // record codes (fetch)
+  DevBuf s_ccnt, s_cbase, s_pack;                        // status transfer form (fetch)
   DevBuf inv_d, stc;                                     // caller-order statuses (fetch)
   DevBuf ord_d, r_mask;                                  // caller-order records: batch order, record lanes
   DevBuf stamps;                                         // KVGPU_STAMPS diagnostics
@@ -1658,6 +1738,7 @@ struct DevSession {
       if (verbose) fprintf(stderr, "[kvgpu] fetch: %s %.1f ms\n", what, ms);
     };
     const bool want_st = O.status && (mode & (KV_MODE_STATUS | KV_MODE_ERRORS)) && nres && nrules;
+    bool side_copy = false;
     if (O.status && O.sflag && rec_compact && nres && nrules) {  // the segments the pass left NOMATCH
       HIPCHK(launch_status_fill(O.status, O.sflag, (uint32_t)nres, (uint32_t)nrules, stream));
       lap("status_fill");
@@ -1666,14 +1747,51 @@ struct DevSession {
     // the device (stc[rule][j] = st[rule][store index of j]) and the records scattered to the
     // caller's (rule, resource) order, so one status matrix crosses PCIe and the host permutes
     // nothing. Its copy runs on the side stream, beside the record kernels.
-    bool caller = want_st && bt && lo == 0 && nres == n_total && !bt->b.order.empty();
+    // Specialized passes: the statuses cross in the transfer form (the segments the pass wrote, 4
+    // bits a status; C3: 0.48 GB for a 2.47 GB matrix) and the host materialises the matrix when an
+    // accessor reads it; records then stay in store order
+    const bool packed = want_st && out->sparse;
+    if (packed) {
+      const uint64_t nwg = (nres + KV_RWG - 1) / KV_RWG, nch = (nwg + KV_WG - 1) / KV_WG;
+      if (s_ccnt.n < nrules * nch * sizeof(uint32_t)) {
+        s_ccnt.alloc(nrules * nch * sizeof(uint32_t), device);
+        s_cbase.alloc(nrules * nch * sizeof(unsigned long long), device);
+      }
+      HIPCHK(launch_status_pack(O.status, O.sflag, (uint32_t)nres, (uint32_t)nrules, nullptr, (uint32_t*)s_ccnt.p,
+                                nullptr, stream));
+      std::vector<uint32_t> cc(nrules * nch);
+      std::vector<unsigned long long> cb(nrules * nch);
+      HIPCHK(hipMemcpyAsync(cc.data(), s_ccnt.p, cc.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      part->nwg = nwg;
+      part->sbase.resize(nrules);
+      unsigned long long t = 0;
+      for (size_t i = 0; i < cc.size(); i++) {
+        if (i % nch == 0) part->sbase[i / nch] = t;
+        cb[i] = t;
+        t += cc[i];
+      }
+      const uint64_t bytes = t * (KV_RWG / 2);
+      if (s_pack.n < std::max<uint64_t>(bytes, 1)) s_pack.alloc(std::max<uint64_t>(bytes, 1), device);
+      HIPCHK(hipMemcpyAsync(s_cbase.p, cb.data(), cb.size() * sizeof(unsigned long long), hipMemcpyHostToDevice, stream));
+      HIPCHK(launch_status_pack(O.status, O.sflag, (uint32_t)nres, (uint32_t)nrules,
+                                (const unsigned long long*)s_cbase.p, nullptr, (uint8_t*)s_pack.p, stream));
+      part->sflag.alloc(nrules * nwg);
+      part->spack.alloc(bytes);
+      HIPCHK(hipEventRecord(ev_fork, stream));
+      HIPCHK(hipStreamWaitEvent(side, ev_fork, 0));
+      HIPCHK(hipMemcpyAsync(part->sflag.data(), O.sflag, nrules * nwg, hipMemcpyDeviceToHost, side));
+      if (bytes) HIPCHK(hipMemcpyAsync(part->spack.data(), s_pack.p, bytes, hipMemcpyDeviceToHost, side));
+      side_copy = true;
+      lap("status_pack");
+    }
+    bool caller = !packed && want_st && bt && lo == 0 && nres == n_total && !bt->b.order.empty();
     if (caller && !stc.p) {  // the gathered copy is a second status matrix: only with room to spare
       size_t fr = 0, tot = 0;
       if (hipMemGetInfo(&fr, &tot) != hipSuccess) caller = false;
       fr += DevPool::get().held_on(device);  // (kept buffers are freed when an allocation needs them)
       if (fr < nrules * nres + nres * 8u + (512ull << 20)) caller = false;
     }
-    bool side_copy = false;
     if (caller) {
       if (!inv_d.p) inv_d.upload_raw(bt->inverse(), nres * sizeof(uint32_t), device);
       if (!stc.p) stc.alloc(nrules * nres, device);
@@ -1684,7 +1802,7 @@ struct DevSession {
       side_copy = true;
       out->caller_order = true;
       lap("status_gather");
-    } else if (want_st) {
+    } else if (want_st && !packed) {
       HIPCHK(hipMemcpy2DAsync(out->status.data() + lo, n_total, st.p, nres, nres, nrules, hipMemcpyDeviceToHost,
                               stream));
       lap("status_d2h");
@@ -1730,56 +1848,64 @@ struct DevSession {
       uint32_t wide = 0;
       HIPCHK(hipMemcpyAsync(&wide, r_wide.p, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
       lap("records_scatter");
-      // Per-rule deduplication: a rule whose records agree in all but their lane crosses as one
-      // record (C3: most of its 454 M records per pass); skipped when some record is wide (the full
-      // records of the re-run below are kept parallel to every compact record)
+      // Record codes: a rule's records cross PCIe as 1-byte codes into a table of its distinct
+      // records (C2: 206 MB of 8-byte records -> 26 MB of codes, C3: 3.6 GB -> 0.45 GB); skipped
+      // when some record is wide (the full records of the re-run below are kept parallel to every
+      // compact record)
       const ErrRec8* src = (const ErrRec8*)r_out8.p;
       uint64_t keep = total;
+      bool coded = false;
+      part->raw.clear();
       if (!wide && total && nrules) {
-        if (!r_uni.p) {
-          r_uni.alloc(nrules * sizeof(uint32_t), device);
-          r_urec.alloc(nrules * sizeof(ErrRec8), device);
+        const size_t tb = (size_t)nrules * KV_REC_CODES;
+        if (r_tkey.n < tb * sizeof(unsigned long long)) {
+          r_tkey.alloc(tb * sizeof(unsigned long long), device);
+          r_raw.alloc(nrules * sizeof(uint32_t), device);
           r_nbase.alloc(nrules * sizeof(unsigned long long), device);
         }
-        HIPCHK(hipMemsetAsync(r_uni.p, 1, r_uni.n, stream));
-        HIPCHK(launch_rec_dedup((const ErrRec8*)r_out8.p, (const unsigned long long*)r_base.p, (uint32_t)nrules,
-                                (uint32_t*)r_uni.p, (ErrRec8*)r_urec.p, nullptr, nullptr, 0, stream));
-        std::vector<uint32_t> uni(nrules);
-        part->urec.resize(nrules);
-        HIPCHK(hipMemcpyAsync(uni.data(), r_uni.p, nrules * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-        HIPCHK(hipMemcpyAsync(part->urec.data(), r_urec.p, nrules * sizeof(ErrRec8), hipMemcpyDeviceToHost, stream));
+        if (r_code.n < total) r_code.alloc(total, device);
+        HIPCHK(hipMemsetAsync(r_tkey.p, 0xFF, tb * sizeof(unsigned long long), stream));
+        HIPCHK(hipMemsetAsync(r_raw.p, 0, nrules * sizeof(uint32_t), stream));
+        HIPCHK(launch_rec_codes((const ErrRec8*)r_out8.p, (const unsigned long long*)r_base.p, (uint32_t)nrules,
+                                (unsigned long long*)r_tkey.p, (uint8_t*)r_code.p, (uint32_t*)r_raw.p, nullptr, nullptr,
+                                0, stream));
+        std::vector<uint32_t> rawf(nrules);
+        std::vector<unsigned long long> keys(tb);
+        HIPCHK(hipMemcpyAsync(rawf.data(), r_raw.p, nrules * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(keys.data(), r_tkey.p, tb * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
-        part->uni.assign(nrules, 0);
+        part->raw.assign(nrules, 0);
         part->nbase.assign(nrules, 0);
+        part->tab.assign(tb, ErrRec8{0u, 0u});
         keep = 0;
         for (uint64_t q = 0; q < nrules; q++) {
-          part->uni[q] = uni[q] ? 1 : 0;
+          part->raw[q] = rawf[q] ? 1 : 0;
           part->nbase[q] = keep;
-          if (!uni[q]) keep += part->base[q + 1] - part->base[q];
+          if (rawf[q]) keep += part->base[q + 1] - part->base[q];
         }
-        if (keep * 10 >= total * 9) {  // (little to gain: every record crosses)
-          part->uni.clear();
-          part->urec.clear();
-          part->nbase.clear();
-          keep = total;
-        } else if (keep) {
+        for (size_t t = 0; t < tb; t++)
+          if (keys[t] != ~0ull) part->tab[t] = ErrRec8{(uint32_t)(keys[t] >> 32), (uint32_t)keys[t]};
+        if (keep) {
           if (r_out8b.n < keep * sizeof(ErrRec8)) r_out8b.alloc(keep * sizeof(ErrRec8), device);
           HIPCHK(hipMemcpyAsync(r_nbase.p, part->nbase.data(), nrules * sizeof(unsigned long long),
                                 hipMemcpyHostToDevice, stream));
-          HIPCHK(launch_rec_dedup((const ErrRec8*)r_out8.p, (const unsigned long long*)r_base.p, (uint32_t)nrules,
-                                  (uint32_t*)r_uni.p, nullptr, (const unsigned long long*)r_nbase.p,
+          HIPCHK(launch_rec_codes((const ErrRec8*)r_out8.p, (const unsigned long long*)r_base.p, (uint32_t)nrules,
+                                  nullptr, nullptr, (uint32_t*)r_raw.p, (const unsigned long long*)r_nbase.p,
                                   (ErrRec8*)r_out8b.p, 1, stream));
           src = (const ErrRec8*)r_out8b.p;
         }
-        lap("records_dedup");
+        coded = true;
+        lap("records_code");
       }
       const auto th0 = std::chrono::steady_clock::now();
       part->rec.alloc(keep);
       if (part == &out->parts[0])
         out->phases.push_back(
             {"host_alloc", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count()});
+      if (coded) part->code.alloc(total);
       tl = std::chrono::steady_clock::now();
       if (keep) HIPCHK(hipMemcpyAsync(part->rec.data(), src, keep * sizeof(ErrRec8), hipMemcpyDeviceToHost, stream));
+      if (coded) HIPCHK(hipMemcpyAsync(part->code.data(), r_code.p, total, hipMemcpyDeviceToHost, stream));
       lap("records_d2h");
       if (wide) {  // re-run the pass once writing full records (same statuses), compact those too
         if (!er.p) er.alloc(nrules * nres * sizeof(ErrRec), device);
@@ -2035,7 +2161,9 @@ struct SessionSet {
     reduce();
     out->counts = counts_;
     if (mode & KV_MODE_SCOPES) out->scope_counts = scope_counts_;
-    if (parts[0]->O.status && (mode & (KV_MODE_STATUS | KV_MODE_ERRORS))) {
+    out->sparse = parts[0]->O.status && parts[0]->O.sflag && (mode & (KV_MODE_STATUS | KV_MODE_ERRORS)) && nres &&
+                  nrules && std::all_of(parts.begin(), parts.end(), [](const auto& p) { return p->rec_compact; });
+    if (parts[0]->O.status && (mode & (KV_MODE_STATUS | KV_MODE_ERRORS)) && !out->sparse) {
       HIPCHK(hipSetDevice(parts[0]->device));
       const auto ta = std::chrono::steady_clock::now();
       out->status.alloc(nrules * nres);
@@ -2240,6 +2368,12 @@ int kv_batch_info(const kv_batch* b, uint64_t* n_res, uint64_t* store_bytes) {
   return 0;
 }
 
+int kv_batch_transfer_bytes(const kv_batch* b, uint64_t* bytes) {
+  if (!b || !bytes) return KV_E_INVALID;
+  *bytes = b->b.transfer_bytes();
+  return 0;
+}
+
 int kv_validate(const kv_policyset* ps, const kv_batch* b, const char* ctx_json, int device, uint32_t mode,
                 kv_result** out, kv_error** err) {
   if (!ps || !b || !out) return fail(err, KV_E_INVALID, "null argument");
@@ -2379,7 +2513,7 @@ int kv_result_path(const kv_result* r, uint32_t rule, uint64_t res, char* buf, s
   if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
   res = r->sidx(res);
   size_t o = (size_t)rule * r->n_res + res;
-  if (r->status[o] != ST_FAIL) return KV_E_INVALID;
+  if (const_cast<kv_result*>(r)->st_store()[o] != ST_FAIL) return KV_E_INVALID;
   ErrRec e;
   const Batch* bt = nullptr;
   if (!r->err(rule, res, &e, &bt)) return KV_E_INVALID;
@@ -2396,7 +2530,7 @@ int kv_result_error(const kv_result* r, uint32_t rule, uint64_t res, uint32_t* k
   if (!r || !r->has_err()) return KV_E_INVALID;
   if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
   res = r->sidx(res);
-  const uint8_t st = r->status[(size_t)rule * r->n_res + res];
+  const uint8_t st = const_cast<kv_result*>(r)->st_store()[(size_t)rule * r->n_res + res];
   if (st != ST_FAIL && st != ST_ERROR && st != ST_SKIP) return KV_E_INVALID;
   ErrRec e;
   const Batch* bt = nullptr;
@@ -2413,7 +2547,7 @@ int kv_result_error_message(const kv_result* r, uint32_t rule, uint64_t res, con
   const uint64_t s = r->store_of(res);  // the batch's tables are in store order
   res = r->sidx(res);  // the caller's document of its resource `res`, the record of its status slot
   size_t o = (size_t)rule * r->n_res + res;
-  const uint8_t st = r->status[o];
+  const uint8_t st = const_cast<kv_result*>(r)->st_store()[o];
   if (st != ST_FAIL && st != ST_ERROR && st != ST_SKIP) return KV_E_INVALID;
   std::string m;
   try {
@@ -2449,12 +2583,12 @@ int kv_result_error_message(const kv_result* r, uint32_t rule, uint64_t res, con
 int kv_result_subst_error(const kv_result* r, uint32_t rule, uint64_t res, char* buf, size_t cap) {
   if (!r) return KV_E_INVALID;
   if (rule >= r->n_rules || res >= r->n_res) return KV_E_RANGE;
-  if (r->status.empty()) return KV_E_INVALID;  // counts-only result: no statuses were fetched
+  if (!r->has_status()) return KV_E_INVALID;  // counts-only result: no statuses were fetched
   const uint64_t s = r->store_of(res);          // (the batch's tables are in store order)
   res = r->sidx(res);
   try {
     const RuleRec& rr = r->ps->ps.rules[rule];
-    if (!rr.dyn || r->status[(size_t)rule * r->n_res + res] != ST_ERROR) return 0;
+    if (!rr.dyn || const_cast<kv_result*>(r)->st_store()[(size_t)rule * r->n_res + res] != ST_ERROR) return 0;
     const ResultPart* p = r->part_of(s);
     if (!p) return 0;
     kv_batch* kb = p->shard ? p->shard.get() : const_cast<kv_batch*>(r->b);
@@ -2487,8 +2621,9 @@ int kv_result_failures(const kv_result* cr, uint64_t* n, const uint32_t** rule, 
       std::unordered_map<uint64_t, uint32_t> compact;      // (path pnode, packed indices) -> path id
       std::unordered_map<std::string, uint32_t> rendered;  // wide records: by rendered path
       const PolicySet& ps = r->ps->ps;
+      const uint8_t* stm = r->st_store();
       for (uint32_t rl = 0; rl < r->n_rules; rl++) {
-        const uint8_t* row = r->status.data() + (size_t)rl * r->n_res;
+        const uint8_t* row = stm + (size_t)rl * r->n_res;
         for (const ResultPart& p : r->parts) {
           uint64_t i = p.base[rl];
           for (uint64_t q = p.lo; q < p.lo + p.n; q++) {

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "kvcell.h"
 #include "kv_layout.h"
 #include "kvdevtypes.h"
 
@@ -41,6 +42,10 @@ hipError_t launch_remap_u32(uint32_t* a, uint64_t n, const uint32_t* map, hipStr
 // record is flagged ERR8_WIDE. With `order` (store index -> caller index) phase 0 ran over the
 // caller-order statuses and phase 1 puts each record at its caller index's place.
 // NOMATCH into the status segments the specialized kernels did not write (DevOut::sflag)
+// the status transfer form: out == nullptr counts the written segments per (rule, chunk of KV_WG
+// segments) into ccnt[rule][chunk]; otherwise packs them (4 bits a status) at cbase[rule][chunk] * KV_RWG / 2
+hipError_t launch_status_pack(const uint8_t* status, const uint8_t* sflag, uint32_t n_res, uint32_t n_rules,
+                              const unsigned long long* cbase, uint32_t* ccnt, uint8_t* out, hipStream_t stream);
 hipError_t launch_status_fill(uint8_t* status, const uint8_t* sflag, uint32_t n_res, uint32_t n_rules,
                               hipStream_t stream);
 // site records of the specialized rule groups -> the members' records at their slots (kvdevtypes.h
@@ -52,12 +57,14 @@ hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const 
                               ErrRec8* out8, ErrRec* outw, uint32_t* wide, int phase, const uint8_t* compact,
                               const uint32_t* order, unsigned long long* masks, hipStream_t stream);
 
-// Per-rule record deduplication of a compacted record array (rule-major, rule r at
-// [base[r], base[r + 1])): phase 0 sets uni[rule] = 0 unless every record of the rule equals its
-// first in all but the lane field (uni preset non-zero) and urec[rule] = that first record; phase 1
-// copies the other rules' records to out[nbase[rule] ...)
-hipError_t launch_rec_dedup(const ErrRec8* rec, const unsigned long long* base, uint32_t n_rules, uint32_t* uni,
-                            ErrRec8* urec, const unsigned long long* nbase, ErrRec8* out, int phase, hipStream_t stream);
+// Record codes of a compacted record array (rule-major, rule r at [base[r], base[r + 1])): phase 0
+// writes each record's slot in its rule's table of KV_REC_CODES distinct records (tkey, keys w0 << 32
+// | w1 without the lane, preset ~0) as a 1-byte code, and flags raw[rule] (preset 0) when the table
+// fills up; phase 1 copies the raw rules' records to out[nbase[rule] ...)
+constexpr uint32_t KV_REC_CODES = 256;
+hipError_t launch_rec_codes(const ErrRec8* rec, const unsigned long long* base, uint32_t n_rules,
+                            unsigned long long* tkey, uint8_t* code, uint32_t* raw, const unsigned long long* nbase,
+                            ErrRec8* out, int phase, hipStream_t stream);
 
 constexpr uint32_t KV_SCOPE_CHUNK = 65536;  // resources per workgroup of the scope-count kernel
 constexpr uint32_t KV_SCOPE_LDS = 2048;     // scopes held in LDS (2048 x 8 x 4 B = 64 KB)
@@ -70,8 +77,8 @@ hipError_t launch_scope_counts(const uint8_t* status, const uint32_t* scope, uin
 
 // nodes[row][lane] = the packed cell of (row, lane) when bit `lane` of rmask[row] is set
 // (rank among the row's set bits, from roff[row]), else the zero cell (row padding)
-hipError_t launch_expand_rows(const Node* pcells, const uint64_t* rmask, const uint32_t* roff, uint64_t n_rows,
-                              Node* nodes, hipStream_t stream);
+hipError_t launch_expand_rows(const uint64_t* tcells, const uint64_t* rmask, const uint64_t* rwide, const uint32_t* roff,
+                              const Val* vals, uint64_t n_rows, Node* nodes, hipStream_t stream);
 
 // Path columns of a batch (kvcol.h, kvdevtypes.h ColDesc / ColFam; n_groups: 64-lane wave
 // groups, a multiple of 4). rows: for every family f > 0 the element rows of each wave group

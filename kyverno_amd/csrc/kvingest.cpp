@@ -435,7 +435,8 @@ struct Ingest {
   }
 
   uint64_t base_row = 0;  // first row of the current group
-  // the current group's padded rows (reused, cache-resident); packed into b.pcells at its end
+  const bool check_cells = getenv("KVGPU_CHECK_CELLS") != nullptr;
+  // the current group's padded rows (reused, cache-resident); packed into b.tcells at its end
   std::vector<Node> gcells;
   std::vector<uint64_t> gmask;  // lanes written per row of the group
   void set_cell(uint32_t row, uint32_t lane, const Node& v) {
@@ -516,12 +517,12 @@ struct Ingest {
     }
     // capacity for the rest of the part from the cells per group so far (+1/8), instead of
     // the vector's doubling (each doubling copies every cell written so far)
-    const size_t want = b.pcells.size() + gcells.size();
-    if (want > b.pcells.capacity()) {
+    const size_t want = b.tcells.size() + gcells.size();
+    if (want > b.tcells.capacity()) {
       size_t cap = want;
       if (expected_res > b.res.size())
         cap = std::max(cap, (size_t)((double)want / (double)b.res.size() * (double)expected_res * 1.125));
-      b.pcells.reserve(std::max(cap, b.pcells.capacity() * 2));
+      b.tcells.reserve(std::max(cap, b.tcells.capacity() * 2));
       if (expected_res > b.res.size()) {  // values, strings and headers grow in proportion
         const double f = (double)expected_res / (double)b.res.size() * 1.125;
         if (b.vals.capacity() < (size_t)(b.vals.size() * f)) b.vals.reserve((size_t)(b.vals.size() * f));
@@ -529,32 +530,49 @@ struct Ingest {
         if (b.res.capacity() < expected_res) b.res.reserve(expected_res);
       }
       b.rmask.reserve(std::max<size_t>(b.rmask.capacity() * 2, cap / KV_LANES + rows));
+      b.rwide.reserve(std::max<size_t>(b.rwide.capacity() * 2, cap / KV_LANES + rows));
       b.roff.reserve(std::max<size_t>(b.roff.capacity() * 2, cap / KV_LANES + rows));
     }
-    // packed rows: the non-zero cells of each row, its lane mask and first packed cell
-    size_t pc = b.pcells.size(), nw = 0;
+    // packed rows: the non-zero cells of each row in their transfer form (kv_layout.h), its
+    // lane mask, wide-lane mask and first 8-byte unit
+    size_t pc = b.tcells.size(), nw = 0;
     for (uint32_t row = 0; row < rows; row++) nw += (size_t)__builtin_popcountll(gmask[row]);
-    b.pcells.resize(pc + nw);
+    b.tcells.resize(pc + 2 * nw);
     const size_t r0 = b.rmask.size();
     b.rmask.resize(r0 + rows);
+    b.rwide.resize(r0 + rows);
     b.roff.resize(r0 + rows);
-    Node* out = b.pcells.data();
+    uint64_t* out = b.tcells.data();
+    uint64_t used = 0;
     for (uint32_t row = 0; row < rows; row++) {
       const Node* c = &gcells[(size_t)row * KV_LANES];
-      uint64_t m = 0;
+      uint64_t m = 0, wm = 0;
       b.roff[r0 + row] = (uint32_t)pc;
       for (uint64_t w = gmask[row]; w; w &= w - 1) {
         const uint32_t l = (uint32_t)__builtin_ctzll(w);
         if (c[l].kt | c[l].a | c[l].b | c[l].c) {
           m |= 1ull << l;
-          out[pc++] = c[l];
+          used++;
+          uint32_t hi;
+          if (cell_narrow(c[l], base_row + row, b.vals.data(), &hi)) {
+            if (check_cells) {  // KVGPU_CHECK_CELLS: the 8-byte form rebuilds the Node exactly
+              const Node r = cell_widen(c[l].kt, hi, base_row + row, b.vals.data());
+              if (memcmp(&r, &c[l], sizeof(Node)) != 0) throw std::runtime_error("ingest: transfer cell does not round-trip");
+            }
+            out[pc++] = (uint64_t)c[l].kt | (uint64_t)hi << 32;
+          } else {
+            wm |= 1ull << l;
+            memcpy(&out[pc], &c[l], sizeof(Node));
+            pc += 2;
+          }
         }
       }
       b.rmask[r0 + row] = m;
+      b.rwide[r0 + row] = wm;
     }
-    b.pcells.resize(pc);
-    if (b.pcells.size() >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: batch too large for 32-bit cell offsets");
-    b.cells_used = b.pcells.size();
+    b.tcells.resize(pc);
+    if (b.tcells.size() >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: batch too large for 32-bit cell offsets");
+    b.cells_used += used;
     group_n = 0;
   }
 
@@ -884,10 +902,11 @@ void order_vals(Batch& b) {
     out[perm[i]] = b.vals[i];
   }
   b.vals.swap(out);
-  for (Node& nd : b.pcells) {
-    const uint32_t t = node_type(nd.kt);
-    if (t == NT_BOOL || t == NT_INT || t == NT_FLOAT || t == NT_STR) nd.a = perm[nd.a];
-  }
+  // a scalar's Val id is the hi word of its first unit in both transfer forms
+  uint64_t* tc = b.tcells.data();
+  b.each_unit([&](uint64_t, uint64_t u, bool) {
+    if (node_scalar_t(node_type((uint32_t)tc[u]))) tc[u] = (tc[u] & 0xFFFFFFFFull) | (uint64_t)perm[tc[u] >> 32] << 32;
+  });
 }
 
 void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
@@ -965,11 +984,12 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
   if (H >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: string heap exceeds 4 GiB");
   if (R * KV_LANES >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: batch too large for 32-bit node indices");
   b.pin_store();
-  std::vector<uint64_t> pcb(P + 1, 0);  // packed-cell base of each part (its non-zero cells)
-  for (size_t k = 0; k < P; k++) pcb[k + 1] = pcb[k] + parts[k].pcells.size();
+  std::vector<uint64_t> pcb(P + 1, 0);  // transfer-unit base of each part (its non-zero cells)
+  for (size_t k = 0; k < P; k++) pcb[k + 1] = pcb[k] + parts[k].tcells.size();
   if (pcb[P] >= 0xFFFFFFF0ull) throw std::runtime_error("ingest: batch too large for 32-bit cell offsets");
-  b.pcells.resize(pcb[P]);
+  b.tcells.resize(pcb[P]);
   b.rmask.resize(R);
+  b.rwide.resize(R);
   b.roff.resize(R);
   b.strs.reserve(H + 16);  // + the word-reader pad appended after the merge (no 2nd copy)
   b.strs.assign(H, '\0');
@@ -1002,20 +1022,24 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
         x.v_off += h;
         b.kvs[kb[k] + i] = x;
       }
-      // packed cells with key ids, rows, values and string offsets rebased (a remapped cell
-      // stays non-zero: its row masks and offsets carry over, offset by the part's base)
-      Node* out = &b.pcells[pcb[k]];
-      for (size_t i = 0; i < q.pcells.size(); i++) {
-        Node nd = q.pcells[i];
-        const uint32_t t = node_type(nd.kt);
-        uint32_t key = node_key(nd.kt);
+      // packed cells with key ids, values and (16-byte cells') rows and string offsets rebased:
+      // each cell keeps its form (the 8-byte forms are rebase-invariant), so row masks and
+      // offsets carry over, offset by the part's base
+      uint64_t* out = &b.tcells[pcb[k]];
+      const uint64_t* in = q.tcells.data();
+      q.each_unit([&](uint64_t, uint64_t u, bool wide) {
+        uint64_t x = in[u];
+        const uint32_t t = node_type((uint32_t)x);
+        uint32_t key = node_key((uint32_t)x);
         if (key >= nstatic && key != KEY_NONE28) key = dmap[k][key - nstatic];
-        nd.kt = key << 4 | t;
-        if (t == NT_MAP || t == NT_ARR) nd.a += r0;
-        else if (t == NT_BOOL || t == NT_INT || t == NT_FLOAT || t == NT_STR) { nd.a = perm[nd.a]; nd.b += h; }
-        out[i] = nd;
-      }
+        uint32_t a = (uint32_t)(x >> 32);
+        if (node_scalar_t(t)) a = perm[a];
+        else if (wide && (t == NT_MAP || t == NT_ARR)) a += r0;
+        out[u] = (uint64_t)(key << 4 | t) | (uint64_t)a << 32;
+        if (wide) out[u + 1] = node_scalar_t(t) ? in[u + 1] + h : in[u + 1];  // (b += h: the low word, no carry)
+      });
       memcpy(&b.rmask[r0], q.rmask.data(), q.n_rows * sizeof(uint64_t));
+      memcpy(&b.rwide[r0], q.rwide.data(), q.n_rows * sizeof(uint64_t));
       for (uint64_t row = 0; row < q.n_rows; row++) b.roff[r0 + row] = q.roff[row] + (uint32_t)pcb[k];
       for (size_t i = 0; i < q.res.size(); i++) {
         Res r = q.res[i];
@@ -1029,10 +1053,11 @@ void merge_batches(std::vector<Batch>& parts, Batch& b, uint32_t nstatic) {
       }
       // the part's arrays are released here, in parallel (freed serially by the parts'
       // destructors they cost ~70 ms per million Pods on the GPU box: page unmapping)
-      StoreVec<Node>().swap(q.pcells);
+      StoreVec<uint64_t>().swap(q.tcells);
       decltype(q.vals)().swap(q.vals);
       decltype(q.res)().swap(q.res);
       decltype(q.rmask)().swap(q.rmask);
+      decltype(q.rwide)().swap(q.rwide);
       decltype(q.roff)().swap(q.roff);
       decltype(q.kvs)().swap(q.kvs);
       HeapStr().swap(q.strs);
@@ -1509,6 +1534,20 @@ void ingest_resources(const PolicySet& ps, const char* json, size_t len, const c
   b->bytes_referenced = b->cells_used * sizeof(Node) + b->vals.size() * sizeof(Val) + b->res.size() * sizeof(Res) +
                         b->kvs.size() * sizeof(KV) + b->strs.size() + b->nsms.size() * sizeof(StrRef) +
                         (b->lsets.size() + b->asets.size()) * sizeof(KVSet);
+  if (verbose)
+    fprintf(stderr,
+            "[kvgpu] ingest: transfer bytes: tcells %zu rmask+rwide %zu roff %zu vals %zu res %zu kvs %zu strs %zu "
+            "(cells used %zu, rows %zu)\n",
+            b->tcells.size() * 8, b->rmask.size() * 16, b->roff.size() * 4, b->vals.size() * sizeof(Val),
+            b->res.size() * sizeof(Res), b->kvs.size() * sizeof(KV), b->strs.size(), (size_t)b->cells_used,
+            (size_t)b->n_rows);
+}
+
+uint64_t Batch::transfer_bytes() const {
+  return tcells.size() * 8 + (rmask.size() + rwide.size()) * 8 + roff.size() * 4 + vals.size() * sizeof(Val) +
+         res.size() * sizeof(Res) + kvs.size() * sizeof(KV) + strs.size() + ns_bits.size() * 4 +
+         nsms.size() * sizeof(StrRef) + (lsets.size() + asets.size()) * sizeof(KVSet) +
+         (tup_rep.size() + tup_kent.size() + kent_rep.size()) * 4;
 }
 
 }  // namespace kvh

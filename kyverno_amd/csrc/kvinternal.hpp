@@ -10,6 +10,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "kvcell.h"
 #include "kv_layout.h"
 #include "kvjson.hpp"
 
@@ -262,22 +263,47 @@ using HeapStr = std::basic_string<char, std::char_traits<char>, StoreAlloc<char>
 struct Batch {
   // Node rows in packed form: the wave-group layout (kvingest.cpp) has n_rows rows of
   // KV_LANES cells (node index = row * KV_LANES + lane); the host keeps only the non-zero
-  // cells of every row in row order (`pcells`), a 64-bit lane mask per row (`rmask`) and
-  // the first packed cell of each row (`roff`). kv_validate uploads these and expands the
-  // rows on the device (kv_expand_rows_kernel), so the row padding (40+ % of the cells at
-  // C2) is never written on the host nor sent over PCIe.
+  // cells of every row in row order, in their transfer form (`tcells`, kv_layout.h: 8 bytes a
+  // cell, 16 for the lanes of the row's `rwide` mask), a 64-bit lane mask per row (`rmask`) and
+  // the first 8-byte unit of each row (`roff`). kv_validate uploads these and expands the rows
+  // on the device (kv_expand_rows_kernel), so neither the row padding (40+ % of the cells at
+  // C2) nor the Node fields that follow from the values cross PCIe.
   uint64_t n_rows = 0;
-  uint64_t cells_used = 0;           // populated cells (incl. absent-slot markers) = pcells.size()
+  uint64_t cells_used = 0;           // populated cells (incl. absent-slot markers)
   StoreVec<kv::Val> vals;
   StoreVec<kv::Res> res;
-  StoreVec<kv::Node> pcells;
-  StoreVec<uint64_t> rmask;
+  StoreVec<uint64_t> tcells;
+  StoreVec<uint64_t> rmask, rwide;
   StoreVec<uint32_t> roff;
+  // the transfer units of (row, lane), a set rmask bit
+  const uint64_t* unit(uint64_t row, uint64_t lane) const {
+    const uint64_t below = (1ull << lane) - 1ull;
+    return tcells.data() + roff[row] + __builtin_popcountll(rmask[row] & below) +
+           __builtin_popcountll(rwide[row] & below);
+  }
   // cell `idx` of the padded layout (zero Node where the row has no cell in that lane)
   kv::Node cell(uint64_t idx) const {
     const uint64_t row = idx / kv::KV_LANES, lane = idx % kv::KV_LANES;
     if (row >= n_rows || !((rmask[row] >> lane) & 1ull)) return kv::Node{0u, 0u, 0u, 0u};
-    return pcells[(uint64_t)roff[row] + (uint64_t)__builtin_popcountll(rmask[row] & ((1ull << lane) - 1ull))];
+    const uint64_t* u = unit(row, lane);
+    if ((rwide[row] >> lane) & 1ull)
+      return kv::Node{(uint32_t)u[0], (uint32_t)(u[0] >> 32), (uint32_t)u[1], (uint32_t)(u[1] >> 32)};
+    return kv::cell_widen((uint32_t)u[0], (uint32_t)(u[0] >> 32), row, vals.data());
+  }
+  // bytes the batch's store crosses PCIe in (kv_validate's upload)
+  uint64_t transfer_bytes() const;
+  // f(row, unit index, wide) for every cell of rows [0, n_rows), in unit order
+  template <class F>
+  void each_unit(F f) const {
+    uint64_t u = 0;
+    for (uint64_t row = 0; row < n_rows; row++) {
+      const uint64_t w = rwide[row];
+      for (uint64_t m = rmask[row]; m; m &= m - 1) {
+        const bool wide = (w >> __builtin_ctzll(m)) & 1ull;
+        f(row, u, wide);
+        u += wide ? 2 : 1;
+      }
+    }
   }
   uint64_t n_cells() const { return n_rows * kv::KV_LANES; }
   // store order: resource i of the store (its wave group, its status column) is resource
@@ -293,8 +319,9 @@ struct Batch {
   void pin_store() {
     vals = StoreVec<kv::Val>(StoreAlloc<kv::Val>(true));
     res = StoreVec<kv::Res>(StoreAlloc<kv::Res>(true));
-    pcells = StoreVec<kv::Node>(StoreAlloc<kv::Node>(true));
+    tcells = StoreVec<uint64_t>(StoreAlloc<uint64_t>(true));
     rmask = StoreVec<uint64_t>(StoreAlloc<uint64_t>(true));
+    rwide = StoreVec<uint64_t>(StoreAlloc<uint64_t>(true));
     roff = StoreVec<uint32_t>(StoreAlloc<uint32_t>(true));
     strs = HeapStr(StoreAlloc<char>(true));
   }

@@ -587,39 +587,47 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_scatter_kernel(const uint8_t* __
   if (e.w0 & ERR8_WIDE) atomicOr(wide, 1u);
 }
 
-// Records of a rule that agree in everything but their lane field (the failing path and message
-// are the same: C3's match-heavy rules fail at one pattern node) cross PCIe once per rule: uni[rule]
-// (preset non-zero) is cleared when some record of the rule differs from its first, urec[rule] =
-// that first record. Grid (x blocks, rules).
-__global__ __launch_bounds__(KV_WG) void kv_rec_uniform_kernel(const ErrRec8* __restrict__ rec,
-                                                                const unsigned long long* __restrict__ base,
-                                                                uint32_t* __restrict__ uni, ErrRec8* __restrict__ urec,
-                                                                uint32_t rule0) {
+// Record codes (fetch): the records of one rule take few distinct values once their lane field is
+// dropped (the failing pattern node and the loop indices: C3's image globs fail at one of a Pod's
+// few containers), so a rule's records cross PCIe as a 1-byte code per record into a per-rule table
+// of KV_REC_CODES distinct records. Per record: its key (w0, w1 without the lane) is looked up in
+// the rule's open-addressing table (keys in tkey, ~0: empty; a plain read first, a CAS only for a
+// key not seen yet) and its slot written as the code; a rule whose table fills up is flagged raw
+// (its records then cross whole, kv_rec_gather_kernel). Grid (x blocks, rules).
+__global__ __launch_bounds__(KV_WG) void kv_rec_code_kernel(const ErrRec8* __restrict__ rec,
+                                                             const unsigned long long* __restrict__ base,
+                                                             unsigned long long* __restrict__ tkey,
+                                                             uint8_t* __restrict__ code, uint32_t* __restrict__ raw,
+                                                             uint32_t rule0) {
   const uint32_t rule = rule0 + blockIdx.y;
   const unsigned long long b0 = base[rule], b1 = base[rule + 1];
-  if (b0 == b1) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) uni[rule] = 0u;  // (no records: nothing to keep)
-    return;
-  }
-  const ErrRec8 f = rec[b0];
-  if (blockIdx.x == 0 && threadIdx.x == 0) urec[rule] = f;
-  bool same = true;
+  unsigned long long* T = tkey + (size_t)rule * KV_REC_CODES;
   for (unsigned long long i = b0 + (unsigned long long)blockIdx.x * KV_WG + threadIdx.x; i < b1;
        i += (unsigned long long)gridDim.x * KV_WG) {
     const ErrRec8 e = rec[i];
-    same &= e.w0 == f.w0 && ((e.w1 ^ f.w1) & ERR8_IDX_MASK) == 0u;
+    const unsigned long long k = (unsigned long long)e.w0 << 32 | (e.w1 & ERR8_IDX_MASK);
+    uint32_t h = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 56) & (KV_REC_CODES - 1u), n = 0;
+    for (; n < KV_REC_CODES; n++, h = (h + 1u) & (KV_REC_CODES - 1u)) {
+      unsigned long long t = __hip_atomic_load(T + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == ~0ull) t = atomicCAS(T + h, ~0ull, k);  // (returns the old key: ~0 when this thread set it)
+      if (t == ~0ull || t == k) break;
+    }
+    if (n == KV_REC_CODES) {
+      raw[rule] = 1u;
+      continue;
+    }
+    code[i] = (uint8_t)h;
   }
-  if (!same) uni[rule] = 0u;
 }
 
-// the records of the rules that are not uniform, rule by rule, to out[nbase[rule] ...)
+// the records of the raw rules, rule by rule, to out[nbase[rule] ...)
 __global__ __launch_bounds__(KV_WG) void kv_rec_gather_kernel(const ErrRec8* __restrict__ rec,
                                                                const unsigned long long* __restrict__ base,
                                                                const unsigned long long* __restrict__ nbase,
-                                                               const uint32_t* __restrict__ uni, ErrRec8* __restrict__ out,
+                                                               const uint32_t* __restrict__ raw, ErrRec8* __restrict__ out,
                                                                uint32_t rule0) {
   const uint32_t rule = rule0 + blockIdx.y;
-  if (uni[rule]) return;
+  if (!raw[rule]) return;
   const unsigned long long b0 = base[rule], b1 = base[rule + 1], d = nbase[rule];
   for (unsigned long long i = b0 + (unsigned long long)blockIdx.x * KV_WG + threadIdx.x; i < b1;
        i += (unsigned long long)gridDim.x * KV_WG)
@@ -628,15 +636,16 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_gather_kernel(const ErrRec8* __r
 
 constexpr uint32_t kMaxGridY = 65535u;
 
-hipError_t launch_rec_dedup(const ErrRec8* rec, const unsigned long long* base, uint32_t n_rules, uint32_t* uni,
-                            ErrRec8* urec, const unsigned long long* nbase, ErrRec8* out, int phase, hipStream_t stream) {
+hipError_t launch_rec_codes(const ErrRec8* rec, const unsigned long long* base, uint32_t n_rules,
+                            unsigned long long* tkey, uint8_t* code, uint32_t* raw, const unsigned long long* nbase,
+                            ErrRec8* out, int phase, hipStream_t stream) {
   if (n_rules == 0) return hipSuccess;
   for (uint32_t q0 = 0; q0 < n_rules; q0 += kMaxGridY) {
     const dim3 grid(64, std::min(kMaxGridY, n_rules - q0));
     if (phase == 0)
-      hipLaunchKernelGGL(kv_rec_uniform_kernel, grid, dim3(KV_WG), 0, stream, rec, base, uni, urec, q0);
+      hipLaunchKernelGGL(kv_rec_code_kernel, grid, dim3(KV_WG), 0, stream, rec, base, tkey, code, raw, q0);
     else
-      hipLaunchKernelGGL(kv_rec_gather_kernel, grid, dim3(KV_WG), 0, stream, rec, base, nbase, uni, out, q0);
+      hipLaunchKernelGGL(kv_rec_gather_kernel, grid, dim3(KV_WG), 0, stream, rec, base, nbase, raw, out, q0);
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -678,6 +687,71 @@ hipError_t launch_gsite_expand(const uint32_t* gsite, const uint32_t* gcnt, cons
   for (uint32_t g0 = 0; g0 < n_groups; g0 += kMaxGridY) {  // (grid y holds at most 65535 groups)
     hipLaunchKernelGGL(kv_gsite_expand_kernel, dim3((nw + KV_WG / 64 - 1) / (KV_WG / 64), std::min(kMaxGridY, n_groups - g0)),
                        dim3(KV_WG), 0, stream, (const uint4*)gsite, gcnt, desc, mem, n_res, err8, g0);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// Status transfer form (kv_result materialises it on the host): the (rule, segment) status segments
+// the pass wrote (DevOut::sflag), 4 bits a status (ST_* < 16), KV_RWG / 2 bytes a segment,
+// rule-major in segment order. One workgroup per (chunk of KV_WG segments, rule): phase 0 counts
+// the chunk's written segments into ccnt[rule][chunk], phase 1 packs them at cbase[rule][chunk]
+// (the host's exclusive scan of ccnt, in segments).
+__device__ __forceinline__ uint32_t kv_nib4(uint32_t x) {  // 4 status bytes -> 16 bits
+  return (x & 0xFu) | ((x >> 4) & 0xF0u) | ((x >> 8) & 0xF00u) | ((x >> 12) & 0xF000u);
+}
+
+__global__ __launch_bounds__(KV_WG) void kv_status_pack_kernel(const uint8_t* __restrict__ status,
+                                                                const uint8_t* __restrict__ sflag,
+                                                                const unsigned long long* __restrict__ cbase,
+                                                                uint32_t* __restrict__ ccnt, uint32_t n_res,
+                                                                uint32_t nwg, uint32_t nch, uint8_t* __restrict__ out,
+                                                                uint32_t rule0) {
+  __shared__ uint32_t s_w[KV_WG / 64];
+  __shared__ uint32_t s_list[KV_WG];
+  const uint32_t rule = rule0 + blockIdx.y, g = blockIdx.x * KV_WG + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const bool f = g < nwg && sflag[(size_t)rule * nwg + g];
+  const unsigned long long m = __ballot(f);
+  if (lane == 0) s_w[w] = (uint32_t)__popcll(m);
+  __syncthreads();
+  uint32_t pre = (uint32_t)__popcll(m & ((1ull << lane) - 1ull)), cnt = 0;
+  for (uint32_t k = 0; k < KV_WG / 64; k++) {
+    if (k < w) pre += s_w[k];
+    cnt += s_w[k];
+  }
+  if (!out) {
+    if (threadIdx.x == 0) ccnt[(size_t)rule * nch + blockIdx.x] = cnt;
+    return;
+  }
+  if (f) s_list[pre] = g;
+  __syncthreads();
+  const uint8_t* row = status + (size_t)rule * n_res;
+  uint8_t* o = out + (size_t)cbase[(size_t)rule * nch + blockIdx.x] * (KV_RWG / 2);
+  constexpr uint32_t TPS = KV_RWG / 8;  // threads per segment, 8 statuses each
+  const uint32_t j = threadIdx.x % TPS;
+  const bool al = (((size_t)rule * n_res) & 7u) == 0;
+  for (uint32_t k = threadIdx.x / TPS; k < cnt; k += KV_WG / TPS) {
+    const uint64_t q = (uint64_t)s_list[k] * KV_RWG + 8u * j;
+    uint32_t v = 0;
+    if (al && q + 8u <= n_res) {
+      const uint2 x = *(const uint2*)(row + q);
+      v = kv_nib4(x.x) | kv_nib4(x.y) << 16;
+    } else {
+      for (uint32_t t = 0; t < 8u; t++)
+        if (q + t < n_res) v |= (uint32_t)(row[q + t] & 15u) << (4u * t);
+    }
+    *(uint32_t*)(o + (size_t)k * (KV_RWG / 2) + 4u * j) = v;
+  }
+}
+
+hipError_t launch_status_pack(const uint8_t* status, const uint8_t* sflag, uint32_t n_res, uint32_t n_rules,
+                              const unsigned long long* cbase, uint32_t* ccnt, uint8_t* out, hipStream_t stream) {
+  if (n_res == 0 || n_rules == 0) return hipSuccess;
+  const uint32_t nwg = (n_res + KV_RWG - 1) / KV_RWG, nch = (nwg + KV_WG - 1) / KV_WG;
+  for (uint32_t q0 = 0; q0 < n_rules; q0 += kMaxGridY) {
+    hipLaunchKernelGGL(kv_status_pack_kernel, dim3(nch, std::min(kMaxGridY, n_rules - q0)), dim3(KV_WG), 0, stream,
+                       status, sflag, cbase, ccnt, n_res, nwg, nch, out, q0);
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -816,29 +890,42 @@ hipError_t launch_scope_totals(const unsigned long long* scounts, uint32_t n_sco
   return hipGetLastError();
 }
 
-// One wave per row of the wave-group layout: lane l takes its packed cell (the number of
-// set mask bits below l is its rank in the row) or the zero cell. Reads the packed cells
-// and masks once, writes every cell once (coalesced 1 KB per row).
-__global__ __launch_bounds__(KV_WG) void kv_expand_rows_kernel(const Node* __restrict__ pcells,
+// One wave per row of the wave-group layout: lane l takes its packed cell (its units start at
+// the row's first unit + the set mask bits below l + the wide-mask bits below l) rebuilt into a
+// Node (kv_layout.h cell_widen: a scalar's string form from its Val), or the zero cell. Reads the
+// units and masks once, writes every cell once (coalesced 1 KB per row).
+__global__ __launch_bounds__(KV_WG) void kv_expand_rows_kernel(const uint64_t* __restrict__ tcells,
                                                                const uint64_t* __restrict__ rmask,
-                                                               const uint32_t* __restrict__ roff, uint64_t n_rows,
+                                                               const uint64_t* __restrict__ rwide,
+                                                               const uint32_t* __restrict__ roff,
+                                                               const Val* __restrict__ vals, uint64_t n_rows,
                                                                Node* __restrict__ nodes) {
   const uint64_t row = (uint64_t)blockIdx.x * (KV_WG / KV_LANES) + threadIdx.x / KV_LANES;
   if (row >= n_rows) return;
   const uint32_t lane = threadIdx.x & (KV_LANES - 1);
-  const uint64_t m = rmask[row];
+  const uint64_t m = rmask[row], below = (1ull << lane) - 1ull;
   Node v{0u, 0u, 0u, 0u};
-  if ((m >> lane) & 1ull) v = pcells[roff[row] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))];
+  if ((m >> lane) & 1ull) {
+    const uint64_t w = rwide[row];
+    const uint64_t* u = tcells + roff[row] + (uint32_t)__popcll(m & below) + (uint32_t)__popcll(w & below);
+    const uint64_t x = u[0];
+    if ((w >> lane) & 1ull) {
+      const uint64_t y = u[1];
+      v = Node{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32)};
+    } else {
+      v = cell_widen((uint32_t)x, (uint32_t)(x >> 32), row, vals);
+    }
+  }
   nodes[row * KV_LANES + lane] = v;
 }
 
-hipError_t launch_expand_rows(const Node* pcells, const uint64_t* rmask, const uint32_t* roff, uint64_t n_rows,
-                              Node* nodes, hipStream_t stream) {
+hipError_t launch_expand_rows(const uint64_t* tcells, const uint64_t* rmask, const uint64_t* rwide, const uint32_t* roff,
+                              const Val* vals, uint64_t n_rows, Node* nodes, hipStream_t stream) {
   if (n_rows == 0) return hipSuccess;
   const uint64_t blocks = (n_rows + KV_WG / KV_LANES - 1) / (KV_WG / KV_LANES);
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(kv_expand_rows_kernel, dim3((uint32_t)blocks), dim3(KV_WG), 0, stream, pcells, rmask, roff, n_rows,
-                     nodes);
+  hipLaunchKernelGGL(kv_expand_rows_kernel, dim3((uint32_t)blocks), dim3(KV_WG), 0, stream, tcells, rmask, rwide, roff,
+                     vals, n_rows, nodes);
   return hipGetLastError();
 }
 

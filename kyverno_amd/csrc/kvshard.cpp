@@ -24,16 +24,22 @@ void make_shard(const Batch& b, uint64_t lo, uint64_t hi, Batch* out) {
   const uint64_t row_lo = lo < b.res.size() ? b.res[lo].root : b.n_rows;
   const uint64_t row_hi = hi < b.res.size() ? b.res[hi].root : b.n_rows;
   s.n_rows = row_hi - row_lo;
-  // the shard's packed cells: rows [row_lo, row_hi)
-  const uint64_t c_lo = row_lo < b.n_rows ? b.roff[row_lo] : b.pcells.size();
-  const uint64_t c_hi = row_hi < b.n_rows ? b.roff[row_hi] : b.pcells.size();
-  const Node* src = b.pcells.data() + c_lo;
-  const size_t ncell = (size_t)(c_hi - c_lo);
-  // values referenced by the shard, renumbered in global order
+  // the shard's packed cells: rows [row_lo, row_hi), their transfer units [c_lo, c_hi)
+  const uint64_t c_lo = row_lo < b.n_rows ? b.roff[row_lo] : b.tcells.size();
+  const uint64_t c_hi = row_hi < b.n_rows ? b.roff[row_hi] : b.tcells.size();
+  const uint64_t* src = b.tcells.data() + c_lo;
+  s.rmask.assign(b.rmask.begin() + row_lo, b.rmask.begin() + row_hi);
+  s.rwide.assign(b.rwide.begin() + row_lo, b.rwide.begin() + row_hi);
+  s.roff.resize(s.n_rows);
+  for (uint64_t r = 0; r < s.n_rows; r++) s.roff[r] = b.roff[row_lo + r] - (uint32_t)c_lo;
+  // values referenced by the shard, renumbered in global order (a scalar's Val id is the hi
+  // word of its first unit in both transfer forms)
   std::vector<uint32_t> vmap(b.vals.size(), 0xFFFFFFFFu);
-  auto scalar = [](uint32_t t) { return t == NT_BOOL || t == NT_INT || t == NT_FLOAT || t == NT_STR; };
-  for (size_t i = 0; i < ncell; i++)
-    if (scalar(node_type(src[i].kt))) vmap[src[i].a] = 0;
+  size_t ncell = 0;
+  s.each_unit([&](uint64_t, uint64_t u, bool) {
+    ncell++;
+    if (node_scalar_t(node_type((uint32_t)src[u]))) vmap[src[u] >> 32] = 0;
+  });
   size_t nv = 0;
   for (uint32_t m : vmap) nv += m == 0;
   s.vals.reserve(nv);
@@ -42,18 +48,16 @@ void make_shard(const Batch& b, uint64_t lo, uint64_t hi, Batch* out) {
       vmap[v] = (uint32_t)s.vals.size();
       s.vals.push_back(b.vals[v]);
     }
-  s.pcells.resize(ncell);
-  for (size_t i = 0; i < ncell; i++) {
-    Node n = src[i];
-    const uint32_t t = node_type(n.kt);
-    if (t == NT_MAP || t == NT_ARR) n.a -= (uint32_t)row_lo;
-    else if (scalar(t)) n.a = vmap[n.a];
-    s.pcells[i] = n;
-  }
+  s.tcells.assign(src, src + (c_hi - c_lo));
+  uint64_t* tc = s.tcells.data();
+  s.each_unit([&](uint64_t, uint64_t u, bool wide) {
+    const uint32_t t = node_type((uint32_t)tc[u]);
+    uint32_t a = (uint32_t)(tc[u] >> 32);
+    if (node_scalar_t(t)) a = vmap[a];
+    else if (wide && (t == NT_MAP || t == NT_ARR)) a -= (uint32_t)row_lo;  // (the 8-byte form is row-relative)
+    tc[u] = (tc[u] & 0xFFFFFFFFull) | (uint64_t)a << 32;
+  });
   s.cells_used = ncell;
-  s.rmask.assign(b.rmask.begin() + row_lo, b.rmask.begin() + row_hi);
-  s.roff.resize(s.n_rows);
-  for (uint64_t r = 0; r < s.n_rows; r++) s.roff[r] = b.roff[row_lo + r] - (uint32_t)c_lo;
   s.res.assign(b.res.begin() + lo, b.res.begin() + hi);
   for (Res& r : s.res) r.root -= (uint32_t)row_lo;
   match_tuples(&s);  // the shard's own tuples (its table holds only those)

@@ -151,15 +151,15 @@ int main(int argc, char** argv) {
     P.n_vals = NV + KV_PTAB_PSEUDO;
     DevBatch B{};
     // the packed rows (what kv_validate uploads), expanded as kv_expand_rows_kernel does
-    if (b.rmask.size() != b.n_rows || b.roff.size() != b.n_rows)
+    if (b.rmask.size() != b.n_rows || b.rwide.size() != b.n_rows || b.roff.size() != b.n_rows)
       throw std::runtime_error("kvemu: packed row arrays do not match the batch");
     std::vector<Node> expanded(b.n_cells(), Node{0u, 0u, 0u, 0u});
     for (uint64_t row = 0; row < b.n_rows; row++)
       for (uint32_t l = 0; l < KV_LANES; l++)
         if ((b.rmask[row] >> l) & 1ull) {
-          const uint64_t at = (uint64_t)b.roff[row] + (uint64_t)__builtin_popcountll(b.rmask[row] & ((1ull << l) - 1ull));
-          if (at >= b.pcells.size()) throw std::runtime_error("kvemu: packed cell index out of range");
-          expanded[row * KV_LANES + l] = b.pcells[at];
+          if ((size_t)(b.unit(row, l) - b.tcells.data()) + ((b.rwide[row] >> l) & 1ull) >= b.tcells.size())
+            throw std::runtime_error("kvemu: packed cell index out of range");
+          expanded[row * KV_LANES + l] = b.cell(row * KV_LANES + l);
         }
     B.nodes = expanded.data();
     B.vals = b.vals.data();
