@@ -198,18 +198,28 @@ def check_rccl(ranks: int, devices) -> None:
 
 def e2e_stream(ps, n_res: int, kind_mix: int, device: int, seed: int, chunk: int) -> dict:
     """Ingest-inclusive rate of a caller streaming NDJSON through the C ABI: the batch is cut into
-    chunks; the host ingests chunk k+1 (kv_ingest, all host threads) while chunk k is uploaded,
-    evaluated and fetched (kv_validate: H2D of the page-locked store, one pass, D2H of statuses and
-    compacted records) on a second host thread (ctypes calls release the GIL). Timed from the
-    first NDJSON byte to the last chunk's results on the host."""
+    chunks; four host workers ingest chunks side by side (kv_ingest, a quarter of the host
+    threads each: one's serial phases overlap the others' parallel ones) while the chunks already ingested are
+    uploaded, evaluated and fetched (kv_validate: H2D of the page-locked store, one pass, D2H of
+    statuses and compacted records, the dense status matrix built on the host) on two more
+    threads (ctypes calls release the GIL). Timed from the first NDJSON byte to the last chunk's
+    results on the host."""
     import concurrent.futures as cf
 
     from kyverno_amd import batch
 
     chunks = [batch.synth(seed, min(chunk, n_res - k), kind_mix, first=k) for k in range(0, n_res, chunk)]
     mode = batch.MODE_STATUS | batch.MODE_ERRORS
-    results, t_ing, t_val = [], [0.0], [0.0]
-    inflight = 2  # chunks being uploaded / evaluated / fetched while the next one is ingested
+    t_ing, t_val = [0.0], [0.0]
+    inflight, ingesters = 2, 4  # chunks being uploaded / evaluated / fetched; chunks being ingested
+    threads = int(os.environ.get("KVGPU_INGEST_THREADS", min(16, os.cpu_count() or 1)))
+    per = max(1, threads // ingesters)
+
+    def ingest(data):
+        t = time.perf_counter()
+        b = batch.Batch(ps, data)
+        t_ing[0] += time.perf_counter() - t
+        return b
 
     def evaluate(b):
         t = time.perf_counter()
@@ -218,24 +228,39 @@ def e2e_stream(ps, n_res: int, kind_mix: int, device: int, seed: int, chunk: int
         t_val[0] += time.perf_counter() - t
         return r
 
-    t0 = time.perf_counter()
-    with cf.ThreadPoolExecutor(max_workers=inflight) as ex:
-        pending = []
-        for data in chunks:
-            t = time.perf_counter()
-            b = batch.Batch(ps, data)
-            t_ing[0] += time.perf_counter() - t
-            while len(pending) >= inflight:
-                results.append(pending.pop(0).result())
-            pending.append(ex.submit(evaluate, b))
-        results.extend(f.result() for f in pending)
-    secs = time.perf_counter() - t0
+    saved = os.environ.get("KVGPU_INGEST_THREADS")
+    os.environ["KVGPU_INGEST_THREADS"] = str(per)  # (read by each kv_ingest call)
+    try:
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(max_workers=ingesters) as ix, cf.ThreadPoolExecutor(max_workers=inflight) as vx:
+            ing = [ix.submit(ingest, d) for d in chunks[:ingesters]]
+            nxt, val, done = ingesters, [], 0
+            while ing:
+                b = ing.pop(0).result()
+                if nxt < len(chunks):
+                    ing.append(ix.submit(ingest, chunks[nxt]))
+                    nxt += 1
+                while len(val) >= inflight:
+                    val.pop(0).result()
+                    done += 1
+                val.append(vx.submit(evaluate, b))
+                del b
+            for f in val:
+                f.result()
+                done += 1
+        secs = time.perf_counter() - t0
+    finally:
+        if saved is None:
+            os.environ.pop("KVGPU_INGEST_THREADS", None)
+        else:
+            os.environ["KVGPU_INGEST_THREADS"] = saved
     n_rules = ps.n_rules
     return {"seconds": secs, "evals_per_s": n_res * n_rules / secs, "resources_per_s": n_res / secs,
-            "chunks": len(chunks), "chunk_resources": chunk, "in_flight": inflight, "ingest_seconds": t_ing[0],
-            "validate_seconds": t_val[0],
-            "includes": "NDJSON -> kv_ingest (host threads) overlapped with kv_validate of the previous chunks "
-                        "(H2D + pass + D2H of statuses and records + the dense status matrix, two in flight)"}
+            "chunks": len(chunks), "chunk_resources": chunk, "in_flight": inflight, "ingesters": ingesters,
+            "ingest_threads_each": per, "ingest_seconds": t_ing[0], "validate_seconds": t_val[0],
+            "includes": "NDJSON -> kv_ingest (four chunks at a time, a quarter of the host threads each) overlapped with "
+                        "kv_validate of the chunks ingested before (H2D + pass + D2H of statuses and records + "
+                        "the dense status matrix, two in flight)"}
 
 
 def main():
@@ -494,7 +519,7 @@ def main():
         del r2, b2
         # the same stream as a caller would push it: ingest overlapped with upload + pass + fetch
         out["e2e_stream"] = e2e_stream(ps, args.n_res, kind_mix, local, workloads.SEED + 13,
-                                       max(KV_LANES_CHUNK, args.n_res // 8))
+                                       max(KV_LANES_CHUNK, args.n_res // 16))
     if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
         # every core this process may run on (the GPU box grants a share of the machine's cores;
         # nproc and the CPU model are recorded beside it)
