@@ -1336,6 +1336,7 @@ struct DevSession {
   DevBuf r_offs, r_tot, r_base, r_out8, r_outw, r_wide;  // record compaction (fetch)
   DevBuf r_tkey, r_raw, r_nbase, r_code, r_out8b;        // record codes (fetch)
   DevBuf s_ccnt, s_cbase, s_pack;                        // status transfer form (fetch)
+  HostArray<uint8_t> hstage;                             // page-locked staging of the fetch's small copies
   DevBuf inv_d, stc;                                     // caller-order statuses (fetch)
   DevBuf ord_d, r_mask;                                  // caller-order records: batch order, record lanes
   DevBuf stamps;                                         // KVGPU_STAMPS diagnostics
@@ -1758,6 +1759,7 @@ struct DevSession {
     };
     const bool want_st = O.status && (mode & (KV_MODE_STATUS | KV_MODE_ERRORS)) && nres && nrules;
     bool side_copy = false;
+    uint64_t spack_bytes = 0;
     if (O.status && O.sflag && rec_compact && nres && nrules) {  // the segments the pass left NOMATCH
       HIPCHK(launch_status_fill(O.status, O.sflag, (uint32_t)nres, (uint32_t)nrules, stream));
       lap("status_fill");
@@ -1797,11 +1799,9 @@ struct DevSession {
                                 (const unsigned long long*)s_cbase.p, nullptr, (uint8_t*)s_pack.p, stream));
       part->sflag.alloc(nrules * nwg);
       part->spack.alloc(bytes);
-      HIPCHK(hipEventRecord(ev_fork, stream));
-      HIPCHK(hipStreamWaitEvent(side, ev_fork, 0));
-      HIPCHK(hipMemcpyAsync(part->sflag.data(), O.sflag, nrules * nwg, hipMemcpyDeviceToHost, side));
-      if (bytes) HIPCHK(hipMemcpyAsync(part->spack.data(), s_pack.p, bytes, hipMemcpyDeviceToHost, side));
-      side_copy = true;
+      // copied after the records: the record steps' small copies (offsets, flags, code tables)
+      // would otherwise queue behind these bytes on the copy engines at every host round trip
+      spack_bytes = bytes;
       lap("status_pack");
     }
     bool caller = !packed && want_st && bt && lo == 0 && nres == n_total && !bt->b.order.empty();
@@ -1847,26 +1847,36 @@ struct DevSession {
       HIPCHK(launch_rec_compact(rank_st, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                 (unsigned long long*)r_tot.p, (unsigned long long*)r_base.p, nullptr, nullptr, nullptr,
                                 0, rec_compact ? (const uint8_t*)dps->rcompact.p : nullptr, nullptr, masks, stream));
+      // the fetch's small device-to-host copies go through one page-locked staging block (a copy
+      // into pageable memory is staged by the runtime and waited for behind the DMA queue)
+      const size_t tb = (size_t)nrules * KV_REC_CODES, sb = ((nrules + 1) * 8 + 63) & ~(size_t)63;
+      if (hstage.size() < sb + nrules * 4 + 64 + tb * 8) hstage.alloc(sb + nrules * 4 + 64 + tb * 8);
       part->base.resize(nrules + 1);
       part->offs.alloc((size_t)nrules * tiles);
-      HIPCHK(hipMemcpyAsync(part->base.data(), r_base.p, part->base.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
-                            stream));
+      HIPCHK(hipMemcpyAsync(hstage.data(), r_base.p, part->base.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
       HIPCHK(hipMemcpyAsync(part->offs.data(), r_offs.p, part->offs.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
                             stream));
       lap("records_count");
+      memcpy(part->base.data(), hstage.data(), part->base.size() * sizeof(uint64_t));
       const uint64_t total = part->base[nrules];
-      if (r_out8.n < total * sizeof(ErrRec8)) r_out8.alloc(std::max<uint64_t>(total, 1) * sizeof(ErrRec8), device);
+      if (r_out8.n < total * sizeof(ErrRec8)) {
+        r_out8.alloc(std::max<uint64_t>(total, 1) * sizeof(ErrRec8), device);
+        lap("records_alloc");
+      }
       HIPCHK(hipMemsetAsync(r_wide.p, 0, sizeof(uint32_t), stream));
-      if (rec_compact && O.gsite)  // the groups' site records to their members' slots
+      if (rec_compact && O.gsite) {  // the groups' site records to their members' slots
         HIPCHK(launch_gsite_expand(O.gsite, O.gcnt, (const GSiteDesc*)dps->gsdesc.p, (const uint32_t*)dps->gsmem.p,
                                    dps->gs_groups, (uint32_t)nres, O.err8, stream));
+        lap("records_expand");
+      }
       HIPCHK(launch_rec_compact(O.status, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                 nullptr, (unsigned long long*)r_base.p, (ErrRec8*)r_out8.p, nullptr,
                                 (uint32_t*)r_wide.p, 1, rec_compact ? (const uint8_t*)dps->rcompact.p : nullptr, ord,
                                 masks, stream));
-      uint32_t wide = 0;
-      HIPCHK(hipMemcpyAsync(&wide, r_wide.p, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(hstage.data() + sb, r_wide.p, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
       lap("records_scatter");
+      uint32_t wide = 0;
+      memcpy(&wide, hstage.data() + sb, sizeof(uint32_t));
       // Record codes: a rule's records cross PCIe as 1-byte codes into a table of its distinct
       // records (C2: 206 MB of 8-byte records -> 26 MB of codes, C3: 3.6 GB -> 0.45 GB); skipped
       // when some record is wide (the full records of the re-run below are kept parallel to every
@@ -1876,7 +1886,6 @@ struct DevSession {
       bool coded = false;
       part->raw.clear();
       if (!wide && total && nrules) {
-        const size_t tb = (size_t)nrules * KV_REC_CODES;
         if (r_tkey.n < tb * sizeof(unsigned long long)) {
           r_tkey.alloc(tb * sizeof(unsigned long long), device);
           r_raw.alloc(nrules * sizeof(uint32_t), device);
@@ -1888,10 +1897,10 @@ struct DevSession {
         HIPCHK(launch_rec_codes((const ErrRec8*)r_out8.p, (const unsigned long long*)r_base.p, (uint32_t)nrules,
                                 (unsigned long long*)r_tkey.p, (uint8_t*)r_code.p, (uint32_t*)r_raw.p, nullptr, nullptr,
                                 0, stream));
-        std::vector<uint32_t> rawf(nrules);
-        std::vector<unsigned long long> keys(tb);
-        HIPCHK(hipMemcpyAsync(rawf.data(), r_raw.p, nrules * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-        HIPCHK(hipMemcpyAsync(keys.data(), r_tkey.p, tb * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+        const uint32_t* rawf = (const uint32_t*)hstage.data();
+        const unsigned long long* keys = (const unsigned long long*)(hstage.data() + ((nrules * 4 + 63) & ~(size_t)63));
+        HIPCHK(hipMemcpyAsync((void*)rawf, r_raw.p, nrules * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync((void*)keys, r_tkey.p, tb * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
         part->raw.assign(nrules, 0);
         part->nbase.assign(nrules, 0);
@@ -1940,6 +1949,11 @@ struct DevSession {
         HIPCHK(hipMemcpyAsync(part->recw.data(), r_outw.p, total * sizeof(ErrRec), hipMemcpyDeviceToHost, stream));
         lap("records_wide_rerun");
       }
+    }
+    if (packed) {  // the statuses' transfer form (kv_status_pack_kernel above; the re-run leaves it)
+      HIPCHK(hipMemcpyAsync(part->sflag.data(), O.sflag, part->sflag.size(), hipMemcpyDeviceToHost, stream));
+      if (spack_bytes) HIPCHK(hipMemcpyAsync(part->spack.data(), s_pack.p, spack_bytes, hipMemcpyDeviceToHost, stream));
+      lap("status_d2h");
     }
     HIPCHK(hipStreamSynchronize(stream));
     if (side_copy) {

@@ -599,24 +599,46 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_code_kernel(const ErrRec8* __res
                                                              unsigned long long* __restrict__ tkey,
                                                              uint8_t* __restrict__ code, uint32_t* __restrict__ raw,
                                                              uint32_t rule0) {
-  const uint32_t rule = rule0 + blockIdx.y;
+  const uint32_t rule = rule0 + blockIdx.y, lane = threadIdx.x & 63u;
   const unsigned long long b0 = base[rule], b1 = base[rule + 1];
   unsigned long long* T = tkey + (size_t)rule * KV_REC_CODES;
-  for (unsigned long long i = b0 + (unsigned long long)blockIdx.x * KV_WG + threadIdx.x; i < b1;
-       i += (unsigned long long)gridDim.x * KV_WG) {
-    const ErrRec8 e = rec[i];
-    const unsigned long long k = (unsigned long long)e.w0 << 32 | (e.w1 & ERR8_IDX_MASK);
-    uint32_t h = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 56) & (KV_REC_CODES - 1u), n = 0;
-    for (; n < KV_REC_CODES; n++, h = (h + 1u) & (KV_REC_CODES - 1u)) {
-      unsigned long long t = __hip_atomic_load(T + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t == ~0ull) t = atomicCAS(T + h, ~0ull, k);  // (returns the old key: ~0 when this thread set it)
-      if (t == ~0ull || t == k) break;
+  // a wave takes 64 consecutive records; its distinct keys are probed once each, by the first lane
+  // holding the key (a rule's records are few distinct values: one probe per lane would send every
+  // wave's loads of the same slot to one L2 channel)
+  for (unsigned long long w0 = b0 + (unsigned long long)blockIdx.x * KV_WG + (threadIdx.x & ~63u); w0 < b1;
+       w0 += (unsigned long long)gridDim.x * KV_WG) {
+    const unsigned long long i = w0 + lane;
+    const bool act = i < b1;
+    unsigned long long k = 0;
+    if (act) {
+      const ErrRec8 e = rec[i];
+      k = (unsigned long long)e.w0 << 32 | (e.w1 & ERR8_IDX_MASK);
     }
-    if (n == KV_REC_CODES) {
-      raw[rule] = 1u;
-      continue;
+    uint32_t slot = 0;
+    unsigned long long pending = __ballot(act);
+    while (pending) {
+      const int lead = __ffsll((long long)pending) - 1;
+      const unsigned long long lk = __shfl(k, lead);
+      const bool mine = ((pending >> lane) & 1ull) && k == lk;
+      const unsigned long long same = __ballot(mine);
+      int h = -1;
+      if (lane == (uint32_t)lead) {
+        uint32_t x = (uint32_t)((lk * 0x9E3779B97F4A7C15ull) >> 56) & (KV_REC_CODES - 1u);
+        for (uint32_t n = 0; n < KV_REC_CODES; n++, x = (x + 1u) & (KV_REC_CODES - 1u)) {
+          unsigned long long t = __hip_atomic_load(T + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (t == ~0ull) t = atomicCAS(T + x, ~0ull, lk);  // (returns the old key: ~0 when this lane set it)
+          if (t == ~0ull || t == lk) {
+            h = (int)x;
+            break;
+          }
+        }
+        if (h < 0) raw[rule] = 1u;  // more than KV_REC_CODES distinct records: the rule crosses raw
+      }
+      h = __shfl(h, lead);
+      if (mine) slot = (uint32_t)h;
+      pending &= ~same;
     }
-    code[i] = (uint8_t)h;
+    if (act) code[i] = (uint8_t)slot;  // (a raw rule's codes are not read)
   }
 }
 
