@@ -175,3 +175,36 @@ def test_ingest_paths_agree(orc):
     ost = oracle_status(orc, pols, ress)
     for tag, st in got.items():
         assert np.array_equal(st, ost), tag
+
+
+def test_wide_transfer_cells(orc):
+    """Cells that do not fit the 8-byte transfer form (kvcell.h: an array of 256+ elements, a
+    label map of 256+ keys) cross as 16-byte Nodes flagged in their row's wide mask; the batch
+    still rebuilds every cell (KVGPU_CHECK_CELLS at ingest, conftest) and the kernels' statuses
+    over it equal the oracle's."""
+    pol = {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "wide"},
+           "spec": {"rules": [
+               {"name": "img", "match": {"resources": {"kinds": ["Pod"]}},
+                "validate": {"pattern": {"spec": {"containers": [{"image": "!*:latest"}]}}}},
+               {"name": "team", "match": {"resources": {"kinds": ["Pod"]}},
+                "validate": {"pattern": {"metadata": {"labels": {"team": "?*"}}}}}]}}
+    ress = []
+    for i in range(200):
+        n = 300 if i % 3 == 0 else 2  # every third Pod: 300 containers (a wide array cell)
+        labels = {f"k{j}": "v" for j in range(260)} if i % 4 == 0 else {}
+        if i % 5:
+            labels["team"] = "a"
+        ress.append({"apiVersion": "v1", "kind": "Pod",
+                     "metadata": {"name": f"p{i}", "namespace": "ns", "labels": labels},
+                     "spec": {"containers": [{"name": f"c{j}", "image": "nginx:latest" if (i + j) % 97 == 5 else "nginx:1.2"}
+                                             for j in range(n)]}})
+    from kyverno_amd import batch
+
+    ps = batch.PolicySet([pol], specialize=False)
+    b = batch.Batch(ps, b"\n".join(json.dumps(r).encode() for r in ress))
+    assert 0 < b.transfer_bytes
+    st, _ = _emulate([pol], ress, "wide")
+    ost = oracle_status(orc, [pol], ress)
+    bad = np.argwhere(st != ost)
+    assert not len(bad), [(int(a), int(c), int(st[a, c]), int(ost[a, c])) for a, c in bad[:20]]
+    assert (st == 1).sum() > 0 and (st == 0).sum() > 0
