@@ -89,8 +89,6 @@ struct Gen {
   // it) and are placed at the top of their chunk / fused-loop body, so the loads of one
   // tree level issue together instead of one dependent wait per lookup.
   explicit Gen(const PolicySet& p) : ps(p), rec_slot(p.rules.size(), 0) {
-    const char* c = getenv("KVGPU_JIT_COLS");
-    cols_on = !(c && !strcmp(c, "0"));
     fams.emplace_back();
     col_of(0, "R");  // column 0 of family 0: the root
   }
@@ -103,7 +101,6 @@ struct Gen {
   // of one array path (a column of family 0). Columns are numbered in order of first use; the
   // column count of each family is a macro (KVC_J<f>) defined at the head of every kernel
   // program once the whole image is generated.
-  bool cols_on = true;
   // Site records of rule groups (kvdevtypes.h GSiteDesc): per group of 2+ members its descriptor
   // (n, gpre, moff, 0) in gs_desc and its members' (rule, pattern-node shift) in gs_mem, numbered
   // in generation order over the image; k_gs0 / k_gsn: the first group and the groups of the kernel
@@ -1541,10 +1538,8 @@ struct Gen {
     std::vector<RGen> gs;
     HoistTable global;
     global.prefix = "g";
-    if (cols_on) {
-      global.fam = 0;
-      global.cell0 = "gc_";
-    }
+    global.fam = 0;
+    global.cell0 = "gc_";
     gT = &global;
     size_t K = 0;
     for (uint32_t q = 0; q < nr; q++) {
@@ -1833,7 +1828,7 @@ struct Gen {
         const std::string troot = "E" + tag;
         // the elements' lookups from the columns of the array's family (the array must be a
         // column itself: its cell carries the offset of its element rows)
-        const uint32_t fam = cols_on && key[0] == 'R' && fams[0].idx.count(key) ? family(key) : kNoCol;
+        const uint32_t fam = key[0] == 'R' && fams[0].idx.count(key) ? family(key) : kNoCol;
         if (fam != kNoCol) {
           T.fam = (int)fam;
           T.troot = troot;
@@ -2023,12 +2018,10 @@ struct Gen {
       << "  uint32_t root = ABSENT, rkind = KEY_NONE, rflags = 0u, rtup = 0u;\n"
       << "  if (valid) { root = ni(kv_gld(&R->root, 0)); rkind = kv_gld(&R->kind, 0); rflags = kv_gld(&R->flags, 0); rtup = kv_gld(&R->tup, 0); }\n"
       << "  Node rootn{0u, 0u, 0u, 0u};\n";
-    if (cols_on)  // path columns (kvdevtypes.h): cell offset of this lane's family-0 columns; column 0 = the root
-      o << "  const uint32_t* __restrict__ PC = B.pcol;\n  const uint32_t* __restrict__ PCB = B.pcolb;\n"
+    // path columns (kvdevtypes.h): cell offset of this lane's family-0 columns; column 0 = the root
+    o << "  const uint32_t* __restrict__ PC = B.pcol;\n  const uint32_t* __restrict__ PCB = B.pcolb;\n"
         << "  const uint32_t ln_ = threadIdx.x & " << u32(KV_LANES - 1) << ", gc_ = (r >> 6) * (KVC_J0 * " << u32(KV_LANES)
         << ") + ln_;\n  if (valid) rootn = kv_ldc(PC, PCB, gc_);\n";
-    else
-      o << "  if (valid) rootn = N[root];\n";
     o
       << "  const uint32_t* __restrict__ mtr_ = P.mtup + rtup;\n  const uint32_t ntup_ = B.n_tup;\n"
       << "  uint8_t* s_w = (uint8_t*)s_stw;\n"
@@ -2375,11 +2368,6 @@ void jit_generate(const PolicySet& ps, uint32_t chunk_rules, JitImage* out) {
   std::string cdefs;  // the column count of every path-column family (KVC_J<f>)
   g.col_plan(out, &cdefs);
 
-  if (!g.cols_on) {
-    out->cols.clear();
-    out->fam_arr.clear();
-    out->fam_ncols.clear();
-  }
   out->memo_preds.clear();
   out->memo_words = 0;
   if (!g.mpreds.empty() && !out->probe) {
