@@ -324,3 +324,32 @@ def test_group_site_records(orc, spec):
         for k in range(len(rules)):
             if r.status[k, j] == 1:
                 assert r.path(k, j) == ov["rules"][k]["path"], (k, j)
+
+
+@engines
+def test_record_codes_raw_rules(orc, spec):
+    """Error records cross PCIe as 1-byte codes into a per-rule table of at most 256 distinct
+    records (kv_rec_code_kernel); a rule with more distinct records (here: one failing container
+    index per resource, 600 indices) crosses raw. Both kinds in one result: paths vs the oracle and
+    the failures export against kv_result_path."""
+    rules = [{"name": "no-latest", "match": {"resources": {"kinds": ["Pod"]}},
+              "validate": {"pattern": {"spec": {"containers": [{"image": "!*:latest"}]}}}},
+             {"name": "team", "match": {"resources": {"kinds": ["Pod"]}},
+              "validate": {"pattern": {"metadata": {"labels": {"team": "?*"}}}}}]
+    pol = {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "codes"}, "spec": {"rules": rules}}
+    ress = []
+    for i in range(700):
+        n = i % 600 + 1
+        cs = [{"name": f"c{j}", "image": "reg.io/app:1"} for j in range(n)]
+        cs[-1]["image"] = "reg.io/app:latest"
+        labels = {"team": "a"} if i % 3 else {}
+        ress.append({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": f"p{i}", "labels": labels},
+                     "spec": {"containers": cs}})
+    mism, r, ost = compare(orc, [pol], ress, check_paths=True, max_path_checks=2000, specialize=spec)
+    assert not mism, "\n".join(mism)
+    assert (r.status[0] == 1).sum() == 700 and (r.status[1] == 1).sum() == 234
+    rule, res, pid, paths = r.failures()
+    assert len(rule) == 934
+    for i in range(0, len(rule), 7):
+        assert paths[pid[i]] == r.path(int(rule[i]), int(res[i]))
+    assert len({paths[p] for p, q in zip(pid, rule) if q == 0}) == 600
