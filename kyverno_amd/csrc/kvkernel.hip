@@ -473,21 +473,27 @@ namespace kv {
 
 __device__ __forceinline__ bool has_record(uint8_t s) { return s == ST_FAIL || s == ST_ERROR || s == ST_SKIP; }
 
+// A workgroup walks tiles blockIdx.x, + gridDim.x, ... of one rule (a workgroup per (tile, rule)
+// was 9.6 M workgroups at C3, 8 ms of dispatch for 2.5 GB of statuses)
 __global__ __launch_bounds__(KV_WG) void kv_rec_count_kernel(const uint8_t* __restrict__ status, uint32_t n_res,
                                                               uint32_t tiles, uint32_t* __restrict__ counts,
-                                                              unsigned long long* __restrict__ masks) {
+                                                              unsigned long long* __restrict__ masks, uint32_t rule0) {
   __shared__ uint32_t s_w[KV_WG / 64];
-  const uint32_t rule = blockIdx.y, r = blockIdx.x * KV_WG + threadIdx.x;
-  const bool f = r < n_res && has_record(status[(size_t)rule * n_res + r]);
-  const uint64_t m = __ballot(f);
-  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = (uint32_t)__popcll(m);
-  // (caller-order fetch: every wave's record lanes, the ranks of the scatter below)
-  if (masks && (threadIdx.x & 63) == 0) masks[(size_t)rule * tiles * (KV_WG / 64) + (r >> 6)] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (int w = 0; w < KV_WG / 64; w++) t += s_w[w];
-    counts[(size_t)rule * tiles + blockIdx.x] = t;
+  const uint32_t rule = rule0 + blockIdx.y;
+  for (uint32_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const uint32_t r = t * KV_WG + threadIdx.x;
+    const bool f = r < n_res && has_record(status[(size_t)rule * n_res + r]);
+    const uint64_t m = __ballot(f);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+    // (caller-order fetch: every wave's record lanes, the ranks of the scatter below)
+    if (masks && (threadIdx.x & 63) == 0) masks[(size_t)rule * tiles * (KV_WG / 64) + (r >> 6)] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t n = 0;
+      for (int w = 0; w < KV_WG / 64; w++) n += s_w[w];
+      counts[(size_t)rule * tiles + t] = n;
+    }
+    __syncthreads();
   }
 }
 
@@ -547,44 +553,51 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_scatter_kernel(const uint8_t* __
                                                                 uint32_t* __restrict__ wide,
                                                                 const uint8_t* __restrict__ compact,
                                                                 const uint32_t* __restrict__ order,
-                                                                const unsigned long long* __restrict__ masks) {
+                                                                const unsigned long long* __restrict__ masks,
+                                                                uint32_t rule0) {
   __shared__ uint32_t s_w[KV_WG / 64];
-  const uint32_t rule = blockIdx.y, r = blockIdx.x * KV_WG + threadIdx.x, lane = threadIdx.x & 63;
-  const size_t o = (size_t)rule * n_res + r;
-  const bool f = r < n_res && has_record(status[o]);
-  const uint64_t m = __ballot(f);
-  if (lane == 0) s_w[threadIdx.x >> 6] = (uint32_t)__popcll(m);
-  __syncthreads();
-  uint32_t before = 0;  // records of the tile's earlier waves
-  for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) before += s_w[w];
-  const unsigned long long tile0 = base[rule] + offs[(size_t)rule * tiles + blockIdx.x] + before;
-  // destination of the record of store slot s (rank `rk` among the wave's record lanes): the store
-  // order, or with `order` the caller's (offs / base over the caller-order statuses, `masks` their
-  // record lanes per wave: the rank of caller index j in its tile)
-  auto dest = [&](uint32_t s, uint32_t rk) -> unsigned long long {
-    if (!order) return tile0 + rk;
-    const uint32_t j = order[s];
-    const unsigned long long* mr = masks + (size_t)rule * tiles * (KV_WG / 64);
-    uint32_t q = (uint32_t)__popcll(mr[j >> 6] & ((1ull << (j & 63u)) - 1ull));
-    for (uint32_t w = (j >> 6) & ~3u; w < (j >> 6); w++) q += (uint32_t)__popcll(mr[w]);
-    return base[rule] + offs[(size_t)rule * tiles + (j >> 8)] + q;
-  };
-  if (compact && compact[rule]) {  // (rule is uniform: a scalar branch)
-    // slot `lane` of the wave's segment holds the wave's lane-th record written; its lane field
-    // gives its rank among the wave's record lanes
-    if (lane >= (uint32_t)__popcll(m)) return;
-    const ErrRec8 e = err8[o];
-    const uint32_t l = e.w1 >> 26;
-    out8[dest((r & ~63u) + l, (uint32_t)__popcll(m & ((1ull << l) - 1ull)))] = e;
-    if (e.w0 & ERR8_WIDE) atomicOr(wide, 1u);
-    return;
+  const uint32_t rule = rule0 + blockIdx.y, lane = threadIdx.x & 63;
+  const bool cmp = compact && compact[rule];  // (rule is uniform: a scalar branch)
+  const unsigned long long rb = base[rule];
+  for (uint32_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const uint32_t r = t * KV_WG + threadIdx.x;
+    const size_t o = (size_t)rule * n_res + r;
+    const bool f = r < n_res && has_record(status[o]);
+    const uint64_t m = __ballot(f);
+    if (lane == 0) s_w[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0;  // records of the tile's earlier waves
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) before += s_w[w];
+    const unsigned long long tile0 = rb + offs[(size_t)rule * tiles + t] + before;
+    // destination of the record of store slot s (rank `rk` among the wave's record lanes): the store
+    // order, or with `order` the caller's (offs / base over the caller-order statuses, `masks` their
+    // record lanes per wave: the rank of caller index j in its tile)
+    auto dest = [&](uint32_t s, uint32_t rk) -> unsigned long long {
+      if (!order) return tile0 + rk;
+      const uint32_t j = order[s];
+      const unsigned long long* mr = masks + (size_t)rule * tiles * (KV_WG / 64);
+      uint32_t q = (uint32_t)__popcll(mr[j >> 6] & ((1ull << (j & 63u)) - 1ull));
+      for (uint32_t w = (j >> 6) & ~3u; w < (j >> 6); w++) q += (uint32_t)__popcll(mr[w]);
+      return rb + offs[(size_t)rule * tiles + (j >> 8)] + q;
+    };
+    if (cmp) {
+      // slot `lane` of the wave's segment holds the wave's lane-th record written; its lane field
+      // gives its rank among the wave's record lanes
+      if (lane < (uint32_t)__popcll(m)) {
+        const ErrRec8 e = err8[o];
+        const uint32_t l = e.w1 >> 26;
+        out8[dest((r & ~63u) + l, (uint32_t)__popcll(m & ((1ull << l) - 1ull)))] = e;
+        if (e.w0 & ERR8_WIDE) atomicOr(wide, 1u);
+      }
+    } else if (f) {
+      const unsigned long long idx = dest(r, (uint32_t)__popcll(m & ((1ull << lane) - 1ull)));
+      const ErrRec8 e = err8[o];
+      out8[idx] = e;
+      if (outw) outw[idx] = errw[o];
+      if (e.w0 & ERR8_WIDE) atomicOr(wide, 1u);
+    }
+    __syncthreads();
   }
-  if (!f) return;
-  const unsigned long long idx = dest(r, (uint32_t)__popcll(m & ((1ull << lane) - 1ull)));
-  const ErrRec8 e = err8[o];
-  out8[idx] = e;
-  if (outw) outw[idx] = errw[o];
-  if (e.w0 & ERR8_WIDE) atomicOr(wide, 1u);
 }
 
 // Record codes (fetch): the records of one rule take few distinct values once their lane field is
@@ -811,14 +824,21 @@ hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const 
                               const uint32_t* order, unsigned long long* masks, hipStream_t stream) {
   if (n_res == 0 || n_rules == 0) return hipSuccess;
   const uint32_t tiles = (n_res + KV_WG - 1) / KV_WG;
-  if (phase == 0) {  // offsets and bases
-    hipLaunchKernelGGL(kv_rec_count_kernel, dim3(tiles, n_rules), dim3(KV_WG), 0, stream, status, n_res, tiles, offs,
-                       masks);
+  // about 65 536 workgroups in all, each walking its rule's tiles (C3: 16 384 in all left the
+  // scatter latency-bound at 6 ms, 9.6 M dispatch-bound at 8.4 ms)
+  const uint32_t gx = std::max(1u, std::min(tiles, 65536u / n_rules));
+  for (uint32_t q0 = 0; q0 < n_rules; q0 += kMaxGridY) {
+    const dim3 grid(gx, std::min(kMaxGridY, n_rules - q0));
+    if (phase == 0)  // offsets (the scan and bases below)
+      hipLaunchKernelGGL(kv_rec_count_kernel, grid, dim3(KV_WG), 0, stream, status, n_res, tiles, offs, masks, q0);
+    else
+      hipLaunchKernelGGL(kv_rec_scatter_kernel, grid, dim3(KV_WG), 0, stream, status, err8, errw, n_res, tiles, offs,
+                         base, out8, outw, wide, compact, order, masks, q0);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  }
+  if (phase == 0) {
     hipLaunchKernelGGL(kv_rec_scan_kernel, dim3(n_rules), dim3(KV_WG), 0, stream, offs, tiles, totals);
     hipLaunchKernelGGL(kv_rec_base_kernel, dim3(1), dim3(KV_WG), 0, stream, totals, n_rules, base);
-  } else {
-    hipLaunchKernelGGL(kv_rec_scatter_kernel, dim3(tiles, n_rules), dim3(KV_WG), 0, stream, status, err8, errw, n_res,
-                       tiles, offs, base, out8, outw, wide, compact, order, masks);
   }
   return hipGetLastError();
 }
