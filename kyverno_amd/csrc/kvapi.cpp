@@ -657,6 +657,7 @@ struct ResultPart {
   uint64_t nwg = 0;
   // statuses [lo, lo + n) of rule `rule` from the transfer form into dst[0, n)
   void unpack_row(uint32_t rule, uint8_t* dst) const {
+    if (!n || sbase.empty()) return;  // (a part without resources packs nothing)
     const uint8_t* f = sflag.data() + (size_t)rule * nwg;
     const uint8_t* src = spack.data() + sbase[rule] * (KV_RWG / 2);
     const __m128i lo4 = _mm_set1_epi8(0x0F);
