@@ -196,7 +196,7 @@ def check_rccl(ranks: int, devices) -> None:
                          f"({distinct} distinct devices among {len(devices)} parts)")
 
 
-def e2e_stream(ps, n_res: int, kind_mix: int, device: int, seed: int, chunk: int) -> dict:
+def e2e_stream(ps, n_res: int, kind_mix: int, device: int, seed: int, chunk: int, ingesters: int = 4) -> dict:
     """Ingest-inclusive rate of a caller streaming NDJSON through the C ABI: the batch is cut into
     chunks; four host workers ingest chunks side by side (kv_ingest, a quarter of the host
     threads each: one's serial phases overlap the others' parallel ones) while the chunks already ingested are
@@ -211,7 +211,7 @@ def e2e_stream(ps, n_res: int, kind_mix: int, device: int, seed: int, chunk: int
     chunks = [batch.synth(seed, min(chunk, n_res - k), kind_mix, first=k) for k in range(0, n_res, chunk)]
     mode = batch.MODE_STATUS | batch.MODE_ERRORS
     t_ing, t_val = [0.0], [0.0]
-    inflight, ingesters = 2, 4  # chunks being uploaded / evaluated / fetched; chunks being ingested
+    inflight = 2  # chunks being uploaded / evaluated / fetched (and `ingesters` chunks being ingested)
     threads = int(os.environ.get("KVGPU_INGEST_THREADS", min(16, os.cpu_count() or 1)))
     per = max(1, threads // ingesters)
 
@@ -281,6 +281,8 @@ def main():
                          "c5: background scan, chart after autogen (105 rules) x mixed kinds, counts")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive kv_validate timing")
+    ap.add_argument("--stream-ingesters", type=int, default=4,
+                    help="e2e_stream: chunks ingested side by side (the host threads split among them)")
     ap.add_argument("--cpu-pairs", type=float, default=6e7,
                     help="resource x rule pairs of the CPU baseline sample (~10 s on 16 EPYC cores at C2)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default=None,
@@ -519,7 +521,7 @@ def main():
         del r2, b2
         # the same stream as a caller would push it: ingest overlapped with upload + pass + fetch
         out["e2e_stream"] = e2e_stream(ps, args.n_res, kind_mix, local, workloads.SEED + 13,
-                                       max(KV_LANES_CHUNK, args.n_res // 16))
+                                       max(KV_LANES_CHUNK, args.n_res // 16), args.stream_ingesters)
     if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
         # every core this process may run on (the GPU box grants a share of the machine's cores;
         # nproc and the CPU model are recorded beside it)
