@@ -353,3 +353,29 @@ def test_record_codes_raw_rules(orc, spec):
     for i in range(0, len(rule), 7):
         assert paths[pid[i]] == r.path(int(rule[i]), int(res[i]))
     assert len({paths[p] for p, q in zip(pid, rule) if q == 0}) == 600
+
+
+@engines
+@pytest.mark.parametrize("n", [1, 255, 256, 257, 513])
+def test_status_transfer_form_edges(orc, spec, n):
+    """The statuses cross as the (rule, 256-resource segment)s a pass wrote, 4 bits a status
+    (kv_status_pack_kernel), and are rebuilt on first read: batches of partial and whole
+    segments, kinds interleaved in the input (a permuted store order), a rule no resource
+    matches (no segment written) and one every resource matches."""
+    rules = [{"name": "pods", "match": {"resources": {"kinds": ["Pod"]}},
+              "validate": {"pattern": {"spec": {"containers": [{"image": "!*:latest"}]}}}},
+             {"name": "none", "match": {"resources": {"kinds": ["CronJob"]}},
+              "validate": {"pattern": {"spec": {"schedule": "?*"}}}},
+             {"name": "all", "match": {"resources": {"kinds": ["*"]}},
+              "validate": {"pattern": {"metadata": {"name": "p*"}}}}]
+    pol = {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "edges"}, "spec": {"rules": rules}}
+    ress = []
+    for i in range(n):
+        if i % 3 == 1:
+            ress.append({"apiVersion": "v1", "kind": "Service", "metadata": {"name": f"s{i}", "namespace": f"n{i % 5}"}})
+        else:
+            ress.append({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": f"p{i}", "namespace": f"n{i % 5}"},
+                         "spec": {"containers": [{"name": "c", "image": "a:latest" if i % 7 == 0 else "a:1"}]}})
+    mism, r, ost = compare(orc, [pol], ress, check_paths=True, specialize=spec)
+    assert not mism, "\n".join(mism)
+    assert r.status.shape == (3, n) and (r.status[1] == 5).all()
