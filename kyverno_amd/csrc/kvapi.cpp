@@ -1356,7 +1356,8 @@ struct DevSession {
   // `stream` builds the value-predicate table (kvj_ptab); the rule kernels wait for both
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  hipEvent_t ev_rkf = nullptr, ev_rkj = nullptr;  // rule kernels over two streams (launch_specialized)
+  hipEvent_t ev_rkf = nullptr, ev_rkj[3] = {};  // rule kernels over several streams (launch_specialized)
+  std::vector<hipStream_t> rkx;                  // (the streams beyond `stream` and `side`)
 
   double upload_ms = 0;  // policy set + batch upload of the constructor (path columns included)
   DevSession(kv_policyset* p, kv_batch* b, const char* ctx_json, int dev, uint32_t m)
@@ -1509,7 +1510,7 @@ struct DevSession {
     HIPCHK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_rkf, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&ev_rkj, hipEventDisableTiming));
+    for (hipEvent_t& e : ev_rkj) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
   // drop the kv_batch (parts sessions: the host batch is the caller's, and may be freed after
   // kv_session_attach_part); the session keeps the device copy through batch_ref, and so does
@@ -1536,7 +1537,9 @@ struct DevSession {
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
     if (ev_rkf) (void)hipEventDestroy(ev_rkf);
-    if (ev_rkj) (void)hipEventDestroy(ev_rkj);
+    for (hipEvent_t e : ev_rkj)
+      if (e) (void)hipEventDestroy(e);
+    for (hipStream_t x : rkx) StreamPool::get().give(device, hipStreamNonBlocking, x);
     for (int b = 0; b < 2; b++) {
       if (ev_pt[b]) (void)hipEventDestroy(ev_pt[b]);
       if (ev_rk[b]) (void)hipEventDestroy(ev_rk[b]);
@@ -1698,21 +1701,26 @@ struct DevSession {
     }
     uint32_t r0 = 0;
     void* args[] = {(void*)&P, (void*)&bview, (void*)&N, (void*)&V, (void*)&S, (void*)&Ov, (void*)&r0};
-    // Three or more rule kernels (they write disjoint rule rows): alternated over `stream` and
-    // `side`, forked from and joined back into `stream`, so a kernel's last workgroups share the
-    // chip with the next kernel's first instead of draining it. C3 (17 kernels) 3.56 -> 3.00 ms per
-    // pass; C4's two kernels of unequal size were 1.8 % slower side by side (0.699 -> 0.712 ms)
+    // Three or more rule kernels (they write disjoint rule rows): dealt round-robin over `stream`,
+    // `side` and a third stream, forked from and joined back into `stream`, so a kernel's last
+    // workgroups share the chip with the next kernels' first instead of draining it. C3 (17
+    // kernels), ms per pass on one box: one stream 3.56, two 2.96-3.00, three 2.66-2.69, four
+    // 2.73-2.75 (a process has 4 hardware queues; the pipeline stream takes one). C4's two kernels
+    // of unequal size were 1.8 % slower side by side (0.699 -> 0.712 ms): one stream below three
+    constexpr uint32_t kRuleStreams = 3;
     const std::vector<hipFunction_t>& fs = dps->fns_for(Ov.full);
-    const bool two = fs.size() >= 3;
-    if (two) {
+    const uint32_t ns = fs.size() >= 3 ? std::min<uint32_t>(kRuleStreams, (uint32_t)fs.size()) : 1u;
+    while (rkx.size() + 2 < ns) rkx.push_back(StreamPool::get().take(device, hipStreamNonBlocking));
+    hipStream_t sts[4] = {stream, side, rkx.size() > 0 ? rkx[0] : nullptr, rkx.size() > 1 ? rkx[1] : nullptr};
+    if (ns > 1) {
       HIPCHK(hipEventRecord(ev_rkf, stream));
-      HIPCHK(hipStreamWaitEvent(side, ev_rkf, 0));
+      for (uint32_t q = 1; q < ns; q++) HIPCHK(hipStreamWaitEvent(sts[q], ev_rkf, 0));
     }
     for (size_t k = 0; k < fs.size(); k++)
-      HIPCHK(hipModuleLaunchKernel(fs[k], blocks, 1, 1, KV_RWG, 1, 1, 0, two && (k & 1) ? side : stream, args, nullptr));
-    if (two) {
-      HIPCHK(hipEventRecord(ev_rkj, side));
-      HIPCHK(hipStreamWaitEvent(stream, ev_rkj, 0));
+      HIPCHK(hipModuleLaunchKernel(fs[k], blocks, 1, 1, KV_RWG, 1, 1, 0, sts[k % ns], args, nullptr));
+    for (uint32_t q = 1; q < ns; q++) {
+      HIPCHK(hipEventRecord(ev_rkj[q - 1], sts[q]));
+      HIPCHK(hipStreamWaitEvent(stream, ev_rkj[q - 1], 0));
     }
   }
   // status-matrix bytes the last pass wrote: the (rule, workgroup) segments whose flag it set (a
