@@ -39,6 +39,11 @@ bool go_parse_float(std::string_view s, double* out) {
   size_t k = 0;
   bool neg = false;
   if (s[0] == '+' || s[0] == '-') { neg = s[0] == '-'; k = 1; }
+  // every form below starts with a digit, '.', "inf" / "infinity" or "nan" (any case): reject the
+  // rest (most strings: image names, resource names) before building the copies
+  if (k >= n) return false;
+  const char c0 = s[k];
+  if (!((c0 >= '0' && c0 <= '9') || c0 == '.' || c0 == 'i' || c0 == 'I' || c0 == 'n' || c0 == 'N')) return false;
   std::string rest(s.substr(k));
   std::string low = rest;
   for (auto& c : low) c = (char)tolower((unsigned char)c);

@@ -114,8 +114,10 @@ struct Ingest {
   std::vector<std::vector<uint32_t>> slot_ids;  // per trie node: key ids of its slots
   std::vector<Probe> slot_tab;                  // per trie node: slot of a key (built on first use)
 
+  bool meta_rules = false;  // some rule reads labels / annotations through ExpandInMetadata (RR_META_*)
   Ingest(const PolicySet& p, Batch& bb) : ps(p), b(bb), nstatic((uint32_t)p.keys.size()), slot_ids(p.trie.nodes.size()),
                                           slot_tab(p.trie.nodes.size()) {
+    for (const RuleRec& rr : p.rules) meta_rules |= meta_bad_flags(rr.flags) != 0u;
     str_off.init(1 << 14);
     vtab.assign(1 << 15, VSlot{});
     dict.init(p.keys.size());
@@ -693,7 +695,8 @@ struct Ingest {
     r.aset = kvset(d, ann, false);
     bool fresh = false;
     r.ns_index = intern(ns_probe, b.namespaces, ns, &fresh);
-    if (const uint32_t bm = bad_meta(d)) r.flags |= RF_BAD_META | bm;
+    if (meta_rules)  // (the flags only route rules whose ExpandInMetadata sites read labels / annotations)
+      if (const uint32_t bm = bad_meta(d)) r.flags |= RF_BAD_META | bm;
     // the anchor-mismatch error substrings (common/anchorKey.go:12-19): both end in
     // "anchor mismatch", so one search finds any candidate
     if (memmem(d.strs.data(), d.strs.size(), "anchor mismatch", 15) &&
