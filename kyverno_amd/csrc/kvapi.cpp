@@ -1358,6 +1358,9 @@ struct DevSession {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_rkf = nullptr, ev_rkj[3] = {};  // rule kernels over several streams (launch_specialized)
   std::vector<hipStream_t> rkx;                  // (the streams beyond `stream` and `side`)
+  std::vector<hipEvent_t> kev;                   // start / end of each rule kernel in the timed pass
+  std::vector<uint32_t> korder;                  // rule kernels, longest first (after a timed pass)
+  bool ktiming = false;
 
   double upload_ms = 0;  // policy set + batch upload of the constructor (path columns included)
   DevSession(kv_policyset* p, kv_batch* b, const char* ctx_json, int dev, uint32_t m)
@@ -1539,6 +1542,7 @@ struct DevSession {
     if (ev_rkf) (void)hipEventDestroy(ev_rkf);
     for (hipEvent_t e : ev_rkj)
       if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : kev) (void)hipEventDestroy(e);
     for (hipStream_t x : rkx) StreamPool::get().give(device, hipStreamNonBlocking, x);
     for (int b = 0; b < 2; b++) {
       if (ev_pt[b]) (void)hipEventDestroy(ev_pt[b]);
@@ -1603,6 +1607,7 @@ struct DevSession {
     }
     HIPCHK(hipEventRecord(e1, stream));
     HIPCHK(hipEventSynchronize(e1));
+    order_kernels();
     if (pipe && iters > 0 && ((iters - 1) & 1)) {  // the last pass counted into set 1: it becomes set 0
       cn.swap(cn1);
       scn.swap(scn1);
@@ -1701,27 +1706,62 @@ struct DevSession {
     }
     uint32_t r0 = 0;
     void* args[] = {(void*)&P, (void*)&bview, (void*)&N, (void*)&V, (void*)&S, (void*)&Ov, (void*)&r0};
-    // Three or more rule kernels (they write disjoint rule rows): dealt round-robin over `stream`,
-    // `side` and a third stream, forked from and joined back into `stream`, so a kernel's last
-    // workgroups share the chip with the next kernels' first instead of draining it. C3 (17
-    // kernels), ms per pass on one box: one stream 3.56, two 2.96-3.00, three 2.66-2.69, four
-    // 2.73-2.75 (a process has 4 hardware queues; the pipeline stream takes one). C4's two kernels
-    // of unequal size were 1.8 % slower side by side (0.699 -> 0.712 ms): one stream below three
+    // Rule kernels of a pass (they write disjoint rule rows): three or more are dealt round-robin
+    // over `stream`, `side` and a third stream, forked from and joined back into `stream`, so a
+    // kernel's last workgroups share the chip with the next kernels' first instead of draining it;
+    // once a pass has timed them, they go longest first (and two kernels then go over two
+    // streams: the short one fills the long one's tail). C3 (17 kernels), ms per pass on one box:
+    // one stream 3.56, two 2.96-3.01, three 2.66-2.69, four 2.73-2.75 (a process has 4 hardware
+    // queues; the pipeline stream takes one). C4 (2 kernels, 150 and 515 us): one stream 0.690,
+    // two in plan order 0.713-0.714, two longest first 0.613-0.617.
     constexpr uint32_t kRuleStreams = 3;
     const std::vector<hipFunction_t>& fs = dps->fns_for(Ov.full);
-    const uint32_t ns = fs.size() >= 3 ? std::min<uint32_t>(kRuleStreams, (uint32_t)fs.size()) : 1u;
+    const uint32_t nk = (uint32_t)fs.size();
+    const bool ordered = korder.size() == nk && nk > 1;
+    const uint32_t ns = nk >= 3 ? std::min<uint32_t>(kRuleStreams, nk) : (ordered ? nk : 1u);
+    // the first pass of a session with 2+ kernels times them (events around each launch)
+    const bool timing = !ordered && nk > 1 && !ktiming;
+    if (timing) {
+      while (kev.size() < 2 * nk) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        kev.push_back(e);
+      }
+      ktiming = true;
+    }
     while (rkx.size() + 2 < ns) rkx.push_back(StreamPool::get().take(device, hipStreamNonBlocking));
     hipStream_t sts[4] = {stream, side, rkx.size() > 0 ? rkx[0] : nullptr, rkx.size() > 1 ? rkx[1] : nullptr};
     if (ns > 1) {
       HIPCHK(hipEventRecord(ev_rkf, stream));
       for (uint32_t q = 1; q < ns; q++) HIPCHK(hipStreamWaitEvent(sts[q], ev_rkf, 0));
     }
-    for (size_t k = 0; k < fs.size(); k++)
-      HIPCHK(hipModuleLaunchKernel(fs[k], blocks, 1, 1, KV_RWG, 1, 1, 0, sts[k % ns], args, nullptr));
+    for (uint32_t k = 0; k < nk; k++) {
+      const uint32_t f = ordered ? korder[k] : k;
+      hipStream_t st = sts[k % ns];
+      if (timing) HIPCHK(hipEventRecord(kev[2 * f], st));
+      HIPCHK(hipModuleLaunchKernel(fs[f], blocks, 1, 1, KV_RWG, 1, 1, 0, st, args, nullptr));
+      if (timing) HIPCHK(hipEventRecord(kev[2 * f + 1], st));
+    }
     for (uint32_t q = 1; q < ns; q++) {
       HIPCHK(hipEventRecord(ev_rkj[q - 1], sts[q]));
       HIPCHK(hipStreamWaitEvent(stream, ev_rkj[q - 1], 0));
     }
+  }
+  // after a timed pass has completed: the rule kernels' launch order, longest first
+  void order_kernels() {
+    if (!ktiming || !korder.empty()) return;
+    const uint32_t nk = (uint32_t)(kev.size() / 2);
+    std::vector<std::pair<float, uint32_t>> d(nk);
+    for (uint32_t k = 0; k < nk; k++) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, kev[2 * k], kev[2 * k + 1]) != hipSuccess) {
+        (void)hipGetLastError();
+        return;  // (not timed in this run: keep the plan order)
+      }
+      d[k] = {ms, k};
+    }
+    std::stable_sort(d.begin(), d.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+    for (const auto& x : d) korder.push_back(x.second);
   }
   // status-matrix bytes the last pass wrote: the (rule, workgroup) segments whose flag it set (a
   // segment left unwritten is all NOMATCH and filled at fetch), or the whole matrix without flags
