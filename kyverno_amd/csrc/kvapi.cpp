@@ -362,6 +362,11 @@ struct DevPolicySet {
     auto it = vfns.find(full);
     return it == vfns.end() ? fns : it->second;
   }
+  // the rule kernels longest first, as the first session to time them found (DevSession::
+  // order_kernels); later sessions of the policy set on this device, kv_validate's single pass
+  // included, start from it
+  std::mutex order_mu;
+  std::vector<uint32_t> korder;
   hipFunction_t ptab_fn = nullptr;  // value-predicate table builder (kvj_ptab)
   uint32_t mtup_words = 0;          // match words per tuple (kv_mfac + kv_mtup, factored match)
   uint32_t fac_slots = 0;
@@ -1717,6 +1722,10 @@ struct DevSession {
     constexpr uint32_t kRuleStreams = 3;
     const std::vector<hipFunction_t>& fs = dps->fns_for(Ov.full);
     const uint32_t nk = (uint32_t)fs.size();
+    if (korder.empty() && nk > 1) {
+      std::lock_guard<std::mutex> g(dps->order_mu);
+      if (dps->korder.size() == nk) korder = dps->korder;
+    }
     const bool ordered = korder.size() == nk && nk > 1;
     const uint32_t ns = nk >= 3 ? std::min<uint32_t>(kRuleStreams, nk) : (ordered ? nk : 1u);
     // the first pass of a session with 2+ kernels times them (events around each launch)
@@ -1762,6 +1771,8 @@ struct DevSession {
     }
     std::stable_sort(d.begin(), d.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
     for (const auto& x : d) korder.push_back(x.second);
+    std::lock_guard<std::mutex> g(dps->order_mu);
+    if (dps->korder.empty()) dps->korder = korder;
   }
   // status-matrix bytes the last pass wrote: the (rule, workgroup) segments whose flag it set (a
   // segment left unwritten is all NOMATCH and filled at fetch), or the whole matrix without flags
