@@ -404,7 +404,17 @@ struct Ingest {
       default:
         sv = d.sval(n);
         memcpy(&k8, sv.data(), std::min<size_t>(8, sv.size()));
-        hv = hash_bytes(sv.data(), sv.size(), 's');
+        if (sv.size() <= 16) {  // (most values: two multiplies instead of the byte-wise hash)
+          uint64_t w1 = 0;
+          if (sv.size() > 8) memcpy(&w1, sv.data() + 8, sv.size() - 8);
+          uint64_t h = (k8 * 0x9E3779B97F4A7C15ull) ^ (w1 * 0xC2B2AE3D27D4EB4Full) ^ (sv.size() * 0x165667B19E3779F9ull);
+          h ^= h >> 32;
+          h *= 0xD6E8FEB86659FD93ull;
+          h ^= h >> 29;
+          hv = h ? h : 1;
+        } else {
+          hv = hash_bytes(sv.data(), sv.size(), 's');
+        }
         break;
     }
     const uint32_t bit = kv_tcls(pos);
