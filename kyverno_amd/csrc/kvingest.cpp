@@ -81,6 +81,17 @@ struct Ingest {
     }
   };
   static uint64_t hash_bytes(const void* p, size_t len, uint64_t seed) {
+    if (len <= 16) {  // (most keys and values: two multiplies instead of the word loop)
+      uint64_t w0 = 0, w1 = 0;
+      if (len) memcpy(&w0, p, len < 8 ? len : 8);  // (an empty view may carry a null pointer)
+      if (len > 8) memcpy(&w1, (const uint8_t*)p + 8, len - 8);
+      uint64_t h = (w0 * 0x9E3779B97F4A7C15ull) ^ (w1 * 0xC2B2AE3D27D4EB4Full) ^ ((len + 1) * 0x165667B19E3779F9ull) ^
+                   (seed * 0x27D4EB2F165667C5ull);
+      h ^= h >> 32;
+      h *= 0xD6E8FEB86659FD93ull;
+      h ^= h >> 29;
+      return h ? h : 1;
+    }
     const uint8_t* s = (const uint8_t*)p;  // FNV-1a 64 over 8-byte words, then a final mix
     uint64_t h = 1469598103934665603ull ^ seed ^ (len * 0x9E3779B97F4A7C15ull);
     size_t i = 0;
@@ -404,17 +415,7 @@ struct Ingest {
       default:
         sv = d.sval(n);
         memcpy(&k8, sv.data(), std::min<size_t>(8, sv.size()));
-        if (sv.size() <= 16) {  // (most values: two multiplies instead of the byte-wise hash)
-          uint64_t w1 = 0;
-          if (sv.size() > 8) memcpy(&w1, sv.data() + 8, sv.size() - 8);
-          uint64_t h = (k8 * 0x9E3779B97F4A7C15ull) ^ (w1 * 0xC2B2AE3D27D4EB4Full) ^ (sv.size() * 0x165667B19E3779F9ull);
-          h ^= h >> 32;
-          h *= 0xD6E8FEB86659FD93ull;
-          h ^= h >> 29;
-          hv = h ? h : 1;
-        } else {
-          hv = hash_bytes(sv.data(), sv.size(), 's');
-        }
+        hv = hash_bytes(sv.data(), sv.size(), 's');
         break;
     }
     const uint32_t bit = kv_tcls(pos);
