@@ -1820,10 +1820,6 @@ struct DevSession {
     const bool want_st = O.status && (mode & (KV_MODE_STATUS | KV_MODE_ERRORS)) && nres && nrules;
     bool side_copy = false;
     uint64_t spack_bytes = 0;
-    if (O.status && O.sflag && rec_compact && nres && nrules) {  // the segments the pass left NOMATCH
-      HIPCHK(launch_status_fill(O.status, O.sflag, (uint32_t)nres, (uint32_t)nrules, stream));
-      lap("status_fill");
-    }
     // A permuted batch fetched whole comes back in the caller's order: the statuses are gathered on
     // the device (stc[rule][j] = st[rule][store index of j]) and the records scattered to the
     // caller's (rule, resource) order, so one status matrix crosses PCIe and the host permutes
@@ -1904,9 +1900,13 @@ struct DevSession {
         masks = (unsigned long long*)r_mask.p;
       }
       const uint8_t* rank_st = caller ? (const uint8_t*)stc.p : O.status;
+      // a specialized pass's unwritten segments hold no records: the record kernels skip them
+      // (their statuses are neither filled nor read)
+      const uint8_t* seg_flags = rec_compact && !caller ? O.sflag : nullptr;
       HIPCHK(launch_rec_compact(rank_st, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                 (unsigned long long*)r_tot.p, (unsigned long long*)r_base.p, nullptr, nullptr, nullptr,
-                                0, rec_compact ? (const uint8_t*)dps->rcompact.p : nullptr, nullptr, masks, stream));
+                                0, rec_compact ? (const uint8_t*)dps->rcompact.p : nullptr, nullptr, masks, seg_flags,
+                                stream));
       // the fetch's small device-to-host copies go through one page-locked staging block (a copy
       // into pageable memory is staged by the runtime and waited for behind the DMA queue)
       const size_t tb = (size_t)nrules * KV_REC_CODES, sb = ((nrules + 1) * 8 + 63) & ~(size_t)63;
@@ -1932,7 +1932,7 @@ struct DevSession {
       HIPCHK(launch_rec_compact(O.status, O.err8, nullptr, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                 nullptr, (unsigned long long*)r_base.p, (ErrRec8*)r_out8.p, nullptr,
                                 (uint32_t*)r_wide.p, 1, rec_compact ? (const uint8_t*)dps->rcompact.p : nullptr, ord,
-                                masks, stream));
+                                masks, seg_flags, stream));
       HIPCHK(hipMemcpyAsync(hstage.data() + sb, r_wide.p, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
       lap("records_scatter");
       uint32_t wide = 0;
@@ -2004,7 +2004,7 @@ struct DevSession {
         if (r_outw.n < total * sizeof(ErrRec)) r_outw.alloc(std::max<uint64_t>(total, 1) * sizeof(ErrRec), device);
         HIPCHK(launch_rec_compact(O.status, O.err8, O.err, (uint32_t)nres, (uint32_t)nrules, (uint32_t*)r_offs.p,
                                   nullptr, (unsigned long long*)r_base.p, (ErrRec8*)r_out8.p, (ErrRec*)r_outw.p,
-                                  (uint32_t*)r_wide.p, 1, nullptr, ord, masks, stream));
+                                  (uint32_t*)r_wide.p, 1, nullptr, ord, masks, nullptr, stream));
         part->recw.alloc(total);
         HIPCHK(hipMemcpyAsync(part->recw.data(), r_outw.p, total * sizeof(ErrRec), hipMemcpyDeviceToHost, stream));
         lap("records_wide_rerun");

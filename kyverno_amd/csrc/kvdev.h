@@ -46,8 +46,7 @@ hipError_t launch_remap_u32(uint32_t* a, uint64_t n, const uint32_t* map, hipStr
 // segments) into ccnt[rule][chunk]; otherwise packs them (4 bits a status) at cbase[rule][chunk] * KV_RWG / 2
 hipError_t launch_status_pack(const uint8_t* status, const uint8_t* sflag, uint32_t n_res, uint32_t n_rules,
                               const unsigned long long* cbase, uint32_t* ccnt, uint8_t* out, hipStream_t stream);
-hipError_t launch_status_fill(uint8_t* status, const uint8_t* sflag, uint32_t n_res, uint32_t n_rules,
-                              hipStream_t stream);
+
 // site records of the specialized rule groups -> the members' records at their slots (kvdevtypes.h
 // GSiteDesc; fetch time, before launch_rec_compact's scatter)
 hipError_t launch_gsite_expand(const uint32_t* gsite, const uint32_t* gcnt, const GSiteDesc* desc, const uint32_t* mem,
@@ -55,7 +54,7 @@ hipError_t launch_gsite_expand(const uint32_t* gsite, const uint32_t* gcnt, cons
 hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const ErrRec* errw, uint32_t n_res,
                               uint32_t n_rules, uint32_t* offs, unsigned long long* totals, unsigned long long* base,
                               ErrRec8* out8, ErrRec* outw, uint32_t* wide, int phase, const uint8_t* compact,
-                              const uint32_t* order, unsigned long long* masks, hipStream_t stream);
+                              const uint32_t* order, unsigned long long* masks, const uint8_t* sflag, hipStream_t stream);
 
 // Record codes of a compacted record array (rule-major, rule r at [base[r], base[r + 1])): phase 0
 // writes each record's slot in its rule's table of KV_REC_CODES distinct records (tkey, keys w0 << 32

@@ -475,12 +475,21 @@ __device__ __forceinline__ bool has_record(uint8_t s) { return s == ST_FAIL || s
 
 // A workgroup walks tiles blockIdx.x, + gridDim.x, ... of one rule (a workgroup per (tile, rule)
 // was 9.6 M workgroups at C3, 8 ms of dispatch for 2.5 GB of statuses)
+static_assert(KV_WG == KV_RWG, "a record tile is one status segment of a rule kernel's workgroup (sflag)");
+// sflag (specialized passes): a tile whose segment the pass did not write is all NOMATCH: no
+// records, and its statuses (never written, never filled) are not read
 __global__ __launch_bounds__(KV_WG) void kv_rec_count_kernel(const uint8_t* __restrict__ status, uint32_t n_res,
                                                               uint32_t tiles, uint32_t* __restrict__ counts,
-                                                              unsigned long long* __restrict__ masks, uint32_t rule0) {
+                                                              unsigned long long* __restrict__ masks,
+                                                              const uint8_t* __restrict__ sflag, uint32_t rule0) {
   __shared__ uint32_t s_w[KV_WG / 64];
   const uint32_t rule = rule0 + blockIdx.y;
   for (uint32_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    if (sflag && !sflag[(size_t)rule * tiles + t]) {  // (uniform: the whole workgroup skips)
+      if (threadIdx.x == 0) counts[(size_t)rule * tiles + t] = 0u;
+      if (masks && (threadIdx.x & 63) == 0) masks[(size_t)rule * tiles * (KV_WG / 64) + ((t * KV_WG + threadIdx.x) >> 6)] = 0ull;
+      continue;
+    }
     const uint32_t r = t * KV_WG + threadIdx.x;
     const bool f = r < n_res && has_record(status[(size_t)rule * n_res + r]);
     const uint64_t m = __ballot(f);
@@ -554,12 +563,13 @@ __global__ __launch_bounds__(KV_WG) void kv_rec_scatter_kernel(const uint8_t* __
                                                                 const uint8_t* __restrict__ compact,
                                                                 const uint32_t* __restrict__ order,
                                                                 const unsigned long long* __restrict__ masks,
-                                                                uint32_t rule0) {
+                                                                const uint8_t* __restrict__ sflag, uint32_t rule0) {
   __shared__ uint32_t s_w[KV_WG / 64];
   const uint32_t rule = rule0 + blockIdx.y, lane = threadIdx.x & 63;
   const bool cmp = compact && compact[rule];  // (rule is uniform: a scalar branch)
   const unsigned long long rb = base[rule];
   for (uint32_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    if (sflag && !sflag[(size_t)rule * tiles + t]) continue;  // (no records; uniform)
     const uint32_t r = t * KV_WG + threadIdx.x;
     const size_t o = (size_t)rule * n_res + r;
     const bool f = r < n_res && has_record(status[o]);
@@ -792,36 +802,12 @@ hipError_t launch_status_pack(const uint8_t* status, const uint8_t* sflag, uint3
   return hipSuccess;
 }
 
-// NOMATCH into the status segments (KV_RWG statuses of a rule kernel's workgroup) the specialized
-// kernels left unwritten (DevOut::sflag): 16 B per lane, KV_RWG / 16 lanes per segment
-__global__ __launch_bounds__(KV_WG) void kv_status_fill_kernel(uint8_t* __restrict__ status,
-                                                                const uint8_t* __restrict__ sflag, uint32_t n_res,
-                                                                uint32_t n_rules, uint32_t rule0) {
-  constexpr uint32_t LPS = (uint32_t)KV_RWG / 16u;
-  const uint32_t nwg = (n_res + KV_RWG - 1) / KV_RWG, g = blockIdx.x * (KV_WG / LPS) + threadIdx.x / LPS;
-  const uint32_t rule = rule0 + blockIdx.y, l = threadIdx.x % LPS;
-  if (g >= nwg || sflag[(size_t)rule * nwg + g]) return;
-  const uint32_t nm = 0x01010101u * (uint32_t)ST_NOMATCH;
-  // (an unwritten segment is a whole workgroup: n_res % 16 == 0 and the segment inside the batch)
-  *(uint4*)(status + (size_t)rule * n_res + (size_t)g * KV_RWG + l * 16u) = make_uint4(nm, nm, nm, nm);
-}
-
-hipError_t launch_status_fill(uint8_t* status, const uint8_t* sflag, uint32_t n_res, uint32_t n_rules,
-                              hipStream_t stream) {
-  if (n_res == 0 || n_rules == 0) return hipSuccess;
-  const uint32_t nwg = (n_res + KV_RWG - 1) / KV_RWG, per = (uint32_t)KV_WG / ((uint32_t)KV_RWG / 16u);
-  for (uint32_t q0 = 0; q0 < n_rules; q0 += kMaxGridY) {  // (grid y holds at most 65535 rules)
-    hipLaunchKernelGGL(kv_status_fill_kernel, dim3((nwg + per - 1) / per, std::min(kMaxGridY, n_rules - q0)),
-                       dim3(KV_WG), 0, stream, status, sflag, n_res, n_rules, q0);
-    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-  }
-  return hipSuccess;
-}
 
 hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const ErrRec* errw, uint32_t n_res,
                               uint32_t n_rules, uint32_t* offs, unsigned long long* totals, unsigned long long* base,
                               ErrRec8* out8, ErrRec* outw, uint32_t* wide, int phase, const uint8_t* compact,
-                              const uint32_t* order, unsigned long long* masks, hipStream_t stream) {
+                              const uint32_t* order, unsigned long long* masks, const uint8_t* sflag,
+                              hipStream_t stream) {
   if (n_res == 0 || n_rules == 0) return hipSuccess;
   const uint32_t tiles = (n_res + KV_WG - 1) / KV_WG;
   // about 65 536 workgroups in all, each walking its rule's tiles (C3: 16 384 in all left the
@@ -830,10 +816,10 @@ hipError_t launch_rec_compact(const uint8_t* status, const ErrRec8* err8, const 
   for (uint32_t q0 = 0; q0 < n_rules; q0 += kMaxGridY) {
     const dim3 grid(gx, std::min(kMaxGridY, n_rules - q0));
     if (phase == 0)  // offsets (the scan and bases below)
-      hipLaunchKernelGGL(kv_rec_count_kernel, grid, dim3(KV_WG), 0, stream, status, n_res, tiles, offs, masks, q0);
+      hipLaunchKernelGGL(kv_rec_count_kernel, grid, dim3(KV_WG), 0, stream, status, n_res, tiles, offs, masks, sflag, q0);
     else
       hipLaunchKernelGGL(kv_rec_scatter_kernel, grid, dim3(KV_WG), 0, stream, status, err8, errw, n_res, tiles, offs,
-                         base, out8, outw, wide, compact, order, masks, q0);
+                         base, out8, outw, wide, compact, order, masks, sflag, q0);
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   }
   if (phase == 0) {
